@@ -1,0 +1,239 @@
+/* bvh_build.cpp - parallel binned-SAH BVH2 builder (see bvh_build.h). */
+#include "bvh_build.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <thread>
+
+namespace lh2 {
+
+namespace {
+
+constexpr int BINS = 16;
+constexpr float C_TRAV = 1.0f, C_ISECT = 1.0f;
+constexpr uint32_t PAR_THRESHOLD = 16384;
+
+struct TNode { Aabb box; int left, right; uint32_t first, count; };
+
+inline void grow( Aabb& a, const Aabb& b )
+{
+	for (int k = 0; k < 3; k++) a.lo[k] = std::min( a.lo[k], b.lo[k] ), a.hi[k] = std::max( a.hi[k], b.hi[k] );
+}
+inline Aabb empty_box()
+{
+	Aabb a;
+	for (int k = 0; k < 3; k++) a.lo[k] = std::numeric_limits<float>::max(), a.hi[k] = -std::numeric_limits<float>::max();
+	return a;
+}
+inline float area( const Aabb& a )
+{
+	const float dx = a.hi[0] - a.lo[0], dy = a.hi[1] - a.lo[1], dz = a.hi[2] - a.lo[2];
+	if (dx < 0 || dy < 0 || dz < 0) return 0;
+	return 2.0f * (dx * dy + dx * dz + dy * dz);
+}
+
+struct Builder
+{
+	const std::vector<Aabb>& prims;
+	std::vector<float> cent;      /* 3 per prim */
+	std::vector<uint32_t> idx;
+	std::vector<TNode> nodes;
+	std::atomic<int> nodeCount{ 0 };
+	std::atomic<int> threadsLeft{ 0 };
+	int maxLeaf;
+
+	explicit Builder( const std::vector<Aabb>& p ) : prims( p ) {}
+
+	int alloc2() { return nodeCount.fetch_add( 2 ); }
+
+	void make_leaf( int ni, uint32_t first, uint32_t count, const Aabb& box )
+	{
+		TNode& n = nodes[ni];
+		n.box = box, n.left = n.right = -1, n.first = first, n.count = count;
+	}
+
+	void build( int ni, uint32_t first, uint32_t count )
+	{
+		Aabb box = empty_box(), cbox = empty_box();
+		for (uint32_t i = first; i < first + count; i++)
+		{
+			const uint32_t p = idx[i];
+			grow( box, prims[p] );
+			for (int k = 0; k < 3; k++) cbox.lo[k] = std::min( cbox.lo[k], cent[p * 3 + k] ), cbox.hi[k] = std::max( cbox.hi[k], cent[p * 3 + k] );
+		}
+		if (count <= 2) { make_leaf( ni, first, count, box ); return; }
+		/* binned SAH over the three axes */
+		float bestCost = std::numeric_limits<float>::max();
+		int bestAxis = -1, bestBin = -1;
+		const float parentArea = area( box );
+		for (int a = 0; a < 3; a++)
+		{
+			const float ext = cbox.hi[a] - cbox.lo[a];
+			if (!(ext > 0)) continue;
+			const float scale = (float)BINS * 0.99999f / ext;
+			Aabb bb[BINS]; uint32_t bc[BINS];
+			for (int b = 0; b < BINS; b++) bb[b] = empty_box(), bc[b] = 0;
+			for (uint32_t i = first; i < first + count; i++)
+			{
+				const uint32_t p = idx[i];
+				int b = (int)((cent[p * 3 + a] - cbox.lo[a]) * scale);
+				b = std::min( std::max( b, 0 ), BINS - 1 );
+				bc[b]++, grow( bb[b], prims[p] );
+			}
+			float rightArea[BINS]; uint32_t rightCount[BINS];
+			Aabb acc = empty_box(); uint32_t n = 0;
+			for (int b = BINS - 1; b > 0; b--) { grow( acc, bb[b] ); n += bc[b]; rightArea[b] = area( acc ), rightCount[b] = n; }
+			acc = empty_box(); n = 0;
+			for (int b = 0; b < BINS - 1; b++)
+			{
+				grow( acc, bb[b] ); n += bc[b];
+				if (n == 0 || rightCount[b + 1] == 0) continue;
+				const float cost = C_TRAV + C_ISECT * (area( acc ) * n + rightArea[b + 1] * rightCount[b + 1]) / std::max( parentArea, 1e-30f );
+				if (cost < bestCost) bestCost = cost, bestAxis = a, bestBin = b;
+			}
+		}
+		const float leafCost = C_ISECT * (float)count;
+		if (count <= (uint32_t)maxLeaf && (bestAxis < 0 || leafCost <= bestCost)) { make_leaf( ni, first, count, box ); return; }
+		uint32_t mid;
+		if (bestAxis >= 0)
+		{
+			const float ext = cbox.hi[bestAxis] - cbox.lo[bestAxis];
+			const float scale = (float)BINS * 0.99999f / ext;
+			const float lo = cbox.lo[bestAxis];
+			const int a = bestAxis, sb = bestBin;
+			uint32_t* it = std::partition( idx.data() + first, idx.data() + first + count, [&]( uint32_t p ) {
+				int b = (int)((cent[p * 3 + a] - lo) * scale);
+				b = std::min( std::max( b, 0 ), BINS - 1 );
+				return b <= sb;
+			} );
+			mid = (uint32_t)(it - idx.data());
+		}
+		else
+		{
+			/* every centroid identical (or degenerate): split the range in the middle */
+			mid = first + count / 2;
+		}
+		if (mid == first || mid == first + count) mid = first + count / 2;
+		const int c = alloc2();
+		TNode& nd = nodes[ni];
+		nd.box = box, nd.left = c, nd.right = c + 1, nd.first = 0, nd.count = 0;
+		const uint32_t lc = mid - first, rc = count - lc;
+		if (count >= PAR_THRESHOLD && threadsLeft.fetch_sub( 1 ) > 0)
+		{
+			std::thread t( [this, c, first, lc]() { build( c, first, lc ); } );
+			build( c + 1, mid, rc );
+			t.join();
+			threadsLeft.fetch_add( 1 );
+		}
+		else
+		{
+			if (count >= PAR_THRESHOLD) threadsLeft.fetch_add( 1 );
+			build( c, first, lc );
+			build( c + 1, mid, rc );
+		}
+	}
+};
+
+inline int make_leaf_ref( uint32_t first, uint32_t count ) { return (int)~((first << 4) | (count - 1)); }
+
+}  // namespace
+
+void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out )
+{
+	const uint32_t N = (uint32_t)prims.size();
+	if (maxLeaf < 1) maxLeaf = 1;
+	if (maxLeaf > 16) maxLeaf = 16;
+	Builder b( prims );
+	b.maxLeaf = maxLeaf;
+	b.cent.resize( (size_t)N * 3 );
+	b.idx.resize( N );
+	for (uint32_t i = 0; i < N; i++)
+	{
+		b.idx[i] = i;
+		for (int k = 0; k < 3; k++) b.cent[i * 3 + k] = 0.5f * prims[i].lo[k] + 0.5f * prims[i].hi[k];
+	}
+	b.nodes.resize( std::max<size_t>( 2 * (size_t)N + 1, 3 ) );
+	b.nodeCount = 1;
+	unsigned hw = std::thread::hardware_concurrency();
+	b.threadsLeft = (threads > 0 ? threads : (int)(hw ? hw : 4)) - 1;
+	out.nodes.clear(); out.perm.clear(); out.maxDepth = 0; out.leafCount = 0; out.sah = 0;
+	const float nanv = std::numeric_limits<float>::quiet_NaN();
+	if (N == 0)
+	{
+		/* root with two empty (NaN) children: never hit */
+		out.nodes.assign( 16, nanv );
+		int refs[4] = { make_leaf_ref( 0, 1 ), make_leaf_ref( 0, 1 ), 0, 0 };
+		memcpy( &out.nodes[12], refs, 16 );
+		return;
+	}
+	b.build( 0, 0, N );
+	out.perm = b.idx;
+	/* flatten interior nodes in DFS pre-order into the child-pair layout */
+	struct Item { int tnode; int gpu; int depth; };
+	std::vector<Item> stack;
+	auto emit = [&]() { out.nodes.resize( out.nodes.size() + 16 ); return (int)(out.nodes.size() / 16) - 1; };
+	const TNode& root = b.nodes[0];
+	const float rootArea = std::max( area( root.box ), 1e-30f );
+	if (root.left < 0)
+	{
+		const int g = emit();
+		float* n = &out.nodes[(size_t)g * 16];
+		n[0] = root.box.lo[0], n[1] = root.box.hi[0], n[2] = root.box.lo[1], n[3] = root.box.hi[1];
+		n[4] = nanv, n[5] = nanv, n[6] = nanv, n[7] = nanv;
+		n[8] = root.box.lo[2], n[9] = root.box.hi[2], n[10] = nanv, n[11] = nanv;
+		int refs[4] = { make_leaf_ref( root.first, root.count ), make_leaf_ref( 0, 1 ), 0, 0 };
+		memcpy( n + 12, refs, 16 );
+		out.maxDepth = 1, out.leafCount = 1, out.sah = C_TRAV + C_ISECT * root.count;
+		return;
+	}
+	stack.push_back( { 0, emit(), 1 } );
+	double sah = 0;
+	while (!stack.empty())
+	{
+		const Item it = stack.back();
+		stack.pop_back();
+		const TNode& t = b.nodes[it.tnode];
+		sah += C_TRAV * area( t.box ) / rootArea;
+		out.maxDepth = std::max( out.maxDepth, it.depth );
+		const TNode* ch[2] = { &b.nodes[t.left], &b.nodes[t.right] };
+		int refs[2];
+		for (int c = 0; c < 2; c++)
+		{
+			if (ch[c]->left < 0)
+			{
+				refs[c] = make_leaf_ref( ch[c]->first, ch[c]->count );
+				out.leafCount++;
+				sah += C_ISECT * ch[c]->count * area( ch[c]->box ) / rootArea;
+			}
+			else refs[c] = -1;  /* patched below */
+		}
+		/* children pushed right-then-left so the left subtree gets the next index */
+		int gidx[2] = { -1, -1 };
+		for (int c = 1; c >= 0; c--) if (ch[c]->left >= 0) { gidx[c] = 0; }
+		float* n;
+		{
+			float tmp[16];
+			tmp[0] = ch[0]->box.lo[0], tmp[1] = ch[0]->box.hi[0], tmp[2] = ch[0]->box.lo[1], tmp[3] = ch[0]->box.hi[1];
+			tmp[4] = ch[1]->box.lo[0], tmp[5] = ch[1]->box.hi[0], tmp[6] = ch[1]->box.lo[1], tmp[7] = ch[1]->box.hi[1];
+			tmp[8] = ch[0]->box.lo[2], tmp[9] = ch[0]->box.hi[2], tmp[10] = ch[1]->box.lo[2], tmp[11] = ch[1]->box.hi[2];
+			memset( tmp + 12, 0, 16 );
+			n = &out.nodes[(size_t)it.gpu * 16];
+			memcpy( n, tmp, 48 );
+		}
+		/* allocate GPU nodes for interior children: left first (DFS pre-order) */
+		if (ch[0]->left >= 0) gidx[0] = emit();
+		if (ch[1]->left >= 0) gidx[1] = emit();
+		n = &out.nodes[(size_t)it.gpu * 16];  /* emit() may reallocate */
+		for (int c = 0; c < 2; c++) if (gidx[c] >= 0) refs[c] = gidx[c];
+		int r4[4] = { refs[0], refs[1], 0, 0 };
+		memcpy( n + 12, r4, 16 );
+		if (ch[1]->left >= 0) stack.push_back( { t.right, gidx[1], it.depth + 1 } );
+		if (ch[0]->left >= 0) stack.push_back( { t.left, gidx[0], it.depth + 1 } );
+	}
+	out.sah = sah;
+}
+
+}  // namespace lh2

@@ -1,0 +1,30 @@
+/* bvh_build.h - binned-SAH BVH2 builder producing the GPU child-pair node layout.
+
+   Algorithm family: RenderCore_Bart/bvh.cpp:57-256 (binned SAH, surface-area x count cost, leaves
+   for small or unsplittable ranges).  MI355X-first changes: O(N) per level via a bin sweep
+   (Bart re-partitions per candidate plane), 16 bins, traversal/intersection cost model, leaves
+   capped at 8 primitives, parallel subtrees, and an output layout in which each 64-B node holds
+   both children's boxes (lh2_device.h).  Hit results do not depend on the tree (tie rule
+   (t, instance, triangle)), only the traversal cost does.
+*/
+#pragma once
+#include <stdint.h>
+#include <vector>
+
+namespace lh2 {
+
+struct Aabb { float lo[3], hi[3]; };
+
+struct BvhOutput
+{
+	std::vector<float> nodes;      /* 16 floats per node (child-pair layout), node 0 = root */
+	std::vector<uint32_t> perm;    /* leaf order -> primitive index */
+	int maxDepth = 0;              /* interior levels on the deepest root-to-leaf path */
+	int leafCount = 0;
+	double sah = 0;                /* SAH cost of the tree (diagnostics) */
+};
+
+/* prims: per-primitive bounds; maxLeaf: largest leaf; threads: worker threads (0 = hw) */
+void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out );
+
+}  // namespace lh2

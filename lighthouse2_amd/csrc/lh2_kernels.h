@@ -1,0 +1,66 @@
+/* lh2_kernels.h - kernel parameter blocks shared by the host driver and lh2_kernels.hip. */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/lh2_core_types.h"
+
+struct DevInstance;
+struct Counters;
+
+struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture, distortion, screenParams) */
+{
+	lh2_float3 pos, p1, right, up;
+	float aperture, distortion, geometryEpsilon;
+	int w, h, pass;
+	uint32_t R0;
+	/* tile of the frame owned by this launch: local row lr maps to frame row
+	   y0 + (lr / band) * bandStride + lr % band  (contiguous tile: band = rows) */
+	int y0, band, bandStride, tileRows;
+};
+
+struct SceneDev       /* everything the traversal and shading kernels read, by value (kernarg) */
+{
+	const float4* nodes;
+	const float4* tris;
+	const DevInstance* inst;
+	int tlasRoot, instCount;
+	const lh2_CoreInstanceDesc* instDesc;
+	const uint4* materials;          /* 128 B CUDAMaterial records (core_settings.h:94-104) */
+	const lh2_CoreLightTri* areaLights;
+	const lh2_CorePointLight* pointLights;
+	const lh2_CoreSpotLight* spotLights;
+	const lh2_CoreDirectionalLight* dirLights;
+	int nArea, nPoint, nSpot, nDir;
+	const float* sky;
+	int skyW, skyH;
+	const uint8_t* blueNoise;
+	float geometryEpsilon, clampValue;
+};
+
+struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path state */
+{
+	const uint32_t* pathCount;
+	const float4* rayO; const float4* rayD; const float4* T4; const float4* Q4; const uint4* hits;
+	float4* rayOut; float4* rayDOut; float4* T4Out; float4* Q4Out;
+	float4* shO; float4* shD; float4* shP; uint32_t shadowCap;
+	float4* acc;
+	Counters* counters;
+	int w, h, pass, pathLength, maxPathLength, probePixel;
+	uint32_t R0;
+};
+
+extern "C" {
+void lh2_launch_init_counters( Counters* c, uint32_t pathCount, hipStream_t st );
+void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, hipStream_t st );
+void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, hipStream_t st );
+void lh2_launch_trace_closest( const SceneDev* s, const float4* rayO, const float4* rayD, const uint32_t* countPtr, uint32_t countFixed, uint4* hits,
+	int* gstack, uint32_t* overflow, int grid, hipStream_t st );
+void lh2_launch_trace_any( const SceneDev* s, const float4* rayO, const float4* rayD, const uint32_t* countPtr, uint32_t countFixed, uint32_t* mask,
+	const float4* potentials, float4* acc, int* gstack, uint32_t* overflow, int grid, int fused, hipStream_t st );
+void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, hipStream_t st );
+void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, hipStream_t st );
+void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, hipStream_t st );
+}
+
+#define LH2_STACK_LDS 24
+#define LH2_STACK_TOTAL 96

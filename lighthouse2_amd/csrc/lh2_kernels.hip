@@ -1,0 +1,1184 @@
+/* lh2_kernels.hip - hand-written gfx950 kernels of the MI355X wavefront path tracer.
+
+   Hot path:
+     k_camera        primary rays          reference: kernels/camera.h:39-111
+     k_trace<CLOSEST> BVH2 + Möller–Trumbore closest hit (replaces rtpQueryExecute CLOSEST,
+                     rendercore.cpp:516-528), LDS-resident traversal stack
+     k_shade         shade / extend / NEE  reference: kernels/pathtracer.h:54-265
+     k_trace<ANY>    shadow rays, fused with finalizeConnection (connections.h:22-44)
+     k_finalize      accumulator / spp     reference: finalize_shared.h:29-45
+   Stream compaction is per wave: __ballot + mbcnt + one atomicAdd per wave (replaces the
+   per-thread atomicAdd of pathtracer.h:114,202,237).  Path counts are read from device
+   counters, so a frame needs no host round trip between bounces (rendercore.cpp:547).
+
+   Numerics: compiled with -ffp-contract=off and correctly rounded div/sqrt; every expression
+   keeps the reference's evaluation order so results are bit-comparable with oracle/pt_oracle.c.
+*/
+#include "lh2_device.h"
+#include "../../include/lh2_core_types.h"
+#include "lh2_kernels.h"
+
+#define S_SPECULAR 1
+#define S_BOUNCED 2
+#define S_VIASPECULAR 4
+#define S_BOUNCEDTWICE 8
+#define ENOUGH_BOUNCES S_BOUNCED
+#define NOHIT -1
+#define EPSILON 0.0001f
+#define INVPI LH2_INVPI
+#define PI LH2_PI
+#define TWOPI LH2_TWOPI
+
+LH2_DEV uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi( ~0u, __builtin_amdgcn_mbcnt_lo( ~0u, 0u ) ); }
+LH2_DEV uint32_t lanes_below( uint64_t m ) { return __builtin_amdgcn_mbcnt_hi( (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo( (uint32_t)m, 0u ) ); }
+
+/* wave-level stream compaction: one atomicAdd per wave, slots in lane order */
+LH2_DEV uint32_t wave_alloc( bool want, uint32_t* counter )
+{
+	const uint64_t m = __ballot( want );
+	if (m == 0) return 0xffffffffu;
+	const uint32_t leader = (uint32_t)__ffsll( (unsigned long long)m ) - 1u;
+	uint32_t base = 0;
+	if (lane_id() == leader) base = atomicAdd( counter, (uint32_t)__popcll( m ) );
+	base = __builtin_amdgcn_readlane( base, leader );
+	return want ? base + lanes_below( m ) : 0xffffffffu;
+}
+
+LH2_DEV void acc_add( float4* acc, uint32_t px, v3 c )
+{
+	float* a = (float*)(acc + px);
+	unsafeAtomicAdd( a + 0, c.x );
+	unsafeAtomicAdd( a + 1, c.y );
+	unsafeAtomicAdd( a + 2, c.z );
+}
+
+/* =====================================================================================
+   camera: kernels/camera.h:22-94
+   ===================================================================================== */
+LH2_DEV float blueNoiseSampler( const uint8_t* bn, int x, int y, int sampleIndex, int sampleDimension ) /* tools_shared.h:336-350 */
+{
+	x &= 127, y &= 127, sampleIndex &= 255, sampleDimension &= 255;
+	int rankedSampleIndex = (sampleIndex ^ (int)bn[sampleDimension + (x + y * 128) * 8 + 65536 * 3]) & 255;
+	int value = (int)bn[sampleDimension + rankedSampleIndex * 256];
+	value ^= (int)bn[(sampleDimension & 7) + (x + y * 128) * 8 + 65536];
+	return (0.5f + (float)value) * (1.0f / 256.0f);
+}
+LH2_DEV uint32_t WangHash( uint32_t s ) { s = (s ^ 61) ^ (s >> 16), s *= 9, s = s ^ (s >> 4), s *= 0x27d4eb2d, s = s ^ (s >> 15); return s; }
+LH2_DEV uint32_t RandomInt( uint32_t& s ) { s ^= s << 13, s ^= s >> 17, s ^= s << 5; return s; }
+LH2_DEV float RandomFloat( uint32_t& s ) { return (float)RandomInt( s ) * 2.3283064365387e-10f; }
+
+LH2_DEV v3 RandomPointOnLens( const float r0, float r1, const v3 pos, const float aperture, const v3 right, const v3 up )
+{
+	const float blade = (float)(int)(r0 * 9);
+	float r2 = (r0 - blade * (1.0f / 9.0f)) * 9.0f;
+	float x1, y1, x2, y2;
+	lh2_sincosf( blade * PI / 4.5f, &x1, &y1 );
+	lh2_sincosf( (blade + 1.0f) * PI / 4.5f, &x2, &y2 );
+	if ((r1 + r2) > 1) r1 = 1.0f - r1, r2 = 1.0f - r2;
+	const float xr = x1 * r1 + x2 * r2;
+	const float yr = y1 * r1 + y2 * r2;
+	return add3( pos, smul( aperture, add3( muls( right, xr ), muls( up, yr ) ) ) );
+}
+
+__global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const uint8_t* __restrict__ bn, float4* __restrict__ rayO,
+	float4* __restrict__ rayD, float4* __restrict__ T4, float4* __restrict__ Q4, const int jobCount )
+{
+	const int slot = threadIdx.x + blockIdx.x * blockDim.x;
+	if (slot >= jobCount) return;
+	/* slot -> (sample, tile row, x) -> global jobIndex = x + (y + s * h) * w, as camera.h:48-53 */
+	const uint32_t w = (uint32_t)p.w, h = (uint32_t)p.h;
+	const uint32_t tilePix = (uint32_t)p.tileRows * w;
+	const uint32_t s = (uint32_t)slot / tilePix, r = (uint32_t)slot % tilePix;
+	const uint32_t lr = r / w, x = r % w;
+	const uint32_t gy = (uint32_t)p.y0 + (lr / (uint32_t)p.band) * (uint32_t)p.bandStride + lr % (uint32_t)p.band;
+	const uint32_t jobIndex = x + (gy + s * h) * w;
+	uint32_t y = jobIndex / w;
+	const uint32_t sampleIndex = (uint32_t)p.pass + y / h;
+	y %= h;
+	float r0, r1, r2, r3;
+	if (sampleIndex < 256)
+	{
+		r0 = blueNoiseSampler( bn, x, y, sampleIndex, 0 );
+		r1 = blueNoiseSampler( bn, x, y, sampleIndex, 1 );
+		r2 = blueNoiseSampler( bn, x, y, sampleIndex, 2 );
+		r3 = blueNoiseSampler( bn, x, y, sampleIndex, 3 );
+	}
+	else
+	{
+		uint32_t seed = WangHash( (uint32_t)jobIndex + p.R0 );
+		r0 = RandomFloat( seed ), r1 = RandomFloat( seed );
+		r2 = RandomFloat( seed ), r3 = RandomFloat( seed );
+	}
+	const v3 p1 = mk3( p.p1.x, p.p1.y, p.p1.z ), right = mk3( p.right.x, p.right.y, p.right.z ), up = mk3( p.up.x, p.up.y, p.up.z );
+	v3 posOnPixel;
+	if (p.distortion == 0)
+	{
+		posOnPixel = add3( add3( p1, smul( (float)x + r0, divs( right, (float)w ) ) ), smul( (float)y + r1, divs( up, (float)h ) ) );
+	}
+	else
+	{
+		const float sx = (float)x / (float)w - 0.5f, sy = (float)y / (float)h - 0.5f;
+		const float rr = sx * sx + sy * sy;
+		const float rq = sqrtf( rr ) * (1.0f + p.distortion * rr + p.distortion * rr * rr);
+		const float theta = lh2_atan2f( sx, sy );
+		float st, ct;
+		lh2_sincosf( theta, &st, &ct );
+		const float bx = (st * rq + 0.5f) * (float)w;
+		const float by = (ct * rq + 0.5f) * (float)h;
+		posOnPixel = add3( add3( p1, smul( bx + r0, divs( right, (float)w ) ) ), smul( by + r1, divs( up, (float)h ) ) );
+	}
+	const v3 posOnLens = RandomPointOnLens( r2, r3, mk3( p.pos.x, p.pos.y, p.pos.z ), p.aperture, right, up );
+	const v3 rayDir = normalize3( sub3( posOnPixel, posOnLens ) );
+	rayO[slot] = make_float4( posOnLens.x, posOnLens.y, posOnLens.z, p.geometryEpsilon );
+	rayD[slot] = make_float4( rayDir.x, rayDir.y, rayDir.z, 1e34f );
+	T4[slot] = make_float4( 1, 1, 1, bitsf( ((x + (y + (sampleIndex - (uint32_t)p.pass) * h) * w) << 8) + 1 /* S_SPECULAR */ ) );
+	Q4[slot] = make_float4( 1, 0, 0, 0 );
+}
+
+/* =====================================================================================
+   traversal: two-level BVH2, ordered, t-culled, LDS short stack + global spill
+   ===================================================================================== */
+#define STACK_LDS LH2_STACK_LDS   /* entries per lane kept in LDS: 24 x 256 x 4 B = 24 KB / block */
+#define STACK_TOTAL LH2_STACK_TOTAL /* + global spill; the host checks the tree depth against it */
+
+LH2_DEV float safe_inv( float d ) { return (d > -1e-30f && d < 1e-30f) ? (d < 0 ? -1e30f : 1e30f) : 1.0f / d; }
+
+struct TRay { v3 O, D, invD, oinv; };
+LH2_DEV void setup_ray( TRay& r, v3 O, v3 D )
+{
+	r.O = O, r.D = D;
+	r.invD = mk3( safe_inv( D.x ), safe_inv( D.y ), safe_inv( D.z ) );
+	r.oinv = mk3( -O.x * r.invD.x, -O.y * r.invD.y, -O.z * r.invD.z );
+}
+
+/* conservative slab test of one child box; culling only (padded, FMA allowed) */
+LH2_DEV bool box_test( float lox, float hix, float loy, float hiy, float loz, float hiz, const TRay& r, float tmin, float tmax, float& tn )
+{
+#pragma clang fp contract(fast)
+	const float t1x = __builtin_fmaf( lox, r.invD.x, r.oinv.x ), t2x = __builtin_fmaf( hix, r.invD.x, r.oinv.x );
+	const float t1y = __builtin_fmaf( loy, r.invD.y, r.oinv.y ), t2y = __builtin_fmaf( hiy, r.invD.y, r.oinv.y );
+	const float t1z = __builtin_fmaf( loz, r.invD.z, r.oinv.z ), t2z = __builtin_fmaf( hiz, r.invD.z, r.oinv.z );
+	tn = fmaxf( fmaxf( fminf( t1x, t2x ), fminf( t1y, t2y ) ), fminf( t1z, t2z ) );
+	const float tf = fminf( fminf( fmaxf( t1x, t2x ), fmaxf( t1y, t2y ) ), fmaxf( t1z, t2z ) );
+	const float tfp = tf * 1.00001f + 1e-30f;
+	return tn <= tfp && tfp >= tmin && tn <= tmax * 1.00001f + 1e-30f;
+}
+
+struct HitRec { float t; int tri, inst; float u, v; };
+
+/* Möller–Trumbore, same arithmetic as oracle intersect_tri (RenderCore_Bart/common.h:19-50,
+   open interval, det == 0 rejected); returns t via tOut */
+LH2_DEV bool mt_test( const float4 a, const float4 b, const float4 c, const TRay& r, float& tOut, float& uOut, float& vOut )
+{
+	const v3 v0 = xyz( a ), e1 = xyz( b ), e2 = xyz( c );
+	const v3 h = cross3( r.D, e2 );
+	const float det = dot3( e1, h );
+	if (det == 0.0f) return false;
+	const float f = 1.0f / det;
+	const v3 s = sub3( r.O, v0 );
+	const float u = f * dot3( s, h );
+	if (u < 0.0f || u > 1.0f) return false;
+	const v3 q = cross3( s, e1 );
+	const float v = f * dot3( r.D, q );
+	if (v < 0.0f || u + v > 1.0f) return false;
+	tOut = f * dot3( e2, q );
+	uOut = u, vOut = v;
+	return true;
+}
+
+template <bool ANY>
+LH2_DEV bool trace_one( const SceneDev& s, const v3 wO, const v3 wD, const float tmin, const float tmax,
+	int* __restrict__ lst, int* __restrict__ gst, const uint32_t gstride, HitRec& best, uint32_t* overflow )
+{
+	TRay r;
+	setup_ray( r, wO, wD );
+	best.t = tmax, best.tri = -1, best.inst = -1, best.u = 0, best.v = 0;
+	int sp = 0, blasSp = -1, curInst = -1;
+	int cur = s.tlasRoot;
+	while (true)
+	{
+		if (cur >= 0)
+		{
+			const float4* n = s.nodes + (size_t)cur * 4;
+			const float4 n0 = n[0], n1 = n[1], n2 = n[2];
+			const int4 n3 = *(const int4*)(n + 3);
+			float tn0, tn1;
+			const bool h0 = box_test( n0.x, n0.y, n0.z, n0.w, n2.x, n2.y, r, tmin, best.t, tn0 );
+			const bool h1 = box_test( n1.x, n1.y, n1.z, n1.w, n2.z, n2.w, r, tmin, best.t, tn1 );
+			if (h0 && h1)
+			{
+				const bool swap = tn1 < tn0;
+				const int nearc = swap ? n3.y : n3.x, farc = swap ? n3.x : n3.y;
+				if (sp < STACK_LDS) lst[sp * 256] = farc;
+				else if (sp < STACK_TOTAL) gst[(size_t)(sp - STACK_LDS) * gstride] = farc;
+				else { atomicOr( overflow, 1u ); break; }
+				sp++;
+				cur = nearc;
+				continue;
+			}
+			if (h0) { cur = n3.x; continue; }
+			if (h1) { cur = n3.y; continue; }
+		}
+		else if (blasSp < 0)
+		{
+			/* TLAS leaf (one instance): move the ray into object space, not renormalised, so t
+			   stays in world units */
+			const int ii = (int)LEAF_FIRST( cur );
+			const DevInstance in = s.inst[ii];
+			const v3 O = mk3( in.inv0.x * wO.x + in.inv0.y * wO.y + in.inv0.z * wO.z + in.inv0.w,
+				in.inv1.x * wO.x + in.inv1.y * wO.y + in.inv1.z * wO.z + in.inv1.w,
+				in.inv2.x * wO.x + in.inv2.y * wO.y + in.inv2.z * wO.z + in.inv2.w );
+			const v3 D = mk3( in.inv0.x * wD.x + in.inv0.y * wD.y + in.inv0.z * wD.z,
+				in.inv1.x * wD.x + in.inv1.y * wD.y + in.inv1.z * wD.z,
+				in.inv2.x * wD.x + in.inv2.y * wD.y + in.inv2.z * wD.z );
+			setup_ray( r, O, D );
+			blasSp = sp, curInst = ii;
+			cur = in.root;
+			continue;
+		}
+		else
+		{
+			const uint32_t first = LEAF_FIRST( cur );
+			const int cnt = LEAF_COUNT( cur );
+			for (int k = 0; k < cnt; k++)
+			{
+				const float4* tp = s.tris + (size_t)(first + k) * 3;
+				const float4 a = tp[0], b = tp[1], c = tp[2];
+				float t, u, v;
+				if (mt_test( a, b, c, r, t, u, v ) && t > tmin)
+				{
+					if (ANY) { if (t < best.t) return true; }
+					else
+					{
+						const int tri = __float_as_int( a.w );
+						if (t < best.t || (t == best.t && (curInst < best.inst || (curInst == best.inst && tri < best.tri))))
+							best.t = t, best.tri = tri, best.inst = curInst, best.u = u, best.v = v;
+					}
+				}
+			}
+		}
+		/* pop */
+		if (sp == blasSp) { blasSp = -1; setup_ray( r, wO, wD ); }
+		if (sp == 0) break;
+		--sp;
+		cur = sp < STACK_LDS ? lst[sp * 256] : gst[(size_t)(sp - STACK_LDS) * gstride];
+	}
+	return false;
+}
+
+/* closest hit for a ray stream; count from device (after compaction) or fixed.
+   Output hit record per ray (16 B): {t, triid, instid, uv16}, uv quantised as pathtracer.h:71 */
+__global__ __launch_bounds__( 256 ) void k_trace_closest( const SceneDev s, const float4* __restrict__ rayO, const float4* __restrict__ rayD,
+	const uint32_t* __restrict__ countPtr, const uint32_t countFixed, uint4* __restrict__ hits, int* __restrict__ gstack, uint32_t* overflow )
+{
+	__shared__ int lstack[STACK_LDS * 256];
+	const uint32_t count = countPtr ? *countPtr : countFixed;
+	const uint32_t gstride = gridDim.x * 256u;
+	int* gst = gstack + blockIdx.x * 256 + threadIdx.x;
+	int* lst = lstack + threadIdx.x;
+	for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < count; idx += gstride)
+	{
+		const float4 o4 = rayO[idx], d4 = rayD[idx];
+		HitRec h;
+		trace_one<false>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, overflow );
+		uint4 out;
+		if (h.tri < 0) out = make_uint4( fbits( -1.0f ), 0xffffffffu, 0xffffffffu, 0u );
+		else out = make_uint4( fbits( h.t ), (uint32_t)h.tri, (uint32_t)h.inst, lh2_f2u( 65535.0f * h.u ) + (lh2_f2u( 65535.0f * h.v ) << 16) );
+		hits[idx] = out;
+	}
+}
+
+/* any hit for shadow rays.  MODE 0: write the occlusion bitmask (RTP_BUFFER_FORMAT_HIT_BITMASK,
+   bit set = occluded) and nothing else;  MODE 1: fused finalizeConnection (connections.h:22-34):
+   unoccluded rays add their potential to the accumulator. */
+template <int MODE>
+__global__ __launch_bounds__( 256 ) void k_trace_any( const SceneDev s, const float4* __restrict__ rayO, const float4* __restrict__ rayD,
+	const uint32_t* __restrict__ countPtr, const uint32_t countFixed, uint32_t* __restrict__ mask, const float4* __restrict__ potentials,
+	float4* __restrict__ acc, int* __restrict__ gstack, uint32_t* overflow )
+{
+	__shared__ int lstack[STACK_LDS * 256];
+	const uint32_t count = countPtr ? *countPtr : countFixed;
+	const uint32_t gstride = gridDim.x * 256u;
+	int* gst = gstack + blockIdx.x * 256 + threadIdx.x;
+	int* lst = lstack + threadIdx.x;
+	for (uint32_t base = blockIdx.x * 256u; base < count; base += gstride)
+	{
+		const uint32_t idx = base + threadIdx.x;
+		bool occluded = false;
+		if (idx < count)
+		{
+			const float4 o4 = rayO[idx], d4 = rayD[idx];
+			HitRec h;
+			occluded = trace_one<true>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, overflow );
+			if (MODE == 1 && !occluded)
+			{
+				const float4 E = potentials[idx];
+				acc_add( acc, __float_as_uint( E.w ), mk3( E.x, E.y, E.z ) );
+			}
+		}
+		if (MODE == 0)
+		{
+			const uint64_t m = __ballot( occluded );
+			if ((threadIdx.x & 63) == 0)
+			{
+				const uint32_t word = (base + (threadIdx.x & ~63u)) >> 5;
+				if (((base + (threadIdx.x & ~63u)) < count)) mask[word] = (uint32_t)m;
+				if (((base + (threadIdx.x & ~63u)) + 32u < count)) mask[word + 1] = (uint32_t)(m >> 32);
+			}
+		}
+	}
+}
+
+/* =====================================================================================
+   shading: material_shared.h, lights_shared.h, disney.h, ggxmdf.h, pathtracer.h
+   ===================================================================================== */
+struct ShadingData
+{
+	v3 color; int flags;
+	v3 transmittance; int matID;
+	float4 tint;
+	uint4 params;
+};
+#define CHAR2FLT(a,s) (((float)(((a)>>s)&255))*(1.0f/255.0f))
+#define METALLIC CHAR2FLT( sd.params.x, 0 )
+#define SUBSURFACE CHAR2FLT( sd.params.x, 8 )
+#define SPECULAR CHAR2FLT( sd.params.x, 16 )
+#define ROUGHNESS (fmaxf( 0.001f, CHAR2FLT( sd.params.x, 24 ) ))
+#define SPECTINT CHAR2FLT( sd.params.y, 0 )
+#define ANISOTROPIC CHAR2FLT( sd.params.y, 8 )
+#define SHEEN CHAR2FLT( sd.params.y, 16 )
+#define SHEENTINT CHAR2FLT( sd.params.y, 24 )
+#define CLEARCOAT CHAR2FLT( sd.params.z, 0 )
+#define CLEARCOATGLOSS CHAR2FLT( sd.params.z, 8 )
+#define TRANSMISSION CHAR2FLT( sd.params.z, 16 )
+#define TINT xyz( sd.tint )
+#define LUMINANCE sd.tint.w
+#define ETA bitsf( sd.params.w )
+#define HASSMOOTHNORMALS (1 << 11)
+
+LH2_DEV v3 linear_rgb_to_ciexyz( const v3 rgb )
+{
+	return mk3( fmaxf( 0.0f, 0.412453f * rgb.x + 0.357580f * rgb.y + 0.180423f * rgb.z ),
+		fmaxf( 0.0f, 0.212671f * rgb.x + 0.715160f * rgb.y + 0.072169f * rgb.z ),
+		fmaxf( 0.0f, 0.019334f * rgb.x + 0.119193f * rgb.y + 0.950227f * rgb.z ) );
+}
+LH2_DEV v3 ciexyz_to_linear_rgb( const v3 x )
+{
+	return mk3( fmaxf( 0.0f, 3.240479f * x.x - 1.537150f * x.y - 0.498535f * x.z ),
+		fmaxf( 0.0f, -0.969256f * x.x + 1.875992f * x.y + 0.041556f * x.z ),
+		fmaxf( 0.0f, 0.055648f * x.x - 0.204043f * x.y + 1.057311f * x.z ) );
+}
+LH2_DEV float h2f( uint32_t bits16 ) { return lh2_h2f( (uint16_t)bits16 ); }
+
+LH2_DEV v3 ConsistentNormal( const v3 D, const v3 iN, const float alpha ) /* tools_shared.h:296-310 */
+{
+	const float t = PI - 2 * alpha, q = (t * t) / (PI * (PI + (2 * PI - 4) * alpha));
+	const float b = dot3( D, iN ), g = 1 + q * (b - 1), rho = sqrtf( q * (1 + g) / (1 + b) );
+	const v3 Rc = sub3( muls( iN, g + rho * b ), smul( rho, D ) );
+	return normalize3( add3( D, Rc ) );
+}
+
+/* GetShadingData, material_shared.h:35-98 (OPTIXPRIMEBUILD, CONSISTENTNORMALS; texture maps are
+   out of scope this round) */
+LH2_DEV void GetShadingData( const SceneDev& s, const v3 D, const float u, const float v, const float4* __restrict__ tri,
+	const int instIdx, ShadingData& sd, v3& N, v3& iN, v3& fN, v3& T )
+{
+	const float4 tdata1 = tri[1], tdata2 = tri[2], tdata3 = tri[3], tdata4 = tri[4], tdata5 = tri[5], alpha4 = tri[7];
+	const uint4* mat = s.materials + (size_t)__float_as_int( tdata1.w ) * 8;
+	const uint4 baseData = mat[0];
+	sd.params = mat[1];
+	sd.color = mk3( h2f( baseData.x & 0xffff ), h2f( baseData.x >> 16 ), h2f( baseData.y & 0xffff ) );
+	sd.flags = 0;
+	sd.transmittance = mk3( h2f( baseData.y >> 16 ), h2f( baseData.z & 0xffff ), h2f( baseData.z >> 16 ) );
+	sd.matID = 0;
+	const uint32_t flags = baseData.w;
+	const v3 tint_xyz = linear_rgb_to_ciexyz( sd.color );
+	const v3 tnt = tint_xyz.y > 0 ? ciexyz_to_linear_rgb( muls( tint_xyz, 1.0f / tint_xyz.y ) ) : s3( 1 );
+	sd.tint = make_float4( tnt.x, tnt.y, tnt.z, tint_xyz.y );
+	N = iN = fN = mk3( tdata2.w, tdata3.w, tdata4.w );
+	T = xyz( tdata5 );
+	const float w = 1 - (u + v);
+	if (flags & HASSMOOTHNORMALS) iN = normalize3( add3( add3( smul( u, xyz( tdata2 ) ), smul( v, xyz( tdata3 ) ) ), smul( w, xyz( tdata4 ) ) ) );
+	const lh2_CoreInstanceDesc* id = s.instDesc + instIdx;
+	const v3 A = mk3( id->A.x, id->A.y, id->A.z ), B = mk3( id->B.x, id->B.y, id->B.z ), C = mk3( id->C.x, id->C.y, id->C.z );
+	const v3 n0 = N, i0 = iN;
+	N = add3( add3( smul( n0.x, A ), smul( n0.y, B ) ), smul( n0.z, C ) );
+	iN = add3( add3( smul( i0.x, A ), smul( i0.y, B ) ), smul( i0.z, C ) );
+	const bool backSide = dot3( D, N ) > 0;
+	const float alpha = u * alpha4.x + v * alpha4.y + w * alpha4.z;
+	iN = smul( backSide ? -1.0f : 1.0f, ConsistentNormal( muls( D, -1.0f ), backSide ? muls( iN, -1.0f ) : iN, alpha ) );
+	fN = iN;
+}
+
+/* ---- lights (lights_shared.h:36-261) ------------------------------------------------------ */
+LH2_DEV float PotentialArea( const SceneDev& s, int idx, v3 O, v3 N, v3 I, v3 bary )
+{
+	const lh2_CoreLightTri& l = s.areaLights[idx];
+	v3 L = I;
+	if (bary.x >= 0)
+	{
+		const v3 V0 = mk3( l.vertex0.x, l.vertex0.y, l.vertex0.z ), V1 = mk3( l.vertex1.x, l.vertex1.y, l.vertex1.z ), V2 = mk3( l.vertex2.x, l.vertex2.y, l.vertex2.z );
+		L = add3( add3( smul( bary.x, V0 ), smul( bary.y, V1 ) ), smul( bary.z, V2 ) );
+	}
+	L = sub3( L, O );
+	const float att = 1.0f / dot3( L, L );
+	L = normalize3( L );
+	const float LNdotL = fmaxf( 0.0f, -dot3( mk3( l.N.x, l.N.y, l.N.z ), L ) );
+	const float NdotL = fmaxf( 0.0f, dot3( N, L ) );
+	return l.energy * LNdotL * NdotL * att;
+}
+LH2_DEV float PotentialPoint( const SceneDev& s, int idx, v3 I, v3 N )
+{
+	const lh2_CorePointLight& l = s.pointLights[idx];
+	const v3 L = sub3( mk3( l.position.x, l.position.y, l.position.z ), I );
+	const float NdotL = fmaxf( 0.0f, dot3( N, L ) );
+	const float att = 1.0f / dot3( L, L );
+	return l.energy * NdotL * att;
+}
+LH2_DEV float PotentialSpot( const SceneDev& s, int idx, v3 I, v3 N )
+{
+	const lh2_CoreSpotLight& l = s.spotLights[idx];
+	v3 L = sub3( mk3( l.position.x, l.position.y, l.position.z ), I );
+	const float att = 1.0f / dot3( L, L );
+	L = normalize3( L );
+	const float d = (fmaxf( 0.0f, -dot3( L, mk3( l.direction.x, l.direction.y, l.direction.z ) ) ) - l.cosOuter) / (l.cosInner - l.cosOuter);
+	const float NdotL = fmaxf( 0.0f, dot3( N, L ) );
+	const float LNdotL = fmaxf( 0.0f, fminf( 1.0f, d ) );
+	return (l.radiance.x + l.radiance.y + l.radiance.z) * LNdotL * NdotL * att;
+}
+LH2_DEV float PotentialDir( const SceneDev& s, int idx, v3 N )
+{
+	const lh2_CoreDirectionalLight& l = s.dirLights[idx];
+	const float LNdotL = fmaxf( 0.0f, -(l.direction.x * N.x + l.direction.y * N.y + l.direction.z * N.z) );
+	return l.energy * LNdotL;
+}
+LH2_DEV float potential_i( const SceneDev& s, int i, v3 I, v3 N, v3 bary, v3 areaI )
+{
+	if (i < s.nArea) return PotentialArea( s, i, I, N, areaI, bary );
+	i -= s.nArea;
+	if (i < s.nPoint) return PotentialPoint( s, i, I, N );
+	i -= s.nPoint;
+	if (i < s.nSpot) return PotentialSpot( s, i, I, N );
+	i -= s.nSpot;
+	return PotentialDir( s, i, N );
+}
+LH2_DEV float LightPickProb( const SceneDev& s, int idx, v3 O, v3 N, v3 I )
+{
+	const int nl = s.nArea + s.nPoint + s.nSpot + s.nDir;
+	float sum = 0, pidx = 0;
+	for (int i = 0; i < nl; i++)
+	{
+		const float c = potential_i( s, i, O, N, s3( -1 ), I );
+		if (i == idx) pidx = c;
+		sum += c;
+	}
+	if (sum <= 0) return 0;
+	if (idx < 0 || idx >= s.nArea) return 0;
+	return pidx / sum;
+}
+LH2_DEV v3 RandomBarycentrics( const float r0 )
+{
+	const uint32_t uf = lh2_f2u( r0 * 4294967296.0f );
+	float Ax = 1, Ay = 0, Bx = 0, By = 1, Cx = 0, Cy = 0;
+	for (int i = 0; i < 16; ++i)
+	{
+		const int d = (uf >> (2 * (15 - i))) & 0x3;
+		float Anx, Any, Bnx, Bny, Cnx, Cny;
+		switch (d)
+		{
+		case 0: Anx = (Bx + Cx) * 0.5f, Any = (By + Cy) * 0.5f; Bnx = (Ax + Cx) * 0.5f, Bny = (Ay + Cy) * 0.5f; Cnx = (Ax + Bx) * 0.5f, Cny = (Ay + By) * 0.5f; break;
+		case 1: Anx = Ax, Any = Ay; Bnx = (Ax + Bx) * 0.5f, Bny = (Ay + By) * 0.5f; Cnx = (Ax + Cx) * 0.5f, Cny = (Ay + Cy) * 0.5f; break;
+		case 2: Anx = (Bx + Ax) * 0.5f, Any = (By + Ay) * 0.5f; Bnx = Bx, Bny = By; Cnx = (Bx + Cx) * 0.5f, Cny = (By + Cy) * 0.5f; break;
+		default: Anx = (Cx + Ax) * 0.5f, Any = (Cy + Ay) * 0.5f; Bnx = (Cx + Bx) * 0.5f, Bny = (Cy + By) * 0.5f; Cnx = Cx, Cny = Cy; break;
+		}
+		Ax = Anx, Ay = Any, Bx = Bnx, By = Bny, Cx = Cnx, Cy = Cny;
+	}
+	const float rx = (Ax + Bx + Cx) * 0.3333333f, ry = (Ay + By + Cy) * 0.3333333f;
+	return mk3( rx, ry, 1 - rx - ry );
+}
+LH2_DEV v3 RandomPointOnLight( const SceneDev& s, float r0, float r1, const v3 I, const v3 N, float& pickProb, float& lightPdf, v3& lightColor )
+{
+	const int nl = s.nArea + s.nPoint + s.nSpot + s.nDir;
+	const float lightCount = (float)nl;
+	const v3 bary = RandomBarycentrics( r0 );
+	float sum = 0, total = 0;
+	int lightIdx = 0;
+	for (int i = 0; i < nl; i++) sum += potential_i( s, i, I, N, bary, s3( 0 ) );
+	if (sum <= 0) { lightPdf = 0; return s3( 1 ); }
+	r1 *= sum;
+	for (int i = 0; i < nl; i++)
+	{
+		total += potential_i( s, i, I, N, bary, s3( 0 ) );
+		if (total >= r1) { lightIdx = i; break; }
+	}
+	pickProb = potential_i( s, lightIdx, I, N, bary, s3( 0 ) ) / sum;
+	{ const int hi = (int)lightCount - 1; lightIdx = lightIdx < 0 ? 0 : lightIdx > hi ? hi : lightIdx; }
+	if (lightIdx < s.nArea)
+	{
+		const lh2_CoreLightTri& l = s.areaLights[lightIdx];
+		lightColor = mk3( l.radiance.x, l.radiance.y, l.radiance.z );
+		const v3 P = add3( add3( smul( bary.x, mk3( l.vertex0.x, l.vertex0.y, l.vertex0.z ) ), smul( bary.y, mk3( l.vertex1.x, l.vertex1.y, l.vertex1.z ) ) ),
+			smul( bary.z, mk3( l.vertex2.x, l.vertex2.y, l.vertex2.z ) ) );
+		v3 L = sub3( I, P );
+		const float sqDist = dot3( L, L );
+		L = normalize3( L );
+		const float LNdotL = L.x * l.N.x + L.y * l.N.y + L.z * l.N.z;
+		const float reciSolidAngle = sqDist / (l.area * LNdotL);
+		lightPdf = (LNdotL > 0 && dot3( L, N ) < 0) ? reciSolidAngle : 0;
+		return P;
+	}
+	else if (lightIdx < s.nArea + s.nPoint)
+	{
+		const lh2_CorePointLight& l = s.pointLights[lightIdx - s.nArea];
+		const v3 pos = mk3( l.position.x, l.position.y, l.position.z );
+		lightColor = mk3( l.radiance.x, l.radiance.y, l.radiance.z );
+		const v3 L = sub3( I, pos );
+		const float sqDist = dot3( L, L );
+		lightPdf = dot3( L, N ) < 0 ? sqDist : 0;
+		return pos;
+	}
+	else if (lightIdx < s.nArea + s.nPoint + s.nSpot)
+	{
+		const lh2_CoreSpotLight& l = s.spotLights[lightIdx - (s.nArea + s.nPoint)];
+		const v3 pos = mk3( l.position.x, l.position.y, l.position.z );
+		v3 L = sub3( I, pos );
+		const float sqDist = dot3( L, L );
+		L = normalize3( L );
+		const float d = (fmaxf( 0.0f, L.x * l.direction.x + L.y * l.direction.y + L.z * l.direction.z ) - l.cosOuter) / (l.cosInner - l.cosOuter);
+		const float LNdotL = fminf( 1.0f, d );
+		lightPdf = (LNdotL > 0 && dot3( L, N ) < 0) ? (sqDist / LNdotL) : 0;
+		lightColor = mk3( l.radiance.x, l.radiance.y, l.radiance.z );
+		return pos;
+	}
+	else
+	{
+		const lh2_CoreDirectionalLight& l = s.dirLights[lightIdx - (s.nArea + s.nPoint + s.nSpot)];
+		const v3 L = mk3( l.direction.x, l.direction.y, l.direction.z );
+		lightColor = mk3( l.radiance.x, l.radiance.y, l.radiance.z );
+		const float NdotL = dot3( L, N );
+		lightPdf = NdotL < 0 ? 1 : 0;
+		return sub3( I, smul( 1000.0f, L ) );
+	}
+}
+
+/* ---- Disney BSDF (disney.h:33-333, ggxmdf.h:23-243) -------------------------------------- */
+LH2_DEV float schlick_fresnel( float u ) { const float m = saturatef_( 1.0f - u ), m2 = sqrf( m ), m4 = sqrf( m2 ); return m4 * m; }
+LH2_DEV v3 mix_spectra( v3 a, v3 b, float t ) { return add3( smul( 1.0f - t, a ), smul( t, b ) ); }
+LH2_DEV v3 mix_one_with_spectra( v3 b, float t ) { return sadd( 1.0f - t, smul( t, b ) ); }
+LH2_DEV v3 mix_spectra_with_one( v3 a, float t ) { return adds( smul( 1.0f - t, a ), t ); }
+LH2_DEV void microfacet_alpha_from_roughness( float roughness, float anisotropy, float& ax, float& ay )
+{
+	const float square_roughness = roughness * roughness;
+	const float aspect = sqrtf( 1.0f + anisotropy * (anisotropy < 0 ? 0.9f : -0.9f) );
+	ax = fmaxf( 0.001f, square_roughness / aspect );
+	ay = fmaxf( 0.001f, square_roughness * aspect );
+}
+LH2_DEV float clearcoat_roughness( const ShadingData& sd ) { return mixf( 0.1f, 0.001f, CLEARCOATGLOSS ); }
+LH2_DEV v3 DisneySpecularFresnel( const ShadingData& sd, v3 o, v3 h )
+{
+	v3 value = mix_one_with_spectra( TINT, SPECTINT );
+	value = muls( value, SPECULAR * 0.08f );
+	value = mix_spectra( value, sd.color, METALLIC );
+	const float cos_oh = fabsf( dot3( o, h ) );
+	return mix_spectra_with_one( value, schlick_fresnel( cos_oh ) );
+}
+LH2_DEV v3 DisneyClearcoatFresnel( const ShadingData& sd, v3 o, v3 h )
+{
+	const float cos_oh = fabsf( dot3( o, h ) );
+	return s3( mixf( 0.04f, 1.0f, schlick_fresnel( cos_oh ) ) * 0.25f * CLEARCOAT );
+}
+LH2_DEV bool force_above_surface( v3& direction, const v3 normal )
+{
+	const float Eps = 1.0e-4f;
+	const float cos_theta = dot3( direction, normal );
+	const float correction = Eps - cos_theta;
+	if (correction <= 0) return false;
+	direction = normalize3( add3( direction, smul( correction, normal ) ) );
+	return true;
+}
+LH2_DEV float Fr_L( float VDotN, float eio )
+{
+	if (VDotN < 0.0f) eio = 1.0f / eio, VDotN = fabsf( VDotN );
+	const float SinThetaT2 = sqrf( eio ) * (1.0f - VDotN * VDotN);
+	if (SinThetaT2 > 1.0f) return 1.0f;
+	const float LDotN = sqrtf( 1.0f - SinThetaT2 );
+	const float r1 = (VDotN - eio * LDotN) / (VDotN + eio * LDotN);
+	const float r2 = (LDotN - eio * VDotN) / (LDotN + eio * VDotN);
+	return 0.5f * (sqrf( r1 ) + sqrf( r2 ));
+}
+LH2_DEV bool Refract_L( const v3 wi, const v3 n, const float eta, v3& wt )
+{
+	const float cosThetaI = fabsf( dot3( n, wi ) );
+	const float sin2ThetaI = fmaxf( 0.0f, 1.0f - cosThetaI * cosThetaI );
+	const float sin2ThetaT = eta * eta * sin2ThetaI;
+	if (sin2ThetaT >= 1) return false;
+	const float cosThetaT = sqrtf( 1.0f - sin2ThetaT );
+	wt = add3( smul( eta, muls( wi, -1.0f ) ), smul( eta * cosThetaI - cosThetaT, n ) );
+	return true;
+}
+LH2_DEV float stretched_roughness( v3 m, float sin_theta, float ax, float ay )
+{
+	if (ax == ay || sin_theta == 0.0f) return 1.0f / sqrf( ax );
+	const float c = sqrf( m.x / (sin_theta * ax) ), s = sqrf( m.y / (sin_theta * ay) );
+	return c + s;
+}
+LH2_DEV float projected_roughness( v3 m, float sin_theta, float ax, float ay )
+{
+	if (ax == ay || sin_theta == 0.0f) return ax;
+	const float c = sqrf( (m.x * ax) / sin_theta ), s = sqrf( (m.y * ay) / sin_theta );
+	return sqrtf( c + s );
+}
+LH2_DEV float GGXMDF_D( v3 m, float ax, float ay )
+{
+	const float cos_theta = m.z;
+	if (cos_theta == 0.0f) return sqrf( ax ) * INVPI;
+	const float cos_theta_2 = sqrf( cos_theta );
+	const float sin_theta = sqrtf( fmaxf( 0.0f, 1.0f - cos_theta_2 ) );
+	const float cos_theta_4 = sqrf( cos_theta_2 );
+	const float tan_theta_2 = (1.0f - cos_theta_2) / cos_theta_2;
+	const float A = stretched_roughness( m, sin_theta, ax, ay );
+	const float tmp = 1.0f + tan_theta_2 * A;
+	return 1.0f / (PI * ax * ay * cos_theta_4 * sqrf( tmp ));
+}
+LH2_DEV float GGXMDF_lambda( v3 v, float ax, float ay )
+{
+	const float cos_theta = v.z;
+	if (cos_theta == 0.0f) return 0.0f;
+	const float cos_theta_2 = sqrf( cos_theta );
+	const float sin_theta = sqrtf( fmaxf( 0.0f, 1.0f - cos_theta_2 ) );
+	const float alpha = projected_roughness( v, sin_theta, ax, ay );
+	const float tan_theta_2 = sqrf( sin_theta ) / cos_theta_2;
+	const float a2_rcp = sqrf( alpha ) * tan_theta_2;
+	return (-1.0f + sqrtf( 1.0f + a2_rcp )) * 0.5f;
+}
+LH2_DEV float GGXMDF_G( v3 wi, v3 wo, float ax, float ay ) { return 1.0f / (1.0f + GGXMDF_lambda( wo, ax, ay ) + GGXMDF_lambda( wi, ax, ay )); }
+LH2_DEV float GGXMDF_G1( v3 v, float ax, float ay ) { return 1.0f / (1.0f + GGXMDF_lambda( v, ax, ay )); }
+LH2_DEV v3 GGXMDF_sample( v3 v, float r0, float r1, float ax, float ay )
+{
+	const float sign_cos_vn = v.z < 0.0f ? -1.0f : 1.0f;
+	v3 stretched = mk3( sign_cos_vn * v.x * ax, sign_cos_vn * v.y * ay, sign_cos_vn * v.z );
+	stretched = normalize3( stretched );
+	const v3 t1 = v.z < 0.9999f ? normalize3( cross3( stretched, mk3( 0, 0, 1 ) ) ) : mk3( 1, 0, 0 );
+	const v3 t2 = cross3( t1, stretched );
+	const float a = 1.0f / (1.0f + stretched.z);
+	const float r = sqrtf( r0 );
+	const float phi = r1 < a ? r1 / a * PI : PI + (r1 - a) / (1.0f - a) * PI;
+	float sp, cp;
+	lh2_sincosf( phi, &sp, &cp );
+	const float p1 = r * cp;
+	const float p2 = r * sp * (r1 < a ? 1.0f : stretched.z);
+	const v3 h = add3( add3( smul( p1, t1 ), smul( p2, t2 ) ), smul( sqrtf( fmaxf( 0.0f, 1.0f - p1 * p1 - p2 * p2 ) ), stretched ) );
+	const v3 m = mk3( h.x * ax, h.y * ay, fmaxf( 0.0f, h.z ) );
+	return normalize3( m );
+}
+LH2_DEV float GGXMDF_pdf( v3 v, v3 m, float ax, float ay )
+{
+	const float cos_theta_v = v.z;
+	if (cos_theta_v == 0.0f) return 0;
+	return GGXMDF_G1( v, ax, ay ) * fabsf( dot3( v, m ) ) * GGXMDF_D( m, ax, ay ) / fabsf( cos_theta_v );
+}
+LH2_DEV float GTR1MDF_D( v3 m, float ax )
+{
+	const float alpha = clampf_( ax, 0.001f, 0.999f );
+	const float alpha_x_2 = sqrf( alpha );
+	const float cos_theta_2 = sqrf( m.z );
+	const float a = (alpha_x_2 - 1.0f) / (PI * lh2_logf( alpha_x_2 ));
+	const float b = (1 / (1 + (alpha_x_2 - 1) * cos_theta_2));
+	return a * b;
+}
+LH2_DEV float GTR1MDF_lambda( v3 v, float ax )
+{
+	const float cos_theta = v.z;
+	if (cos_theta == 0) return 0;
+	const float cos_theta_2 = sqrf( cos_theta );
+	const float sin_theta = sqrtf( fmaxf( 0.0f, 1.0f - cos_theta_2 ) );
+	if (sin_theta == 0.0f) return 0.0f;
+	const float cot_theta_2 = cos_theta_2 / sqrf( sin_theta );
+	const float cot_theta = sqrtf( cot_theta_2 );
+	const float alpha = clampf_( ax, 0.001f, 0.999f );
+	const float alpha_2 = sqrf( alpha );
+	const float a = sqrtf( cot_theta_2 + alpha_2 );
+	const float b = sqrtf( cot_theta_2 + 1.0f );
+	const float c = lh2_logf( cot_theta + b );
+	const float d = lh2_logf( cot_theta + a );
+	return (a - b + cot_theta * (c - d)) / (cot_theta * lh2_logf( alpha_2 ));
+}
+LH2_DEV float GTR1MDF_G( v3 wi, v3 wo, float ax ) { return 1.0f / (1.0f + GTR1MDF_lambda( wo, ax ) + GTR1MDF_lambda( wi, ax )); }
+LH2_DEV v3 GTR1MDF_sample( float r0, float r1, float ax )
+{
+	const float alpha = clampf_( ax, 0.001f, 0.999f );
+	const float alpha_2 = sqrf( alpha );
+	const float a = 1.0f - lh2_powf( alpha_2, 1.0f - r0 );
+	const float cos_theta_2 = a / (1.0f - alpha_2);
+	const float cos_theta = sqrtf( cos_theta_2 );
+	const float sin_theta = sqrtf( fmaxf( 0.0f, 1.0f - cos_theta_2 ) );
+	float sin_phi, cos_phi;
+	lh2_sincosf( TWOPI * r1, &sin_phi, &cos_phi );
+	return mk3( cos_phi * sin_theta, sin_phi * sin_theta, cos_theta );
+}
+LH2_DEV float GTR1MDF_pdf( v3 m, float ax ) { return GTR1MDF_D( m, ax ) * fabsf( m.z ); }
+LH2_DEV v3 World2Tangent( v3 V, v3 N, v3 T, v3 B ) { return mk3( dot3( V, T ), dot3( V, B ), dot3( V, N ) ); }
+LH2_DEV v3 Tangent2World( v3 V, v3 N, v3 T, v3 B ) { return add3( add3( smul( V.x, T ), smul( V.y, B ) ), smul( V.z, N ) ); }
+LH2_DEV v3 DiffuseReflectionCosWeighted( float r0, float r1 )
+{
+	const float term1 = TWOPI * r0, term2 = sqrtf( 1 - r1 );
+	float s, c;
+	lh2_sincosf( term1, &s, &c );
+	return mk3( c * term2, s * term2, sqrtf( r1 ) );
+}
+
+template <bool GGX>
+LH2_DEV void sample_mf( const ShadingData& sd, float r0, float r1, float ax, float ay, v3 N, v3 T, v3 B, v3 gN, v3 wow, v3& wiw, float& pdf, v3& value )
+{
+	v3 wo = World2Tangent( wow, N, T, B );
+	if (wo.z == 0) return;
+	v3 m = GGX ? GGXMDF_sample( wo, r0, r1, ax, ay ) : GTR1MDF_sample( r0, r1, ax );
+	v3 wi = reflect3( muls( wo, -1.0f ), m );
+	const v3 ng = World2Tangent( gN, N, T, B );
+	if (force_above_surface( wi, ng )) m = normalize3( add3( wo, wi ) );
+	if (wi.z == 0) return;
+	const float cos_oh = dot3( wo, m );
+	pdf = (GGX ? GGXMDF_pdf( wo, m, ax, ay ) : GTR1MDF_pdf( m, ax )) / fabsf( 4.0f * cos_oh );
+	if (pdf < 1.0e-6f) return;
+	const float D = GGX ? GGXMDF_D( m, ax, ay ) : GTR1MDF_D( m, ax );
+	const float G = GGX ? GGXMDF_G( wi, wo, ax, ay ) : GTR1MDF_G( wi, wo, ax );
+	value = GGX ? DisneySpecularFresnel( sd, wo, m ) : DisneyClearcoatFresnel( sd, wo, m );
+	value = muls( value, D * G / fabsf( 4.0f * wo.z * wi.z ) );
+	wiw = Tangent2World( wi, N, T, B );
+}
+template <bool GGX>
+LH2_DEV float evaluate_mf( const ShadingData& sd, float ax, float ay, v3 N, v3 T, v3 B, v3 wow, v3 wiw, v3& bsdf )
+{
+	const v3 wo = World2Tangent( wow, N, T, B );
+	const v3 wi = World2Tangent( wiw, N, T, B );
+	if (wo.z == 0 || wi.z == 0) return 0;
+	const v3 m = normalize3( add3( wi, wo ) );
+	const float cos_oh = dot3( wo, m );
+	if (cos_oh == 0) return 0;
+	const float D = GGX ? GGXMDF_D( m, ax, ay ) : GTR1MDF_D( m, ax );
+	const float G = GGX ? GGXMDF_G( wi, wo, ax, ay ) : GTR1MDF_G( wi, wo, ax );
+	bsdf = GGX ? DisneySpecularFresnel( sd, wo, m ) : DisneyClearcoatFresnel( sd, wo, m );
+	bsdf = muls( bsdf, D * G / fabsf( 4.0f * wo.z * wi.z ) );
+	return (GGX ? GGXMDF_pdf( wo, m, ax, ay ) : GTR1MDF_pdf( m, ax )) / fabsf( 4.0f * cos_oh );
+}
+LH2_DEV float evaluate_diffuse( const ShadingData& sd, v3 iN, v3 wow, v3 wiw, v3& value )
+{
+	const v3 n = iN;
+	const v3 h = normalize3( add3( wiw, wow ) );
+	const float cos_on = dot3( n, wow );
+	const float cos_in = dot3( n, wiw );
+	const float cos_ih = dot3( wiw, h );
+	const float fl = schlick_fresnel( cos_in );
+	const float fv = schlick_fresnel( cos_on );
+	float fd = 0;
+	if (SUBSURFACE != 1.0f)
+	{
+		const float fd90 = 0.5f + 2.0f * sqrf( cos_ih ) * ROUGHNESS;
+		fd = mixf( 1.0f, fd90, fl ) * mixf( 1.0f, fd90, fv );
+	}
+	if (SUBSURFACE > 0)
+	{
+		const float fss90 = sqrf( cos_ih ) * ROUGHNESS;
+		const float fss = mixf( 1.0f, fss90, fl ) * mixf( 1.0f, fss90, fv );
+		const float ss = 1.25f * (fss * (1.0f / (fabsf( cos_on ) + fabsf( cos_in )) - 0.5f) + 0.5f);
+		fd = mixf( fd, ss, SUBSURFACE );
+	}
+	value = muls( muls( muls( sd.color, fd ), INVPI ), 1.0f - METALLIC );
+	return fabsf( cos_in ) * INVPI;
+}
+LH2_DEV float evaluate_sheen( const ShadingData& sd, v3 wow, v3 wiw, v3& value )
+{
+	const v3 h = normalize3( add3( wow, wow ) );
+	const float cos_ih = dot3( wiw, h );
+	const float fh = schlick_fresnel( cos_ih );
+	value = mix_one_with_spectra( TINT, SHEENTINT );
+	value = muls( value, fh * SHEEN * (1.0f - METALLIC) );
+	return 1.0f / (2 * PI);
+}
+LH2_DEV v3 SampleBSDF( const ShadingData& sd, v3 iN, const v3 N, const v3 iT, const v3 wow, const float distance, const float r0, const float r1,
+	v3& wiw, float& pdf, bool& specular )
+{
+	const float flip = (dot3( wow, N ) < 0) ? -1 : 1;
+	iN = muls( iN, flip );
+	if (r0 < TRANSMISSION)
+	{
+		specular = true, pdf = 1;
+		const float eio = flip < 0 ? (1.0f / ETA) : ETA, F = Fr_L( dot3( iN, wow ), eio );
+		v3 beer;
+		beer.x = lh2_expf( -sd.transmittance.x * distance * 2.0f );
+		beer.y = lh2_expf( -sd.transmittance.y * distance * 2.0f );
+		beer.z = lh2_expf( -sd.transmittance.z * distance * 2.0f );
+		if (r1 < F)
+		{
+			wiw = reflect3( muls( wow, -1.0f ), iN );
+			if (dot3( muls( N, flip ), wiw ) <= 0) pdf = 0;
+			return muls( mul3( sd.color, beer ), 1 / fabsf( dot3( iN, wiw ) ) );
+		}
+		else
+		{
+			if (!Refract_L( wow, iN, eio, wiw )) return s3( 0 );
+			const float ajointCorrection = 1.0f;
+			return muls( muls( mul3( sd.color, beer ), ajointCorrection ), 1 / fabsf( dot3( iN, wiw ) ) );
+		}
+	}
+	const float r3 = (r0 - TRANSMISSION) / (1 - TRANSMISSION);
+	const v3 B = normalize3( cross3( iN, iT ) );
+	const v3 T = normalize3( cross3( iN, B ) );
+	float wx = lerpf_( LUMINANCE, 0, METALLIC ), wy = lerpf_( SHEEN, 0, METALLIC ), wz = lerpf_( SPECULAR, 1, METALLIC ), ww = CLEARCOAT * 0.25f;
+	const float wsum = 1.0f / (wx + wy + wz + ww);
+	wx *= wsum, wy *= wsum, wz *= wsum, ww *= wsum;
+	const float cdfx = wx, cdfy = wx + wy, cdfz = wx + wy + wz;
+	float probability, component_pdf = 0;
+	v3 contrib = s3( 0 ), value = s3( 0 );
+	if (r3 < cdfx)
+	{
+		const float r2 = r3 / cdfx;
+		const v3 wi = DiffuseReflectionCosWeighted( r2, r1 );
+		wiw = normalize3( Tangent2World( wi, iN, T, B ) );
+		component_pdf = evaluate_diffuse( sd, iN, wow, wiw, value );
+		probability = wx * component_pdf, wx = 0;
+	}
+	else if (r3 < cdfy)
+	{
+		const float r2 = (r3 - cdfx) / (cdfy - cdfx);
+		const v3 wi = DiffuseReflectionCosWeighted( r2, r1 );
+		wiw = normalize3( Tangent2World( wi, iN, T, B ) );
+		component_pdf = evaluate_sheen( sd, wow, wiw, value );
+		probability = wy * component_pdf, wy = 0;
+	}
+	else if (r3 < cdfz)
+	{
+		const float r2 = (r3 - cdfy) / (cdfz - cdfy);
+		float ax, ay;
+		microfacet_alpha_from_roughness( ROUGHNESS, ANISOTROPIC, ax, ay );
+		sample_mf<true>( sd, r2, r1, ax, ay, iN, T, B, muls( N, flip ), wow, wiw, component_pdf, value );
+		probability = wz * component_pdf, wz = 0;
+	}
+	else
+	{
+		const float r2 = (r3 - cdfz) / (1 - cdfz);
+		const float alpha = clearcoat_roughness( sd );
+		sample_mf<false>( sd, r2, r1, alpha, alpha, iN, T, B, muls( N, flip ), wow, wiw, component_pdf, value );
+		probability = ww * component_pdf, ww = 0;
+	}
+	if (wx > 0) probability += wx * evaluate_diffuse( sd, iN, wow, wiw, contrib ), value = add3( value, contrib );
+	if (wy > 0) probability += wy * evaluate_sheen( sd, wow, wiw, contrib ), value = add3( value, contrib );
+	if (wz > 0)
+	{
+		float ax, ay;
+		microfacet_alpha_from_roughness( ROUGHNESS, ANISOTROPIC, ax, ay );
+		probability += wz * evaluate_mf<true>( sd, ax, ay, iN, T, B, wow, wiw, contrib );
+		value = add3( value, contrib );
+	}
+	if (ww > 0)
+	{
+		const float alpha = clearcoat_roughness( sd );
+		probability += ww * evaluate_mf<false>( sd, alpha, alpha, iN, T, B, wow, wiw, contrib );
+		value = add3( value, contrib );
+	}
+	if (probability > 1.0e-6f) pdf = probability; else pdf = 0;
+	return value;
+}
+LH2_DEV v3 EvaluateBSDF( const ShadingData& sd, const v3 iN, const v3 iT, const v3 wow, const v3 wiw, float& pdf )
+{
+	if (TRANSMISSION > 0.999f || ROUGHNESS <= 0.001f) { pdf = 0; return s3( 0 ); }
+	const v3 B = normalize3( cross3( iN, iT ) );
+	const v3 T = normalize3( cross3( iN, B ) );
+	float wx = lerpf_( LUMINANCE, 0, METALLIC ), wy = lerpf_( SHEEN, 0, METALLIC ), wz = lerpf_( SPECULAR, 1, METALLIC ), ww = CLEARCOAT * 0.25f;
+	const float wsum = 1.0f / (wx + wy + wz + ww);
+	wx *= wsum, wy *= wsum, wz *= wsum, ww *= wsum;
+	pdf = 0;
+	v3 value = s3( 0 );
+	if (wx > 0) pdf += wx * evaluate_diffuse( sd, iN, wow, wiw, value );
+	if (wy > 0) pdf += wy * evaluate_sheen( sd, wow, wiw, value );
+	if (wz > 0)
+	{
+		float ax, ay;
+		microfacet_alpha_from_roughness( ROUGHNESS, ANISOTROPIC, ax, ay );
+		v3 contrib = s3( 0 );
+		const float spec_pdf = evaluate_mf<true>( sd, ax, ay, iN, T, B, wow, wiw, contrib );
+		if (spec_pdf > 0) pdf += wz * spec_pdf, value = add3( value, contrib );
+	}
+	if (ww > 0)
+	{
+		const float alpha = clearcoat_roughness( sd );
+		v3 contrib = s3( 0 );
+		const float clearcoat_pdf = evaluate_mf<false>( sd, alpha, alpha, iN, T, B, wow, wiw, contrib );
+		if (clearcoat_pdf > 0) pdf += ww * clearcoat_pdf, value = add3( value, contrib );
+	}
+	return value;
+}
+
+/* ---- tools --------------------------------------------------------------------------------- */
+LH2_DEV uint32_t PackNormal( const v3 N )
+{
+	const float f = 65535.0f / fmaxf( sqrtf( 8.0f * N.z + 8.0f ), 0.0001f );
+	return lh2_f2u( N.x * f + 32767.0f ) + (lh2_f2u( N.y * f + 32767.0f ) << 16);
+}
+LH2_DEV v3 UnpackNormal( const uint32_t p )
+{
+	float nx = (float)(p & 65535) * (2.0f / 65535.0f), ny = (float)(p >> 16) * (2.0f / 65535.0f), nz = 0, nw = 0;
+	nx = nx + -1.0f, ny = ny + -1.0f, nz = nz + 1.0f, nw = nw + -1.0f;
+	float l = nx * -nx + ny * -ny + nz * -nw;
+	nz = l, l = sqrtf( l ), nx *= l, ny *= l;
+	return mk3( nx * 2.0f + 0.0f, ny * 2.0f + 0.0f, nz * 2.0f + -1.0f );
+}
+LH2_DEV v3 SampleSkydome( const SceneDev& s, const v3 D )
+{
+	const uint32_t u = lh2_f2u( (float)s.skyW * 0.5f * (1.0f + lh2_atan2f( D.x, -D.z ) * INVPI) );
+	const uint32_t v = lh2_f2u( (float)s.skyH * lh2_acosf( D.y ) * INVPI );
+	const uint32_t idx = u + v * (uint32_t)s.skyW;
+	if (idx < (uint32_t)(s.skyW * s.skyH)) return mk3( s.sky[idx * 3], s.sky[idx * 3 + 1], s.sky[idx * 3 + 2] );
+	return s3( 0 );
+}
+LH2_DEV v3 SafeOrigin( const v3 O, const v3 R, const v3 N, const float eps )
+{
+	const float parallel = 1 - fabsf( dot3( N, R ) );
+	const float v = parallel * parallel;
+	const float side = 1.0f;
+	return add3( add3( O, muls( muls( R, eps ), 1 - v ) ), muls( muls( muls( N, side ), eps ), v ) );
+}
+LH2_DEV v3 clampintensity( const float clampValue, v3 c )
+{
+	const float v = fmaxf( c.x, fmaxf( c.y, c.z ) );
+	if (v > clampValue) { const float m = clampValue / v; c.x *= m; c.y *= m; c.z *= m; }
+	return c;
+}
+LH2_DEV v3 fixnan( v3 a ) { if (!isfinite_( a.x + a.y + a.z )) a = s3( 0 ); return a; }
+LH2_DEV float SurvivalProbability( const v3 a ) { return fminf( 1.0f, fmaxf( fmaxf( a.x, a.y ), a.z ) ); }
+
+/* ---- shade kernel: pathtracer.h:54-245 --------------------------------------------------- */
+__global__ __launch_bounds__( 256 ) void k_shade( const SceneDev s, const ShadeParams p )
+{
+	const uint32_t count = *p.pathCount;
+	const uint32_t gstride = gridDim.x * 256u;
+	const int w = p.w, h = p.h;
+	for (uint32_t base = blockIdx.x * 256u; base < count; base += gstride)
+	{
+		const uint32_t jobIndex = base + threadIdx.x;
+		bool doExt = false, doShadow = false;
+		float4 eO, eD, eT, eQ, sO, sD, sP;
+		if (jobIndex < count)
+		{
+			const float4 O4 = p.rayO[jobIndex], D4 = p.rayD[jobIndex];
+			const float4 T4 = p.T4[jobIndex], Q4 = p.Q4[jobIndex];
+			const uint4 hd = p.hits[jobIndex];
+			const float HIT_T = __uint_as_float( hd.x );
+			const int PRIMIDX = (int)hd.y;
+			const int INSTANCEIDX = PRIMIDX == -1 ? 0 : (int)hd.z;
+			const float HIT_U = (float)(hd.w & 65535) * (1.0f / 65535.0f);
+			const float HIT_V = (float)(hd.w >> 16) * (1.0f / 65535.0f);
+			uint32_t data = fbits( T4.w );
+			const float bsdfPdf = Q4.x;
+			const v3 D = xyz( D4 ), RAY_O = xyz( O4 );
+			v3 throughput = xyz( T4 );
+			const uint32_t pathIdx = data >> 8;
+			const uint32_t pixelIdx = pathIdx % (uint32_t)(w * h);
+			const uint32_t sampleIdx = pathIdx / (uint32_t)(w * h) + (uint32_t)p.pass;
+			if (p.pathLength == 1) unsafeAtomicAdd( &p.acc[pixelIdx].w, PRIMIDX == NOHIT ? 10000.0f : HIT_T );
+			if (PRIMIDX == NOHIT)
+			{
+				v3 contribution = muls( mul3( throughput, SampleSkydome( s, D ) ), 1.0f / bsdfPdf );
+				contribution = clampintensity( s.clampValue, contribution );
+				contribution = fixnan( contribution );
+				acc_add( p.acc, pixelIdx, contribution );
+				goto compact;
+			}
+			if ((int)pixelIdx == p.probePixel && p.pathLength == 1 && sampleIdx == 0)
+				p.counters->probedInstid = INSTANCEIDX, p.counters->probedTriid = PRIMIDX, p.counters->probedDist = HIT_T;
+			{
+				ShadingData sd;
+				v3 N, iN, fN, T;
+				const v3 I = add3( RAY_O, smul( HIT_T, D ) );
+				const float4* tri = (const float4*)s.instDesc[INSTANCEIDX].triangles + (size_t)PRIMIDX * 11;
+				GetShadingData( s, D, HIT_U, HIT_V, tri, INSTANCEIDX, sd, N, iN, fN, T );
+				if (sd.flags & 1)
+				{
+					if (p.pathLength < p.maxPathLength)
+					{
+						throughput = fixnan( throughput );
+						doExt = true;
+						eO = make_float4( I.x, I.y, I.z, EPSILON ), eD = make_float4( D.x, D.y, D.z, 1e34f );
+						eT = make_float4( throughput.x, throughput.y, throughput.z, bitsf( data ) ), eQ = make_float4( bsdfPdf, 0, 0, 0 );
+					}
+					goto compact;
+				}
+				if (sd.color.x > 1.0f || sd.color.y > 1.0f || sd.color.z > 1.0f)
+				{
+					const float DdotNL = -dot3( D, N );
+					v3 contribution = s3( 0 );
+					if (DdotNL > 0)
+					{
+						if (p.pathLength == 1 || (data & S_SPECULAR) > 0) contribution = sd.color;
+						else
+						{
+							const v3 lastN = UnpackNormal( fbits( Q4.y ) );
+							const float4 tdata0 = tri[0], tdata5 = tri[5];
+							const float lightPdf = (HIT_T * HIT_T) / (-dot3( D, N ) * tdata5.w);     /* CalculateLightPDF, tri.area */
+							const float pickProb = LightPickProb( s, __float_as_int( tdata0.w ), RAY_O, lastN, I );
+							if ((bsdfPdf + lightPdf * pickProb) > 0) contribution = muls( mul3( throughput, sd.color ), 1.0f / (bsdfPdf + lightPdf * pickProb) );
+						}
+						contribution = clampintensity( s.clampValue, contribution );
+						contribution = fixnan( contribution );
+						acc_add( p.acc, pixelIdx, contribution );
+					}
+					goto compact;
+				}
+				if (ROUGHNESS <= 0.001f || TRANSMISSION > 0.999f) data |= S_SPECULAR; else data &= ~S_SPECULAR;
+				uint32_t seed = WangHash( pathIdx * 17 + p.R0 );
+				const float faceDir = (dot3( D, N ) > 0) ? -1 : 1;
+				if (faceDir == 1) sd.transmittance = s3( 0 );
+				throughput = muls( throughput, 1.0f / bsdfPdf );
+				if (!(data & S_SPECULAR))
+				{
+					float r0, r1, pickProb = 0, lightPdf = 0;
+					if (sampleIdx < 2)
+					{
+						const uint32_t x = (pixelIdx % (uint32_t)w) & 127, y = (pixelIdx / (uint32_t)w) & 127;
+						r0 = blueNoiseSampler( s.blueNoise, x, y, sampleIdx, 4 + 4 * p.pathLength );
+						r1 = blueNoiseSampler( s.blueNoise, x, y, sampleIdx, 5 + 4 * p.pathLength );
+					}
+					else
+					{
+						r0 = RandomFloat( seed );
+						r1 = RandomFloat( seed );
+					}
+					v3 lightColor = s3( 0 );
+					v3 L = sub3( RandomPointOnLight( s, r0, r1, I, muls( fN, faceDir ), pickProb, lightPdf, lightColor ), I );
+					const float dist = length3( L );
+					L = muls( L, 1.0f / dist );
+					const float NdotL = dot3( L, muls( fN, faceDir ) );
+					if (NdotL > 0 && lightPdf > 0)
+					{
+						float bsdfPdf2;
+						const v3 sampledBSDF = EvaluateBSDF( sd, fN, T, muls( D, -1.0f ), L, bsdfPdf2 );
+						if (bsdfPdf2 > 0)
+						{
+							v3 contribution = muls( mul3( mul3( throughput, sampledBSDF ), lightColor ), NdotL / (pickProb * lightPdf + bsdfPdf2) );
+							contribution = fixnan( contribution );
+							contribution = clampintensity( s.clampValue, contribution );
+							const v3 so = SafeOrigin( I, L, muls( N, faceDir ), s.geometryEpsilon );
+							doShadow = true;
+							sO = make_float4( so.x, so.y, so.z, 0 );
+							sD = make_float4( L.x, L.y, L.z, dist - 2 * s.geometryEpsilon );
+							sP = make_float4( contribution.x, contribution.y, contribution.z, __uint_as_float( pixelIdx ) );
+						}
+					}
+				}
+				if (data & ENOUGH_BOUNCES || p.pathLength == p.maxPathLength) goto compact;
+				{
+					v3 R = s3( 0 );
+					float newBsdfPdf = 0, r3, r4;
+					if (sampleIdx < 256)
+					{
+						const uint32_t x = (pixelIdx % (uint32_t)w) & 127, y = (pixelIdx / (uint32_t)w) & 127;
+						r3 = blueNoiseSampler( s.blueNoise, x, y, sampleIdx, 6 + 4 * p.pathLength );
+						r4 = blueNoiseSampler( s.blueNoise, x, y, sampleIdx, 7 + 4 * p.pathLength );
+					}
+					else
+					{
+						r3 = RandomFloat( seed );
+						r4 = RandomFloat( seed );
+					}
+					bool specular = false;
+					const v3 bsdf = SampleBSDF( sd, fN, N, T, muls( D, -1.0f ), HIT_T, r3, r4, R, newBsdfPdf, specular );
+					if (newBsdfPdf < EPSILON || newBsdfPdf != newBsdfPdf) goto compact;
+					if (specular) data |= S_SPECULAR;
+					const float pr = ((data & S_SPECULAR) || ((data & S_BOUNCED) == 0)) ? 1 : SurvivalProbability( bsdf );
+					if (pr < RandomFloat( seed )) goto compact;
+					throughput = muls( throughput, 1 / pr );
+					const uint32_t packedNormal = PackNormal( muls( fN, faceDir ) );
+					if (!(data & S_SPECULAR)) data |= data & S_BOUNCED ? S_BOUNCEDTWICE : S_BOUNCED; else data |= S_VIASPECULAR;
+					const v3 eo = SafeOrigin( I, R, muls( N, faceDir ), s.geometryEpsilon );
+					throughput = fixnan( throughput );
+					const v3 nt = muls( mul3( throughput, bsdf ), fabsf( dot3( muls( fN, faceDir ), R ) ) );
+					doExt = true;
+					eO = make_float4( eo.x, eo.y, eo.z, 0 ), eD = make_float4( R.x, R.y, R.z, 1e34f );
+					eT = make_float4( nt.x, nt.y, nt.z, bitsf( data ) ), eQ = make_float4( newBsdfPdf, bitsf( packedNormal ), 0, 0 );
+				}
+			}
+		}
+	compact:
+		/* wave-level compaction of extension and shadow rays (one atomicAdd per wave each) */
+		{
+			const uint32_t es = wave_alloc( doExt, &p.counters->extensionRays );
+			if (doExt) { p.rayOut[es] = eO; p.rayDOut[es] = eD; p.T4Out[es] = eT; p.Q4Out[es] = eQ; }
+			const uint32_t ss = wave_alloc( doShadow, &p.counters->shadowRays );
+			if (doShadow)
+			{
+				if (ss < p.shadowCap) { p.shO[ss] = sO; p.shD[ss] = sD; p.shP[ss] = sP; }
+				else atomicOr( &p.counters->shadowOverflow, 1u );
+			}
+		}
+	}
+}
+
+/* counters: .cuda.cu:64-84 */
+__global__ void k_init_counters( Counters* c, uint32_t pathCount )
+{
+	if (threadIdx.x != 0) return;
+	c->activePaths = pathCount, c->extensionRays = 0, c->shadowRays = 0;
+	c->totalExtensionRays = pathCount, c->totalShadowRays = 0;
+	c->probedInstid = -1, c->probedTriid = -1, c->probedDist = 0;
+	c->stackOverflow = 0, c->shadowOverflow = 0;
+}
+__global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength )
+{
+	if (threadIdx.x != 0) return;
+	rayCountLog[pathLength] = c->extensionRays;     /* rays traced at pathLength + 1 */
+	c->totalExtensionRays += c->extensionRays;
+	c->activePaths = c->extensionRays;
+	c->extensionRays = 0;
+}
+__global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale )
+{
+	const int i = threadIdx.x + blockIdx.x * blockDim.x;
+	if (i >= n) return;
+	const float4 a = acc[i];
+	out[i] = make_float4( a.x * scale, a.y * scale, a.z * scale, a.w * scale );
+}
+
+/* copy the rows this tile owns (local row order) out of the full-frame accumulator, for the
+   multi-GPU gather; same row mapping as k_camera */
+__global__ void k_pack_rows( const float4* __restrict__ acc, float4* __restrict__ dst, const int w, const int y0, const int band,
+	const int bandStride, const int rows )
+{
+	const int i = threadIdx.x + blockIdx.x * blockDim.x;
+	if (i >= rows * w) return;
+	const int lr = i / w, x = i % w;
+	const int gy = y0 + (lr / band) * bandStride + lr % band;
+	dst[i] = acc[gy * w + x];
+}
+
+/* ---- host-side launchers (extern "C", no torch / no HIP types beyond the stream) ---------- */
+extern "C" {
+void lh2_launch_init_counters( Counters* c, uint32_t pathCount, hipStream_t st ) { k_init_counters<<<1, 64, 0, st>>>( c, pathCount ); }
+void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, hipStream_t st ) { k_counters_next<<<1, 64, 0, st>>>( c, log, pathLength ); }
+void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, hipStream_t st )
+{
+	if (jobCount <= 0) return;
+	k_camera<<<(jobCount + 255) / 256, 256, 0, st>>>( *p, bn, rayO, rayD, T4, Q4, jobCount );
+}
+void lh2_launch_trace_closest( const SceneDev* s, const float4* rayO, const float4* rayD, const uint32_t* countPtr, uint32_t countFixed, uint4* hits,
+	int* gstack, uint32_t* overflow, int grid, hipStream_t st )
+{
+	k_trace_closest<<<grid, 256, 0, st>>>( *s, rayO, rayD, countPtr, countFixed, hits, gstack, overflow );
+}
+void lh2_launch_trace_any( const SceneDev* s, const float4* rayO, const float4* rayD, const uint32_t* countPtr, uint32_t countFixed, uint32_t* mask,
+	const float4* potentials, float4* acc, int* gstack, uint32_t* overflow, int grid, int fused, hipStream_t st )
+{
+	if (fused) k_trace_any<1><<<grid, 256, 0, st>>>( *s, rayO, rayD, countPtr, countFixed, mask, potentials, acc, gstack, overflow );
+	else k_trace_any<0><<<grid, 256, 0, st>>>( *s, rayO, rayD, countPtr, countFixed, mask, potentials, acc, gstack, overflow );
+}
+void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, hipStream_t st ) { k_shade<<<grid, 256, 0, st>>>( *s, *p ); }
+void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, hipStream_t st )
+{
+	if (rows * w <= 0) return;
+	k_pack_rows<<<(rows * w + 255) / 256, 256, 0, st>>>( acc, dst, w, y0, band, bandStride, rows );
+}
+void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, hipStream_t st )
+{
+	if (n <= 0) return;
+	k_finalize<<<(n + 255) / 256, 256, 0, st>>>( acc, out, n, scale );
+}
+}

@@ -1,0 +1,630 @@
+/* rendercore.cpp - host driver of the MI355X wavefront path tracer.
+
+   Counterpart of RenderCore_OptixPrime_B/rendercore.cpp (method-for-method, same semantics),
+   re-designed for MI355X:
+     - the acceleration structure is our own binned-SAH BVH2 (bvh_build.cpp) instead of the
+       closed OptiX Prime BLAS/TLAS (core_mesh.cpp:53-66, rendercore.cpp:250-270);
+     - path / ray / hit buffers are SoA float4 planes (coalesced 16-B lane accesses);
+     - per-bounce path counts stay on the device (wave-compacted counters), so a frame is one
+       stream of launches with no blocking counter copy per bounce (rendercore.cpp:547);
+     - shadow rays never overflow (<= 2 per path with ENOUGH_BOUNCES = S_BOUNCED) and are traced
+       once per frame with finalizeConnection fused into the any-hit kernel.
+*/
+#include "rendercore.h"
+
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+#include "../../include/lh2_detmath.h"
+#include "lh2_device.h"
+
+namespace lh2 {
+
+void FatalError( const char* fmt, ... )
+{
+	char buf[1024];
+	va_list args;
+	va_start( args, fmt );
+	vsnprintf( buf, sizeof( buf ), fmt, args );
+	va_end( args );
+	throw std::runtime_error( buf );
+}
+
+#define CHK_HIP( stmt ) do { hipError_t e_ = (stmt); if (e_ != hipSuccess) FatalError( "%s failed: %s (%s:%d)", #stmt, hipGetErrorString( e_ ), __FILE__, __LINE__ ); } while (0)
+
+static std::string LibraryDir()
+{
+	Dl_info info;
+	if (dladdr( (void*)&LibraryDir, &info ) && info.dli_fname)
+	{
+		std::string p( info.dli_fname );
+		const size_t s = p.find_last_of( '/' );
+		return s == std::string::npos ? std::string( "." ) : p.substr( 0, s );
+	}
+	return ".";
+}
+
+/* mat4::Inverted (RenderSystem/common_types.h:586-628); same formula as the oracle */
+static void Mat4Inverse( const float* c, float* out )
+{
+	const float inv[16] = {
+		c[5] * c[10] * c[15] - c[5] * c[11] * c[14] - c[9] * c[6] * c[15] + c[9] * c[7] * c[14] + c[13] * c[6] * c[11] - c[13] * c[7] * c[10],
+		-c[1] * c[10] * c[15] + c[1] * c[11] * c[14] + c[9] * c[2] * c[15] - c[9] * c[3] * c[14] - c[13] * c[2] * c[11] + c[13] * c[3] * c[10],
+		c[1] * c[6] * c[15] - c[1] * c[7] * c[14] - c[5] * c[2] * c[15] + c[5] * c[3] * c[14] + c[13] * c[2] * c[7] - c[13] * c[3] * c[6],
+		-c[1] * c[6] * c[11] + c[1] * c[7] * c[10] + c[5] * c[2] * c[11] - c[5] * c[3] * c[10] - c[9] * c[2] * c[7] + c[9] * c[3] * c[6],
+		-c[4] * c[10] * c[15] + c[4] * c[11] * c[14] + c[8] * c[6] * c[15] - c[8] * c[7] * c[14] - c[12] * c[6] * c[11] + c[12] * c[7] * c[10],
+		c[0] * c[10] * c[15] - c[0] * c[11] * c[14] - c[8] * c[2] * c[15] + c[8] * c[3] * c[14] + c[12] * c[2] * c[11] - c[12] * c[3] * c[10],
+		-c[0] * c[6] * c[15] + c[0] * c[7] * c[14] + c[4] * c[2] * c[15] - c[4] * c[3] * c[14] - c[12] * c[2] * c[7] + c[12] * c[3] * c[6],
+		c[0] * c[6] * c[11] - c[0] * c[7] * c[10] - c[4] * c[2] * c[11] + c[4] * c[3] * c[10] + c[8] * c[2] * c[7] - c[8] * c[3] * c[6],
+		c[4] * c[9] * c[15] - c[4] * c[11] * c[13] - c[8] * c[5] * c[15] + c[8] * c[7] * c[13] + c[12] * c[5] * c[11] - c[12] * c[7] * c[9],
+		-c[0] * c[9] * c[15] + c[0] * c[11] * c[13] + c[8] * c[1] * c[15] - c[8] * c[3] * c[13] - c[12] * c[1] * c[11] + c[12] * c[3] * c[9],
+		c[0] * c[5] * c[15] - c[0] * c[7] * c[13] - c[4] * c[1] * c[15] + c[4] * c[3] * c[13] + c[12] * c[1] * c[7] - c[12] * c[3] * c[5],
+		-c[0] * c[5] * c[11] + c[0] * c[7] * c[9] + c[4] * c[1] * c[11] - c[4] * c[3] * c[9] - c[8] * c[1] * c[7] + c[8] * c[3] * c[5],
+		-c[4] * c[9] * c[14] + c[4] * c[10] * c[13] + c[8] * c[5] * c[14] - c[8] * c[6] * c[13] - c[12] * c[5] * c[10] + c[12] * c[6] * c[9],
+		c[0] * c[9] * c[14] - c[0] * c[10] * c[13] - c[8] * c[1] * c[14] + c[8] * c[2] * c[13] + c[12] * c[1] * c[10] - c[12] * c[2] * c[9],
+		-c[0] * c[5] * c[14] + c[0] * c[6] * c[13] + c[4] * c[1] * c[14] - c[4] * c[2] * c[13] - c[12] * c[1] * c[6] + c[12] * c[2] * c[5],
+		c[0] * c[5] * c[10] - c[0] * c[6] * c[9] - c[4] * c[1] * c[10] + c[4] * c[2] * c[9] + c[8] * c[1] * c[6] - c[8] * c[2] * c[5] };
+	const float det = c[0] * inv[0] + c[1] * inv[4] + c[2] * inv[8] + c[3] * inv[12];
+	if (det != 0) { const float invdet = 1.0f / det; for (int i = 0; i < 16; i++) out[i] = inv[i] * invdet; }
+	else for (int i = 0; i < 16; i++) out[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+void RenderCore::Init()   /* rendercore.cpp:96-143 */
+{
+	if (initialized) return;
+	CHK_HIP( hipGetDevice( &device ) );
+	hipDeviceProp_t props;
+	CHK_HIP( hipGetDeviceProperties( &props, device ) );
+	smCount = props.multiProcessorCount;
+	coreStats.SMcount = (uint32_t)smCount;
+	coreStats.ccMajor = (uint32_t)props.major, coreStats.ccMinor = (uint32_t)props.minor;
+	coreStats.VRAM = (uint32_t)(props.totalGlobalMem >> 20);
+	const char* name = props.gcnArchName[0] ? props.gcnArchName : props.name;
+	coreStats.deviceName = new char[strlen( name ) + 1];   /* owned (and leaked) by the core: core_api_base.h:33 */
+	memcpy( coreStats.deviceName, name, strlen( name ) + 1 );
+	CHK_HIP( hipStreamCreateWithFlags( &stream, hipStreamNonBlocking ) );
+	/* blue noise sampler tables (rendercore.cpp:125-134), shipped as data/bluenoise.bin */
+	std::string path = getenv( "LH2_BLUENOISE" ) ? getenv( "LH2_BLUENOISE" ) : LibraryDir() + "/data/bluenoise.bin";
+	FILE* f = fopen( path.c_str(), "rb" );
+	if (!f) FatalError( "blue noise table not found: %s", path.c_str() );
+	/* +256 zero bytes: tools_shared.h:343 reads past the table for dimensions > 7 at pixel (127,127)
+	   (undefined in the reference; defined as 0 here and in the oracle) */
+	std::vector<uint8_t> bn( 65536 * 5 + 256, 0 );
+	const size_t got = fread( bn.data(), 1, 65536 * 5, f );
+	fclose( f );
+	if (got != 65536 * 5) FatalError( "blue noise table truncated: %s", path.c_str() );
+	dBlueNoise.upload( bn.data(), bn.size(), stream );
+	counters.resize( 1 );
+	rayLog.resize( 32 );
+	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocDefault ) );
+	memset( hostStats, 0, sizeof( FrameStats ) );
+	for (auto& e : evTrace) CHK_HIP( hipEventCreate( &e ) );
+	for (auto& e : evShade) CHK_HIP( hipEventCreate( &e ) );
+	for (auto& e : evShadow) CHK_HIP( hipEventCreate( &e ) );
+	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	initialized = true;
+}
+
+void RenderCore::SetTarget( uint32_t w, uint32_t h, uint32_t spp )  /* rendercore.cpp:149-209 */
+{
+	if (spp < 1) spp = 1;
+	if ((uint64_t)w * h * spp > (1u << 24)) FatalError( "path index exceeds 24 bits (camera.h:92): %ux%u x %u spp", w, h, spp );
+	scrwidth = (int)w, scrheight = (int)h, scrspp = (int)spp;
+	EnsureBuffers();
+	CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)w * h, stream ) );
+	samplesTaken = 0;
+}
+
+void RenderCore::EnsureBuffers()
+{
+	const size_t paths = (size_t)scrwidth * scrheight * scrspp;
+	if (paths > maxPaths)
+	{
+		maxPaths = paths + (paths >> 4);   /* reserve a bit extra, as the reference does */
+		for (int i = 0; i < 2; i++) rayO[i].resize( maxPaths ), rayD[i].resize( maxPaths ), T4[i].resize( maxPaths ), Q4[i].resize( maxPaths );
+		hits.resize( maxPaths );
+		shO.resize( 2 * maxPaths ), shD.resize( 2 * maxPaths ), shP.resize( 2 * maxPaths );
+		shMask.resize( (2 * maxPaths + 63) / 32 + 2 );
+	}
+	accumulator.resize( (size_t)scrwidth * scrheight );
+	frame.resize( (size_t)scrwidth * scrheight );
+	gstack.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
+}
+
+void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439-457 */
+{
+	if (!strcmp( name, "epsilon" )) geometryEpsilon = value;
+	else if (!strcmp( name, "clampValue" )) clampValue = value;
+	else if (!strcmp( name, "maxPathLength" )) maxPathLength = std::min( 16, std::max( 1, (int)value ) );
+	else if (!strcmp( name, "blocksPerCU" )) { blocksPerCU = std::min( 16, std::max( 1, (int)value ) ); if (scrwidth) EnsureBuffers(); }
+	/* other names ("clampDirect", "filter", "TAA", ...) are ignored, as in the reference */
+}
+
+void RenderCore::SetTextures( const lh2_CoreTexDesc*, int textureCount )
+{
+	coreStats.argb32TexelCount = coreStats.argb128TexelCount = coreStats.nrm32TexelCount = 0;
+	(void)textureCount;   /* texture maps: SURVEY §8f row 2 (next round) */
+}
+
+#define TOCHAR(a) lh2_f2u( (a) * 255.0f )
+#define TOUINT4(a,b,c,d) (TOCHAR(a)+(TOCHAR(b)<<8)+(TOCHAR(c)<<16)+(TOCHAR(d)<<24))
+void RenderCore::SetMaterials( const lh2_CoreMaterial* mat, int n )   /* rendercore.cpp:353-399 */
+{
+	std::vector<uint4> recs( (size_t)std::max( n, 1 ) * 8 );
+	memset( recs.data(), 0, recs.size() * sizeof( uint4 ) );
+	for (int i = 0; i < n; i++)
+	{
+		const lh2_CoreMaterial& m = mat[i];
+		const uint32_t r = lh2_f2h( m.color.value.x ), g = lh2_f2h( m.color.value.y ), b = lh2_f2h( m.color.value.z );
+		const uint32_t tr = lh2_f2h( 1 - m.absorption.value.x ), tg = lh2_f2h( 1 - m.absorption.value.y ), tb = lh2_f2h( 1 - m.absorption.value.z );
+		const uint32_t flags = (m.eta.value < 1 ? 1u : 0u) + ((m.flags & 1) ? (1u << 11) : 0u) + ((m.flags & 2) ? (1u << 12) : 0u);
+		recs[i * 8 + 0] = make_uint4( r | (g << 16), b | (tr << 16), tg | (tb << 16), flags );
+		recs[i * 8 + 1] = make_uint4( TOUINT4( m.metallic.value, m.subsurface.value, m.specular.value, m.roughness.value ),
+			TOUINT4( m.specularTint.value, m.anisotropic.value, m.sheen.value, m.sheenTint.value ),
+			TOUINT4( m.clearcoat.value, m.clearcoatGloss.value, m.transmission.value, 0 ), lh2_f2b( m.eta.value ) );
+	}
+	dMaterials.upload( recs.data(), recs.size(), stream );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+}
+
+void RenderCore::SetLights( const lh2_CoreLightTri* a, int na, const lh2_CorePointLight* p, int np, const lh2_CoreSpotLight* s, int ns,
+	const lh2_CoreDirectionalLight* d, int nd )   /* rendercore.cpp:405-419 */
+{
+	dArea.upload( a, na, stream ), dPoint.upload( p, np, stream ), dSpot.upload( s, ns, stream ), dDir.upload( d, nd, stream );
+	dArea.resize( 1 ), dPoint.resize( 1 ), dSpot.resize( 1 ), dDir.resize( 1 );
+	nArea = na, nPoint = np, nSpot = ns, nDir = nd;
+	CHK_HIP( hipStreamSynchronize( stream ) );
+}
+
+void RenderCore::SetSkyData( const float* pixels, uint32_t width, uint32_t height )   /* rendercore.cpp:425-433 */
+{
+	dSky.upload( pixels, (size_t)width * height * 3, stream );
+	dSky.resize( 1 );
+	skyW = (int)width, skyH = (int)height;
+	CHK_HIP( hipStreamSynchronize( stream ) );
+}
+
+void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount, const lh2_CoreTri* tris, const uint32_t* )
+{
+	/* rendercore.cpp:215-223 + core_mesh.cpp:36-67: meshes arrive first-time in sequential order */
+	if (meshIdx < 0 || meshIdx > (int)meshes.size()) FatalError( "SetGeometry: mesh index %d out of sequence", meshIdx );
+	if (meshIdx == (int)meshes.size()) meshes.push_back( new CoreMeshHost() );
+	CoreMeshHost& m = *meshes[meshIdx];
+	const auto t0 = std::chrono::high_resolution_clock::now();
+	m.tris.assign( tris, tris + triangleCount );
+	std::vector<Aabb> prims( triangleCount );
+	for (int k = 0; k < 3; k++) m.aabbLo[k] = 1e30f, m.aabbHi[k] = -1e30f;
+	for (int i = 0; i < triangleCount; i++)
+	{
+		const lh2_CoreTri& t = tris[i];
+		const float v[3][3] = { { t.vertex0.x, t.vertex0.y, t.vertex0.z }, { t.vertex1.x, t.vertex1.y, t.vertex1.z }, { t.vertex2.x, t.vertex2.y, t.vertex2.z } };
+		for (int k = 0; k < 3; k++)
+		{
+			prims[i].lo[k] = std::min( std::min( v[0][k], v[1][k] ), v[2][k] );
+			prims[i].hi[k] = std::max( std::max( v[0][k], v[1][k] ), v[2][k] );
+			m.aabbLo[k] = std::min( m.aabbLo[k], prims[i].lo[k] ), m.aabbHi[k] = std::max( m.aabbHi[k], prims[i].hi[k] );
+		}
+	}
+	BuildBvh2( prims, 4, 0, m.bvh );
+	m.shadeTris.upload( (const float4*)tris, (size_t)triangleCount * 11, stream );
+	m.shadeTris.resize( 11 );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	m.dirty = true;
+	geometryDirty = true;
+	coreStats.bvhBuildTime += std::chrono::duration<float>( std::chrono::high_resolution_clock::now() - t0 ).count();
+}
+
+void RenderCore::SetInstance( int instanceIdx, int meshIdx, const float* M )   /* rendercore.cpp:229-243 */
+{
+	if (meshIdx == -1) { if ((int)instances.size() > instanceIdx) instances.resize( instanceIdx ); instancesDirty = true; return; }
+	if (meshIdx < 0 || meshIdx >= (int)meshes.size()) FatalError( "SetInstance: unknown mesh %d", meshIdx );
+	if (instanceIdx >= (int)instances.size()) instances.resize( instanceIdx + 1 );
+	instances[instanceIdx].mesh = meshIdx;
+	memcpy( instances[instanceIdx].T, M, 64 );
+	instancesDirty = true;
+}
+
+void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 (instance descriptors) */
+{
+	const int ni = (int)instances.size();
+	/* TLAS over instance world bounds (8 transformed corners of the mesh bounds), 1 instance per leaf */
+	std::vector<Aabb> prims;
+	std::vector<int> primInst;
+	for (int i = 0; i < ni; i++)
+	{
+		CoreInstanceHost& in = instances[i];
+		Mat4Inverse( in.T, in.inv );
+		const CoreMeshHost& m = *meshes[in.mesh];
+		if (m.tris.empty()) continue;
+		Aabb b;
+		for (int k = 0; k < 3; k++) b.lo[k] = 1e30f, b.hi[k] = -1e30f;
+		for (int c = 0; c < 8; c++)
+		{
+			const float p[3] = { (c & 1) ? m.aabbHi[0] : m.aabbLo[0], (c & 2) ? m.aabbHi[1] : m.aabbLo[1], (c & 4) ? m.aabbHi[2] : m.aabbLo[2] };
+			for (int k = 0; k < 3; k++)
+			{
+				const float* r = in.T + k * 4;
+				const float v = r[0] * p[0] + r[1] * p[1] + r[2] * p[2] + r[3];
+				b.lo[k] = std::min( b.lo[k], v ), b.hi[k] = std::max( b.hi[k], v );
+			}
+		}
+		/* pad by a relative epsilon: the ray is transformed in fp32 on the device */
+		for (int k = 0; k < 3; k++)
+		{
+			const float e = 1e-5f * std::max( std::fabs( b.lo[k] ), std::fabs( b.hi[k] ) ) + 1e-30f;
+			b.lo[k] -= e, b.hi[k] += e;
+		}
+		prims.push_back( b ), primInst.push_back( i );
+	}
+	BvhOutput tlas;
+	BuildBvh2( prims, 1, 1, tlas );
+	/* concatenate BLAS nodes / triangles (only when geometry changed) */
+	const int tlasNodes = (int)(tlas.nodes.size() / 16);
+	if (geometryDirty || (size_t)(blasNodeCount + tlasNodes) * 4 > dNodes.count)
+	{
+		meshNodeBase.assign( meshes.size(), 0 ), meshTriBase.assign( meshes.size(), 0 );
+		int nodeTotal = 0, triTotal = 0, maxBlasDepth = 0;
+		for (size_t mi = 0; mi < meshes.size(); mi++)
+		{
+			meshNodeBase[mi] = nodeTotal, meshTriBase[mi] = triTotal;
+			nodeTotal += (int)(meshes[mi]->bvh.nodes.size() / 16);
+			triTotal += (int)meshes[mi]->tris.size();
+			maxBlasDepth = std::max( maxBlasDepth, meshes[mi]->bvh.maxDepth );
+		}
+		std::vector<float> nodes( ((size_t)nodeTotal + tlasNodes + 2 * (size_t)ni + 16) * 16 );
+		std::vector<float> tris48( (size_t)std::max( triTotal, 1 ) * 12 );
+		for (size_t mi = 0; mi < meshes.size(); mi++)
+		{
+			const CoreMeshHost& m = *meshes[mi];
+			const int nb = meshNodeBase[mi], tb = meshTriBase[mi];
+			const size_t nn = m.bvh.nodes.size() / 16;
+			memcpy( &nodes[(size_t)nb * 16], m.bvh.nodes.data(), m.bvh.nodes.size() * sizeof( float ) );
+			for (size_t k = 0; k < nn; k++)
+			{
+				int* refs = (int*)&nodes[((size_t)nb + k) * 16 + 12];
+				for (int c = 0; c < 2; c++)
+				{
+					if (refs[c] >= 0) refs[c] += nb;
+					else refs[c] = MAKE_LEAF( LEAF_FIRST( refs[c] ) + (uint32_t)tb, LEAF_COUNT( refs[c] ) );
+				}
+			}
+			for (size_t j = 0; j < m.bvh.perm.size(); j++)
+			{
+				const uint32_t ti = m.bvh.perm[j];
+				const lh2_CoreTri& t = m.tris[ti];
+				float* o = &tris48[((size_t)tb + j) * 12];
+				/* v0, e1 = v1 - v0, e2 = v2 - v0 in fp32, exactly as the oracle's intersect_tri */
+				o[0] = t.vertex0.x, o[1] = t.vertex0.y, o[2] = t.vertex0.z; memcpy( &o[3], &ti, 4 );
+				o[4] = t.vertex1.x - t.vertex0.x, o[5] = t.vertex1.y - t.vertex0.y, o[6] = t.vertex1.z - t.vertex0.z, o[7] = 0;
+				o[8] = t.vertex2.x - t.vertex0.x, o[9] = t.vertex2.y - t.vertex0.y, o[10] = t.vertex2.z - t.vertex0.z, o[11] = 0;
+			}
+		}
+		blasNodeCount = nodeTotal, blasTriCount = triTotal;
+		dNodes.upload( (const float4*)nodes.data(), nodes.size() / 4, stream );
+		dTris.upload( (const float4*)tris48.data(), tris48.size() / 4, stream );
+		sceneMaxDepth = maxBlasDepth;
+		for (auto* m : meshes) m->dirty = false;
+		geometryDirty = false;
+	}
+	/* TLAS: leaf first -> instance index, interior refs offset behind the BLAS nodes */
+	const size_t tn = tlas.nodes.size() / 16;
+	for (size_t k = 0; k < tn; k++)
+	{
+		int* refs = (int*)&tlas.nodes[k * 16 + 12];
+		for (int c = 0; c < 2; c++)
+		{
+			if (refs[c] >= 0) refs[c] += blasNodeCount;
+			else if (!prims.empty()) refs[c] = MAKE_LEAF( (uint32_t)primInst[tlas.perm[LEAF_FIRST( refs[c] )]], 1 );
+		}
+	}
+	tlasRoot = blasNodeCount;
+	CHK_HIP( hipMemcpyAsync( dNodes.ptr + (size_t)blasNodeCount * 4, tlas.nodes.data(), tlas.nodes.size() * sizeof( float ), hipMemcpyHostToDevice, stream ) );
+	int maxBlasDepth = 0;
+	for (auto* m : meshes) maxBlasDepth = std::max( maxBlasDepth, m->bvh.maxDepth );
+	sceneMaxDepth = tlas.maxDepth + maxBlasDepth;
+	if (sceneMaxDepth >= LH2_STACK_TOTAL - 1) FatalError( "BVH depth %d exceeds the traversal stack (%d)", sceneMaxDepth, LH2_STACK_TOTAL );
+	/* instance records for traversal and shading */
+	std::vector<DevInstance> di( std::max( ni, 1 ) );
+	std::vector<lh2_CoreInstanceDesc> desc( std::max( ni, 1 ) );
+	for (int i = 0; i < ni; i++)
+	{
+		const CoreInstanceHost& in = instances[i];
+		di[i].inv0 = make_float4( in.inv[0], in.inv[1], in.inv[2], in.inv[3] );
+		di[i].inv1 = make_float4( in.inv[4], in.inv[5], in.inv[6], in.inv[7] );
+		di[i].inv2 = make_float4( in.inv[8], in.inv[9], in.inv[10], in.inv[11] );
+		di[i].root = meshNodeBase[in.mesh], di[i].triBase = meshTriBase[in.mesh], di[i].mesh = in.mesh, di[i].pad = 0;
+		memset( &desc[i], 0, sizeof( desc[i] ) );
+		desc[i].triangles = meshes[in.mesh]->shadeTris.ptr;
+		desc[i].A = { in.inv[0], in.inv[1], in.inv[2], in.inv[3] };
+		desc[i].B = { in.inv[4], in.inv[5], in.inv[6], in.inv[7] };
+		desc[i].C = { in.inv[8], in.inv[9], in.inv[10], in.inv[11] };
+		desc[i].D = { in.inv[12], in.inv[13], in.inv[14], in.inv[15] };
+	}
+	dInst.upload( (const uint8_t*)di.data(), di.size() * sizeof( DevInstance ), stream );
+	dInstDesc.upload( desc.data(), desc.size(), stream );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	instancesDirty = false;
+}
+
+SceneDev RenderCore::MakeSceneDev() const
+{
+	SceneDev s;
+	s.nodes = dNodes.ptr, s.tris = dTris.ptr, s.inst = (const DevInstance*)dInst.ptr;
+	s.tlasRoot = tlasRoot, s.instCount = (int)instances.size();
+	s.instDesc = dInstDesc.ptr, s.materials = dMaterials.ptr;
+	s.areaLights = dArea.ptr, s.pointLights = dPoint.ptr, s.spotLights = dSpot.ptr, s.dirLights = dDir.ptr;
+	s.nArea = nArea, s.nPoint = nPoint, s.nSpot = nSpot, s.nDir = nDir;
+	s.sky = dSky.ptr, s.skyW = skyW, s.skyH = skyH;
+	s.blueNoise = dBlueNoise.ptr;
+	s.geometryEpsilon = geometryEpsilon, s.clampValue = clampValue;
+	return s;
+}
+
+static inline uint32_t XorShift( uint32_t& s ) { s ^= s << 13; s ^= s >> 17; s ^= s << 5; return s; }  /* platform/system.cpp:48 */
+
+void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* rendercore.cpp:463-609 */
+{
+	if (!initialized) FatalError( "Render before Init" );
+	if (!scrwidth) FatalError( "Render before SetTarget" );
+	if (geometryDirty || instancesDirty) UpdateToplevel();
+	if (!dMaterials.ptr) FatalError( "Render before SetMaterials" );
+	const auto t0 = std::chrono::high_resolution_clock::now();
+	if (converge == LH2_RESTART || firstConvergingFrame)
+	{
+		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
+		samplesTaken = 0;
+		firstConvergingFrame = true;
+		camRNGseed = 0x12345678;
+	}
+	if (converge == LH2_CONVERGE) firstConvergingFrame = false;
+	const int tileRows = TileRows();
+	const int tilePix = tileRows * scrwidth;
+	const uint32_t pathCount = (uint32_t)tilePix * (uint32_t)scrspp;
+	const SceneDev sd = MakeSceneDev();
+	Counters* c = counters.ptr;
+	lh2_launch_init_counters( c, pathCount, stream );
+	/* primary rays (camera.h) for every sample of the tile */
+	CameraParams cp;
+	cp.pos = view.pos, cp.p1 = view.p1;
+	cp.right = { view.p2.x - view.p1.x, view.p2.y - view.p1.y, view.p2.z - view.p1.z };
+	cp.up = { view.p3.x - view.p1.x, view.p3.y - view.p1.y, view.p3.z - view.p1.z };
+	cp.aperture = view.aperture, cp.distortion = view.distortion, cp.geometryEpsilon = geometryEpsilon;
+	cp.w = scrwidth, cp.h = scrheight, cp.pass = samplesTaken;
+	cp.R0 = XorShift( camRNGseed );
+	cp.y0 = std::max( 0, tileY0 ), cp.tileRows = tileRows;
+	cp.band = tileBand > 0 ? tileBand : std::max( 1, tileRows ), cp.bandStride = tileBand > 0 ? tileStride : std::max( 1, tileRows );
+	lh2_launch_camera( &cp, dBlueNoise.ptr, rayO[0].ptr, rayD[0].ptr, T4[0].ptr, Q4[0].ptr, (int)pathCount, stream );
+	int in = 0, pl = 0;
+	const int grid = TraceGrid();
+	for (int pathLength = 1; pathLength <= maxPathLength; pathLength++)
+	{
+		pl = pathLength;
+		CHK_HIP( hipEventRecord( evTrace[2 * pathLength], stream ) );
+		lh2_launch_trace_closest( &sd, rayO[in].ptr, rayD[in].ptr, &c->activePaths, 0, hits.ptr, gstack.ptr, &c->stackOverflow, grid, stream );
+		CHK_HIP( hipEventRecord( evTrace[2 * pathLength + 1], stream ) );
+		ShadeParams sp;
+		sp.pathCount = &c->activePaths;
+		sp.rayO = rayO[in].ptr, sp.rayD = rayD[in].ptr, sp.T4 = T4[in].ptr, sp.Q4 = Q4[in].ptr, sp.hits = hits.ptr;
+		sp.rayOut = rayO[1 - in].ptr, sp.rayDOut = rayD[1 - in].ptr, sp.T4Out = T4[1 - in].ptr, sp.Q4Out = Q4[1 - in].ptr;
+		sp.shO = shO.ptr, sp.shD = shD.ptr, sp.shP = shP.ptr, sp.shadowCap = (uint32_t)shO.count;
+		sp.acc = accumulator.ptr, sp.counters = c;
+		sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPathLength;
+		sp.probePixel = probeX + scrwidth * probeY;
+		sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
+		CHK_HIP( hipEventRecord( evShade[2 * pathLength], stream ) );
+		lh2_launch_shade( &sd, &sp, grid, stream );
+		CHK_HIP( hipEventRecord( evShade[2 * pathLength + 1], stream ) );
+		if (pathLength == maxPathLength) break;
+		lh2_launch_counters_next( c, rayLog.ptr, pathLength, stream );
+		in = 1 - in;
+	}
+	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
+	CHK_HIP( hipEventRecord( evShadow[0], stream ) );
+	lh2_launch_trace_any( &sd, shO.ptr, shD.ptr, &c->shadowRays, 0, shMask.ptr, shP.ptr, accumulator.ptr, gstack.ptr, &c->stackOverflow, grid, 1, stream );
+	CHK_HIP( hipEventRecord( evShadow[1], stream ) );
+	samplesTaken += scrspp;
+	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, stream );
+	CHK_HIP( hipMemcpyAsync( &hostStats->counters, c, sizeof( Counters ), hipMemcpyDeviceToHost, stream ) );
+	CHK_HIP( hipMemcpyAsync( hostStats->rayCount + 1, rayLog.ptr + 1, sizeof( uint32_t ) * 16, hipMemcpyDeviceToHost, stream ) );
+	CHK_HIP( hipEventRecord( evFrame[1], stream ) );
+	hostStats->rayCount[0] = pathCount;
+	framePathLengths = pl;
+	statsPending = true;
+	frameHostMs = std::chrono::duration<double, std::milli>( std::chrono::high_resolution_clock::now() - t0 ).count();
+}
+
+int RenderCore::TileRows() const
+{
+	if (tileBand > 0)
+	{
+		int rows = 0;
+		for (int y = tileY0; y < scrheight; y += tileStride) rows += std::min( tileBand, scrheight - y );
+		return rows;
+	}
+	const int y0 = std::max( 0, tileY0 ), y1 = tileY1 < 0 ? scrheight : std::min( scrheight, tileY1 );
+	return std::max( 0, y1 - y0 );
+}
+
+void RenderCore::Synchronize()
+{
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	if (statsPending)
+	{
+		statsPending = false;
+		const Counters& cnt = hostStats->counters;
+		if (cnt.stackOverflow) FatalError( "traversal stack overflow (BVH deeper than %d)", LH2_STACK_TOTAL );
+		if (cnt.shadowOverflow) FatalError( "shadow ray buffer overflow" );
+		uint32_t* rc = hostStats->rayCount;   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
+		auto ms = [&]( hipEvent_t a, hipEvent_t b ) { float t = 0; (void)hipEventElapsedTime( &t, a, b ); return t * 1e-3f; };
+		coreStats.primaryRayCount = rc[0];
+		coreStats.traceTime0 = ms( evTrace[2], evTrace[3] );
+		coreStats.bounce1RayCount = framePathLengths >= 2 ? rc[1] : 0;
+		coreStats.traceTime1 = framePathLengths >= 2 ? ms( evTrace[4], evTrace[5] ) : 0;
+		coreStats.deepRayCount = 0, coreStats.traceTimeX = 0;
+		for (int L = 3; L <= framePathLengths; L++) coreStats.deepRayCount = rc[L - 1], coreStats.traceTimeX = ms( evTrace[2 * L], evTrace[2 * L + 1] );
+		coreStats.shadowTraceTime = ms( evShadow[0], evShadow[1] );
+		float shade = 0;
+		for (int L = 1; L <= framePathLengths; L++) shade += ms( evShade[2 * L], evShade[2 * L + 1] );
+		coreStats.shadeTime = shade;
+		for (int L = 1; L <= framePathLengths && L <= 8; L++) lastKernelMs[L - 1] = ms( evTrace[2 * L], evTrace[2 * L + 1] ) * 1e3f;
+		coreStats.totalShadowRays = cnt.shadowRays;
+		coreStats.totalExtensionRays = cnt.totalExtensionRays;
+		coreStats.totalRays = coreStats.totalExtensionRays + coreStats.totalShadowRays;
+		coreStats.renderTime = (float)(frameHostMs * 1e-3);
+		coreStats.probedInstid = cnt.probedInstid, coreStats.probedTriid = cnt.probedTriid, coreStats.probedDist = cnt.probedDist;
+	}
+}
+
+lh2_CoreStats RenderCore::GetCoreStats()
+{
+	Synchronize();
+	return coreStats;
+}
+
+void RenderCore::GetRayCounts( uint32_t* out17 )
+{
+	Synchronize();
+	for (int i = 0; i < 17; i++) out17[i] = i < framePathLengths ? hostStats->rayCount[i] : 0;
+	out17[16] = hostStats->counters.shadowRays;
+}
+
+void RenderCore::GetAccumulator( float* hostOut4 )
+{
+	Synchronize();
+	CHK_HIP( hipMemcpy( hostOut4, accumulator.ptr, sizeof( float4 ) * (size_t)scrwidth * scrheight, hipMemcpyDeviceToHost ) );
+}
+
+void RenderCore::CopyAccumulatorRows( void* devDst, int y0, int y1 )
+{
+	CHK_HIP( hipMemcpyAsync( devDst, accumulator.ptr + (size_t)y0 * scrwidth, sizeof( float4 ) * (size_t)(y1 - y0) * scrwidth, hipMemcpyDeviceToDevice, stream ) );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+}
+
+void RenderCore::PackTile( void* devDst )
+{
+	const int rows = TileRows();
+	const int band = tileBand > 0 ? tileBand : std::max( 1, rows ), stride = tileBand > 0 ? tileStride : std::max( 1, rows );
+	lh2_launch_pack_rows( accumulator.ptr, (float4*)devDst, scrwidth, std::max( 0, tileY0 ), band, stride, rows, stream );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+}
+
+void RenderCore::GetFrame( float* hostOut4 )
+{
+	Synchronize();
+	CHK_HIP( hipMemcpy( hostOut4, frame.ptr, sizeof( float4 ) * (size_t)scrwidth * scrheight, hipMemcpyDeviceToHost ) );
+}
+
+void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t* hits4 )
+{
+	if (geometryDirty || instancesDirty) UpdateToplevel();
+	DevBuf<float4> o, d; DevBuf<uint4> h; DevBuf<int> gs; DevBuf<uint32_t> ovf;
+	o.upload( (const float4*)ot, n, stream ), d.upload( (const float4*)dt, n, stream );
+	h.resize( n ), ovf.resize( 1 );
+	gs.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
+	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, 4, stream ) );
+	const SceneDev sd = MakeSceneDev();
+	lh2_launch_trace_closest( &sd, o.ptr, d.ptr, nullptr, (uint32_t)n, h.ptr, gs.ptr, ovf.ptr, TraceGrid(), stream );
+	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
+	uint32_t of = 0;
+	CHK_HIP( hipMemcpyAsync( &of, ovf.ptr, 4, hipMemcpyDeviceToHost, stream ) );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	if (of) FatalError( "traversal stack overflow" );
+}
+
+void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* occluded )
+{
+	if (geometryDirty || instancesDirty) UpdateToplevel();
+	DevBuf<float4> o, d; DevBuf<uint32_t> m; DevBuf<int> gs; DevBuf<uint32_t> ovf;
+	o.upload( (const float4*)ot, n, stream ), d.upload( (const float4*)dt, n, stream );
+	const size_t words = ((size_t)n + 63) / 64 * 2;
+	m.resize( words ), ovf.resize( 1 );
+	gs.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
+	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, 4, stream ) );
+	CHK_HIP( hipMemsetAsync( m.ptr, 0, words * 4, stream ) );
+	const SceneDev sd = MakeSceneDev();
+	lh2_launch_trace_any( &sd, o.ptr, d.ptr, nullptr, (uint32_t)n, m.ptr, nullptr, nullptr, gs.ptr, ovf.ptr, TraceGrid(), 0, stream );
+	std::vector<uint32_t> tmp( words );
+	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	memcpy( occluded, tmp.data(), ((size_t)n + 31) / 32 * 4 );
+}
+
+void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void* hitsOut, int iterations, float* msOut )
+{
+	if (geometryDirty || instancesDirty) UpdateToplevel();
+	if (gstack.count < (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256) gstack.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
+	if (!counters.ptr) counters.resize( 1 );
+	const SceneDev sd = MakeSceneDev();
+	hipEvent_t a, b;
+	CHK_HIP( hipEventCreate( &a ) ); CHK_HIP( hipEventCreate( &b ) );
+	CHK_HIP( hipEventRecord( a, stream ) );
+	for (int i = 0; i < iterations; i++)
+		lh2_launch_trace_closest( &sd, (const float4*)ro, (const float4*)rd, nullptr, (uint32_t)n, (uint4*)hitsOut, gstack.ptr, &counters.ptr->stackOverflow, TraceGrid(), stream );
+	CHK_HIP( hipEventRecord( b, stream ) );
+	CHK_HIP( hipEventSynchronize( b ) );
+	float t = 0;
+	CHK_HIP( hipEventElapsedTime( &t, a, b ) );
+	if (msOut) *msOut = t / std::max( 1, iterations );
+	(void)hipEventDestroy( a ); (void)hipEventDestroy( b );
+}
+
+void RenderCore::GenerateEyeRays( const lh2_ViewPyramid& view, uint32_t R0, int pass, float* ot, float* dt, float* st )
+{
+	const int n = scrwidth * scrheight * scrspp;
+	DevBuf<float4> o, d, t4, q4;
+	o.resize( n ), d.resize( n ), t4.resize( n ), q4.resize( n );
+	CameraParams cp;
+	cp.pos = view.pos, cp.p1 = view.p1;
+	cp.right = { view.p2.x - view.p1.x, view.p2.y - view.p1.y, view.p2.z - view.p1.z };
+	cp.up = { view.p3.x - view.p1.x, view.p3.y - view.p1.y, view.p3.z - view.p1.z };
+	cp.aperture = view.aperture, cp.distortion = view.distortion, cp.geometryEpsilon = geometryEpsilon;
+	cp.w = scrwidth, cp.h = scrheight, cp.pass = pass, cp.R0 = R0;
+	cp.y0 = 0, cp.tileRows = scrheight, cp.band = scrheight, cp.bandStride = scrheight;
+	lh2_launch_camera( &cp, dBlueNoise.ptr, o.ptr, d.ptr, t4.ptr, q4.ptr, n, stream );
+	std::vector<float4> T( n ), Q( n );
+	CHK_HIP( hipMemcpyAsync( ot, o.ptr, sizeof( float4 ) * n, hipMemcpyDeviceToHost, stream ) );
+	CHK_HIP( hipMemcpyAsync( dt, d.ptr, sizeof( float4 ) * n, hipMemcpyDeviceToHost, stream ) );
+	CHK_HIP( hipMemcpyAsync( T.data(), t4.ptr, sizeof( float4 ) * n, hipMemcpyDeviceToHost, stream ) );
+	CHK_HIP( hipMemcpyAsync( Q.data(), q4.ptr, sizeof( float4 ) * n, hipMemcpyDeviceToHost, stream ) );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	for (int i = 0; i < n; i++) memcpy( st + i * 8, &T[i], 16 ), memcpy( st + i * 8 + 4, &Q[i], 16 );
+}
+
+void RenderCore::SceneInfo( int* nodeCount, int* triCount, int* maxDepth, int* instCount )
+{
+	if (geometryDirty || instancesDirty) UpdateToplevel();
+	if (nodeCount) *nodeCount = blasNodeCount;
+	if (triCount) *triCount = blasTriCount;
+	if (maxDepth) *maxDepth = sceneMaxDepth;
+	if (instCount) *instCount = (int)instances.size();
+}
+
+void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
+{
+	if (!initialized) return;
+	(void)hipStreamSynchronize( stream );
+	for (auto* m : meshes) delete m;
+	meshes.clear();
+	instances.clear();
+	for (auto& e : evTrace) (void)hipEventDestroy( e );
+	for (auto& e : evShade) (void)hipEventDestroy( e );
+	for (auto& e : evShadow) (void)hipEventDestroy( e );
+	for (auto& e : evFrame) (void)hipEventDestroy( e );
+	if (hostStats) (void)hipHostFree( hostStats );
+	hostStats = nullptr;
+	(void)hipStreamDestroy( stream );
+	stream = nullptr;
+	initialized = false;
+}
+
+}  // namespace lh2

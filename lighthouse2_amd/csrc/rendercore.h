@@ -1,0 +1,148 @@
+/* rendercore.h - host side of the MI355X render core (counterpart of
+   RenderCore_OptixPrime_B/rendercore.h:48-142; same method names and call contract). */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "../../include/lh2_core_types.h"
+#include "bvh_build.h"
+#include "lh2_kernels.h"
+#include "lh2_device.h"
+
+namespace lh2 {
+
+void FatalError( const char* fmt, ... );
+
+template <class T> struct DevBuf
+{
+	T* ptr = nullptr;
+	size_t count = 0;
+	DevBuf() = default;
+	DevBuf( const DevBuf& ) = delete;
+	DevBuf& operator=( const DevBuf& ) = delete;
+	~DevBuf() { free(); }
+	void free() { if (ptr) (void)hipFree( ptr ); ptr = nullptr; count = 0; }
+	void resize( size_t n )   /* discards contents */
+	{
+		if (n <= count && ptr) return;
+		free();
+		if (n == 0) n = 1;
+		if (hipMalloc( (void**)&ptr, n * sizeof( T ) ) != hipSuccess) FatalError( "hipMalloc of %zu bytes failed", n * sizeof( T ) );
+		count = n;
+	}
+	void upload( const T* src, size_t n, hipStream_t st )
+	{
+		resize( n );
+		if (n) if (hipMemcpyAsync( ptr, src, n * sizeof( T ), hipMemcpyHostToDevice, st ) != hipSuccess) FatalError( "upload failed" );
+	}
+};
+
+struct CoreMeshHost
+{
+	std::vector<lh2_CoreTri> tris;       /* RenderCore always copies what it needs (rendercore.h:57) */
+	BvhOutput bvh;
+	float aabbLo[3], aabbHi[3];
+	DevBuf<float4> shadeTris;            /* CoreTri4[] in original order, for shading */
+	bool dirty = true;
+};
+
+struct CoreInstanceHost { int mesh; float T[16]; float inv[16]; };
+
+struct FrameStats   /* per-frame values read back from the device */
+{
+	uint32_t rayCount[17];
+	Counters counters;
+};
+
+class RenderCore
+{
+public:
+	void Init();
+	void SetProbePos( int x, int y ) { probeX = x, probeY = y; }
+	void SetTarget( uint32_t w, uint32_t h, uint32_t spp );
+	void Setting( const char* name, float value );
+	void Render( const lh2_ViewPyramid& view, int converge );
+	void Shutdown();
+	void SetTextures( const lh2_CoreTexDesc* tex, int textureCount );
+	void SetMaterials( const lh2_CoreMaterial* mat, int materialCount );
+	void SetLights( const lh2_CoreLightTri* areaLights, int areaLightCount, const lh2_CorePointLight* pointLights, int pointLightCount,
+		const lh2_CoreSpotLight* spotLights, int spotLightCount, const lh2_CoreDirectionalLight* directionalLights, int directionalLightCount );
+	void SetSkyData( const float* pixels, uint32_t width, uint32_t height );
+	void SetGeometry( int meshIdx, const float* vertexData, int vertexCount, int triangleCount, const lh2_CoreTri* triangles, const uint32_t* alphaFlags );
+	void SetInstance( int instanceIdx, int meshIdx, const float* matrix16 );
+	void UpdateToplevel();
+	lh2_CoreStats GetCoreStats();
+
+	/* extensions beyond the reference ABI (tile partition, headless output, unit-level kernels) */
+	void SetTile( int y0, int y1 ) { tileY0 = y0, tileY1 = y1, tileBand = 0, tileStride = 0; }
+	/* rank r of n owns the row bands [r*band + k*n*band, +band): balanced multi-GPU partition */
+	void SetTileBands( int rank, int nranks, int band ) { tileY0 = rank * band, tileY1 = -1, tileBand = band, tileStride = nranks * band; }
+	int TileRows() const;
+	void Synchronize();
+	void GetAccumulator( float* hostOut4 );                /* full frame, raw accumulator */
+	void CopyAccumulatorRows( void* devDst, int y0, int y1 ); /* D2D copy of rows [y0,y1) */
+	void PackTile( void* devDst );                         /* owned rows, local order, then sync */
+	void GetFrame( float* hostOut4 );                      /* finalizeRender output: acc / samplesTaken */
+	int SamplesTaken() const { return samplesTaken; }
+	void GetRayCounts( uint32_t* out17 );
+	void TraceClosest( const float* orgTmin4, const float* dirTmax4, int n, uint32_t* hits4 );   /* host in/out */
+	void TraceAny( const float* orgTmin4, const float* dirTmax4, int n, uint32_t* occluded );
+	void TraceClosestDevice( const void* rayO, const void* rayD, int n, void* hits, int iterations, float* msOut );
+	void GenerateEyeRays( const lh2_ViewPyramid& view, uint32_t R0, int pass, float* orgTmin4, float* dirTmax4, float* state8 );
+	void SceneInfo( int* nodeCount, int* triCount, int* maxDepth, int* instCount );
+	float lastKernelMs[8] = {};  /* traceTime of the last frame per bounce (diagnostics) */
+
+	lh2_CoreStats coreStats{};
+	hipStream_t stream = nullptr;
+
+private:
+	void EnsureBuffers();
+	void UploadScene();
+	SceneDev MakeSceneDev() const;
+	int TraceGrid() const { return smCount * blocksPerCU; }
+
+	int device = 0, smCount = 256, blocksPerCU = 5;
+	bool initialized = false;
+	/* scene */
+	std::vector<CoreMeshHost*> meshes;
+	std::vector<CoreInstanceHost> instances;
+	bool geometryDirty = true, instancesDirty = true;
+	DevBuf<float4> dNodes, dTris;
+	DevBuf<uint8_t> dInst;                 /* DevInstance[] */
+	DevBuf<lh2_CoreInstanceDesc> dInstDesc;
+	int tlasRoot = 0, blasNodeCount = 0, blasTriCount = 0, sceneMaxDepth = 0;
+	std::vector<int> meshNodeBase, meshTriBase;
+	DevBuf<uint4> dMaterials;
+	DevBuf<lh2_CoreLightTri> dArea; DevBuf<lh2_CorePointLight> dPoint; DevBuf<lh2_CoreSpotLight> dSpot; DevBuf<lh2_CoreDirectionalLight> dDir;
+	int nArea = 0, nPoint = 0, nSpot = 0, nDir = 0;
+	DevBuf<float> dSky; int skyW = 0, skyH = 0;
+	DevBuf<uint8_t> dBlueNoise;
+	/* settings (rendercore.h DeviceVars; constant-memory defaults: .cuda.cu:38-39) */
+	float geometryEpsilon = 0.0f, clampValue = 10.0f;
+	int maxPathLength = 16;
+	int probeX = 0, probeY = 0;
+	/* target + frame buffers */
+	int scrwidth = 0, scrheight = 0, scrspp = 1;
+	size_t maxPaths = 0;
+	int tileY0 = 0, tileY1 = -1, tileBand = 0, tileStride = 0;
+	DevBuf<float4> rayO[2], rayD[2], T4[2], Q4[2];
+	DevBuf<uint4> hits;
+	DevBuf<float4> shO, shD, shP;
+	DevBuf<uint32_t> shMask;
+	DevBuf<float4> accumulator, frame;
+	DevBuf<int> gstack;
+	DevBuf<Counters> counters;
+	DevBuf<uint32_t> rayLog;
+	FrameStats* hostStats = nullptr;     /* pinned */
+	bool statsPending = false;
+	hipEvent_t evTrace[2 * 17] = {}, evShade[2 * 17] = {}, evShadow[2] = {}, evFrame[2] = {};
+	int framePathLengths = 0;
+	double frameHostMs = 0;
+	int samplesTaken = 0;
+	bool firstConvergingFrame = false;
+	uint32_t camRNGseed = 0x12345678;
+};
+
+}  // namespace lh2

@@ -1,0 +1,414 @@
+"""Synthetic scenes for the benchmark configurations (BASELINE.json `configs`) and a
+headless stand-in for the reference RenderSystem's call sequence.
+
+The reference drives a core through RenderSystem::SynchronizeSceneData (rendersystem.cpp:214-222):
+sky -> textures -> materials -> meshes (SetGeometry) -> instances + UpdateToplevel -> lights, then
+per frame Setting("epsilon"), Setting("clampValue") and Render (rendersystem.cpp:228-238).
+`Scene.load_into` and `Scene.render_frame` replay exactly that order on any object with the
+CoreAPI method names (the MI355X core, or the CPU oracle in tests).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import numpy as np
+
+from . import abi
+
+# ---------------------------------------------------------------------------------------------
+# Marsaglia xorshift32 stream (platform/system.cpp:44-46), vectorised by GF(2) jump-ahead
+# ---------------------------------------------------------------------------------------------
+_MASK = 0xFFFFFFFF
+
+
+def _step(s: int) -> int:
+    s ^= (s << 13) & _MASK
+    s ^= s >> 17
+    s ^= (s << 5) & _MASK
+    return s
+
+
+def _apply(cols: list[int], v: int) -> int:
+    r = 0
+    j = 0
+    while v:
+        if v & 1:
+            r ^= cols[j]
+        v >>= 1
+        j += 1
+    return r
+
+
+_JUMP_CACHE: dict[int, np.ndarray] = {}
+
+
+def _jump_tables(log2b: int) -> np.ndarray:
+    """Byte tables of M^(2^log2b) where M is the xorshift32 step as a GF(2) linear map."""
+    if log2b in _JUMP_CACHE:
+        return _JUMP_CACHE[log2b]
+    cols = [_step(1 << j) for j in range(32)]
+    for _ in range(log2b):
+        cols = [_apply(cols, c) for c in cols]
+    tab = np.zeros((4, 256), np.uint32)
+    for k in range(4):
+        for b in range(256):
+            tab[k, b] = _apply(cols, b << (8 * k))
+    _JUMP_CACHE[log2b] = tab
+    return tab
+
+
+def xorshift_uints(seed: int, n: int, log2b: int = 14) -> np.ndarray:
+    """The first n values of RandomUInt() starting from `seed` (each value is the state after a step)."""
+    B = 1 << log2b
+    out = np.empty(n, np.uint32)
+    s = seed & _MASK
+    first = min(n, B)
+    for i in range(first):
+        s = _step(s)
+        out[i] = s
+    if n <= B:
+        return out
+    tab = _jump_tables(log2b)
+    prev = out[:B].copy()
+    pos = B
+    while pos < n:
+        nxt = tab[0][prev & 255] ^ tab[1][(prev >> 8) & 255] ^ tab[2][(prev >> 16) & 255] ^ tab[3][prev >> 24]
+        m = min(B, n - pos)
+        out[pos:pos + m] = nxt[:m]
+        prev = nxt
+        pos += m
+    return out
+
+
+def xorshift_floats(seed: int, n: int) -> np.ndarray:
+    """RandomFloat() stream: RandomUInt() * 2.3283064365387e-10f in fp32 (platform/system.cpp:46)."""
+    return xorshift_uints(seed, n).astype(np.float32) * np.float32(2.3283064365387e-10)
+
+
+# ---------------------------------------------------------------------------------------------
+# camera -> ViewPyramid (RenderSystem/camera.cpp:38-55 CalculateMatrix, :96-117 GetView)
+# ---------------------------------------------------------------------------------------------
+def _f3(*v) -> np.ndarray:
+    return np.array(v, np.float32)
+
+
+def _norm(v: np.ndarray) -> np.ndarray:
+    return (v * (np.float32(1) / np.sqrt(np.float32(np.dot(v, v))))).astype(np.float32)
+
+
+def camera_view(pos, direction, fov_deg: float = 40.0, aspect: float = 16 / 9, focal: float = 5.0,
+                aperture: float = 0.0, distortion: float = 0.0, pixel_height: int = 1080) -> abi.ViewPyramid:
+    pos = _f3(*pos)
+    z = _norm(_f3(*direction))
+    if abs(float(z[1])) > 0.99:
+        y = _f3(1, 0, 0)
+    else:
+        y = _f3(0, 1, 0)
+    x = _norm(np.cross(z, y).astype(np.float32))
+    y = np.cross(x, z).astype(np.float32)
+    right, up, forward = x, y, z
+    fov = np.float32(fov_deg)
+    pi = np.float32(math.pi)
+    screen = np.float32(math.tan(float(fov) / 2 / (180 / math.pi)))
+    f = np.float32(focal)
+    a = np.float32(aspect)
+    C = pos + f * forward
+    p1 = C - screen * right * f * a + screen * f * up
+    p2 = C + screen * right * f * a + screen * f * up
+    p3 = C - screen * right * f * a - screen * f * up
+    v = abi.ViewPyramid()
+    v.pos = abi.float3(*map(float, pos))
+    v.p1 = abi.float3(*map(float, p1.astype(np.float32)))
+    v.p2 = abi.float3(*map(float, p2.astype(np.float32)))
+    v.p3 = abi.float3(*map(float, p3.astype(np.float32)))
+    v.aperture = float(aperture)
+    v.spreadAngle = float(fov * pi / np.float32(180) / np.float32(pixel_height))
+    v.focalDistance = float(focal)
+    v.distortion = float(distortion)
+    u1 = C - screen * right * a + screen * up
+    u2 = C + screen * right * a + screen * up
+    u3 = C - screen * right * a - screen * up
+    v.imagePlane = float(np.linalg.norm(u1 - u2) * np.linalg.norm(u1 - u3))
+    return v
+
+
+# ---------------------------------------------------------------------------------------------
+# scene container + RenderSystem call order
+# ---------------------------------------------------------------------------------------------
+@dataclasses.dataclass
+class Scene:
+    meshes: list                       # CoreTri arrays (N, 44) float32
+    instances: list                    # (mesh index, 4x4 row-major float32)
+    materials: list                    # abi.CoreMaterial
+    area_lights: list = dataclasses.field(default_factory=list)
+    point_lights: list = dataclasses.field(default_factory=list)
+    spot_lights: list = dataclasses.field(default_factory=list)
+    dir_lights: list = dataclasses.field(default_factory=list)
+    sky: np.ndarray | None = None      # (h, w, 3) float32
+    view: abi.ViewPyramid | None = None
+    name: str = "scene"
+
+    @property
+    def tri_count(self) -> int:
+        return int(sum(len(m) for m in self.meshes))
+
+    def load_into(self, core) -> None:
+        """RenderSystem::SynchronizeSceneData order (rendersystem.cpp:214-222)."""
+        if self.sky is not None:
+            core.set_sky(self.sky)
+        core.set_materials(self.materials)
+        for i, m in enumerate(self.meshes):
+            core.set_geometry(i, m)
+        for i, (mesh, T) in enumerate(self.instances):
+            core.set_instance(i, mesh, T)
+        core.set_instance(len(self.instances), -1, None)
+        core.update_toplevel()
+        core.set_lights(self.area_lights, self.point_lights, self.spot_lights, self.dir_lights)
+
+    def render_frame(self, core, converge: int = 1, view: abi.ViewPyramid | None = None,
+                     epsilon: float = 1e-4, clamp: float = 10.0) -> None:
+        """RenderSystem::Render (rendersystem.cpp:228-238)."""
+        core.setting("epsilon", epsilon)
+        core.setting("clampValue", clamp)
+        core.render(view or self.view, converge)
+
+
+def light_from_tri(tri: np.ndarray, tri_idx: int, inst_idx: int, radiance) -> abi.CoreLightTri:
+    """HostAreaLight constructor + ConvertToCoreLightTri (host_light.cpp:25-62)."""
+    v0 = tri[32:35].astype(np.float32)
+    v1 = tri[36:39].astype(np.float32)
+    v2 = tri[40:43].astype(np.float32)
+    L = abi.CoreLightTri()
+    c = (np.float32(0.333333) * (v0 + v1 + v2)).astype(np.float32)
+    a = np.float32(np.linalg.norm(v1 - v0))
+    b = np.float32(np.linalg.norm(v2 - v1))
+    cc = np.float32(np.linalg.norm(v0 - v2))
+    s = (a + b + cc) * np.float32(0.5)
+    area = np.float32(math.sqrt(max(float(s * (s - a) * (s - b) * (s - cc)), 0.0)))
+    rad = np.array(radiance, np.float32)
+    E = rad * area
+    L.centre = abi.float3(*map(float, c))
+    L.N = abi.float3(float(tri[11]), float(tri[15]), float(tri[19]))
+    L.area = float(area)
+    L.radiance = abi.float3(*map(float, rad))
+    L.energy = float(E[0] + E[1] + E[2])
+    L.vertex0 = abi.float3(*map(float, v0))
+    L.vertex1 = abi.float3(*map(float, v1))
+    L.vertex2 = abi.float3(*map(float, v2))
+    L.triIdx = tri_idx
+    L.instIdx = inst_idx
+    return L
+
+
+def quad_tris(N, pos, width: float, height: float, material: int) -> np.ndarray:
+    """HostScene::AddQuad (host_scene.cpp:346-393): two triangles, explicit normal N."""
+    N = _norm(_f3(*N))
+    pos = _f3(*pos)
+    tmp = _f3(0, 1, 0) if N[0] > 0.9 else _f3(1, 0, 0)
+    T = (np.float32(0.5 * width) * _norm(np.cross(N, tmp).astype(np.float32))).astype(np.float32)
+    B = (np.float32(0.5 * height) * _norm(np.cross(_norm(T), N).astype(np.float32))).astype(np.float32)
+    v = [pos - B - T, pos + B - T, pos - B + T, pos + B - T, pos + B + T, pos - B + T]
+    t = abi.new_tris(2)
+    for k, (a, b, c) in enumerate(((v[0], v[1], v[2]), (v[3], v[4], v[5]))):
+        for key in ("vN0", "vN1", "vN2"):
+            t[k, abi.TRI[key]:abi.TRI[key] + 3] = N
+        t[k, abi.TRI["Nx"]], t[k, abi.TRI["Ny"]], t[k, abi.TRI["Nz"]] = N
+        t[k, 32:35], t[k, 36:39], t[k, 40:43] = a, b, c
+        t.view(np.uint32)[k, abi.TRI["material"]] = material
+        Tt = _norm((b - a).astype(np.float32))
+        t[k, abi.TRI["T"]:abi.TRI["T"] + 3] = Tt
+        t[k, abi.TRI["B"]:abi.TRI["B"] + 3] = _norm(np.cross(N, Tt).astype(np.float32))
+        la, lb, lc = (np.linalg.norm(b - a), np.linalg.norm(c - b), np.linalg.norm(a - c))
+        s = (la + lb + lc) * 0.5
+        t[k, abi.TRI["area"]] = math.sqrt(max(s * (s - la) * (s - lb) * (s - lc), 0))
+    return t
+
+
+# ---------------------------------------------------------------------------------------------
+# config 2: 100k random triangles
+# ---------------------------------------------------------------------------------------------
+def random_triangles(n: int = 100_000, seed: int = 0x12345678, edge: float = 0.5, spread: float = 10.0) -> np.ndarray:
+    r = xorshift_floats(seed, 9 * n).reshape(n, 9)
+    half = np.float32(spread / 2)
+    v0 = r[:, 0:3] * np.float32(spread) - half
+    e = np.float32(edge)
+    v1 = v0 + (r[:, 3:6] - np.float32(0.5)) * e
+    v2 = v0 + (r[:, 6:9] - np.float32(0.5)) * e
+    return abi.tris_from_vertices(v0, v1, v2, 0)
+
+
+def config2_scene(n: int = 100_000, width: int = 1920, height: int = 1080, sky: bool = False,
+                  light: bool = False) -> Scene:
+    """Primary-ray BVH2 config: xorshift32 seed 0x12345678, v0 ~ U[-5,5]^3, edges 0.5, camera (0,0,-12)
+    looking +z, FOV 40, 16:9, aperture 0, distortion 0, focal distance 5; material 0 = white 0.8,
+    roughness 1.  `sky` / `light` add an environment / an area light for parity runs."""
+    tris = random_triangles(n)
+    mats = [abi.make_material((0.8, 0.8, 0.8), roughness=1.0)]
+    sc = Scene(meshes=[tris], instances=[(0, np.eye(4, dtype=np.float32))], materials=mats, name=f"config2-{n}")
+    if light:
+        mats.append(abi.make_material((20.0, 20.0, 18.0)))
+        q = quad_tris((0, -1, 0), (0, 7.5, 0), 6, 6, 1)
+        sc.meshes.append(q)
+        q.view(np.int32)[:, abi.TRI["ltriIdx"]] = [0, 1]
+        sc.instances.append((1, np.eye(4, dtype=np.float32)))
+        sc.area_lights = [light_from_tri(q[i], i, 1, (20.0, 20.0, 18.0)) for i in range(2)]
+    if sky:
+        sc.sky = gradient_sky(64, 32)
+    sc.view = camera_view((0, 0, -12), (0, 0, 1), fov_deg=40, aspect=width / height, focal=5, pixel_height=height)
+    return sc
+
+
+def gradient_sky(w: int = 64, h: int = 32) -> np.ndarray:
+    y = np.linspace(1.0, 0.1, h, dtype=np.float32)[:, None]
+    x = np.linspace(0.0, 1.0, w, dtype=np.float32)[None, :]
+    ones = np.ones((h, w), np.float32)
+    sky = np.stack([(0.4 * y + 0.1 * x) * ones, (0.5 * y + 0.05) * ones, (0.9 * y + 0.05 * (1 - x)) * ones], -1).astype(np.float32)
+    return np.ascontiguousarray(sky)
+
+
+# ---------------------------------------------------------------------------------------------
+# config 3: procedural "Sponza-class" room
+# ---------------------------------------------------------------------------------------------
+def _grid_quads(origin, du, dv, nu: int, nv: int) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    o = np.asarray(origin, np.float32)
+    du = np.asarray(du, np.float32)
+    dv = np.asarray(dv, np.float32)
+    i, j = np.meshgrid(np.arange(nu, dtype=np.float32), np.arange(nv, dtype=np.float32), indexing="ij")
+    i = i.ravel()[:, None]
+    j = j.ravel()[:, None]
+    a = o + (i / nu) * du + (j / nv) * dv
+    b = o + ((i + 1) / nu) * du + (j / nv) * dv
+    c = o + ((i + 1) / nu) * du + ((j + 1) / nv) * dv
+    d = o + (i / nu) * du + ((j + 1) / nv) * dv
+    v0 = np.concatenate([a, a]).astype(np.float32)
+    v1 = np.concatenate([b, c]).astype(np.float32)
+    v2 = np.concatenate([c, d]).astype(np.float32)
+    return v0, v1, v2
+
+
+def _box(lo, hi, nseg: int):
+    lo = np.asarray(lo, np.float32)
+    hi = np.asarray(hi, np.float32)
+    d = hi - lo
+    ex, ey, ez = np.array([d[0], 0, 0], np.float32), np.array([0, d[1], 0], np.float32), np.array([0, 0, d[2]], np.float32)
+    faces = [(lo, ey, ex), (lo + ez, ex, ey), (lo, ez, ey), (lo + ex, ey, ez), (lo, ex, ez), (lo + ey, ez, ex)]
+    parts = [_grid_quads(o, u, v, nseg, nseg) for o, u, v in faces]
+    return tuple(np.concatenate([p[k] for p in parts]) for k in range(3))
+
+
+def room_scene(target_tris: int = 1_000_000, width: int = 1920, height: int = 1080, seed: int = 0x1234,
+               sky: bool = True) -> Scene:
+    """Closed room 40 x 16 x 24 (tessellated walls), 32 columns, seeded clutter, two emissive quads.
+    Materials: 70 % roughness-1 diffuse (NEE), 20 % default roughness 0 (specular chain),
+    10 % glass (transmission 1, eta 1.5); lights radiance 50."""
+    rng = np.random.default_rng(seed)
+    mats = [
+        abi.make_material((0.75, 0.75, 0.72), roughness=1.0),   # 0 floor / ceiling
+        abi.make_material((0.7, 0.35, 0.3), roughness=1.0),     # 1 walls red
+        abi.make_material((0.3, 0.45, 0.7), roughness=1.0),     # 2 walls blue
+        abi.make_material((0.8, 0.8, 0.8)),                     # 3 specular (default roughness 0)
+        abi.make_material((0.95, 0.95, 0.95), transmission=1.0, eta=1.5, absorption=(0.1, 0.05, 0.02)),  # 4 glass
+        abi.make_material((0.6, 0.6, 0.4), roughness=1.0, metallic=0.3, specular=0.5),  # 5 diffuse mixed
+        abi.make_material((50.0, 50.0, 50.0)),                  # 6 light
+    ]
+    # budget: walls 40 %, columns 20 %, clutter 40 %
+    wall_budget = int(target_tris * 0.4)
+    W, H, D = 40.0, 16.0, 24.0
+    area_tot = 2 * (W * H + W * D + H * D)
+    cell = math.sqrt(area_tot * 2 / max(wall_budget, 12))
+    def nseg(x):
+        return max(1, int(round(x / cell)))
+    x0, x1, y0, y1, z0, z1 = -W / 2, W / 2, 0.0, H, -D / 2, D / 2
+    walls = [
+        ((x0, y0, z0), (W, 0, 0), (0, 0, D), nseg(W), nseg(D), 0),      # floor (normal +y)
+        ((x0, y1, z0), (0, 0, D), (W, 0, 0), nseg(D), nseg(W), 0),      # ceiling (normal -y)
+        ((x0, y0, z0), (0, H, 0), (W, 0, 0), nseg(H), nseg(W), 1),      # back wall z0 (normal +z)
+        ((x0, y0, z1), (W, 0, 0), (0, H, 0), nseg(W), nseg(H), 2),      # front wall z1
+        ((x0, y0, z0), (0, 0, D), (0, H, 0), nseg(D), nseg(H), 2),      # left wall x0
+        ((x1, y0, z0), (0, H, 0), (0, 0, D), nseg(H), nseg(D), 1),      # right wall x1
+    ]
+    V0, V1, V2, M = [], [], [], []
+    for o, du, dv, nu, nv, mat in walls:
+        a, b, c = _grid_quads(o, du, dv, nu, nv)
+        V0.append(a), V1.append(b), V2.append(c), M.append(np.full(len(a), mat, np.uint32))
+    # 32 columns: 2 rows of 16 boxes
+    col_budget = int(target_tris * 0.2)
+    ns_col = max(1, int(math.sqrt(col_budget / 32 / 12)))
+    for k in range(32):
+        x = -18 + (k % 16) * 2.4
+        z = -6.0 if k < 16 else 6.0
+        a, b, c = _box((x - 0.4, 0, z - 0.4), (x + 0.4, H, z + 0.4), ns_col)
+        V0.append(a), V1.append(b), V2.append(c)
+        mat = 3 if k % 5 == 0 else 5 if k % 3 == 0 else 0
+        M.append(np.full(len(a), mat, np.uint32))
+    # clutter: random boxes on the floor
+    clutter_budget = target_tris - sum(len(a) for a in V0)
+    ns_cl = 2
+    per_box = 12 * ns_cl * ns_cl
+    nboxes = max(1, clutter_budget // per_box)
+    pos = rng.uniform((-19, 0, -11), (19, 6, 11), size=(nboxes, 3)).astype(np.float32)
+    size = rng.uniform(0.1, 0.6, size=(nboxes, 3)).astype(np.float32)
+    matsel = rng.choice([0, 1, 2, 5, 3, 4], size=nboxes, p=[0.3, 0.15, 0.15, 0.1, 0.2, 0.1])
+    base_a, base_b, base_c = _box((0, 0, 0), (1, 1, 1), ns_cl)
+    a = (base_a[None] * size[:, None] + pos[:, None]).reshape(-1, 3)
+    b = (base_b[None] * size[:, None] + pos[:, None]).reshape(-1, 3)
+    c = (base_c[None] * size[:, None] + pos[:, None]).reshape(-1, 3)
+    V0.append(a.astype(np.float32)), V1.append(b.astype(np.float32)), V2.append(c.astype(np.float32))
+    M.append(np.repeat(matsel.astype(np.uint32), per_box))
+    tris = abi.tris_from_vertices(np.concatenate(V0), np.concatenate(V1), np.concatenate(V2), np.concatenate(M))
+    # two emissive quads just below the ceiling, facing down
+    q1 = quad_tris((0, -1, 0), (-8, H - 0.05, 0), 4, 4, 6)
+    q2 = quad_tris((0, -1, 0), (8, H - 0.05, 0), 4, 4, 6)
+    base = len(tris)
+    lights = np.concatenate([q1, q2])
+    lights.view(np.int32)[:, abi.TRI["ltriIdx"]] = np.arange(4)
+    tris = np.concatenate([tris, lights])
+    area = [light_from_tri(tris[base + i], base + i, 0, (50.0, 50.0, 50.0)) for i in range(4)]
+    sc = Scene(meshes=[tris], instances=[(0, np.eye(4, dtype=np.float32))], materials=mats, area_lights=area,
+               name=f"room-{len(tris)}")
+    if sky:
+        sc.sky = gradient_sky(64, 32)
+    sc.view = camera_view((0, 6, 11), (0, -0.15, -1), fov_deg=60, aspect=width / height, focal=5,
+                          pixel_height=height)
+    return sc
+
+
+# ---------------------------------------------------------------------------------------------
+# config 5: instanced meshes with per-frame transforms
+# ---------------------------------------------------------------------------------------------
+def rotation_y(a: float) -> np.ndarray:
+    """mat4::RotateY (common_types.h:490)."""
+    m = np.eye(4, dtype=np.float32)
+    c, s = np.float32(math.cos(a)), np.float32(math.sin(a))
+    m[0, 0], m[0, 2], m[2, 0], m[2, 2] = c, s, -s, c
+    return m
+
+
+def instanced_scene(meshes: int = 100, tris_per_mesh: int = 100_000, width: int = 1920, height: int = 1080,
+                    grid: int = 10, spacing: float = 12.0) -> Scene:
+    mlist = [random_triangles(tris_per_mesh, seed=0x12345678 + k) for k in range(meshes)]
+    inst = []
+    for k in range(meshes):
+        T = np.eye(4, dtype=np.float32)
+        T[0, 3] = (k % grid - (grid - 1) / 2) * spacing
+        T[2, 3] = (k // grid - (grid - 1) / 2) * spacing
+        inst.append((k, T))
+    mats = [abi.make_material((0.8, 0.8, 0.8), roughness=1.0)]
+    sc = Scene(meshes=mlist, instances=inst, materials=mats, name=f"instanced-{meshes}x{tris_per_mesh}")
+    sc.sky = gradient_sky(64, 32)
+    sc.view = camera_view((0, 60, -80), (0, -0.6, 1), fov_deg=50, aspect=width / height, pixel_height=height)
+    return sc
+
+
+def animate_instances(sc: Scene, frame: int, seed: int = 7) -> None:
+    """Seeded per-frame rotations of every instance (the refit stress of config 5)."""
+    rng = np.random.default_rng(seed + frame)
+    angles = rng.uniform(0, 2 * math.pi, size=len(sc.instances))
+    new = []
+    for (mesh, T), a in zip(sc.instances, angles):
+        R = rotation_y(float(a))
+        M = R.copy()
+        M[:, 3] = T[:, 3]
+        new.append((mesh, M.astype(np.float32)))
+    sc.instances = new

@@ -1,0 +1,169 @@
+"""GPU parity tests: the HIP render core (through the C-ABI) against the CPU oracle.
+
+Bar (BASELINE.md "Parity"): bit-exact primary rays and hit records
+{t, triid, instid, uv16}; identical occlusion bits; identical per-bounce ray counts; accumulator
+relative L2 <= 1e-4 (north_star tolerance; only the float atomic summation order differs)."""
+import numpy as np
+import pytest
+
+from lighthouse2_amd import abi, scene
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+REL_L2_TOL = 1e-4
+
+
+def rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _load_both(core, sc, w, h, spp=1):
+    sc.load_into(core)
+    core.set_target(w, h, spp)
+    o = Oracle()
+    sc.load_into(o)
+    o.set_target(w, h, spp)
+    return o
+
+
+def test_native_library_is_loaded(core):
+    maps = open("/proc/self/maps").read()
+    assert "libRenderCore_MI355X.so" in maps
+    assert core.stats().SMcount >= 1
+
+
+@pytest.mark.parametrize("pass_,spp", [(0, 1), (0, 2), (300, 1)])
+def test_camera_rays_bitexact(core, pass_, spp):
+    w, h = 96, 54
+    sc = scene.config2_scene(n=2000, width=w, height=h)
+    sc.view = scene.camera_view((0.3, 0.2, -12), (0.05, -0.02, 1), fov_deg=50, aspect=w / h, aperture=0.05,
+                                distortion=0.0 if pass_ == 0 else 0.05, pixel_height=h)
+    o = _load_both(core, sc, w, h, spp)
+    o.setting("epsilon", 1e-4)
+    core.setting("epsilon", 1e-4)
+    R0 = 0x9E3779B9
+    go, gd, gs = core.generate_eye_rays(sc.view, R0, pass_)
+    oo, od, os_ = o.generate_eye_rays(sc.view, R0, pass_)
+    assert np.array_equal(go.view(np.uint32), oo.view(np.uint32))
+    assert np.array_equal(gd.view(np.uint32), od.view(np.uint32))
+    assert np.array_equal(gs.view(np.uint32), os_.view(np.uint32))
+
+
+def _random_rays(n, seed, center=(0, 0, 0), radius=14.0, tmin=1e-4):
+    rng = np.random.default_rng(seed)
+    o = rng.normal(size=(n, 3)).astype(np.float32)
+    o = o / np.linalg.norm(o, axis=1, keepdims=True) * np.float32(radius) + np.array(center, np.float32)
+    tgt = rng.uniform(-4, 4, size=(n, 3)).astype(np.float32)
+    d = tgt - o
+    d = (d * (np.float32(1) / np.sqrt((d * d).sum(1, dtype=np.float32)))[:, None]).astype(np.float32)
+    O4 = np.concatenate([o, np.full((n, 1), tmin, np.float32)], 1)
+    D4 = np.concatenate([d, np.full((n, 1), 1e34, np.float32)], 1)
+    return O4, D4
+
+
+def test_trace_closest_bitexact_random_tris(core):
+    w, h = 160, 90
+    sc = scene.config2_scene(n=20000, width=w, height=h)
+    o = _load_both(core, sc, w, h)
+    O4, D4 = _random_rays(50000, 1)
+    hg = core.trace_closest(O4, D4)
+    ho = o.trace_closest(O4, D4)
+    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.3
+    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+
+
+def test_trace_closest_primary_rays_bitexact(core):
+    w, h = 192, 108
+    sc = scene.config2_scene(n=20000, width=w, height=h)
+    o = _load_both(core, sc, w, h)
+    core.setting("epsilon", 1e-4)
+    o.setting("epsilon", 1e-4)
+    O4, D4, _ = o.generate_eye_rays(sc.view, 0, 0)
+    assert np.array_equal(core.trace_closest(O4, D4), o.trace_closest(O4, D4))
+
+
+def test_trace_closest_instanced_transformed(core):
+    sc = scene.instanced_scene(meshes=6, tris_per_mesh=3000, width=64, height=36, grid=3, spacing=12.0)
+    scene.animate_instances(sc, 3)
+    # non-uniform scale + shear on one instance: the ray is transformed without renormalisation
+    T = sc.instances[2][1].copy()
+    T[0, 0] *= 1.7
+    T[1, 0] += 0.3
+    sc.instances[2] = (2, T)
+    o = _load_both(core, sc, 64, 36)
+    O4, D4 = _random_rays(40000, 2, center=(0, 0, 0), radius=40.0)
+    rng = np.random.default_rng(3)
+    tgt = np.concatenate([rng.uniform(-20, 20, (40000, 1)), rng.uniform(-4, 4, (40000, 1)), rng.uniform(-20, 20, (40000, 1))], 1)
+    d = (tgt - O4[:, :3]).astype(np.float32)
+    D4[:, :3] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    hg = core.trace_closest(O4, D4)
+    ho = o.trace_closest(O4, D4)
+    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.05
+    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+
+
+def test_trace_any_matches(core):
+    sc = scene.config2_scene(n=20000, width=64, height=36)
+    o = _load_both(core, sc, 64, 36)
+    O4, D4 = _random_rays(30001, 4, tmin=0.0)
+    rng = np.random.default_rng(5)
+    D4[:, 3] = rng.uniform(1.0, 20.0, len(D4)).astype(np.float32)   # finite tmax, like shadow rays
+    mg = core.trace_any(O4, D4)
+    mo = o.trace_any(O4, D4)
+    assert 0.05 < np.unpackbits(mo.view(np.uint8)).mean() < 0.95
+    assert np.array_equal(mg, mo)
+
+
+@pytest.mark.parametrize("name", ["config2_light", "room"])
+def test_render_frame_parity(core, name):
+    w, h = 160, 90
+    if name == "room":
+        sc = scene.room_scene(30000, w, h)
+    else:
+        sc = scene.config2_scene(n=20000, width=w, height=h, sky=True, light=True)
+    o = _load_both(core, sc, w, h)
+    core.set_probe(w // 2, h // 2)
+    o.set_probe(w // 2, h // 2)
+    sc.render_frame(core)
+    sc.render_frame(o)
+    cg, co = core.ray_counts(), o.ray_counts()
+    assert np.array_equal(cg, co), (cg, co)
+    ag, ao = core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+    assert rel_l2(ag[..., 3], ao[..., 3]) <= 1e-6
+    st, ost = core.stats(), o.stats()
+    assert (st.probedTriid, st.probedInstid) == (ost.probedTriid, ost.probedInstid)
+    assert st.primaryRayCount == co[0] and st.bounce1RayCount == co[1]
+
+
+def test_converging_frames_and_spp(core):
+    w, h = 96, 54
+    sc = scene.room_scene(20000, w, h)
+    o = _load_both(core, sc, w, h, spp=2)
+    for f in range(3):
+        conv = 1 if f == 0 else 0
+        sc.render_frame(core, converge=conv)
+        sc.render_frame(o, converge=conv)
+        assert np.array_equal(core.ray_counts(), o.ray_counts())
+    ag, ao = core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+    assert rel_l2(core.frame()[..., :3], o.frame()[..., :3]) <= REL_L2_TOL
+
+
+def test_tile_partition_invariance(core):
+    """Rendering the frame as row tiles (the multi-GPU partition) gives the untiled result."""
+    w, h = 128, 72
+    sc = scene.room_scene(20000, w, h)
+    sc.load_into(core)
+    core.set_target(w, h, 1)
+    sc.render_frame(core)
+    full = core.accumulator()
+    parts = np.zeros_like(full)
+    for y0, y1 in ((0, 30), (30, 31), (31, 72)):
+        core.set_target(w, h, 1)
+        core.set_tile(y0, y1)
+        sc.render_frame(core)
+        parts[y0:y1] = core.accumulator()[y0:y1]
+    core.set_tile(0, -1)
+    assert rel_l2(parts[..., :3], full[..., :3]) <= 1e-6
