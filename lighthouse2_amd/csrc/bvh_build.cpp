@@ -64,7 +64,7 @@ struct Builder
 			grow( box, prims[p] );
 			for (int k = 0; k < 3; k++) cbox.lo[k] = std::min( cbox.lo[k], cent[p * 3 + k] ), cbox.hi[k] = std::max( cbox.hi[k], cent[p * 3 + k] );
 		}
-		if (count <= 2) { make_leaf( ni, first, count, box ); return; }
+		if (count <= (uint32_t)std::min( 2, maxLeaf )) { make_leaf( ni, first, count, box ); return; }
 		/* binned SAH over the three axes */
 		float bestCost = std::numeric_limits<float>::max();
 		int bestAxis = -1, bestBin = -1;

@@ -324,7 +324,11 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		for (int c = 0; c < 2; c++)
 		{
 			if (refs[c] >= 0) refs[c] += blasNodeCount;
-			else if (!prims.empty()) refs[c] = MAKE_LEAF( (uint32_t)primInst[tlas.perm[LEAF_FIRST( refs[c] )]], 1 );
+			else if (!prims.empty())
+			{
+				if (LEAF_COUNT( refs[c] ) != 1) FatalError( "TLAS leaf with %d instances", LEAF_COUNT( refs[c] ) );
+				refs[c] = MAKE_LEAF( (uint32_t)primInst[tlas.perm[LEAF_FIRST( refs[c] )]], 1 );
+			}
 		}
 	}
 	tlasRoot = blasNodeCount;
