@@ -16,6 +16,7 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	/* tile of the frame owned by this launch: local row lr maps to frame row
 	   y0 + (lr / band) * bandStride + lr % band  (contiguous tile: band = rows) */
 	int y0, band, bandStride, tileRows;
+	int tiled;   /* store rays in 8x8 pixel blocks per wave (coherent traversal); 0 = row-major */
 };
 
 struct SceneDev       /* everything the traversal and shading kernels read, by value (kernarg) */
@@ -49,14 +50,24 @@ struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path st
 	uint32_t R0;
 };
 
+struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (any) out */
+{
+	const float4* rayO; const float4* rayD;
+	const uint32_t* countPtr; uint32_t countFixed;   /* count from device memory, or fixed */
+	uint32_t* cursor;                                 /* zeroed work-queue head (64 rays per fetch) */
+	uint4* hits;                                      /* closest: {t, triid, instid, uv16} */
+	uint32_t* mask;                                   /* any, mode 0: occlusion bits */
+	const float4* potentials; float4* acc;            /* any, mode 1: fused finalizeConnection */
+	int* gstack; uint32_t* overflow;
+};
+
 extern "C" {
 void lh2_launch_init_counters( Counters* c, uint32_t pathCount, hipStream_t st );
 void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, hipStream_t st );
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, hipStream_t st );
-void lh2_launch_trace_closest( const SceneDev* s, const float4* rayO, const float4* rayD, const uint32_t* countPtr, uint32_t countFixed, uint4* hits,
-	int* gstack, uint32_t* overflow, int grid, hipStream_t st );
-void lh2_launch_trace_any( const SceneDev* s, const float4* rayO, const float4* rayD, const uint32_t* countPtr, uint32_t countFixed, uint32_t* mask,
-	const float4* potentials, float4* acc, int* gstack, uint32_t* overflow, int grid, int fused, hipStream_t st );
+void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, hipStream_t st );
+void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, hipStream_t st );
+int lh2_trace_blocks_per_cu( void );
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, hipStream_t st );
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, hipStream_t st );
 void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, hipStream_t st );

@@ -89,7 +89,18 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 	const uint32_t w = (uint32_t)p.w, h = (uint32_t)p.h;
 	const uint32_t tilePix = (uint32_t)p.tileRows * w;
 	const uint32_t s = (uint32_t)slot / tilePix, r = (uint32_t)slot % tilePix;
-	const uint32_t lr = r / w, x = r % w;
+	uint32_t lr = r / w, x = r % w;
+	if (p.tiled && (w & 7u) == 0)
+	{
+		/* storage order only: each wave (64 slots) holds an 8x8 pixel block, so a wave's rays are
+		   coherent; the path index (and therefore every random number) is unchanged */
+		const uint32_t rb = r / (8u * w);
+		if (rb < (uint32_t)p.tileRows / 8u)
+		{
+			const uint32_t q = r - rb * 8u * w, k = q & 63u;
+			x = (q >> 6) * 8u + (k & 7u), lr = rb * 8u + (k >> 3);
+		}
+	}
 	const uint32_t gy = (uint32_t)p.y0 + (lr / (uint32_t)p.band) * (uint32_t)p.bandStride + lr % (uint32_t)p.band;
 	const uint32_t jobIndex = x + (gy + s * h) * w;
 	uint32_t y = jobIndex / w;
@@ -266,64 +277,76 @@ LH2_DEV bool trace_one( const SceneDev& s, const v3 wO, const v3 wD, const float
 	return false;
 }
 
-/* closest hit for a ray stream; count from device (after compaction) or fixed.
-   Output hit record per ray (16 B): {t, triid, instid, uv16}, uv quantised as pathtracer.h:71 */
-__global__ __launch_bounds__( 256 ) void k_trace_closest( const SceneDev s, const float4* __restrict__ rayO, const float4* __restrict__ rayD,
-	const uint32_t* __restrict__ countPtr, const uint32_t countFixed, uint4* __restrict__ hits, int* __restrict__ gstack, uint32_t* overflow )
+/* Closest hit for a ray stream.  Persistent waves pull 64 rays at a time from a device work
+   queue (one atomicAdd per wave), so the grid only needs to cover the resident waves and the
+   cost imbalance between rays never idles a CU.  Hit record per ray (16 B): {t, triid, instid,
+   uv16}, uv quantised exactly as pathtracer.h:71 does. */
+__global__ __launch_bounds__( 256 ) void k_trace_closest( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	const uint32_t count = countPtr ? *countPtr : countFixed;
+	const uint32_t count = a.countPtr ? *a.countPtr : a.countFixed;
 	const uint32_t gstride = gridDim.x * 256u;
-	int* gst = gstack + blockIdx.x * 256 + threadIdx.x;
+	int* gst = a.gstack + blockIdx.x * 256 + threadIdx.x;
 	int* lst = lstack + threadIdx.x;
-	for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < count; idx += gstride)
+	const uint32_t lane = threadIdx.x & 63u;
+	while (true)
 	{
-		const float4 o4 = rayO[idx], d4 = rayD[idx];
-		HitRec h;
-		trace_one<false>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, overflow );
-		uint4 out;
-		if (h.tri < 0) out = make_uint4( fbits( -1.0f ), 0xffffffffu, 0xffffffffu, 0u );
-		else out = make_uint4( fbits( h.t ), (uint32_t)h.tri, (uint32_t)h.inst, lh2_f2u( 65535.0f * h.u ) + (lh2_f2u( 65535.0f * h.v ) << 16) );
-		hits[idx] = out;
+		uint32_t base = 0;
+		if (lane == 0) base = atomicAdd( a.cursor, 64u );
+		base = __builtin_amdgcn_readfirstlane( base );
+		if (base >= count) break;
+		const uint32_t idx = base + lane;
+		if (idx < count)
+		{
+			const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
+			HitRec h;
+			trace_one<false>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, a.overflow );
+			uint4 out;
+			if (h.tri < 0) out = make_uint4( fbits( -1.0f ), 0xffffffffu, 0xffffffffu, 0u );
+			else out = make_uint4( fbits( h.t ), (uint32_t)h.tri, (uint32_t)h.inst, lh2_f2u( 65535.0f * h.u ) + (lh2_f2u( 65535.0f * h.v ) << 16) );
+			a.hits[idx] = out;
+		}
 	}
 }
 
-/* any hit for shadow rays.  MODE 0: write the occlusion bitmask (RTP_BUFFER_FORMAT_HIT_BITMASK,
-   bit set = occluded) and nothing else;  MODE 1: fused finalizeConnection (connections.h:22-34):
+/* Any hit for shadow rays.  MODE 0: occlusion bitmask (RTP_BUFFER_FORMAT_HIT_BITMASK, bit set =
+   occluded), one 64-bit ballot per wave;  MODE 1: fused finalizeConnection (connections.h:22-34):
    unoccluded rays add their potential to the accumulator. */
 template <int MODE>
-__global__ __launch_bounds__( 256 ) void k_trace_any( const SceneDev s, const float4* __restrict__ rayO, const float4* __restrict__ rayD,
-	const uint32_t* __restrict__ countPtr, const uint32_t countFixed, uint32_t* __restrict__ mask, const float4* __restrict__ potentials,
-	float4* __restrict__ acc, int* __restrict__ gstack, uint32_t* overflow )
+__global__ __launch_bounds__( 256 ) void k_trace_any( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	const uint32_t count = countPtr ? *countPtr : countFixed;
+	const uint32_t count = a.countPtr ? *a.countPtr : a.countFixed;
 	const uint32_t gstride = gridDim.x * 256u;
-	int* gst = gstack + blockIdx.x * 256 + threadIdx.x;
+	int* gst = a.gstack + blockIdx.x * 256 + threadIdx.x;
 	int* lst = lstack + threadIdx.x;
-	for (uint32_t base = blockIdx.x * 256u; base < count; base += gstride)
+	const uint32_t lane = threadIdx.x & 63u;
+	while (true)
 	{
-		const uint32_t idx = base + threadIdx.x;
+		uint32_t base = 0;
+		if (lane == 0) base = atomicAdd( a.cursor, 64u );
+		base = __builtin_amdgcn_readfirstlane( base );
+		if (base >= count) break;
+		const uint32_t idx = base + lane;
 		bool occluded = false;
 		if (idx < count)
 		{
-			const float4 o4 = rayO[idx], d4 = rayD[idx];
+			const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
 			HitRec h;
-			occluded = trace_one<true>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, overflow );
+			occluded = trace_one<true>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, a.overflow );
 			if (MODE == 1 && !occluded)
 			{
-				const float4 E = potentials[idx];
-				acc_add( acc, __float_as_uint( E.w ), mk3( E.x, E.y, E.z ) );
+				const float4 E = a.potentials[idx];
+				acc_add( a.acc, __float_as_uint( E.w ), mk3( E.x, E.y, E.z ) );
 			}
 		}
 		if (MODE == 0)
 		{
 			const uint64_t m = __ballot( occluded );
-			if ((threadIdx.x & 63) == 0)
+			if (lane == 0)
 			{
-				const uint32_t word = (base + (threadIdx.x & ~63u)) >> 5;
-				if (((base + (threadIdx.x & ~63u)) < count)) mask[word] = (uint32_t)m;
-				if (((base + (threadIdx.x & ~63u)) + 32u < count)) mask[word + 1] = (uint32_t)(m >> 32);
+				a.mask[base >> 5] = (uint32_t)m;
+				if (base + 32u < count) a.mask[(base >> 5) + 1] = (uint32_t)(m >> 32);
 			}
 		}
 	}
@@ -1121,6 +1144,7 @@ __global__ void k_init_counters( Counters* c, uint32_t pathCount )
 	c->totalExtensionRays = pathCount, c->totalShadowRays = 0;
 	c->probedInstid = -1, c->probedTriid = -1, c->probedDist = 0;
 	c->stackOverflow = 0, c->shadowOverflow = 0;
+	for (int i = 0; i < 32; i++) c->cursor[i] = 0;
 }
 __global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength )
 {
@@ -1159,16 +1183,18 @@ void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, 
 	if (jobCount <= 0) return;
 	k_camera<<<(jobCount + 255) / 256, 256, 0, st>>>( *p, bn, rayO, rayD, T4, Q4, jobCount );
 }
-void lh2_launch_trace_closest( const SceneDev* s, const float4* rayO, const float4* rayD, const uint32_t* countPtr, uint32_t countFixed, uint4* hits,
-	int* gstack, uint32_t* overflow, int grid, hipStream_t st )
+void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, hipStream_t st ) { k_trace_closest<<<grid, 256, 0, st>>>( *s, *a ); }
+void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, hipStream_t st )
 {
-	k_trace_closest<<<grid, 256, 0, st>>>( *s, rayO, rayD, countPtr, countFixed, hits, gstack, overflow );
+	if (fused) k_trace_any<1><<<grid, 256, 0, st>>>( *s, *a );
+	else k_trace_any<0><<<grid, 256, 0, st>>>( *s, *a );
 }
-void lh2_launch_trace_any( const SceneDev* s, const float4* rayO, const float4* rayD, const uint32_t* countPtr, uint32_t countFixed, uint32_t* mask,
-	const float4* potentials, float4* acc, int* gstack, uint32_t* overflow, int grid, int fused, hipStream_t st )
+int lh2_trace_blocks_per_cu( void )
 {
-	if (fused) k_trace_any<1><<<grid, 256, 0, st>>>( *s, rayO, rayD, countPtr, countFixed, mask, potentials, acc, gstack, overflow );
-	else k_trace_any<0><<<grid, 256, 0, st>>>( *s, rayO, rayD, countPtr, countFixed, mask, potentials, acc, gstack, overflow );
+	int n1 = 0, n2 = 0;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest, 256, 0 ) != hipSuccess) n1 = 4;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_any<1>, 256, 0 ) != hipSuccess) n2 = 4;
+	return n1 > n2 ? n1 : n2;
 }
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, hipStream_t st ) { k_shade<<<grid, 256, 0, st>>>( *s, *p ); }
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, hipStream_t st )

@@ -105,12 +105,15 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	dBlueNoise.upload( bn.data(), bn.size(), stream );
 	counters.resize( 1 );
 	rayLog.resize( 32 );
+	blocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocDefault ) );
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evTrace) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evShade) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evShadow) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
+	for (auto& e : evCount) CHK_HIP( hipEventCreateWithFlags( &e, hipEventDisableTiming ) );
+	CHK_HIP( hipHostMalloc( (void**)&activeLog, sizeof( uint32_t ) * 20, hipHostMallocDefault ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
 }
@@ -146,6 +149,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	if (!strcmp( name, "epsilon" )) geometryEpsilon = value;
 	else if (!strcmp( name, "clampValue" )) clampValue = value;
 	else if (!strcmp( name, "maxPathLength" )) maxPathLength = std::min( 16, std::max( 1, (int)value ) );
+	else if (!strcmp( name, "tiledRays" )) tiledRays = value != 0;
 	else if (!strcmp( name, "blocksPerCU" )) { blocksPerCU = std::min( 16, std::max( 1, (int)value ) ); if (scrwidth) EnsureBuffers(); }
 	/* other names ("clampDirect", "filter", "TAA", ...) are ignored, as in the reference */
 }
@@ -407,6 +411,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	cp.R0 = XorShift( camRNGseed );
 	cp.y0 = std::max( 0, tileY0 ), cp.tileRows = tileRows;
 	cp.band = tileBand > 0 ? tileBand : std::max( 1, tileRows ), cp.bandStride = tileBand > 0 ? tileStride : std::max( 1, tileRows );
+	cp.tiled = tiledRays;
 	lh2_launch_camera( &cp, dBlueNoise.ptr, rayO[0].ptr, rayD[0].ptr, T4[0].ptr, Q4[0].ptr, (int)pathCount, stream );
 	int in = 0, pl = 0;
 	const int grid = TraceGrid();
@@ -414,7 +419,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	{
 		pl = pathLength;
 		CHK_HIP( hipEventRecord( evTrace[2 * pathLength], stream ) );
-		lh2_launch_trace_closest( &sd, rayO[in].ptr, rayD[in].ptr, &c->activePaths, 0, hits.ptr, gstack.ptr, &c->stackOverflow, grid, stream );
+		TraceArgs ta{};
+		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.countPtr = &c->activePaths, ta.cursor = &c->cursor[pathLength];
+		ta.hits = hits.ptr, ta.gstack = gstack.ptr, ta.overflow = &c->stackOverflow;
+		lh2_launch_trace_closest( &sd, &ta, grid, stream );
 		CHK_HIP( hipEventRecord( evTrace[2 * pathLength + 1], stream ) );
 		ShadeParams sp;
 		sp.pathCount = &c->activePaths;
@@ -430,11 +438,25 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipEventRecord( evShade[2 * pathLength + 1], stream ) );
 		if (pathLength == maxPathLength) break;
 		lh2_launch_counters_next( c, rayLog.ptr, pathLength, stream );
+		CHK_HIP( hipMemcpyAsync( activeLog + pathLength, &c->activePaths, sizeof( uint32_t ), hipMemcpyDeviceToHost, stream ) );
+		CHK_HIP( hipEventRecord( evCount[pathLength], stream ) );
+		/* early exit without stalling the GPU: wait for the count of the previous bounce while this
+		   bounce is queued; when it was 0, this bounce is empty and so is everything after it */
+		if (pathLength >= 2)
+		{
+			CHK_HIP( hipEventSynchronize( evCount[pathLength - 1] ) );
+			if (activeLog[pathLength - 1] == 0) break;
+		}
 		in = 1 - in;
 	}
 	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
 	CHK_HIP( hipEventRecord( evShadow[0], stream ) );
-	lh2_launch_trace_any( &sd, shO.ptr, shD.ptr, &c->shadowRays, 0, shMask.ptr, shP.ptr, accumulator.ptr, gstack.ptr, &c->stackOverflow, grid, 1, stream );
+	{
+		TraceArgs ta{};
+		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = &c->cursor[20];
+		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr, ta.overflow = &c->stackOverflow;
+		lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
+	}
 	CHK_HIP( hipEventRecord( evShadow[1], stream ) );
 	samplesTaken += scrspp;
 	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, stream );
@@ -533,11 +555,13 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	DevBuf<float4> o, d; DevBuf<uint4> h; DevBuf<int> gs; DevBuf<uint32_t> ovf;
 	o.upload( (const float4*)ot, n, stream ), d.upload( (const float4*)dt, n, stream );
-	h.resize( n ), ovf.resize( 1 );
+	h.resize( n ), ovf.resize( 2 );
 	gs.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
-	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, 4, stream ) );
+	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, 8, stream ) );
 	const SceneDev sd = MakeSceneDev();
-	lh2_launch_trace_closest( &sd, o.ptr, d.ptr, nullptr, (uint32_t)n, h.ptr, gs.ptr, ovf.ptr, TraceGrid(), stream );
+	TraceArgs ta{};
+	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr + 1, ta.hits = h.ptr, ta.gstack = gs.ptr, ta.overflow = ovf.ptr;
+	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	uint32_t of = 0;
 	CHK_HIP( hipMemcpyAsync( &of, ovf.ptr, 4, hipMemcpyDeviceToHost, stream ) );
@@ -551,12 +575,14 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	DevBuf<float4> o, d; DevBuf<uint32_t> m; DevBuf<int> gs; DevBuf<uint32_t> ovf;
 	o.upload( (const float4*)ot, n, stream ), d.upload( (const float4*)dt, n, stream );
 	const size_t words = ((size_t)n + 63) / 64 * 2;
-	m.resize( words ), ovf.resize( 1 );
+	m.resize( words ), ovf.resize( 2 );
 	gs.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
-	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, 4, stream ) );
+	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, 8, stream ) );
 	CHK_HIP( hipMemsetAsync( m.ptr, 0, words * 4, stream ) );
 	const SceneDev sd = MakeSceneDev();
-	lh2_launch_trace_any( &sd, o.ptr, d.ptr, nullptr, (uint32_t)n, m.ptr, nullptr, nullptr, gs.ptr, ovf.ptr, TraceGrid(), 0, stream );
+	TraceArgs ta{};
+	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr + 1, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.overflow = ovf.ptr;
+	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, stream );
 	std::vector<uint32_t> tmp( words );
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -569,11 +595,19 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 	if (gstack.count < (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256) gstack.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
 	if (!counters.ptr) counters.resize( 1 );
 	const SceneDev sd = MakeSceneDev();
+	DevBuf<uint32_t> cursors;
+	cursors.resize( (size_t)std::max( 1, iterations ) + 1 );
+	CHK_HIP( hipMemsetAsync( cursors.ptr, 0, sizeof( uint32_t ) * ((size_t)std::max( 1, iterations ) + 1), stream ) );
 	hipEvent_t a, b;
 	CHK_HIP( hipEventCreate( &a ) ); CHK_HIP( hipEventCreate( &b ) );
 	CHK_HIP( hipEventRecord( a, stream ) );
 	for (int i = 0; i < iterations; i++)
-		lh2_launch_trace_closest( &sd, (const float4*)ro, (const float4*)rd, nullptr, (uint32_t)n, (uint4*)hitsOut, gstack.ptr, &counters.ptr->stackOverflow, TraceGrid(), stream );
+	{
+		TraceArgs ta{};
+		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.cursor = cursors.ptr + i;
+		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr, ta.overflow = cursors.ptr + iterations;
+		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
+	}
 	CHK_HIP( hipEventRecord( b, stream ) );
 	CHK_HIP( hipEventSynchronize( b ) );
 	float t = 0;
@@ -593,7 +627,7 @@ void RenderCore::GenerateEyeRays( const lh2_ViewPyramid& view, uint32_t R0, int 
 	cp.up = { view.p3.x - view.p1.x, view.p3.y - view.p1.y, view.p3.z - view.p1.z };
 	cp.aperture = view.aperture, cp.distortion = view.distortion, cp.geometryEpsilon = geometryEpsilon;
 	cp.w = scrwidth, cp.h = scrheight, cp.pass = pass, cp.R0 = R0;
-	cp.y0 = 0, cp.tileRows = scrheight, cp.band = scrheight, cp.bandStride = scrheight;
+	cp.y0 = 0, cp.tileRows = scrheight, cp.band = scrheight, cp.bandStride = scrheight, cp.tiled = 0;
 	lh2_launch_camera( &cp, dBlueNoise.ptr, o.ptr, d.ptr, t4.ptr, q4.ptr, n, stream );
 	std::vector<float4> T( n ), Q( n );
 	CHK_HIP( hipMemcpyAsync( ot, o.ptr, sizeof( float4 ) * n, hipMemcpyDeviceToHost, stream ) );
@@ -624,6 +658,9 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto& e : evShade) (void)hipEventDestroy( e );
 	for (auto& e : evShadow) (void)hipEventDestroy( e );
 	for (auto& e : evFrame) (void)hipEventDestroy( e );
+	for (auto& e : evCount) (void)hipEventDestroy( e );
+	if (activeLog) (void)hipHostFree( activeLog );
+	activeLog = nullptr;
 	if (hostStats) (void)hipHostFree( hostStats );
 	hostStats = nullptr;
 	(void)hipStreamDestroy( stream );

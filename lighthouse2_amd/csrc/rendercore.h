@@ -138,6 +138,9 @@ private:
 	FrameStats* hostStats = nullptr;     /* pinned */
 	bool statsPending = false;
 	hipEvent_t evTrace[2 * 17] = {}, evShade[2 * 17] = {}, evShadow[2] = {}, evFrame[2] = {};
+	hipEvent_t evCount[18] = {};
+	uint32_t* activeLog = nullptr;     /* pinned: active paths after each bounce */
+	int tiledRays = 1;
 	int framePathLengths = 0;
 	double frameHostMs = 0;
 	int samplesTaken = 0;

@@ -51,7 +51,7 @@ def lib() -> C.CDLL:
             "orc_set_lights": [_P, _P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int],
             "orc_set_sky": [_P, _F, C.c_int, C.c_int], "orc_setting": [_P, C.c_char_p, C.c_float],
             "orc_set_target": [_P, C.c_int, C.c_int, C.c_int], "orc_set_probe": [_P, C.c_int, C.c_int],
-            "orc_set_tile": [_P, C.c_int, C.c_int],
+            "orc_set_tile": [_P, C.c_int, C.c_int], "orc_set_tile_bands": [_P, C.c_int, C.c_int, C.c_int],
             "orc_render": [_P, C.POINTER(abi.ViewPyramid), C.c_int, C.c_int], "orc_get_accumulator": [_P, _F],
             "orc_get_stats": [_P, C.POINTER(OracleStats)],
             "orc_generate_eye_rays": [_P, C.POINTER(abi.ViewPyramid), C.c_uint32, C.c_int, _F, _F, _F],
@@ -121,6 +121,9 @@ class Oracle:
 
     def set_tile(self, y0, y1):
         self.L.orc_set_tile(self.o, y0, y1)
+
+    def set_tile_bands(self, rank, nranks, band):
+        self.L.orc_set_tile_bands(self.o, rank, nranks, band)
 
     def set_materials(self, mats):
         self._mats = abi.material_array(mats)

@@ -122,6 +122,7 @@ struct Oracle
 	uint32_t camRNGseed;
 	int probeX, probeY;
 	int tileY0, tileY1;
+	int bandRank, bandCount, band;   /* band partition (0 bands = contiguous tile) */
 	OracleStats stats;
 };
 
@@ -1459,6 +1460,7 @@ static void* render_worker( void* arg )
 	const int np = o->w * o->h;
 	for (int s = 0; s < o->spp; s++) for (int px = j->px0; px < j->px1; px++)
 	{
+		if (o->band > 0 && ((px / o->w) / o->band) % o->bandCount != o->bandRank) continue;
 		const int jobIndex = px + s * np;
 		PathSeg cur, nxt;
 		eye_ray( o, j->view, j->camR0, j->pass, jobIndex, &cur );
@@ -1584,7 +1586,8 @@ float orc_bluenoise( const Oracle* o, int x, int y, int si, int dim ) { return b
 uint32_t orc_pack_normal( float x, float y, float z ) { return PackNormal( mk3( x, y, z ) ); }
 void orc_unpack_normal( uint32_t p, float* out ) { const f3 n = UnpackNormal( p ); out[0] = n.x, out[1] = n.y, out[2] = n.z; }
 
-void orc_set_tile( Oracle* o, int y0, int y1 ) { o->tileY0 = y0, o->tileY1 = y1; }
+void orc_set_tile( Oracle* o, int y0, int y1 ) { o->tileY0 = y0, o->tileY1 = y1, o->band = 0; }
+void orc_set_tile_bands( Oracle* o, int rank, int nranks, int band ) { o->tileY0 = 0, o->tileY1 = -1, o->bandRank = rank, o->bandCount = nranks, o->band = band; }
 
 /* elementary-function evaluation for tests/test_detmath.py */
 void orc_detmath_eval( int fn, const float* x, const float* y, int n, float* out )

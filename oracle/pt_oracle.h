@@ -45,6 +45,7 @@ void orc_setting( Oracle* o, const char* name, float value );
 void orc_set_target( Oracle* o, int w, int h, int spp );
 void orc_set_probe( Oracle* o, int x, int y );
 void orc_set_tile( Oracle* o, int y0, int y1 );   /* render rows [y0, y1) only (-1 = all) */
+void orc_set_tile_bands( Oracle* o, int rank, int nranks, int band );   /* rows in bands, round-robin */
 void orc_render( Oracle* o, const lh2_ViewPyramid* view, int converge, int nthreads );
 void orc_get_accumulator( const Oracle* o, float* out4 );     /* w*h float4, raw */
 int  orc_samples_taken( const Oracle* o );

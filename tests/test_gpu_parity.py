@@ -167,3 +167,31 @@ def test_tile_partition_invariance(core):
         parts[y0:y1] = core.accumulator()[y0:y1]
     core.set_tile(0, -1)
     assert rel_l2(parts[..., :3], full[..., :3]) <= 1e-6
+
+
+def test_band_partition_matches_full_frame(core):
+    """The N-GPU partition (8-row bands round-robin, packed by lh2_core_pack_tile) rendered rank by rank
+    on one GPU and reassembled equals the untiled frame."""
+    import torch
+    from lighthouse2_amd import parallel
+    w, h, world = 96, 60, 3
+    sc = scene.room_scene(20000, w, h)
+    sc.load_into(core)
+    core.set_target(w, h, 1)
+    core.set_tile(0, -1)
+    sc.render_frame(core)
+    full = core.accumulator()
+    tiles = []
+    for r in range(world):
+        core.set_target(w, h, 1)
+        core.set_tile_bands(r, world, parallel.BAND)
+        sc.render_frame(core)
+        rows = core.tile_rows()
+        assert rows == len(parallel.band_rows(r, world, h))
+        t = torch.empty((rows, w, 4), dtype=torch.float32, device="cuda")
+        core.pack_tile(t.data_ptr())
+        tiles.append(t.cpu().numpy())
+    core.set_tile(0, -1)
+    frame = parallel.assemble(tiles, world, h)
+    assert rel_l2(frame[..., :3], full[..., :3]) <= 1e-6
+    assert np.array_equal(frame[..., 3], full[..., 3])

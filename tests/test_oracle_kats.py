@@ -1,0 +1,130 @@
+"""Known-answer tests of the oracle's building blocks against independent Python/numpy restatements
+of the reference formulas (tools_shared.h, platform/system.cpp, common_types.h, half.hpp)."""
+import math
+
+import numpy as np
+import pytest
+
+from lighthouse2_amd import scene
+from oracle import oracle as orc
+
+
+def wanghash(s):
+    s &= 0xFFFFFFFF
+    s = (s ^ 61) ^ (s >> 16)
+    s = (s * 9) & 0xFFFFFFFF
+    s = s ^ (s >> 4)
+    s = (s * 0x27D4EB2D) & 0xFFFFFFFF
+    return s ^ (s >> 15)
+
+
+def test_wanghash_and_xorshift():
+    L = orc.lib()
+    rng = np.random.default_rng(0)
+    for s in list(rng.integers(0, 2**32, 200)) + [0, 1, 0xFFFFFFFF, 0x12345678]:
+        s = int(s)
+        assert L.orc_wanghash(s) == wanghash(s)
+        x = s
+        x ^= (x << 13) & 0xFFFFFFFF
+        x ^= x >> 17
+        x ^= (x << 5) & 0xFFFFFFFF
+        assert L.orc_xorshift(s) == x
+
+
+def test_xorshift_stream_jump_ahead():
+    """The vectorised generator used by the scene builder equals the sequential recurrence."""
+    u = scene.xorshift_uints(0x12345678, 40000, log2b=10)
+    s, ref = 0x12345678, []
+    for _ in range(40000):
+        s ^= (s << 13) & 0xFFFFFFFF
+        s ^= s >> 17
+        s ^= (s << 5) & 0xFFFFFFFF
+        ref.append(s)
+    assert np.array_equal(u, np.array(ref, np.uint32))
+
+
+def test_bluenoise_sampler_matches_table_formula():
+    """blueNoiseSampler (tools_shared.h:336-350) evaluated on the raw tables."""
+    o = orc.Oracle(threads=1)
+    bn = np.concatenate([o._bn.astype(np.int64), np.zeros(256, np.int64)])
+    rng = np.random.default_rng(1)
+    for _ in range(500):
+        x, y, si, dim = (int(v) for v in rng.integers(0, [300, 300, 600, 80]))
+        xx, yy, ss, dd = x & 127, y & 127, si & 255, dim & 255
+        ranked = (ss ^ bn[dd + (xx + yy * 128) * 8 + 65536 * 3]) & 255
+        value = bn[dd + ranked * 256] ^ bn[(dd & 7) + (xx + yy * 128) * 8 + 65536]
+        ref = np.float32(np.float32(0.5) + np.float32(value)) * np.float32(1 / 256)
+        assert o.L.orc_bluenoise(o.o, x, y, si, dim) == ref
+
+
+def test_pack_unpack_normal_roundtrip():
+    L = orc.lib()
+    rng = np.random.default_rng(2)
+    v = rng.normal(size=(300, 3))
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    v = v[v[:, 2] > -0.95]
+    out = np.zeros(3, np.float32)
+    for n in v.astype(np.float32):
+        p = L.orc_pack_normal(*map(float, n))
+        L.orc_unpack_normal(p, orc._fp(out))
+        assert np.allclose(out, n, atol=2e-3), (n, out)
+
+
+def test_mat4_inverse_matches_numpy():
+    L = orc.lib()
+    rng = np.random.default_rng(3)
+    for _ in range(50):
+        M = np.eye(4, dtype=np.float32)
+        M[:3, :3] = rng.normal(size=(3, 3)).astype(np.float32) + 2 * np.eye(3, dtype=np.float32)
+        M[:3, 3] = rng.normal(size=3)
+        out = np.zeros(16, np.float32)
+        L.orc_mat4_inverse(orc._fp(M.ravel().copy()), orc._fp(out))
+        assert np.allclose(out.reshape(4, 4), np.linalg.inv(M.astype(np.float64)), rtol=1e-4, atol=1e-5)
+    I = np.eye(4, dtype=np.float32).ravel().copy()
+    out = np.zeros(16, np.float32)
+    L.orc_mat4_inverse(orc._fp(I), orc._fp(out))
+    assert np.array_equal(out, I)     # exact identity: the single-instance fast path relies on it
+
+
+@pytest.mark.parametrize("fn,lo,hi,ref,tol", [
+    (0, -7.0, 7.0, np.sin, 3e-7), (1, -7.0, 7.0, np.cos, 3e-7), (2, -80.0, 80.0, np.exp, 4e-7),
+    (3, 1e-30, 1e30, np.log, 2e-7), (6, -1.0, 1.0, np.arccos, 4e-7)])
+def test_detmath_accuracy(fn, lo, hi, ref, tol):
+    rng = np.random.default_rng(fn)
+    if fn == 3:
+        x = np.exp(rng.uniform(np.log(lo), np.log(hi), 20000)).astype(np.float32)
+    else:
+        x = rng.uniform(lo, hi, 20000).astype(np.float32)
+    got = orc.detmath(fn, x).astype(np.float64)
+    want = ref(x.astype(np.float64))
+    scale = np.maximum(np.abs(want), 1.0 if fn in (0, 1, 6) else 1e-30)
+    assert np.max(np.abs(got - want) / scale) < tol * 4
+
+
+def test_detmath_pow_atan2():
+    rng = np.random.default_rng(7)
+    x = rng.uniform(1e-6, 1.0, 20000).astype(np.float32)
+    y = rng.uniform(0.0, 1.0, 20000).astype(np.float32)
+    assert np.max(np.abs(orc.detmath(4, x, y) - np.power(x.astype(np.float64), y)) / np.power(x.astype(np.float64), y)) < 4e-6
+    a = rng.normal(size=20000).astype(np.float32)
+    b = rng.normal(size=20000).astype(np.float32)
+    assert np.max(np.abs(orc.detmath(5, a, b) - np.arctan2(a.astype(np.float64), b))) < 1e-6
+    # quadrant edge cases
+    for (yy, xx) in [(0.0, 1.0), (1.0, 0.0), (-1.0, 0.0), (0.0, -1.0), (0.0, 0.0), (-1e-30, -1.0)]:
+        v = orc.detmath(5, np.array([yy], np.float32), np.array([xx], np.float32))[0]
+        assert abs(v - math.atan2(yy, xx)) < 1e-6 or (yy == 0 and xx == 0)
+
+
+def test_half_conversion_matches_numpy():
+    rng = np.random.default_rng(8)
+    x = np.concatenate([rng.normal(scale=s, size=5000) for s in (1e-6, 1e-3, 1, 100, 3e4)]).astype(np.float32)
+    x = np.concatenate([x, np.float32([0, -0.0, 65504, 65519, 65520, 1e10, 5.96e-8, 2.98e-8, 2.99e-8])])
+    got = orc.detmath(7, x)
+    want = x.astype(np.float16).astype(np.float32)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_saturating_float_to_uint():
+    x = np.float32([-1.0, 0.0, 0.5, 1.5, 4294967040.0, 4294967296.0, 1e20, np.nan])
+    got = orc.detmath(8, x)
+    assert list(got) == [0.0, 0.0, 0.0, 1.0, 4294967040.0, 4294967295.0, 4294967295.0, 0.0]

@@ -1,0 +1,85 @@
+"""Microbenchmark of the closest-hit traversal kernel (k_trace_closest) on the config-2 scene.
+
+Ray sets: the 1080p primary rays, and diffuse 'bounce' rays (cosine-weighted around the face normal
+of each primary hit, origin offset by 1e-4 along the normal), i.e. what the first shade pass emits.
+Used for kernel tuning and as the target process of the rocprofv3 --pmc passes.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import pathlib
+import sys
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402
+
+from lighthouse2_amd import abi, scene  # noqa: E402
+from lighthouse2_amd.core import RenderCore  # noqa: E402
+
+
+def bounce_rays(tris, O4, D4, hits, seed=1):
+    hit = hits[:, 1] != 0xFFFFFFFF
+    idx = np.nonzero(hit)[0]
+    tri = hits[idx, 1].astype(np.int64)
+    t = hits[idx, 0].view(np.float32)
+    P = O4[idx, :3] + t[:, None] * D4[idx, :3]
+    N = np.stack([tris[tri, abi.TRI["Nx"]], tris[tri, abi.TRI["Ny"]], tris[tri, abi.TRI["Nz"]]], 1)
+    N = np.where(((N * D4[idx, :3]).sum(1) > 0)[:, None], -N, N)
+    rng = np.random.default_rng(seed)
+    r0, r1 = rng.random(len(idx)), rng.random(len(idx))
+    phi = 2 * np.pi * r0
+    local = np.stack([np.cos(phi) * np.sqrt(1 - r1), np.sin(phi) * np.sqrt(1 - r1), np.sqrt(r1)], 1)
+    a = np.where(np.abs(N[:, 0:1]) > 0.9, np.array([[0, 1, 0]]), np.array([[1, 0, 0]]))
+    T = np.cross(N, a)
+    T /= np.linalg.norm(T, axis=1, keepdims=True)
+    B = np.cross(N, T)
+    d = local[:, 0:1] * T + local[:, 1:2] * B + local[:, 2:3] * N
+    o = P + 1e-4 * N
+    O = np.concatenate([o, np.zeros((len(o), 1))], 1).astype(np.float32)
+    D = np.concatenate([d, np.full((len(d), 1), 1e34)], 1).astype(np.float32)
+    return O, D
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tris", type=int, default=100_000)
+    ap.add_argument("--set", default="both")
+    ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    sc = scene.config2_scene(n=args.tris)
+    core = RenderCore(device=0)
+    sc.load_into(core)
+    core.set_target(1920, 1080, 1)
+    core.setting("epsilon", 1e-4)
+    for s in args.setting:
+        k, v = s.split("=")
+        core.setting(k, float(v))
+    O4, D4, _ = core.generate_eye_rays(sc.view, 0, 0)
+    sets = {"primary": (O4, D4)}
+    if args.set in ("both", "bounce"):
+        hits = core.trace_closest(O4, D4)
+        sets["bounce"] = bounce_rays(sc.meshes[0], O4, D4, hits)
+    res = {}
+    for name, (o, d) in sets.items():
+        if args.set not in ("both", name):
+            continue
+        n = len(o)
+        ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
+        h = torch.empty((n, 4), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, h.data_ptr(), 2)
+        ms = core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, h.data_ptr(), args.iters)
+        res[name] = {"rays": n, "ms": round(ms, 4), "Mrays_s": round(n / ms / 1e3, 1)}
+    print(json.dumps(res))
+    core.close()
+
+
+if __name__ == "__main__":
+    main()
