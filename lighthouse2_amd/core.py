@@ -29,7 +29,11 @@ class CoreError(RuntimeError):
 
 
 def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
-    """Load the render core (fails loudly when the HIP library has not been built)."""
+    """Load the render core (fails loudly when the HIP library has not been built).
+
+    When the process also uses PyTorch (bench.py, the distributed gather), import torch FIRST: its
+    bundled libamdhip64.so carries the soname libamdhip64.so.7, which this library then binds to,
+    so device pointers are shared by one HIP runtime."""
     global _LIB
     if _LIB is not None and path is None:
         return _LIB

@@ -206,8 +206,11 @@ LH2_DEV bool trace_one( const SceneDev& s, const v3 wO, const v3 wD, const float
 	best.t = tmax, best.tri = -1, best.inst = -1, best.u = 0, best.v = 0;
 	int sp = 0, blasSp = -1, curInst = -1;
 	int cur = s.tlasRoot;
+	uint32_t steps = 0;
 	while (true)
 	{
+		/* watchdog: a malformed tree must not hang the GPU; flag it and give up on this ray */
+		if (++steps > (1u << 22)) { atomicOr( overflow, 2u ); break; }
 		if (cur >= 0)
 		{
 			const float4* n = s.nodes + (size_t)cur * 4;
@@ -278,7 +281,7 @@ LH2_DEV bool trace_one( const SceneDev& s, const v3 wO, const v3 wD, const float
 }
 
 /* Closest hit for a ray stream.  Persistent waves pull 64 rays at a time from a device work
-   queue (one atomicAdd per wave), so the grid only needs to cover the resident waves and the
+   queue (one merged atomicAdd per wave), so the grid only needs to cover the resident waves and the
    cost imbalance between rays never idles a CU.  Hit record per ray (16 B): {t, triid, instid,
    uv16}, uv quantised exactly as pathtracer.h:71 does. */
 __global__ __launch_bounds__( 256 ) void k_trace_closest( const SceneDev s, const TraceArgs a )
@@ -288,29 +291,24 @@ __global__ __launch_bounds__( 256 ) void k_trace_closest( const SceneDev s, cons
 	const uint32_t gstride = gridDim.x * 256u;
 	int* gst = a.gstack + blockIdx.x * 256 + threadIdx.x;
 	int* lst = lstack + threadIdx.x;
-	const uint32_t lane = threadIdx.x & 63u;
 	while (true)
 	{
-		uint32_t base = 0;
-		if (lane == 0) base = atomicAdd( a.cursor, 64u );
-		base = __builtin_amdgcn_readfirstlane( base );
-		if (base >= count) break;
-		const uint32_t idx = base + lane;
-		if (idx < count)
-		{
-			const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
-			HitRec h;
-			trace_one<false>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, a.overflow );
-			uint4 out;
-			if (h.tri < 0) out = make_uint4( fbits( -1.0f ), 0xffffffffu, 0xffffffffu, 0u );
-			else out = make_uint4( fbits( h.t ), (uint32_t)h.tri, (uint32_t)h.inst, lh2_f2u( 65535.0f * h.u ) + (lh2_f2u( 65535.0f * h.v ) << 16) );
-			a.hits[idx] = out;
-		}
+		/* per-lane fetch; the compiler merges the active lanes' adds into one atomic per wave and
+		   hands out consecutive indices in lane order, so a wave keeps 64 neighbouring rays */
+		const uint32_t idx = atomicAdd( a.cursor, 1u );
+		if (idx >= count) break;
+		const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
+		HitRec h;
+		trace_one<false>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, a.overflow );
+		uint4 out;
+		if (h.tri < 0) out = make_uint4( fbits( -1.0f ), 0xffffffffu, 0xffffffffu, 0u );
+		else out = make_uint4( fbits( h.t ), (uint32_t)h.tri, (uint32_t)h.inst, lh2_f2u( 65535.0f * h.u ) + (lh2_f2u( 65535.0f * h.v ) << 16) );
+		a.hits[idx] = out;
 	}
 }
 
 /* Any hit for shadow rays.  MODE 0: occlusion bitmask (RTP_BUFFER_FORMAT_HIT_BITMASK, bit set =
-   occluded), one 64-bit ballot per wave;  MODE 1: fused finalizeConnection (connections.h:22-34):
+   occluded);  MODE 1: fused finalizeConnection (connections.h:22-34):
    unoccluded rays add their potential to the accumulator. */
 template <int MODE>
 __global__ __launch_bounds__( 256 ) void k_trace_any( const SceneDev s, const TraceArgs a )
@@ -320,35 +318,19 @@ __global__ __launch_bounds__( 256 ) void k_trace_any( const SceneDev s, const Tr
 	const uint32_t gstride = gridDim.x * 256u;
 	int* gst = a.gstack + blockIdx.x * 256 + threadIdx.x;
 	int* lst = lstack + threadIdx.x;
-	const uint32_t lane = threadIdx.x & 63u;
 	while (true)
 	{
-		uint32_t base = 0;
-		if (lane == 0) base = atomicAdd( a.cursor, 64u );
-		base = __builtin_amdgcn_readfirstlane( base );
-		if (base >= count) break;
-		const uint32_t idx = base + lane;
-		bool occluded = false;
-		if (idx < count)
+		const uint32_t idx = atomicAdd( a.cursor, 1u );
+		if (idx >= count) break;
+		const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
+		HitRec h;
+		const bool occluded = trace_one<true>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, a.overflow );
+		if (MODE == 1 && !occluded)
 		{
-			const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
-			HitRec h;
-			occluded = trace_one<true>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, a.overflow );
-			if (MODE == 1 && !occluded)
-			{
-				const float4 E = a.potentials[idx];
-				acc_add( a.acc, __float_as_uint( E.w ), mk3( E.x, E.y, E.z ) );
-			}
+			const float4 E = a.potentials[idx];
+			acc_add( a.acc, __float_as_uint( E.w ), mk3( E.x, E.y, E.z ) );
 		}
-		if (MODE == 0)
-		{
-			const uint64_t m = __ballot( occluded );
-			if (lane == 0)
-			{
-				a.mask[base >> 5] = (uint32_t)m;
-				if (base + 32u < count) a.mask[(base >> 5) + 1] = (uint32_t)(m >> 32);
-			}
-		}
+		if (MODE == 0 && occluded) atomicOr( a.mask + (idx >> 5), 1u << (idx & 31u) );   /* mask zeroed by the caller */
 	}
 }
 

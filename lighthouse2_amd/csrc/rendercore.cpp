@@ -488,6 +488,7 @@ void RenderCore::Synchronize()
 	{
 		statsPending = false;
 		const Counters& cnt = hostStats->counters;
+		if (cnt.stackOverflow & 2u) FatalError( "traversal step limit exceeded (corrupt BVH)" );
 		if (cnt.stackOverflow) FatalError( "traversal stack overflow (BVH deeper than %d)", LH2_STACK_TOTAL );
 		if (cnt.shadowOverflow) FatalError( "shadow ray buffer overflow" );
 		uint32_t* rc = hostStats->rayCount;   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
@@ -566,6 +567,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	uint32_t of = 0;
 	CHK_HIP( hipMemcpyAsync( &of, ovf.ptr, 4, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
+	if (of & 2u) FatalError( "traversal step limit exceeded (corrupt BVH)" );
 	if (of) FatalError( "traversal stack overflow" );
 }
 

@@ -4,6 +4,11 @@ import sys
 
 import pytest
 
+try:  # torch first: the render core then binds to the same HIP runtime (one libamdhip64.so.7)
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    torch = None
+
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 if str(ROOT) not in sys.path:
     sys.path.insert(0, str(ROOT))
