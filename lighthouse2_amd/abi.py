@@ -105,9 +105,11 @@ def new_tris(n: int) -> np.ndarray:
     return t
 
 
-def tris_from_vertices(v0: np.ndarray, v1: np.ndarray, v2: np.ndarray, material: np.ndarray | int) -> np.ndarray:
+def tris_from_vertices(v0: np.ndarray, v1: np.ndarray, v2: np.ndarray, material: np.ndarray | int,
+                       vertex_normals: tuple[np.ndarray, np.ndarray, np.ndarray] | None = None) -> np.ndarray:
     """CoreTri records the way HostScene::AddTriToMesh builds them (host_scene.cpp:208-223):
-    flat normal N = normalize(cross(v1 - v0, v2 - v0)) for the face and all three vertices."""
+    flat normal N = normalize(cross(v1 - v0, v2 - v0)) for the face and, unless `vertex_normals`
+    (vN0, vN1, vN2 as HostMesh::LoadGeometryFromOBJ stores them, host_mesh.cpp:246-253) is given, all three vertices."""
     v0 = np.asarray(v0, np.float32)
     v1 = np.asarray(v1, np.float32)
     v2 = np.asarray(v2, np.float32)
@@ -117,8 +119,8 @@ def tris_from_vertices(v0: np.ndarray, v1: np.ndarray, v2: np.ndarray, material:
     ln = np.sqrt((N * N).sum(1, dtype=np.float32)).astype(np.float32)
     ln[ln == 0] = 1
     N = (N * (np.float32(1) / ln)[:, None]).astype(np.float32)
-    for k in ("vN0", "vN1", "vN2"):
-        t[:, TRI[k]:TRI[k] + 3] = N
+    for i, k in enumerate(("vN0", "vN1", "vN2")):
+        t[:, TRI[k]:TRI[k] + 3] = N if vertex_normals is None else np.asarray(vertex_normals[i], np.float32)
     t[:, TRI["Nx"]] = N[:, 0]
     t[:, TRI["Ny"]] = N[:, 1]
     t[:, TRI["Nz"]] = N[:, 2]

@@ -277,6 +277,9 @@ LH2_DEV bool trace_one( const SceneDev& s, const v3 wO, const v3 wD, const float
 		--sp;
 		cur = sp < STACK_LDS ? lst[sp * 256] : gst[(size_t)(sp - STACK_LDS) * gstride];
 	}
+	/* OptiX Prime barycentric convention (u = weight of vertex0, v = weight of vertex1), the one
+	   material_shared.h:77-78 interpolates with; Möller–Trumbore produced the weights of v1, v2 */
+	if (!ANY && best.tri >= 0) { const float w = 1.0f - (best.u + best.v); best.v = best.u; best.u = w; }
 	return false;
 }
 

@@ -297,11 +297,28 @@ def _box(lo, hi, nseg: int):
     return tuple(np.concatenate([p[k] for p in parts]) for k in range(3))
 
 
+def _sphere(center, radius: float, nu: int, nv: int):
+    """UV sphere: (v0, v1, v2) corners and their analytic vertex normals (smooth shading)."""
+    th = np.linspace(0.0, np.pi, nv + 1)
+    ph = np.linspace(0.0, 2 * np.pi, nu + 1)
+    P = np.stack([np.sin(th)[:, None] * np.cos(ph)[None], np.cos(th)[:, None] * np.ones_like(ph)[None],
+                  np.sin(th)[:, None] * np.sin(ph)[None]], -1)             # (nv+1, nu+1, 3) unit normals
+    a, b, c, d = P[:-1, :-1], P[:-1, 1:], P[1:, :-1], P[1:, 1:]
+    n0 = np.concatenate([a.reshape(-1, 3), b.reshape(-1, 3)])
+    n1 = np.concatenate([b.reshape(-1, 3), d.reshape(-1, 3)])
+    n2 = np.concatenate([c.reshape(-1, 3), c.reshape(-1, 3)])
+    keep = np.linalg.norm(np.cross(n1 - n0, n2 - n0), axis=1) > 1e-9      # drop the degenerate pole tris
+    n0, n1, n2 = (x[keep].astype(np.float32) for x in (n0, n1, n2))
+    ctr = np.asarray(center, np.float32)
+    r = np.float32(radius)
+    return n0 * r + ctr, n1 * r + ctr, n2 * r + ctr, (n0, n1, n2)
+
+
 def room_scene(target_tris: int = 1_000_000, width: int = 1920, height: int = 1080, seed: int = 0x1234,
                sky: bool = True) -> Scene:
-    """Closed room 40 x 16 x 24 (tessellated walls), 32 columns, seeded clutter, two emissive quads.
-    Materials: 70 % roughness-1 diffuse (NEE), 20 % default roughness 0 (specular chain),
-    10 % glass (transmission 1, eta 1.5); lights radiance 50."""
+    """Closed room 40 x 16 x 24 (tessellated walls), 32 columns, 10 smooth-shaded spheres (vertex
+    normals), seeded clutter, two emissive quads.  Materials: 70 % roughness-1 diffuse (NEE), 20 %
+    default roughness 0 (specular chain), 10 % glass (transmission 1, eta 1.5); lights radiance 50."""
     rng = np.random.default_rng(seed)
     mats = [
         abi.make_material((0.75, 0.75, 0.72), roughness=1.0),   # 0 floor / ceiling
@@ -342,8 +359,20 @@ def room_scene(target_tris: int = 1_000_000, width: int = 1920, height: int = 10
         V0.append(a), V1.append(b), V2.append(c)
         mat = 3 if k % 5 == 0 else 5 if k % 3 == 0 else 0
         M.append(np.full(len(a), mat, np.uint32))
+    # 10 smooth spheres (vertex normals: exercises the hit barycentrics in GetShadingData)
+    sph_budget = int(target_tris * 0.05)
+    nu = max(6, int(math.sqrt(sph_budget / 10 / 2 * 2)))
+    S0, S1, S2, SN, SM = [], [], [], [[], [], []], []
+    for k in range(10):
+        ctr = (-15 + k * 3.3, 1.0 + 0.6 * (k % 3), -1.5 if k % 2 else 1.5)
+        a, b, c, vn = _sphere(ctr, 0.8 + 0.1 * (k % 4), nu, max(3, nu // 2))
+        S0.append(a), S1.append(b), S2.append(c), SM.append(np.full(len(a), (4, 3, 0, 5)[k % 4], np.uint32))
+        for i in range(3):
+            SN[i].append(vn[i])
+    spheres = abi.tris_from_vertices(np.concatenate(S0), np.concatenate(S1), np.concatenate(S2), np.concatenate(SM),
+                                     vertex_normals=tuple(np.concatenate(x) for x in SN))
     # clutter: random boxes on the floor
-    clutter_budget = target_tris - sum(len(a) for a in V0)
+    clutter_budget = target_tris - sum(len(a) for a in V0) - len(spheres)
     ns_cl = 2
     per_box = 12 * ns_cl * ns_cl
     nboxes = max(1, clutter_budget // per_box)
@@ -357,6 +386,7 @@ def room_scene(target_tris: int = 1_000_000, width: int = 1920, height: int = 10
     V0.append(a.astype(np.float32)), V1.append(b.astype(np.float32)), V2.append(c.astype(np.float32))
     M.append(np.repeat(matsel.astype(np.uint32), per_box))
     tris = abi.tris_from_vertices(np.concatenate(V0), np.concatenate(V1), np.concatenate(V2), np.concatenate(M))
+    tris = np.concatenate([tris, spheres])
     # two emissive quads just below the ceiling, facing down
     q1 = quad_tris((0, -1, 0), (-8, H - 0.05, 0), 4, 4, 6)
     q2 = quad_tris((0, -1, 0), (8, H - 0.05, 0), 4, 4, 6)

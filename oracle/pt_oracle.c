@@ -418,7 +418,8 @@ static inline int box_hit( const TRay* r, f3 bmin, f3 bmax, float tmax, float* t
 
 /* Möller–Trumbore, after RenderCore_Bart/common.h:19-50 with the open interval (tmin, tmax)
    of OptiX Prime's ray format (optix_prime_declarations.h:76) and an exact-zero determinant
-   test.  u weights vertex1, v weights vertex2 (w = 1-u-v weights vertex0). */
+   test.  Here u weights vertex1, v weights vertex2 (w = 1-u-v weights vertex0); trace_ray
+   converts the final hit to the Prime convention (to_prime_bary). */
 static inline int intersect_tri( const TRay* r, const lh2_CoreTri* tri, float* t, float* uo, float* vo )
 {
 	const f3 v0 = lf3( tri->vertex0 ), v1 = lf3( tri->vertex1 ), v2 = lf3( tri->vertex2 );
@@ -499,6 +500,12 @@ static int traverse_blas( const Mesh* m, const TRay* r, int instIdx, THit* best,
 	return 0;
 }
 
+/* Hit-record barycentrics in the OptiX Prime convention the Prime_B shading code assumes
+   (material_shared.h:77-78,91-92,105-107 interpolate u*v0 + v*v1 + (1-u-v)*v2; SURVEY.md §7
+   "Barycentric convention"): u = weight of vertex0, v = weight of vertex1.  Möller–Trumbore gives
+   the weights of vertex1 and vertex2, so u' = 1 - (u + v), v' = u. */
+static inline void to_prime_bary( THit* h ) { const float w = 1.0f - (h->u + h->v); h->v = h->u; h->u = w; }
+
 static void trace_ray( const Oracle* o, f3 O, f3 D, float tmin, float tmax, int anyHit, THit* best, uint32_t* nodes, uint32_t* ttests, int* occluded )
 {
 	best->t = tmax, best->tri = -1, best->inst = -1, best->u = best->v = 0;
@@ -518,6 +525,7 @@ static void trace_ray( const Oracle* o, f3 O, f3 D, float tmin, float tmax, int 
 		r.invD = mk3( safe_inv( r.D.x ), safe_inv( r.D.y ), safe_inv( r.D.z ) );
 		if (traverse_blas( &o->meshes[in->mesh], &r, i, best, anyHit, nodes, ttests )) { *occluded = 1; return; }
 	}
+	if (best->tri >= 0) to_prime_bary( best );
 }
 
 /* ------------------------------------------------------------------------------------- */

@@ -128,3 +128,34 @@ def test_saturating_float_to_uint():
     x = np.float32([-1.0, 0.0, 0.5, 1.5, 4294967040.0, 4294967296.0, 1e20, np.nan])
     got = orc.detmath(8, x)
     assert list(got) == [0.0, 0.0, 0.0, 1.0, 4294967040.0, 4294967295.0, 4294967295.0, 0.0]
+
+
+def test_hit_barycentrics_follow_prime_convention():
+    """Hit records carry OptiX Prime barycentrics (u = weight of vertex0, v = weight of vertex1, the
+    convention material_shared.h:77-78 interpolates with): u*v0 + v*v1 + (1-u-v)*v2 = O + t*D, to the
+    16-bit quantisation of the uv word (pathtracer.h:71)."""
+    from lighthouse2_amd import abi
+    tris = scene.random_triangles(2000, seed=7, edge=2.0)
+    o = orc.Oracle(threads=2)
+    o.set_materials([abi.make_material()])
+    o.set_geometry(0, tris)
+    o.set_instance(0, 0, None)
+    o.update_toplevel()
+    rng = np.random.default_rng(3)
+    n = 4000
+    org = (rng.normal(size=(n, 3)) * 12).astype(np.float32)
+    d = (rng.uniform(-4, 4, (n, 3)) - org).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    O4 = np.concatenate([org, np.full((n, 1), 1e-4, np.float32)], 1)
+    D4 = np.concatenate([d, np.full((n, 1), 1e34, np.float32)], 1)
+    hits = o.trace_closest(O4, D4)
+    hit = hits[:, 1] != 0xFFFFFFFF
+    assert hit.mean() > 0.3
+    h = hits[hit]
+    u = (h[:, 3] & 0xFFFF) / 65535.0
+    v = (h[:, 3] >> 16) / 65535.0
+    T = tris[h[:, 1].astype(np.int64)]
+    V = [T[:, abi.TRI[k]:abi.TRI[k] + 3].astype(np.float64) for k in ("vertex0", "vertex1", "vertex2")]
+    P = u[:, None] * V[0] + v[:, None] * V[1] + (1 - u - v)[:, None] * V[2]
+    Q = org[hit] + h[:, 0].view(np.float32)[:, None].astype(np.float64) * d[hit]
+    assert np.max(np.linalg.norm(P - Q, axis=1)) < 2e-3 * 2.0
