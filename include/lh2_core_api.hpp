@@ -6,8 +6,9 @@
    keeps the reference's virtual-function ORDER and parameter types (Itanium C++ ABI, g++/clang
    on Linux), using the POD mirrors of include/lh2_core_types.h, so that an unchanged
    RenderSystem can load libRenderCore_MI355X.so.  There is no virtual destructor (as in the
-   reference).  tests/native/abi_probe.cpp checks the vtable slot order against the reference
-   header when /root/reference is present.
+   reference).  tests/test_abi_layout.py checks the slot order against the reference header
+   (when /root/reference is present), and tools/headless_rendersystem.cpp drives a core through
+   this vtable the way RenderSystem does (tests/test_boundary_replay.py).
 */
 #pragma once
 #include "lh2_core_types.h"
