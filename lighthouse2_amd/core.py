@@ -37,7 +37,7 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = pathlib.Path(path) if path else LIB_PATH
+    p = pathlib.Path(path) if path else pathlib.Path(os.environ.get("LH2_CORE_LIB", LIB_PATH))
     if not p.exists():
         raise CoreError(f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)

@@ -58,7 +58,8 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	uint4* hits;                                      /* closest: {t, triid, instid, uv16} */
 	uint32_t* mask;                                   /* any, mode 0: occlusion bits */
 	const float4* potentials; float4* acc;            /* any, mode 1: fused finalizeConnection */
-	int* gstack; uint32_t* overflow;
+	int* gstack;                                      /* stack entries past LH2_STACK_LDS */
+	uint32_t refill;                                  /* refill idle lanes once >= refill are idle (1..64) */
 };
 
 extern "C" {
@@ -73,5 +74,7 @@ void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int ba
 void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, hipStream_t st );
 }
 
+#ifndef LH2_STACK_LDS
 #define LH2_STACK_LDS 24
+#endif
 #define LH2_STACK_TOTAL 96

@@ -149,6 +149,9 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 /* =====================================================================================
    traversal: two-level BVH2, ordered, t-culled, LDS short stack + global spill
    ===================================================================================== */
+#ifndef LH2_TRACE_MINWAVES
+#define LH2_TRACE_MINWAVES 1   /* min waves per SIMD the traversal kernels are compiled for (VGPR cap) */
+#endif
 #define STACK_LDS LH2_STACK_LDS   /* entries per lane kept in LDS: 24 x 256 x 4 B = 24 KB / block */
 #define STACK_TOTAL LH2_STACK_TOTAL /* + global spill; the host checks the tree depth against it */
 
@@ -197,20 +200,67 @@ LH2_DEV bool mt_test( const float4 a, const float4 b, const float4 c, const TRay
 	return true;
 }
 
-template <bool ANY>
-LH2_DEV bool trace_one( const SceneDev& s, const v3 wO, const v3 wD, const float tmin, const float tmax,
-	int* __restrict__ lst, int* __restrict__ gst, const uint32_t gstride, HitRec& best, uint32_t* overflow )
+#define LH2_POP INT_MIN   /* "pop the stack next" marker in cur (no valid node or leaf ref) */
+
+/* Ray-stream traversal with dynamic ray fetch (persistent waves, Aila & Laine 2009 "speculative
+   fetch").  Each lane carries one ray's traversal state across loop iterations.  Every iteration
+   runs one step: a node visit, an instance entry, or one leaf's triangle tests, and then a pop when
+   the step ends a subtree.  A lane whose ray is finished writes its result and goes idle.  Once at
+   least a.refill lanes of the wave are idle (64: whole batches), they take new rays from the device work queue: one
+   merged atomicAdd per wave, with consecutive indices in lane order.  So the long rays of a batch
+   no longer hold up 63 finished lanes.
+     KIND 0: closest hit -> hits[idx] = {t, triid, instid, uv16} (uv quantised as pathtracer.h:71,
+             OptiX Prime barycentric convention, converted at the end)
+     KIND 1: any hit -> occlusion bit (RTP_BUFFER_FORMAT_HIT_BITMASK; mask zeroed by the caller)
+     KIND 2: any hit fused with finalizeConnection (connections.h:22-34): unoccluded rays add their
+             potential to the accumulator
+   The world-space ray is re-read from the ray buffer on the rare instance entry / exit instead of
+   being kept in registers.  Termination: the builder emits children after their parent
+   (bvh_build.cpp flatten), so descending strictly increases the node index, and every pop undoes
+   one push.  The stack depth stays within the tree depth, which UpdateToplevel checks against
+   LH2_STACK_TOTAL. */
+template <int KIND>
+LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restrict__ lst, int* __restrict__ gst, const uint32_t gstride )
 {
+	constexpr bool ANY = KIND != 0;
+	const uint32_t count = a.countPtr ? *a.countPtr : a.countFixed;
+	const uint32_t refill = a.refill ? a.refill : 64u;
+	bool active = false, exhausted = false;
+	uint32_t idx = 0;
 	TRay r;
-	setup_ray( r, wO, wD );
-	best.t = tmax, best.tri = -1, best.inst = -1, best.u = 0, best.v = 0;
-	int sp = 0, blasSp = -1, curInst = -1;
-	int cur = s.tlasRoot;
-	uint32_t steps = 0;
+	float tmin = 0;
+	HitRec best;
+	int sp = 0, blasSp = -1, cur = 0, curInst = -1;
 	while (true)
 	{
-		/* watchdog: a malformed tree must not hang the GPU; flag it and give up on this ray */
-		if (++steps > (1u << 22)) { atomicOr( overflow, 2u ); break; }
+		/* ---- refill idle lanes (wave-uniform decision) ---- */
+		if (!exhausted && __popcll( __ballot( !active ) ) >= refill)
+		{
+			bool dry = false;
+			if (!active)
+			{
+				idx = atomicAdd( a.cursor, 1u );
+				if (idx < count)
+				{
+					const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
+					setup_ray( r, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ) );
+					tmin = o4.w;
+					best.t = d4.w, best.tri = -1, best.inst = -1, best.u = 0, best.v = 0;
+					sp = 0, blasSp = -1, cur = s.tlasRoot;
+					active = true;
+				}
+				else dry = true;
+			}
+			exhausted = __ballot( dry ) != 0;   /* the cursor only grows: once dry, always dry */
+		}
+		if (__ballot( active ) == 0)
+		{
+			if (exhausted) break;
+			continue;
+		}
+		if (!active) continue;
+		/* ---- one traversal step ---- */
+		bool fin = false, occluded = false;
 		if (cur >= 0)
 		{
 			const float4* n = s.nodes + (size_t)cur * 4;
@@ -222,119 +272,108 @@ LH2_DEV bool trace_one( const SceneDev& s, const v3 wO, const v3 wD, const float
 			if (h0 && h1)
 			{
 				const bool swap = tn1 < tn0;
-				const int nearc = swap ? n3.y : n3.x, farc = swap ? n3.x : n3.y;
+				const int farc = swap ? n3.x : n3.y;
+				cur = swap ? n3.y : n3.x;
+				/* depth <= LH2_STACK_TOTAL is guaranteed by the host (UpdateToplevel) */
 				if (sp < STACK_LDS) lst[sp * 256] = farc;
-				else if (sp < STACK_TOTAL) gst[(size_t)(sp - STACK_LDS) * gstride] = farc;
-				else { atomicOr( overflow, 1u ); break; }
+				else gst[(size_t)(sp - STACK_LDS) * gstride] = farc;
 				sp++;
-				cur = nearc;
-				continue;
 			}
-			if (h0) { cur = n3.x; continue; }
-			if (h1) { cur = n3.y; continue; }
+			else cur = h0 ? n3.x : h1 ? n3.y : LH2_POP;
 		}
-		else if (blasSp < 0)
+		else if (cur != LH2_POP)
 		{
-			/* TLAS leaf (one instance): move the ray into object space, not renormalised, so t
-			   stays in world units */
-			const int ii = (int)LEAF_FIRST( cur );
-			const DevInstance in = s.inst[ii];
-			const v3 O = mk3( in.inv0.x * wO.x + in.inv0.y * wO.y + in.inv0.z * wO.z + in.inv0.w,
-				in.inv1.x * wO.x + in.inv1.y * wO.y + in.inv1.z * wO.z + in.inv1.w,
-				in.inv2.x * wO.x + in.inv2.y * wO.y + in.inv2.z * wO.z + in.inv2.w );
-			const v3 D = mk3( in.inv0.x * wD.x + in.inv0.y * wD.y + in.inv0.z * wD.z,
-				in.inv1.x * wD.x + in.inv1.y * wD.y + in.inv1.z * wD.z,
-				in.inv2.x * wD.x + in.inv2.y * wD.y + in.inv2.z * wD.z );
-			setup_ray( r, O, D );
-			blasSp = sp, curInst = ii;
-			cur = in.root;
-			continue;
-		}
-		else
-		{
-			const uint32_t first = LEAF_FIRST( cur );
-			const int cnt = LEAF_COUNT( cur );
-			for (int k = 0; k < cnt; k++)
+			if (blasSp < 0)
 			{
-				const float4* tp = s.tris + (size_t)(first + k) * 3;
-				const float4 a = tp[0], b = tp[1], c = tp[2];
-				float t, u, v;
-				if (mt_test( a, b, c, r, t, u, v ) && t > tmin)
+				/* TLAS leaf (one instance): object-space ray, not renormalised */
+				const int ii = (int)LEAF_FIRST( cur );
+				const DevInstance in = s.inst[ii];
+				const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
+				const v3 O = mk3( in.inv0.x * o4.x + in.inv0.y * o4.y + in.inv0.z * o4.z + in.inv0.w,
+					in.inv1.x * o4.x + in.inv1.y * o4.y + in.inv1.z * o4.z + in.inv1.w,
+					in.inv2.x * o4.x + in.inv2.y * o4.y + in.inv2.z * o4.z + in.inv2.w );
+				const v3 D = mk3( in.inv0.x * d4.x + in.inv0.y * d4.y + in.inv0.z * d4.z,
+					in.inv1.x * d4.x + in.inv1.y * d4.y + in.inv1.z * d4.z,
+					in.inv2.x * d4.x + in.inv2.y * d4.y + in.inv2.z * d4.z );
+				setup_ray( r, O, D );
+				blasSp = sp, curInst = ii;
+				cur = in.root;
+			}
+			else
+			{
+				const uint32_t first = LEAF_FIRST( cur );
+				const int cnt = LEAF_COUNT( cur );
+				for (int k = 0; k < cnt; k++)
 				{
-					if (ANY) { if (t < best.t) return true; }
-					else
+					const float4* tp = s.tris + (size_t)(first + k) * 3;
+					const float4 ta = tp[0], tb = tp[1], tc = tp[2];
+					float t, u, v;
+					if (mt_test( ta, tb, tc, r, t, u, v ) && t > tmin)
 					{
-						const int tri = __float_as_int( a.w );
-						if (t < best.t || (t == best.t && (curInst < best.inst || (curInst == best.inst && tri < best.tri))))
-							best.t = t, best.tri = tri, best.inst = curInst, best.u = u, best.v = v;
+						if (ANY) { if (t < best.t) { occluded = fin = true; break; } }
+						else
+						{
+							const int tri = __float_as_int( ta.w );
+							if (t < best.t || (t == best.t && (curInst < best.inst || (curInst == best.inst && tri < best.tri))))
+								best.t = t, best.tri = tri, best.inst = curInst, best.u = u, best.v = v;
+						}
 					}
 				}
+				cur = LH2_POP;
 			}
 		}
-		/* pop */
-		if (sp == blasSp) { blasSp = -1; setup_ray( r, wO, wD ); }
-		if (sp == 0) break;
-		--sp;
-		cur = sp < STACK_LDS ? lst[sp * 256] : gst[(size_t)(sp - STACK_LDS) * gstride];
-	}
-	/* OptiX Prime barycentric convention (u = weight of vertex0, v = weight of vertex1), the one
-	   material_shared.h:77-78 interpolates with; Möller–Trumbore produced the weights of v1, v2 */
-	if (!ANY && best.tri >= 0) { const float w = 1.0f - (best.u + best.v); best.v = best.u; best.u = w; }
-	return false;
-}
-
-/* Closest hit for a ray stream.  Persistent waves pull 64 rays at a time from a device work
-   queue (one merged atomicAdd per wave), so the grid only needs to cover the resident waves and the
-   cost imbalance between rays never idles a CU.  Hit record per ray (16 B): {t, triid, instid,
-   uv16}, uv quantised exactly as pathtracer.h:71 does. */
-__global__ __launch_bounds__( 256 ) void k_trace_closest( const SceneDev s, const TraceArgs a )
-{
-	__shared__ int lstack[STACK_LDS * 256];
-	const uint32_t count = a.countPtr ? *a.countPtr : a.countFixed;
-	const uint32_t gstride = gridDim.x * 256u;
-	int* gst = a.gstack + blockIdx.x * 256 + threadIdx.x;
-	int* lst = lstack + threadIdx.x;
-	while (true)
-	{
-		/* per-lane fetch; the compiler merges the active lanes' adds into one atomic per wave and
-		   hands out consecutive indices in lane order, so a wave keeps 64 neighbouring rays */
-		const uint32_t idx = atomicAdd( a.cursor, 1u );
-		if (idx >= count) break;
-		const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
-		HitRec h;
-		trace_one<false>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, a.overflow );
-		uint4 out;
-		if (h.tri < 0) out = make_uint4( fbits( -1.0f ), 0xffffffffu, 0xffffffffu, 0u );
-		else out = make_uint4( fbits( h.t ), (uint32_t)h.tri, (uint32_t)h.inst, lh2_f2u( 65535.0f * h.u ) + (lh2_f2u( 65535.0f * h.v ) << 16) );
-		a.hits[idx] = out;
-	}
-}
-
-/* Any hit for shadow rays.  MODE 0: occlusion bitmask (RTP_BUFFER_FORMAT_HIT_BITMASK, bit set =
-   occluded);  MODE 1: fused finalizeConnection (connections.h:22-34):
-   unoccluded rays add their potential to the accumulator. */
-template <int MODE>
-__global__ __launch_bounds__( 256 ) void k_trace_any( const SceneDev s, const TraceArgs a )
-{
-	__shared__ int lstack[STACK_LDS * 256];
-	const uint32_t count = a.countPtr ? *a.countPtr : a.countFixed;
-	const uint32_t gstride = gridDim.x * 256u;
-	int* gst = a.gstack + blockIdx.x * 256 + threadIdx.x;
-	int* lst = lstack + threadIdx.x;
-	while (true)
-	{
-		const uint32_t idx = atomicAdd( a.cursor, 1u );
-		if (idx >= count) break;
-		const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
-		HitRec h;
-		const bool occluded = trace_one<true>( s, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ), o4.w, d4.w, lst, gst, gstride, h, a.overflow );
-		if (MODE == 1 && !occluded)
+		if (!fin && cur == LH2_POP)
 		{
-			const float4 E = a.potentials[idx];
-			acc_add( a.acc, __float_as_uint( E.w ), mk3( E.x, E.y, E.z ) );
+			if (sp == blasSp)
+			{
+				blasSp = -1;
+				const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
+				setup_ray( r, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ) );
+			}
+			if (sp == 0) fin = true;
+			else
+			{
+				--sp;
+				cur = sp < STACK_LDS ? lst[sp * 256] : gst[(size_t)(sp - STACK_LDS) * gstride];
+			}
 		}
-		if (MODE == 0 && occluded) atomicOr( a.mask + (idx >> 5), 1u << (idx & 31u) );   /* mask zeroed by the caller */
+		if (fin)
+		{
+			active = false;
+			if (KIND == 0)
+			{
+				uint4 out;
+				if (best.tri < 0) out = make_uint4( fbits( -1.0f ), 0xffffffffu, 0xffffffffu, 0u );
+				else
+				{
+					/* OptiX Prime barycentric convention (u = weight of vertex0, v = weight of vertex1),
+					   the one material_shared.h:77-78 interpolates with; MT gave the weights of v1, v2 */
+					const float bu = 1.0f - (best.u + best.v), bv = best.u;
+					out = make_uint4( fbits( best.t ), (uint32_t)best.tri, (uint32_t)best.inst, lh2_f2u( 65535.0f * bu ) + (lh2_f2u( 65535.0f * bv ) << 16) );
+				}
+				a.hits[idx] = out;
+			}
+			else if (KIND == 1) { if (occluded) atomicOr( a.mask + (idx >> 5), 1u << (idx & 31u) ); }
+			else if (!occluded)
+			{
+				const float4 E = a.potentials[idx];
+				acc_add( a.acc, __float_as_uint( E.w ), mk3( E.x, E.y, E.z ) );
+			}
+		}
 	}
+}
+
+__global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_closest( const SceneDev s, const TraceArgs a )
+{
+	__shared__ int lstack[STACK_LDS * 256];
+	trace_stream<0>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+}
+
+template <int MODE>
+__global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_any( const SceneDev s, const TraceArgs a )
+{
+	__shared__ int lstack[STACK_LDS * 256];
+	trace_stream<MODE == 0 ? 1 : 2>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 }
 
 /* =====================================================================================
@@ -1128,7 +1167,7 @@ __global__ void k_init_counters( Counters* c, uint32_t pathCount )
 	c->activePaths = pathCount, c->extensionRays = 0, c->shadowRays = 0;
 	c->totalExtensionRays = pathCount, c->totalShadowRays = 0;
 	c->probedInstid = -1, c->probedTriid = -1, c->probedDist = 0;
-	c->stackOverflow = 0, c->shadowOverflow = 0;
+	c->reserved0 = 0, c->shadowOverflow = 0;
 	for (int i = 0; i < 32; i++) c->cursor[i] = 0;
 }
 __global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength )

@@ -150,6 +150,10 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "clampValue" )) clampValue = value;
 	else if (!strcmp( name, "maxPathLength" )) maxPathLength = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "tiledRays" )) tiledRays = value != 0;
+	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle (64 = whole batches);
+	   coherent 8x8-tiled primary rays trace best in batches, incoherent bounce rays with refills */
+	else if (!strcmp( name, "refillPrimary" )) refillPrimary = std::min( 64, std::max( 1, (int)value ) );
+	else if (!strcmp( name, "refill" )) refillOther = std::min( 64, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "blocksPerCU" )) { blocksPerCU = std::min( 16, std::max( 1, (int)value ) ); if (scrwidth) EnsureBuffers(); }
 	/* other names ("clampDirect", "filter", "TAA", ...) are ignored, as in the reference */
 }
@@ -421,7 +425,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipEventRecord( evTrace[2 * pathLength], stream ) );
 		TraceArgs ta{};
 		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.countPtr = &c->activePaths, ta.cursor = &c->cursor[pathLength];
-		ta.hits = hits.ptr, ta.gstack = gstack.ptr, ta.overflow = &c->stackOverflow;
+		ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
+		ta.hits = hits.ptr, ta.gstack = gstack.ptr;
 		lh2_launch_trace_closest( &sd, &ta, grid, stream );
 		CHK_HIP( hipEventRecord( evTrace[2 * pathLength + 1], stream ) );
 		ShadeParams sp;
@@ -453,8 +458,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	CHK_HIP( hipEventRecord( evShadow[0], stream ) );
 	{
 		TraceArgs ta{};
-		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = &c->cursor[20];
-		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr, ta.overflow = &c->stackOverflow;
+		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = &c->cursor[20], ta.refill = (uint32_t)refillOther;
+		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
 		lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
 	}
 	CHK_HIP( hipEventRecord( evShadow[1], stream ) );
@@ -488,8 +493,6 @@ void RenderCore::Synchronize()
 	{
 		statsPending = false;
 		const Counters& cnt = hostStats->counters;
-		if (cnt.stackOverflow & 2u) FatalError( "traversal step limit exceeded (corrupt BVH)" );
-		if (cnt.stackOverflow) FatalError( "traversal stack overflow (BVH deeper than %d)", LH2_STACK_TOTAL );
 		if (cnt.shadowOverflow) FatalError( "shadow ray buffer overflow" );
 		uint32_t* rc = hostStats->rayCount;   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
 		auto ms = [&]( hipEvent_t a, hipEvent_t b ) { float t = 0; (void)hipEventElapsedTime( &t, a, b ); return t * 1e-3f; };
@@ -561,14 +564,10 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, 8, stream ) );
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
-	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr + 1, ta.hits = h.ptr, ta.gstack = gs.ptr, ta.overflow = ovf.ptr;
+	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr + 1, ta.hits = h.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther;
 	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
-	uint32_t of = 0;
-	CHK_HIP( hipMemcpyAsync( &of, ovf.ptr, 4, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
-	if (of & 2u) FatalError( "traversal step limit exceeded (corrupt BVH)" );
-	if (of) FatalError( "traversal stack overflow" );
 }
 
 void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* occluded )
@@ -583,7 +582,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	CHK_HIP( hipMemsetAsync( m.ptr, 0, words * 4, stream ) );
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
-	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr + 1, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.overflow = ovf.ptr;
+	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr + 1, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther;
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, stream );
 	std::vector<uint32_t> tmp( words );
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
@@ -607,7 +606,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 	{
 		TraceArgs ta{};
 		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.cursor = cursors.ptr + i;
-		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr, ta.overflow = cursors.ptr + iterations;
+		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr, ta.refill = (uint32_t)refillOther;
 		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	}
 	CHK_HIP( hipEventRecord( b, stream ) );

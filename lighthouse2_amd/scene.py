@@ -174,6 +174,21 @@ class Scene:
         core.render(view or self.view, converge)
 
 
+def tiled_order(w: int, h: int) -> np.ndarray:
+    """Pixel index held by each ray slot when the core stores primary rays in 8x8 pixel blocks per wave
+    (setting "tiledRays", k_camera): frame-order arrays indexed with this give the in-frame ray order."""
+    r = np.arange(w * h, dtype=np.int64)
+    x, y = r % w, r // w
+    if w % 8 == 0:
+        rb = r // (8 * w)
+        full = rb < h // 8
+        q = r - rb * 8 * w
+        k = q & 63
+        x = np.where(full, (q >> 6) * 8 + (k & 7), x)
+        y = np.where(full, rb * 8 + (k >> 3), y)
+    return y * w + x
+
+
 def light_from_tri(tri: np.ndarray, tri_idx: int, inst_idx: int, radiance) -> abi.CoreLightTri:
     """HostAreaLight constructor + ConvertToCoreLightTri (host_light.cpp:25-62)."""
     v0 = tri[32:35].astype(np.float32)

@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tris", type=int, default=100_000)
     ap.add_argument("--set", default="both")
+    ap.add_argument("--refill", type=int, default=32)
+    ap.add_argument("--refill-primary", type=int, default=64)
     ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -62,15 +64,17 @@ def main():
         k, v = s.split("=")
         core.setting(k, float(v))
     O4, D4, _ = core.generate_eye_rays(sc.view, 0, 0)
-    sets = {"primary": (O4, D4)}
+    perm = scene.tiled_order(1920, 1080)    # in-frame order of the primary rays (k_camera, tiledRays)
+    sets = {"primary": (np.ascontiguousarray(O4[perm]), np.ascontiguousarray(D4[perm]))}
     if args.set in ("both", "bounce"):
         hits = core.trace_closest(O4, D4)
-        sets["bounce"] = bounce_rays(sc.meshes[0], O4, D4, hits)
+        sets["bounce"] = bounce_rays(sc.meshes[0], O4[perm], D4[perm], hits[perm])   # compacted, in-frame order
     res = {}
     for name, (o, d) in sets.items():
         if args.set not in ("both", name):
             continue
         n = len(o)
+        core.setting("refill", args.refill_primary if name == "primary" else args.refill)
         ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
         h = torch.empty((n, 4), dtype=torch.int32, device=dev)
         torch.cuda.synchronize()
