@@ -36,7 +36,6 @@ struct Counters   /* core_settings.h:81-91 plus device-side error flags */
 	uint32_t activePaths, extensionRays, shadowRays, totalExtensionRays;
 	uint32_t totalShadowRays; int probedInstid, probedTriid; float probedDist;
 	uint32_t reserved0, shadowOverflow, pad0, pad1;
-	uint32_t cursor[32];   /* dynamic ray-fetch cursors: [L] closest hit at path length L, [20] shadow */
 };
 
 /* ---- small vector helpers with the reference's evaluation order --------------------------- */

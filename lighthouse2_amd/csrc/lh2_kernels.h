@@ -54,7 +54,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 {
 	const float4* rayO; const float4* rayD;
 	const uint32_t* countPtr; uint32_t countFixed;   /* count from device memory, or fixed */
-	uint32_t* cursor;                                 /* zeroed work-queue head (64 rays per fetch) */
+	uint32_t* cursor;                                 /* LH2_CHUNKS zeroed work-queue heads, LH2_CURSOR_STRIDE apart */
 	uint4* hits;                                      /* closest: {t, triid, instid, uv16} */
 	uint32_t* mask;                                   /* any, mode 0: occlusion bits */
 	const float4* potentials; float4* acc;            /* any, mode 1: fused finalizeConnection */
@@ -63,7 +63,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 };
 
 extern "C" {
-void lh2_launch_init_counters( Counters* c, uint32_t pathCount, hipStream_t st );
+void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t* cursors, int cursorWords, hipStream_t st );
 void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, hipStream_t st );
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, hipStream_t st );
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, hipStream_t st );
@@ -74,6 +74,14 @@ void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int ba
 void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, hipStream_t st );
 }
 
+/* ray-fetch work queue: the ray range is split into LH2_CHUNKS contiguous chunks with one cursor
+   each (128 B apart), so the per-wave atomics of a launch spread over 8 addresses instead of one */
+#ifndef LH2_CHUNKS
+#define LH2_CHUNKS 8
+#endif
+#define LH2_CURSOR_STRIDE 32
+#define LH2_CURSOR_WORDS (LH2_CHUNKS * LH2_CURSOR_STRIDE)   /* per trace launch */
+#define LH2_CURSOR_SLOTS 24                                  /* launches per frame: [L] bounce L, [20] shadow */
 #ifndef LH2_STACK_LDS
 #define LH2_STACK_LDS 24
 #endif

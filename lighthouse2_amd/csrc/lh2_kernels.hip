@@ -224,9 +224,14 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 {
 	constexpr bool ANY = KIND != 0;
 	const uint32_t count = a.countPtr ? *a.countPtr : a.countFixed;
+	if (count == 0) return;
 	const uint32_t refill = a.refill ? a.refill : 64u;
 	bool active = false, exhausted = false;
 	uint32_t idx = 0;
+	/* this wave's chunk of the ray range: blocks go round-robin over the 8 XCDs, so blockIdx % 8
+	   gives each XCD its own chunk and cursor; a dry chunk moves the wave on to the next one */
+	uint32_t chunk = blockIdx.x % LH2_CHUNKS, tried = 0;
+	uint32_t lo = (uint32_t)(((uint64_t)count * chunk) / LH2_CHUNKS), hi = (uint32_t)(((uint64_t)count * (chunk + 1)) / LH2_CHUNKS);
 	TRay r;
 	float tmin = 0;
 	HitRec best;
@@ -239,8 +244,10 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 			bool dry = false;
 			if (!active)
 			{
-				idx = atomicAdd( a.cursor, 1u );
-				if (idx < count)
+				/* uniform address (readfirstlane): the compiler then merges the idle lanes' adds into
+				   one atomic per wave, handing out consecutive indices in lane order */
+				idx = lo + atomicAdd( a.cursor + __builtin_amdgcn_readfirstlane( chunk ) * LH2_CURSOR_STRIDE, 1u );
+				if (idx < hi)
 				{
 					const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
 					setup_ray( r, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ) );
@@ -251,7 +258,12 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 				}
 				else dry = true;
 			}
-			exhausted = __ballot( dry ) != 0;   /* the cursor only grows: once dry, always dry */
+			if (__ballot( dry ) != 0)   /* cursors only grow: a dry chunk stays dry */
+			{
+				if (++tried == LH2_CHUNKS) exhausted = true;
+				chunk = (chunk + 1) % LH2_CHUNKS;
+				lo = (uint32_t)(((uint64_t)count * chunk) / LH2_CHUNKS), hi = (uint32_t)(((uint64_t)count * (chunk + 1)) / LH2_CHUNKS);
+			}
 		}
 		if (__ballot( active ) == 0)
 		{
@@ -1161,14 +1173,15 @@ __global__ __launch_bounds__( 256 ) void k_shade( const SceneDev s, const ShadeP
 }
 
 /* counters: .cuda.cu:64-84 */
-__global__ void k_init_counters( Counters* c, uint32_t pathCount )
+__global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t* cursors, int cursorWords )
 {
-	if (threadIdx.x != 0) return;
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < cursorWords) cursors[i] = 0;
+	if (i != 0) return;
 	c->activePaths = pathCount, c->extensionRays = 0, c->shadowRays = 0;
 	c->totalExtensionRays = pathCount, c->totalShadowRays = 0;
 	c->probedInstid = -1, c->probedTriid = -1, c->probedDist = 0;
 	c->reserved0 = 0, c->shadowOverflow = 0;
-	for (int i = 0; i < 32; i++) c->cursor[i] = 0;
 }
 __global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength )
 {
@@ -1200,7 +1213,10 @@ __global__ void k_pack_rows( const float4* __restrict__ acc, float4* __restrict_
 
 /* ---- host-side launchers (extern "C", no torch / no HIP types beyond the stream) ---------- */
 extern "C" {
-void lh2_launch_init_counters( Counters* c, uint32_t pathCount, hipStream_t st ) { k_init_counters<<<1, 64, 0, st>>>( c, pathCount ); }
+void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t* cursors, int cursorWords, hipStream_t st )
+{
+	k_init_counters<<<(cursorWords + 255) / 256 + 1, 256, 0, st>>>( c, pathCount, cursors, cursorWords );
+}
 void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, hipStream_t st ) { k_counters_next<<<1, 64, 0, st>>>( c, log, pathLength ); }
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, hipStream_t st )
 {

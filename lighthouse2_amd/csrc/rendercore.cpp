@@ -104,6 +104,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	if (got != 65536 * 5) FatalError( "blue noise table truncated: %s", path.c_str() );
 	dBlueNoise.upload( bn.data(), bn.size(), stream );
 	counters.resize( 1 );
+	fetchCursors.resize( (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
 	rayLog.resize( 32 );
 	blocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocDefault ) );
@@ -404,7 +405,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const uint32_t pathCount = (uint32_t)tilePix * (uint32_t)scrspp;
 	const SceneDev sd = MakeSceneDev();
 	Counters* c = counters.ptr;
-	lh2_launch_init_counters( c, pathCount, stream );
+	lh2_launch_init_counters( c, pathCount, fetchCursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, stream );
 	/* primary rays (camera.h) for every sample of the tile */
 	CameraParams cp;
 	cp.pos = view.pos, cp.p1 = view.p1;
@@ -424,7 +425,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		pl = pathLength;
 		CHK_HIP( hipEventRecord( evTrace[2 * pathLength], stream ) );
 		TraceArgs ta{};
-		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.countPtr = &c->activePaths, ta.cursor = &c->cursor[pathLength];
+		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.countPtr = &c->activePaths, ta.cursor = fetchCursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
 		ta.hits = hits.ptr, ta.gstack = gstack.ptr;
 		lh2_launch_trace_closest( &sd, &ta, grid, stream );
@@ -458,7 +459,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	CHK_HIP( hipEventRecord( evShadow[0], stream ) );
 	{
 		TraceArgs ta{};
-		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = &c->cursor[20], ta.refill = (uint32_t)refillOther;
+		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = fetchCursors.ptr + (size_t)20 * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther;
 		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
 		lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
 	}
@@ -559,12 +560,12 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	DevBuf<float4> o, d; DevBuf<uint4> h; DevBuf<int> gs; DevBuf<uint32_t> ovf;
 	o.upload( (const float4*)ot, n, stream ), d.upload( (const float4*)dt, n, stream );
-	h.resize( n ), ovf.resize( 2 );
+	h.resize( n ), ovf.resize( LH2_CURSOR_WORDS );
 	gs.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
-	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, 8, stream ) );
+	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
-	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr + 1, ta.hits = h.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther;
+	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther;
 	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -576,13 +577,13 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	DevBuf<float4> o, d; DevBuf<uint32_t> m; DevBuf<int> gs; DevBuf<uint32_t> ovf;
 	o.upload( (const float4*)ot, n, stream ), d.upload( (const float4*)dt, n, stream );
 	const size_t words = ((size_t)n + 63) / 64 * 2;
-	m.resize( words ), ovf.resize( 2 );
+	m.resize( words ), ovf.resize( LH2_CURSOR_WORDS );
 	gs.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
-	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, 8, stream ) );
+	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
 	CHK_HIP( hipMemsetAsync( m.ptr, 0, words * 4, stream ) );
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
-	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr + 1, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther;
+	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther;
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, stream );
 	std::vector<uint32_t> tmp( words );
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
@@ -597,15 +598,15 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 	if (!counters.ptr) counters.resize( 1 );
 	const SceneDev sd = MakeSceneDev();
 	DevBuf<uint32_t> cursors;
-	cursors.resize( (size_t)std::max( 1, iterations ) + 1 );
-	CHK_HIP( hipMemsetAsync( cursors.ptr, 0, sizeof( uint32_t ) * ((size_t)std::max( 1, iterations ) + 1), stream ) );
+	cursors.resize( (size_t)std::max( 1, iterations ) * LH2_CURSOR_WORDS );
+	CHK_HIP( hipMemsetAsync( cursors.ptr, 0, sizeof( uint32_t ) * (size_t)std::max( 1, iterations ) * LH2_CURSOR_WORDS, stream ) );
 	hipEvent_t a, b;
 	CHK_HIP( hipEventCreate( &a ) ); CHK_HIP( hipEventCreate( &b ) );
 	CHK_HIP( hipEventRecord( a, stream ) );
 	for (int i = 0; i < iterations; i++)
 	{
 		TraceArgs ta{};
-		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.cursor = cursors.ptr + i;
+		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.cursor = cursors.ptr + (size_t)i * LH2_CURSOR_WORDS;
 		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr, ta.refill = (uint32_t)refillOther;
 		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	}

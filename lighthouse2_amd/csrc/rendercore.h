@@ -134,6 +134,7 @@ private:
 	DevBuf<float4> accumulator, frame;
 	DevBuf<int> gstack;
 	DevBuf<Counters> counters;
+	DevBuf<uint32_t> fetchCursors;    /* LH2_CURSOR_SLOTS x LH2_CURSOR_WORDS work-queue heads */
 	DevBuf<uint32_t> rayLog;
 	FrameStats* hostStats = nullptr;     /* pinned */
 	bool statsPending = false;
