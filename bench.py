@@ -180,7 +180,7 @@ def main():
         core.setting("refill", 64)            # the primary-ray launch setting (refillPrimary)
         core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), 2)
         ms = core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), args.kernel_iters)
-        core.setting("refill", 32)
+        core.setting("refill", 16)
         fix = json.load(open(ROOT / "tests" / "golden" / "config2_visits.json"))
         bpr = 32 + 20 + 32 * fix["mean_node_records"] + 36 * fix["mean_tri_tests"]
         algo = bpr * n

@@ -142,7 +142,7 @@ private:
 	hipEvent_t evCount[18] = {};
 	uint32_t* activeLog = nullptr;     /* pinned: active paths after each bounce */
 	int tiledRays = 1;
-	int refillPrimary = 64, refillOther = 32;
+	int refillPrimary = 64, refillOther = 16;
 	int framePathLengths = 0;
 	double frameHostMs = 0;
 	int samplesTaken = 0;

@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tris", type=int, default=100_000)
     ap.add_argument("--set", default="both")
-    ap.add_argument("--refill", type=int, default=32)
+    ap.add_argument("--refill", type=int, default=16)
     ap.add_argument("--refill-primary", type=int, default=64)
     ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
     args = ap.parse_args()
