@@ -70,6 +70,7 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
         "lh2_core_ray_counts": [_P, _U],
         "lh2_core_pack_tile": [_P, _P],
         "lh2_core_tile_rows": [_P, C.POINTER(C.c_int)],
+        "lh2_core_stream": [_P, C.POINTER(_P)],
         "lh2_core_trace_closest": [_P, _F, _F, C.c_int, _U],
         "lh2_core_trace_any": [_P, _F, _F, C.c_int, _U],
         "lh2_core_trace_closest_device": [_P, _P, _P, C.c_int, _P, C.c_int, _F],
@@ -207,8 +208,19 @@ class RenderCore:
     def copy_accumulator_rows(self, device_ptr: int, y0: int, y1: int) -> None:
         self._chk(self.lib.lh2_core_copy_accumulator_rows(self.h, C.c_void_p(device_ptr), int(y0), int(y1)))
 
-    def pack_tile(self, device_ptr: int) -> None:
+    def pack_tile(self, device_ptr: int, order_torch: bool = True) -> None:
+        """Pack the owned accumulator rows into device memory (asynchronously, on the core stream).
+        With order_torch, torch's current stream is made to wait for it (no host synchronisation), so
+        torch ops and collectives on the tile see the finished rows."""
         self._chk(self.lib.lh2_core_pack_tile(self.h, C.c_void_p(device_ptr)))
+        if order_torch:
+            import torch
+            torch.cuda.current_stream().wait_stream(torch.cuda.ExternalStream(self.stream_ptr()))
+
+    def stream_ptr(self) -> int:
+        s = C.c_void_p()
+        self._chk(self.lib.lh2_core_stream(self.h, C.byref(s)))
+        return s.value or 0
 
     def tile_rows(self) -> int:
         r = C.c_int(0)

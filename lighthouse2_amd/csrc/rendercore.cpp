@@ -545,8 +545,9 @@ void RenderCore::PackTile( void* devDst )
 {
 	const int rows = TileRows();
 	const int band = tileBand > 0 ? tileBand : std::max( 1, rows ), stride = tileBand > 0 ? tileStride : std::max( 1, rows );
+	/* asynchronous: consumers on other streams order themselves after the core stream (lh2_core_stream),
+	   so the host can queue the next frame while this one finishes */
 	lh2_launch_pack_rows( accumulator.ptr, (float4*)devDst, scrwidth, std::max( 0, tileY0 ), band, stride, rows, stream );
-	CHK_HIP( hipStreamSynchronize( stream ) );
 }
 
 void RenderCore::GetFrame( float* hostOut4 )

@@ -83,7 +83,7 @@ public:
 	void Synchronize();
 	void GetAccumulator( float* hostOut4 );                /* full frame, raw accumulator */
 	void CopyAccumulatorRows( void* devDst, int y0, int y1 ); /* D2D copy of rows [y0,y1) */
-	void PackTile( void* devDst );                         /* owned rows, local order, then sync */
+	void PackTile( void* devDst );                         /* owned rows, local order (async) */
 	void GetFrame( float* hostOut4 );                      /* finalizeRender output: acc / samplesTaken */
 	int SamplesTaken() const { return samplesTaken; }
 	void GetRayCounts( uint32_t* out17 );
