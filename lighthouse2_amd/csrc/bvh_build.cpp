@@ -13,7 +13,7 @@ namespace lh2 {
 namespace {
 
 constexpr int BINS = 16;
-constexpr float C_TRAV = 1.0f, C_ISECT = 1.0f;
+constexpr float C_ISECT = 1.0f;   /* node-visit cost C_TRAV is a build parameter (relative to one triangle test) */
 constexpr uint32_t PAR_THRESHOLD = 16384;
 
 struct TNode { Aabb box; int left, right; uint32_t first, count; };
@@ -44,6 +44,7 @@ struct Builder
 	std::atomic<int> nodeCount{ 0 };
 	std::atomic<int> threadsLeft{ 0 };
 	int maxLeaf;
+	float C_TRAV = 1.0f;
 
 	explicit Builder( const std::vector<Aabb>& p ) : prims( p ) {}
 
@@ -141,13 +142,15 @@ inline int make_leaf_ref( uint32_t first, uint32_t count ) { return (int)~((firs
 
 }  // namespace
 
-void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out )
+void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost )
 {
 	const uint32_t N = (uint32_t)prims.size();
 	if (maxLeaf < 1) maxLeaf = 1;
 	if (maxLeaf > 16) maxLeaf = 16;
 	Builder b( prims );
 	b.maxLeaf = maxLeaf;
+	b.C_TRAV = traversalCost > 0 ? traversalCost : 1.0f;
+	const float C_TRAV = b.C_TRAV;
 	b.cent.resize( (size_t)N * 3 );
 	b.idx.resize( N );
 	for (uint32_t i = 0; i < N; i++)

@@ -24,7 +24,8 @@ struct BvhOutput
 	double sah = 0;                /* SAH cost of the tree (diagnostics) */
 };
 
-/* prims: per-primitive bounds; maxLeaf: largest leaf; threads: worker threads (0 = hw) */
-void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out );
+/* prims: per-primitive bounds; maxLeaf: largest leaf; threads: worker threads (0 = hw);
+   traversalCost: SAH cost of a node visit relative to one triangle test */
+void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost = 1.0f );
 
 }  // namespace lh2

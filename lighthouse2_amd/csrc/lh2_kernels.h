@@ -83,6 +83,6 @@ void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, hi
 #define LH2_CURSOR_WORDS (LH2_CHUNKS * LH2_CURSOR_STRIDE)   /* per trace launch */
 #define LH2_CURSOR_SLOTS 24                                  /* launches per frame: [L] bounce L, [20] shadow */
 #ifndef LH2_STACK_LDS
-#define LH2_STACK_LDS 24
+#define LH2_STACK_LDS 16
 #endif
 #define LH2_STACK_TOTAL 96

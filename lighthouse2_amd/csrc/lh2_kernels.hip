@@ -150,9 +150,9 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
    traversal: two-level BVH2, ordered, t-culled, LDS short stack + global spill
    ===================================================================================== */
 #ifndef LH2_TRACE_MINWAVES
-#define LH2_TRACE_MINWAVES 1   /* min waves per SIMD the traversal kernels are compiled for (VGPR cap) */
+#define LH2_TRACE_MINWAVES 7   /* min waves per SIMD the traversal kernels are compiled for (VGPR cap 72; A/B: tools/build_variants.sh) */
 #endif
-#define STACK_LDS LH2_STACK_LDS   /* entries per lane kept in LDS: 24 x 256 x 4 B = 24 KB / block */
+#define STACK_LDS LH2_STACK_LDS   /* entries per lane kept in LDS: 16 x 256 x 4 B = 16 KB / block */
 #define STACK_TOTAL LH2_STACK_TOTAL /* + global spill; the host checks the tree depth against it */
 
 LH2_DEV float safe_inv( float d ) { return (d > -1e-30f && d < 1e-30f) ? (d < 0 ? -1e30f : 1e30f) : 1.0f / d; }

@@ -155,6 +155,9 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	   coherent 8x8-tiled primary rays trace best in batches, incoherent bounce rays with refills */
 	else if (!strcmp( name, "refillPrimary" )) refillPrimary = std::min( 64, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "refill" )) refillOther = std::min( 64, std::max( 1, (int)value ) );
+	/* BLAS build parameters, used by later SetGeometry calls */
+	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
+	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
 	else if (!strcmp( name, "blocksPerCU" )) { blocksPerCU = std::min( 16, std::max( 1, (int)value ) ); if (scrwidth) EnsureBuffers(); }
 	/* other names ("clampDirect", "filter", "TAA", ...) are ignored, as in the reference */
 }
@@ -224,7 +227,7 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 			m.aabbLo[k] = std::min( m.aabbLo[k], prims[i].lo[k] ), m.aabbHi[k] = std::max( m.aabbHi[k], prims[i].hi[k] );
 		}
 	}
-	BuildBvh2( prims, 4, 0, m.bvh );
+	BuildBvh2( prims, bvhMaxLeaf, 0, m.bvh, bvhTraversalCost );
 	m.shadeTris.upload( (const float4*)tris, (size_t)triangleCount * 11, stream );
 	m.shadeTris.resize( 11 );
 	CHK_HIP( hipStreamSynchronize( stream ) );

@@ -143,6 +143,8 @@ private:
 	uint32_t* activeLog = nullptr;     /* pinned: active paths after each bounce */
 	int tiledRays = 1;
 	int refillPrimary = 64, refillOther = 16;
+	int bvhMaxLeaf = 2;
+	float bvhTraversalCost = 1.0f;
 	int framePathLengths = 0;
 	double frameHostMs = 0;
 	int samplesTaken = 0;

@@ -52,11 +52,15 @@ def main():
     ap.add_argument("--set", default="both")
     ap.add_argument("--refill", type=int, default=16)
     ap.add_argument("--refill-primary", type=int, default=64)
+    ap.add_argument("--pre-setting", action="append", default=[], help="name=value set before loading (BVH build)")
     ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     sc = scene.config2_scene(n=args.tris)
     core = RenderCore(device=0)
+    for s in args.pre_setting:               # build parameters: before the scene is loaded
+        k, v = s.split("=")
+        core.setting(k, float(v))
     sc.load_into(core)
     core.set_target(1920, 1080, 1)
     core.setting("epsilon", 1e-4)
@@ -81,6 +85,7 @@ def main():
         core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, h.data_ptr(), 2)
         ms = core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, h.data_ptr(), args.iters)
         res[name] = {"rays": n, "ms": round(ms, 4), "Mrays_s": round(n / ms / 1e3, 1)}
+    res["scene"] = core.scene_info()
     print(json.dumps(res))
     core.close()
 
