@@ -60,6 +60,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	const float4* potentials; float4* acc;            /* any, mode 1: fused finalizeConnection */
 	int* gstack;                                      /* stack entries past LH2_STACK_LDS */
 	uint32_t refill;                                  /* refill idle lanes once >= refill are idle (1..64) */
+	uint32_t leafBatch;                               /* run triangle tests once >= leafBatch lanes parked a leaf */
 };
 
 extern "C" {

@@ -219,23 +219,133 @@ LH2_DEV bool mt_test( const float4 a, const float4 b, const float4 c, const TRay
    (bvh_build.cpp flatten), so descending strictly increases the node index, and every pop undoes
    one push.  The stack depth stays within the tree depth, which UpdateToplevel checks against
    LH2_STACK_TOTAL. */
-template <int KIND>
+/* per-lane traversal state of one ray */
+struct TraceState
+{
+	TRay r;
+	float tmin;
+	HitRec best;
+	uint32_t idx;
+	int sp, blasSp, cur, curInst, leaf;   /* leaf: parked BLAS leaf (0 = none) */
+};
+
+/* interior node: test both child boxes, descend into the nearer hit child, push the farther one */
+LH2_DEV void visit_node( const SceneDev& s, TraceState& q, int* __restrict__ lst, int* __restrict__ gst, const uint32_t gstride )
+{
+	const float4* n = s.nodes + (size_t)q.cur * 4;
+	const float4 n0 = n[0], n1 = n[1], n2 = n[2];
+	const int4 n3 = *(const int4*)(n + 3);
+	float tn0, tn1;
+	const bool h0 = box_test( n0.x, n0.y, n0.z, n0.w, n2.x, n2.y, q.r, q.tmin, q.best.t, tn0 );
+	const bool h1 = box_test( n1.x, n1.y, n1.z, n1.w, n2.z, n2.w, q.r, q.tmin, q.best.t, tn1 );
+	if (h0 && h1)
+	{
+		const bool swap = tn1 < tn0;
+		const int farc = swap ? n3.x : n3.y;
+		q.cur = swap ? n3.y : n3.x;
+		/* depth <= LH2_STACK_TOTAL is guaranteed by the host (UpdateToplevel) */
+		if (q.sp < STACK_LDS) lst[q.sp * 256] = farc;
+		else gst[(size_t)(q.sp - STACK_LDS) * gstride] = farc;
+		q.sp++;
+	}
+	else q.cur = h0 ? n3.x : h1 ? n3.y : LH2_POP;
+}
+
+/* TLAS leaf (one instance): object-space ray, not renormalised, so t stays in world units (SURVEY §7
+   step 3); the world ray is re-read from the ray buffer instead of being kept in registers */
+LH2_DEV void enter_instance( const SceneDev& s, const TraceArgs& a, TraceState& q )
+{
+	const int ii = (int)LEAF_FIRST( q.cur );
+	const DevInstance in = s.inst[ii];
+	const float4 o4 = a.rayO[q.idx], d4 = a.rayD[q.idx];
+	const v3 O = mk3( in.inv0.x * o4.x + in.inv0.y * o4.y + in.inv0.z * o4.z + in.inv0.w,
+		in.inv1.x * o4.x + in.inv1.y * o4.y + in.inv1.z * o4.z + in.inv1.w,
+		in.inv2.x * o4.x + in.inv2.y * o4.y + in.inv2.z * o4.z + in.inv2.w );
+	const v3 D = mk3( in.inv0.x * d4.x + in.inv0.y * d4.y + in.inv0.z * d4.z,
+		in.inv1.x * d4.x + in.inv1.y * d4.y + in.inv1.z * d4.z,
+		in.inv2.x * d4.x + in.inv2.y * d4.y + in.inv2.z * d4.z );
+	setup_ray( q.r, O, D );
+	q.blasSp = q.sp, q.curInst = ii;
+	q.cur = in.root;
+}
+
+/* the triangles of one BLAS leaf; any hit: returns true on the first occluder */
+template <bool ANY>
+LH2_DEV bool test_leaf( const SceneDev& s, TraceState& q, const int leafRef )
+{
+	const uint32_t first = LEAF_FIRST( leafRef );
+	const int cnt = LEAF_COUNT( leafRef );
+	for (int k = 0; k < cnt; k++)
+	{
+		const float4* tp = s.tris + (size_t)(first + k) * 3;
+		const float4 ta = tp[0], tb = tp[1], tc = tp[2];
+		float t, u, v;
+		if (mt_test( ta, tb, tc, q.r, t, u, v ) && t > q.tmin)
+		{
+			if (ANY) { if (t < q.best.t) return true; }
+			else
+			{
+				const int tri = __float_as_int( ta.w );
+				if (t < q.best.t || (t == q.best.t && (q.curInst < q.best.inst || (q.curInst == q.best.inst && tri < q.best.tri))))
+					q.best.t = t, q.best.tri = tri, q.best.inst = q.curInst, q.best.u = u, q.best.v = v;
+			}
+		}
+	}
+	return false;
+}
+
+/* cur == LH2_POP: leave the BLAS when its subtree is done (not while a leaf of it is parked),
+   then pop the next subtree; returns true when the ray is finished */
+LH2_DEV bool pop_next( const TraceArgs& a, TraceState& q, int* __restrict__ lst, int* __restrict__ gst, const uint32_t gstride )
+{
+	if (q.sp == q.blasSp && q.leaf == 0)
+	{
+		q.blasSp = -1;
+		const float4 o4 = a.rayO[q.idx], d4 = a.rayD[q.idx];
+		setup_ray( q.r, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ) );
+	}
+	if (q.sp == q.blasSp) return false;            /* waiting for the parked leaf */
+	if (q.sp == 0) return q.leaf == 0;
+	--q.sp;
+	q.cur = q.sp < STACK_LDS ? lst[q.sp * 256] : gst[(size_t)(q.sp - STACK_LDS) * gstride];
+	return false;
+}
+
+/* Ray-stream traversal with dynamic ray fetch (persistent waves, Aila & Laine 2009 "speculative
+   fetch").  Each lane carries one ray's traversal state across loop iterations.  A lane whose ray
+   is finished writes its result and goes idle.  Once at least a.refill lanes of the wave are idle
+   (64: whole batches), they take new rays from the device work queue: one merged atomicAdd per
+   wave, with consecutive indices in lane order.  So the long rays of a batch no longer hold up 63
+   finished lanes.
+   PARK false (coherent primary rays): every iteration runs one step per lane: a node visit, an
+   instance entry, or one leaf's triangle tests, then a pop when the step ends a subtree.
+   PARK true (incoherent rays): lanes that reach a BLAS leaf park it and keep walking.  The
+   triangle tests run for the whole wave at once when at least a.leafBatch lanes hold a parked
+   leaf, or when no lane can take a node step.  Node visits and triangle tests then each run with
+   most lanes busy, instead of both paths serialising in every iteration.
+     KIND 0: closest hit -> hits[idx] = {t, triid, instid, uv16} (uv quantised as pathtracer.h:71,
+             OptiX Prime barycentric convention, converted at the end)
+     KIND 1: any hit -> occlusion bit (RTP_BUFFER_FORMAT_HIT_BITMASK; mask zeroed by the caller)
+     KIND 2: any hit fused with finalizeConnection (connections.h:22-34): unoccluded rays add their
+             potential to the accumulator
+   Termination: the builder emits children after their parent (bvh_build.cpp flatten), so
+   descending strictly increases the node index, and every pop undoes one push.  The stack depth
+   stays within the tree depth, which UpdateToplevel checks against LH2_STACK_TOTAL. */
+template <int KIND, bool PARK>
 LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restrict__ lst, int* __restrict__ gst, const uint32_t gstride )
 {
 	constexpr bool ANY = KIND != 0;
 	const uint32_t count = a.countPtr ? *a.countPtr : a.countFixed;
 	if (count == 0) return;
 	const uint32_t refill = a.refill ? a.refill : 64u;
+	const uint32_t leafBatch = a.leafBatch ? a.leafBatch : 1u;
 	bool active = false, exhausted = false;
-	uint32_t idx = 0;
 	/* this wave's chunk of the ray range: blocks go round-robin over the 8 XCDs, so blockIdx % 8
 	   gives each XCD its own chunk and cursor; a dry chunk moves the wave on to the next one */
 	uint32_t chunk = blockIdx.x % LH2_CHUNKS, tried = 0;
 	uint32_t lo = (uint32_t)(((uint64_t)count * chunk) / LH2_CHUNKS), hi = (uint32_t)(((uint64_t)count * (chunk + 1)) / LH2_CHUNKS);
-	TRay r;
-	float tmin = 0;
-	HitRec best;
-	int sp = 0, blasSp = -1, cur = 0, curInst = -1;
+	TraceState q;
+	q.idx = 0, q.tmin = 0, q.sp = 0, q.blasSp = -1, q.cur = 0, q.curInst = -1, q.leaf = 0;
 	while (true)
 	{
 		/* ---- refill idle lanes (wave-uniform decision) ---- */
@@ -246,14 +356,14 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 			{
 				/* uniform address (readfirstlane): the compiler then merges the idle lanes' adds into
 				   one atomic per wave, handing out consecutive indices in lane order */
-				idx = lo + atomicAdd( a.cursor + __builtin_amdgcn_readfirstlane( chunk ) * LH2_CURSOR_STRIDE, 1u );
-				if (idx < hi)
+				q.idx = lo + atomicAdd( a.cursor + __builtin_amdgcn_readfirstlane( chunk ) * LH2_CURSOR_STRIDE, 1u );
+				if (q.idx < hi)
 				{
-					const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
-					setup_ray( r, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ) );
-					tmin = o4.w;
-					best.t = d4.w, best.tri = -1, best.inst = -1, best.u = 0, best.v = 0;
-					sp = 0, blasSp = -1, cur = s.tlasRoot;
+					const float4 o4 = a.rayO[q.idx], d4 = a.rayD[q.idx];
+					setup_ray( q.r, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ) );
+					q.tmin = o4.w;
+					q.best.t = d4.w, q.best.tri = -1, q.best.inst = -1, q.best.u = 0, q.best.v = 0;
+					q.sp = 0, q.blasSp = -1, q.cur = s.tlasRoot, q.leaf = 0;
 					active = true;
 				}
 				else dry = true;
@@ -270,83 +380,45 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 			if (exhausted) break;
 			continue;
 		}
-		if (!active) continue;
-		/* ---- one traversal step ---- */
 		bool fin = false, occluded = false;
-		if (cur >= 0)
+		if (!PARK)
 		{
-			const float4* n = s.nodes + (size_t)cur * 4;
-			const float4 n0 = n[0], n1 = n[1], n2 = n[2];
-			const int4 n3 = *(const int4*)(n + 3);
-			float tn0, tn1;
-			const bool h0 = box_test( n0.x, n0.y, n0.z, n0.w, n2.x, n2.y, r, tmin, best.t, tn0 );
-			const bool h1 = box_test( n1.x, n1.y, n1.z, n1.w, n2.z, n2.w, r, tmin, best.t, tn1 );
-			if (h0 && h1)
+			if (!active) continue;
+			if (q.cur >= 0) visit_node( s, q, lst, gst, gstride );
+			else if (q.cur != LH2_POP)
 			{
-				const bool swap = tn1 < tn0;
-				const int farc = swap ? n3.x : n3.y;
-				cur = swap ? n3.y : n3.x;
-				/* depth <= LH2_STACK_TOTAL is guaranteed by the host (UpdateToplevel) */
-				if (sp < STACK_LDS) lst[sp * 256] = farc;
-				else gst[(size_t)(sp - STACK_LDS) * gstride] = farc;
-				sp++;
-			}
-			else cur = h0 ? n3.x : h1 ? n3.y : LH2_POP;
-		}
-		else if (cur != LH2_POP)
-		{
-			if (blasSp < 0)
-			{
-				/* TLAS leaf (one instance): object-space ray, not renormalised */
-				const int ii = (int)LEAF_FIRST( cur );
-				const DevInstance in = s.inst[ii];
-				const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
-				const v3 O = mk3( in.inv0.x * o4.x + in.inv0.y * o4.y + in.inv0.z * o4.z + in.inv0.w,
-					in.inv1.x * o4.x + in.inv1.y * o4.y + in.inv1.z * o4.z + in.inv1.w,
-					in.inv2.x * o4.x + in.inv2.y * o4.y + in.inv2.z * o4.z + in.inv2.w );
-				const v3 D = mk3( in.inv0.x * d4.x + in.inv0.y * d4.y + in.inv0.z * d4.z,
-					in.inv1.x * d4.x + in.inv1.y * d4.y + in.inv1.z * d4.z,
-					in.inv2.x * d4.x + in.inv2.y * d4.y + in.inv2.z * d4.z );
-				setup_ray( r, O, D );
-				blasSp = sp, curInst = ii;
-				cur = in.root;
-			}
-			else
-			{
-				const uint32_t first = LEAF_FIRST( cur );
-				const int cnt = LEAF_COUNT( cur );
-				for (int k = 0; k < cnt; k++)
+				if (q.blasSp < 0) enter_instance( s, a, q );
+				else
 				{
-					const float4* tp = s.tris + (size_t)(first + k) * 3;
-					const float4 ta = tp[0], tb = tp[1], tc = tp[2];
-					float t, u, v;
-					if (mt_test( ta, tb, tc, r, t, u, v ) && t > tmin)
-					{
-						if (ANY) { if (t < best.t) { occluded = fin = true; break; } }
-						else
-						{
-							const int tri = __float_as_int( ta.w );
-							if (t < best.t || (t == best.t && (curInst < best.inst || (curInst == best.inst && tri < best.tri))))
-								best.t = t, best.tri = tri, best.inst = curInst, best.u = u, best.v = v;
-						}
-					}
+					occluded = fin = test_leaf<ANY>( s, q, q.cur );
+					q.cur = LH2_POP;
 				}
-				cur = LH2_POP;
 			}
+			if (!fin && q.cur == LH2_POP) fin = pop_next( a, q, lst, gst, gstride );
 		}
-		if (!fin && cur == LH2_POP)
+		else
 		{
-			if (sp == blasSp)
+			const uint32_t parked = (uint32_t)__popcll( __ballot( active && q.leaf != 0 ) );
+			const bool walkers = __ballot( active && q.leaf == 0 ) != 0;
+			if (parked >= leafBatch || !walkers)
 			{
-				blasSp = -1;
-				const float4 o4 = a.rayO[idx], d4 = a.rayD[idx];
-				setup_ray( r, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ) );
+				/* a lane whose leaf was parked at the BLAS exit or with an empty stack resumes with
+				   cur == LH2_POP, and its next node step pops / leaves the BLAS */
+				if (q.leaf != 0)
+				{
+					occluded = fin = test_leaf<ANY>( s, q, q.leaf );
+					q.leaf = 0;
+				}
 			}
-			if (sp == 0) fin = true;
-			else
+			else if (active && q.leaf == 0)
 			{
-				--sp;
-				cur = sp < STACK_LDS ? lst[sp * 256] : gst[(size_t)(sp - STACK_LDS) * gstride];
+				if (q.cur >= 0) visit_node( s, q, lst, gst, gstride );
+				else if (q.cur != LH2_POP)
+				{
+					if (q.blasSp < 0) enter_instance( s, a, q );
+					else { q.leaf = q.cur; q.cur = LH2_POP; }   /* park the BLAS leaf; keep walking */
+				}
+				if (q.cur == LH2_POP) fin = pop_next( a, q, lst, gst, gstride );
 			}
 		}
 		if (fin)
@@ -355,37 +427,38 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 			if (KIND == 0)
 			{
 				uint4 out;
-				if (best.tri < 0) out = make_uint4( fbits( -1.0f ), 0xffffffffu, 0xffffffffu, 0u );
+				if (q.best.tri < 0) out = make_uint4( fbits( -1.0f ), 0xffffffffu, 0xffffffffu, 0u );
 				else
 				{
 					/* OptiX Prime barycentric convention (u = weight of vertex0, v = weight of vertex1),
 					   the one material_shared.h:77-78 interpolates with; MT gave the weights of v1, v2 */
-					const float bu = 1.0f - (best.u + best.v), bv = best.u;
-					out = make_uint4( fbits( best.t ), (uint32_t)best.tri, (uint32_t)best.inst, lh2_f2u( 65535.0f * bu ) + (lh2_f2u( 65535.0f * bv ) << 16) );
+					const float bu = 1.0f - (q.best.u + q.best.v), bv = q.best.u;
+					out = make_uint4( fbits( q.best.t ), (uint32_t)q.best.tri, (uint32_t)q.best.inst, lh2_f2u( 65535.0f * bu ) + (lh2_f2u( 65535.0f * bv ) << 16) );
 				}
-				a.hits[idx] = out;
+				a.hits[q.idx] = out;
 			}
-			else if (KIND == 1) { if (occluded) atomicOr( a.mask + (idx >> 5), 1u << (idx & 31u) ); }
+			else if (KIND == 1) { if (occluded) atomicOr( a.mask + (q.idx >> 5), 1u << (q.idx & 31u) ); }
 			else if (!occluded)
 			{
-				const float4 E = a.potentials[idx];
+				const float4 E = a.potentials[q.idx];
 				acc_add( a.acc, __float_as_uint( E.w ), mk3( E.x, E.y, E.z ) );
 			}
 		}
 	}
 }
 
+template <bool PARK>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_closest( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	trace_stream<0>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	trace_stream<0, PARK>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 }
 
 template <int MODE>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_any( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	trace_stream<MODE == 0 ? 1 : 2>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	trace_stream<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 }
 
 /* =====================================================================================
@@ -1223,7 +1296,11 @@ void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, 
 	if (jobCount <= 0) return;
 	k_camera<<<(jobCount + 255) / 256, 256, 0, st>>>( *p, bn, rayO, rayD, T4, Q4, jobCount );
 }
-void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, hipStream_t st ) { k_trace_closest<<<grid, 256, 0, st>>>( *s, *a ); }
+void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, hipStream_t st )
+{
+	if (a->leafBatch) k_trace_closest<true><<<grid, 256, 0, st>>>( *s, *a );   /* incoherent rays: parked leaves */
+	else k_trace_closest<false><<<grid, 256, 0, st>>>( *s, *a );
+}
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, hipStream_t st )
 {
 	if (fused) k_trace_any<1><<<grid, 256, 0, st>>>( *s, *a );
@@ -1232,7 +1309,7 @@ void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int 
 int lh2_trace_blocks_per_cu( void )
 {
 	int n1 = 0, n2 = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest, 256, 0 ) != hipSuccess) n1 = 4;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest<true>, 256, 0 ) != hipSuccess) n1 = 4;
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_any<1>, 256, 0 ) != hipSuccess) n2 = 4;
 	return n1 > n2 ? n1 : n2;
 }

@@ -155,6 +155,9 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	   coherent 8x8-tiled primary rays trace best in batches, incoherent bounce rays with refills */
 	else if (!strcmp( name, "refillPrimary" )) refillPrimary = std::min( 64, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "refill" )) refillOther = std::min( 64, std::max( 1, (int)value ) );
+	/* traversal: test parked BLAS leaves once this many lanes of a wave hold one (0 = every step) */
+	else if (!strcmp( name, "leafBatch" )) leafBatch = std::min( 64, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "leafBatchPrimary" )) leafBatchPrimary = std::min( 64, std::max( 0, (int)value ) );
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
@@ -430,6 +433,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		TraceArgs ta{};
 		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.countPtr = &c->activePaths, ta.cursor = fetchCursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
+		ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
 		ta.hits = hits.ptr, ta.gstack = gstack.ptr;
 		lh2_launch_trace_closest( &sd, &ta, grid, stream );
 		CHK_HIP( hipEventRecord( evTrace[2 * pathLength + 1], stream ) );
@@ -462,7 +466,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	CHK_HIP( hipEventRecord( evShadow[0], stream ) );
 	{
 		TraceArgs ta{};
-		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = fetchCursors.ptr + (size_t)20 * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther;
+		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = fetchCursors.ptr + (size_t)20 * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
 		lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
 	}
@@ -569,7 +573,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
-	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther;
+	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -587,7 +591,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	CHK_HIP( hipMemsetAsync( m.ptr, 0, words * 4, stream ) );
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
-	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther;
+	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, stream );
 	std::vector<uint32_t> tmp( words );
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
@@ -611,7 +615,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 	{
 		TraceArgs ta{};
 		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.cursor = cursors.ptr + (size_t)i * LH2_CURSOR_WORDS;
-		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr, ta.refill = (uint32_t)refillOther;
+		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	}
 	CHK_HIP( hipEventRecord( b, stream ) );

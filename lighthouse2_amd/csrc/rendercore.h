@@ -142,7 +142,7 @@ private:
 	hipEvent_t evCount[18] = {};
 	uint32_t* activeLog = nullptr;     /* pinned: active paths after each bounce */
 	int tiledRays = 1;
-	int refillPrimary = 64, refillOther = 16;
+	int refillPrimary = 64, refillOther = 16, leafBatch = 16, leafBatchPrimary = 0;
 	int bvhMaxLeaf = 2;
 	float bvhTraversalCost = 1.0f;
 	int framePathLengths = 0;

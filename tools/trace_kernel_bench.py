@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--set", default="both")
     ap.add_argument("--refill", type=int, default=16)
     ap.add_argument("--refill-primary", type=int, default=64)
+    ap.add_argument("--leaf-batch", type=int, default=16)
+    ap.add_argument("--leaf-batch-primary", type=int, default=0)
     ap.add_argument("--pre-setting", action="append", default=[], help="name=value set before loading (BVH build)")
     ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
     args = ap.parse_args()
@@ -79,6 +81,7 @@ def main():
             continue
         n = len(o)
         core.setting("refill", args.refill_primary if name == "primary" else args.refill)
+        core.setting("leafBatch", args.leaf_batch_primary if name == "primary" else args.leaf_batch)
         ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
         h = torch.empty((n, 4), dtype=torch.int32, device=dev)
         torch.cuda.synchronize()
