@@ -1080,7 +1080,10 @@ LH2_DEV v3 fixnan( v3 a ) { if (!isfinite_( a.x + a.y + a.z )) a = s3( 0 ); retu
 LH2_DEV float SurvivalProbability( const v3 a ) { return fminf( 1.0f, fmaxf( fmaxf( a.x, a.y ), a.z ) ); }
 
 /* ---- shade kernel: pathtracer.h:54-245 --------------------------------------------------- */
-__global__ __launch_bounds__( 256 ) void k_shade( const SceneDev s, const ShadeParams p )
+#ifndef LH2_SHADE_MINWAVES
+#define LH2_SHADE_MINWAVES 1
+#endif
+__global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const SceneDev s, const ShadeParams p )
 {
 	const uint32_t count = *p.pathCount;
 	const uint32_t gstride = gridDim.x * 256u;

@@ -195,3 +195,41 @@ def test_band_partition_matches_full_frame(core):
     frame = parallel.assemble(tiles, world, h)
     assert rel_l2(frame[..., :3], full[..., :3]) <= 1e-6
     assert np.array_equal(frame[..., 3], full[..., 3])
+
+
+def test_instanced_animated_frames_parity(core):
+    """Config 5 in miniature: several instanced meshes, new instance transforms every frame
+    (SetInstance + UpdateToplevel), 2 spp, converging frames."""
+    w, h = 96, 54
+    sc = scene.instanced_scene(meshes=4, tris_per_mesh=3000, width=w, height=h, grid=2, spacing=12.0)
+    sc.view = scene.camera_view((0, 6, -12), (0, -0.3, 1), fov_deg=60, aspect=w / h, pixel_height=h)
+    o = _load_both(core, sc, w, h, spp=2)
+    for f in range(3):
+        scene.animate_instances(sc, f)
+        for tgt in (core, o):
+            for k, (mesh, T) in enumerate(sc.instances):
+                tgt.set_instance(k, mesh, T)
+            tgt.update_toplevel()
+        sc.render_frame(core, converge=1 if f == 0 else 0)
+        sc.render_frame(o, converge=1 if f == 0 else 0)
+        assert np.array_equal(core.ray_counts(), o.ray_counts())
+    ag, ao = core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+
+
+def test_room_depth4_parity(core):
+    """Config 3 in miniature: the procedural room (specular chains, glass, smooth spheres, two area
+    lights) with maxPathLength 4."""
+    w, h = 128, 72
+    sc = scene.room_scene(40000, w, h)
+    o = _load_both(core, sc, w, h)
+    for tgt in (core, o):
+        tgt.setting("maxPathLength", 4)
+    sc.render_frame(core)
+    sc.render_frame(o)
+    cg, co = core.ray_counts(), o.ray_counts()
+    assert np.array_equal(cg, co), (cg, co)
+    assert co[4] == 0 and co[3] > 0                 # bounded at 4 vertices, specular chains reach it
+    ag, ao = core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+    core.setting("maxPathLength", 16)
