@@ -24,7 +24,7 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
 def _pmc(path, kernel):
     vals, durs = [], []
     for r in csv.DictReader(open(path)):
-        if r["Kernel_Name"].startswith(kernel):
+        if kernel in r["Kernel_Name"]:
             vals.append(float(r["Counter_Value"]))
             durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     return vals, durs
@@ -45,7 +45,7 @@ def main():
     fetch, fd = _pmc(src / "pmc_fetch" / "run_counter_collection.csv", kernel)
     write, wd = _pmc(src / "pmc_write" / "run_counter_collection.csv", kernel)
     # kernel-trace durations of the roofline launches in the profiled bench run (the last kernel_iters)
-    rows = [r for r in csv.DictReader(open(src / "stats" / "run_kernel_trace.csv")) if r["Kernel_Name"].startswith(kernel)]
+    rows = [r for r in csv.DictReader(open(src / "stats" / "run_kernel_trace.csv")) if kernel in r["Kernel_Name"]]
     iters = 20
     trace_ms = statistics.mean(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[-iters:]) / 1e6
     rays = bench["roofline"]["rays_per_launch"]
