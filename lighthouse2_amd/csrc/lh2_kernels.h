@@ -36,6 +36,7 @@ struct SceneDev       /* everything the traversal and shading kernels read, by v
 	int skyW, skyH;
 	const uint8_t* blueNoise;
 	float geometryEpsilon, clampValue;
+	const int* sceneError;           /* nonzero: the scene is unsafe to traverse (TLAS too deep); trace kernels exit */
 };
 
 struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path state */

@@ -336,7 +336,7 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 {
 	constexpr bool ANY = KIND != 0;
 	const uint32_t count = a.countPtr ? *a.countPtr : a.countFixed;
-	if (count == 0) return;
+	if (count == 0 || *s.sceneError) return;
 	const uint32_t refill = a.refill ? a.refill : 64u;
 	const uint32_t leafBatch = a.leafBatch ? a.leafBatch : 1u;
 	bool active = false, exhausted = false;

@@ -114,6 +114,10 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	for (auto& e : evShadow) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evCount) CHK_HIP( hipEventCreateWithFlags( &e, hipEventDisableTiming ) );
+	for (auto& e : evStage) CHK_HIP( hipEventCreateWithFlags( &e, hipEventDisableTiming ) );
+	dSceneError.resize( 1 ), dTlasDepth.resize( 1 );
+	CHK_HIP( hipMemsetAsync( dSceneError.ptr, 0, sizeof( int ), stream ) );
+	CHK_HIP( hipMemsetAsync( dTlasDepth.ptr, 0, sizeof( int ), stream ) );
 	CHK_HIP( hipHostMalloc( (void**)&activeLog, sizeof( uint32_t ) * 20, hipHostMallocDefault ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
@@ -161,6 +165,9 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
+	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
+	else if (!strcmp( name, "gpuTlas" )) { gpuTlas = value != 0; instancesDirty = true; }
+	else if (!strcmp( name, "plocRadius" )) gpuBvh.radius = std::min( 32, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "blocksPerCU" )) { blocksPerCU = std::min( 16, std::max( 1, (int)value ) ); if (scrwidth) EnsureBuffers(); }
 	/* other names ("clampDirect", "filter", "TAA", ...) are ignored, as in the reference */
 }
@@ -216,25 +223,58 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 	if (meshIdx == (int)meshes.size()) meshes.push_back( new CoreMeshHost() );
 	CoreMeshHost& m = *meshes[meshIdx];
 	const auto t0 = std::chrono::high_resolution_clock::now();
-	m.tris.assign( tris, tris + triangleCount );
-	std::vector<Aabb> prims( triangleCount );
-	for (int k = 0; k < 3; k++) m.aabbLo[k] = 1e30f, m.aabbHi[k] = -1e30f;
-	for (int i = 0; i < triangleCount; i++)
-	{
-		const lh2_CoreTri& t = tris[i];
-		const float v[3][3] = { { t.vertex0.x, t.vertex0.y, t.vertex0.z }, { t.vertex1.x, t.vertex1.y, t.vertex1.z }, { t.vertex2.x, t.vertex2.y, t.vertex2.z } };
-		for (int k = 0; k < 3; k++)
-		{
-			prims[i].lo[k] = std::min( std::min( v[0][k], v[1][k] ), v[2][k] );
-			prims[i].hi[k] = std::max( std::max( v[0][k], v[1][k] ), v[2][k] );
-			m.aabbLo[k] = std::min( m.aabbLo[k], prims[i].lo[k] ), m.aabbHi[k] = std::max( m.aabbHi[k], prims[i].hi[k] );
-		}
-	}
-	BuildBvh2( prims, bvhMaxLeaf, 0, m.bvh, bvhTraversalCost );
+	m.triCount = triangleCount;
 	m.shadeTris.upload( (const float4*)tris, (size_t)triangleCount * 11, stream );
 	m.shadeTris.resize( 11 );
-	CHK_HIP( hipStreamSynchronize( stream ) );
-	m.dirty = true;
+	bool cpuBuild = !(gpuBuild && triangleCount >= 2);
+	if (!cpuBuild)
+	{
+		/* GPU PLOC build straight from the uploaded CoreTri records (bvh_gpu.h) */
+		float4 *nodes = nullptr, *tris48 = nullptr;
+		GpuBuildResult r;
+		gpuBvh.BuildBlas( m.shadeTris.ptr, triangleCount, bvhMaxLeaf, bvhTraversalCost, &nodes, &tris48, r, stream );
+		m.bvhNodes.adopt( nodes, (size_t)r.nodeCount * 4 );
+		m.bvhTris.adopt( tris48, (size_t)triangleCount * 3 );
+		m.nodeCount = r.nodeCount, m.maxDepth = r.maxDepth;
+		for (int k = 0; k < 3; k++) m.aabbLo[k] = r.lo[k], m.aabbHi[k] = r.hi[k];
+		/* pathological inputs (e.g. long runs of nearly coincident triangles) can make a clustered tree
+		   deep; the top-down SAH build bounds the depth by splitting such ranges in the middle */
+		if (r.maxDepth > LH2_STACK_TOTAL / 2) cpuBuild = true;
+	}
+	if (cpuBuild)
+	{
+		/* CPU binned-SAH build (bvh_build.cpp) */
+		std::vector<Aabb> prims( triangleCount );
+		for (int k = 0; k < 3; k++) m.aabbLo[k] = 1e30f, m.aabbHi[k] = -1e30f;
+		for (int i = 0; i < triangleCount; i++)
+		{
+			const lh2_CoreTri& t = tris[i];
+			const float v[3][3] = { { t.vertex0.x, t.vertex0.y, t.vertex0.z }, { t.vertex1.x, t.vertex1.y, t.vertex1.z }, { t.vertex2.x, t.vertex2.y, t.vertex2.z } };
+			for (int k = 0; k < 3; k++)
+			{
+				prims[i].lo[k] = std::min( std::min( v[0][k], v[1][k] ), v[2][k] );
+				prims[i].hi[k] = std::max( std::max( v[0][k], v[1][k] ), v[2][k] );
+				m.aabbLo[k] = std::min( m.aabbLo[k], prims[i].lo[k] ), m.aabbHi[k] = std::max( m.aabbHi[k], prims[i].hi[k] );
+			}
+		}
+		BvhOutput bvh;
+		BuildBvh2( prims, bvhMaxLeaf, 0, bvh, bvhTraversalCost );
+		std::vector<float> tris48( (size_t)std::max( triangleCount, 1 ) * 12, 0.0f );
+		for (size_t j = 0; j < bvh.perm.size(); j++)
+		{
+			const uint32_t ti = bvh.perm[j];
+			const lh2_CoreTri& t = tris[ti];
+			float* o = &tris48[j * 12];
+			/* v0, e1 = v1 - v0, e2 = v2 - v0 in fp32, exactly as the oracle's intersect_tri */
+			o[0] = t.vertex0.x, o[1] = t.vertex0.y, o[2] = t.vertex0.z; memcpy( &o[3], &ti, 4 );
+			o[4] = t.vertex1.x - t.vertex0.x, o[5] = t.vertex1.y - t.vertex0.y, o[6] = t.vertex1.z - t.vertex0.z, o[7] = 0;
+			o[8] = t.vertex2.x - t.vertex0.x, o[9] = t.vertex2.y - t.vertex0.y, o[10] = t.vertex2.z - t.vertex0.z, o[11] = 0;
+		}
+		m.bvhNodes.upload( (const float4*)bvh.nodes.data(), bvh.nodes.size() / 4, stream );
+		m.bvhTris.upload( (const float4*)tris48.data(), tris48.size() / 4, stream );
+		m.nodeCount = (int)(bvh.nodes.size() / 16), m.maxDepth = bvh.maxDepth;
+	}
+	CHK_HIP( hipStreamSynchronize( stream ) );   /* the caller's triangle array is borrowed for this call only */
 	geometryDirty = true;
 	coreStats.bvhBuildTime += std::chrono::duration<float>( std::chrono::high_resolution_clock::now() - t0 ).count();
 }
@@ -249,136 +289,173 @@ void RenderCore::SetInstance( int instanceIdx, int meshIdx, const float* M )   /
 	instancesDirty = true;
 }
 
+/* scene node array = all BLAS (relocated, device to device) followed by room for the TLAS */
+void RenderCore::ConcatenateBlas( int ni )
+{
+	meshNodeBase.assign( meshes.size(), 0 ), meshTriBase.assign( meshes.size(), 0 );
+	int nodeTotal = 0, triTotal = 0;
+	maxBlasDepth = 0;
+	std::vector<float> bounds( std::max<size_t>( meshes.size(), 1 ) * 6, 0.0f );
+	for (size_t mi = 0; mi < meshes.size(); mi++)
+	{
+		const CoreMeshHost& m = *meshes[mi];
+		meshNodeBase[mi] = nodeTotal, meshTriBase[mi] = triTotal;
+		nodeTotal += m.nodeCount, triTotal += m.triCount;
+		maxBlasDepth = std::max( maxBlasDepth, m.maxDepth );
+		for (int k = 0; k < 3; k++) bounds[mi * 6 + k] = m.aabbLo[k], bounds[mi * 6 + 3 + k] = m.aabbHi[k];
+		if (m.triCount == 0) bounds[mi * 6] = 1.0f, bounds[mi * 6 + 3] = 0.0f;   /* empty-mesh marker */
+	}
+	tlasCapacity = std::max( 64, 2 * ni + 16 );
+	CHK_HIP( hipStreamSynchronize( stream ) );   /* frames in flight may still read the old arrays */
+	dNodes.free(), dTris.free();
+	dNodes.resize( ((size_t)nodeTotal + tlasCapacity) * 4 );
+	dTris.resize( (size_t)std::max( triTotal, 1 ) * 3 );
+	for (size_t mi = 0; mi < meshes.size(); mi++)
+	{
+		const CoreMeshHost& m = *meshes[mi];
+		GpuBvhBuilder::Relocate( m.bvhNodes.ptr, m.nodeCount, meshNodeBase[mi], (uint32_t)meshTriBase[mi], dNodes.ptr, stream );
+		if (m.triCount) CHK_HIP( hipMemcpyAsync( dTris.ptr + (size_t)meshTriBase[mi] * 3, m.bvhTris.ptr, sizeof( float4 ) * 3 * (size_t)m.triCount, hipMemcpyDeviceToDevice, stream ) );
+	}
+	dMeshBounds.upload( bounds.data(), bounds.size(), stream );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	blasNodeCount = nodeTotal, blasTriCount = triTotal;
+	geometryDirty = false;
+}
+
 void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 (instance descriptors) */
 {
 	const int ni = (int)instances.size();
-	/* TLAS over instance world bounds (8 transformed corners of the mesh bounds), 1 instance per leaf */
-	std::vector<Aabb> prims;
-	std::vector<int> primInst;
+	if (geometryDirty || ni + 1 > tlasCapacity) ConcatenateBlas( ni );
+	tlasRoot = blasNodeCount;
+	/* host part: inverse transforms and instance records, written to pinned staging (double-buffered)
+	   and copied asynchronously; no host-device round trip per frame */
+	const int slot = stageSlot;
+	stageSlot ^= 1;
+	const size_t nRec = (size_t)std::max( ni, 1 );
+	const size_t offInst = 0, offDesc = offInst + nRec * sizeof( DevInstance ), offT = offDesc + nRec * sizeof( lh2_CoreInstanceDesc );
+	const size_t offMesh = offT + nRec * 64, offNodes = offMesh + nRec * 4, need = offNodes + 4 * 64 * nRec + 64;
+	CHK_HIP( hipEventSynchronize( evStage[slot] ) );   /* the copies from this slot two updates ago are done */
+	if (need > stageBytes[slot])
+	{
+		if (stage[slot]) CHK_HIP( hipHostFree( stage[slot] ) );
+		stageBytes[slot] = need + need / 2;
+		CHK_HIP( hipHostMalloc( (void**)&stage[slot], stageBytes[slot], hipHostMallocDefault ) );
+	}
+	uint8_t* sb = stage[slot];
+	DevInstance* di = (DevInstance*)(sb + offInst);
+	lh2_CoreInstanceDesc* desc = (lh2_CoreInstanceDesc*)(sb + offDesc);
+	float* Ts = (float*)(sb + offT);
+	int* meshIds = (int*)(sb + offMesh);
+	memset( sb, 0, offMesh + nRec * 4 );
 	for (int i = 0; i < ni; i++)
 	{
 		CoreInstanceHost& in = instances[i];
 		Mat4Inverse( in.T, in.inv );
-		const CoreMeshHost& m = *meshes[in.mesh];
-		if (m.tris.empty()) continue;
-		Aabb b;
-		for (int k = 0; k < 3; k++) b.lo[k] = 1e30f, b.hi[k] = -1e30f;
-		for (int c = 0; c < 8; c++)
-		{
-			const float p[3] = { (c & 1) ? m.aabbHi[0] : m.aabbLo[0], (c & 2) ? m.aabbHi[1] : m.aabbLo[1], (c & 4) ? m.aabbHi[2] : m.aabbLo[2] };
-			for (int k = 0; k < 3; k++)
-			{
-				const float* r = in.T + k * 4;
-				const float v = r[0] * p[0] + r[1] * p[1] + r[2] * p[2] + r[3];
-				b.lo[k] = std::min( b.lo[k], v ), b.hi[k] = std::max( b.hi[k], v );
-			}
-		}
-		/* pad by a relative epsilon: the ray is transformed in fp32 on the device */
-		for (int k = 0; k < 3; k++)
-		{
-			const float e = 1e-5f * std::max( std::fabs( b.lo[k] ), std::fabs( b.hi[k] ) ) + 1e-30f;
-			b.lo[k] -= e, b.hi[k] += e;
-		}
-		prims.push_back( b ), primInst.push_back( i );
-	}
-	BvhOutput tlas;
-	BuildBvh2( prims, 1, 1, tlas );
-	/* concatenate BLAS nodes / triangles (only when geometry changed) */
-	const int tlasNodes = (int)(tlas.nodes.size() / 16);
-	if (geometryDirty || (size_t)(blasNodeCount + tlasNodes) * 4 > dNodes.count)
-	{
-		meshNodeBase.assign( meshes.size(), 0 ), meshTriBase.assign( meshes.size(), 0 );
-		int nodeTotal = 0, triTotal = 0, maxBlasDepth = 0;
-		for (size_t mi = 0; mi < meshes.size(); mi++)
-		{
-			meshNodeBase[mi] = nodeTotal, meshTriBase[mi] = triTotal;
-			nodeTotal += (int)(meshes[mi]->bvh.nodes.size() / 16);
-			triTotal += (int)meshes[mi]->tris.size();
-			maxBlasDepth = std::max( maxBlasDepth, meshes[mi]->bvh.maxDepth );
-		}
-		std::vector<float> nodes( ((size_t)nodeTotal + tlasNodes + 2 * (size_t)ni + 16) * 16 );
-		std::vector<float> tris48( (size_t)std::max( triTotal, 1 ) * 12 );
-		for (size_t mi = 0; mi < meshes.size(); mi++)
-		{
-			const CoreMeshHost& m = *meshes[mi];
-			const int nb = meshNodeBase[mi], tb = meshTriBase[mi];
-			const size_t nn = m.bvh.nodes.size() / 16;
-			memcpy( &nodes[(size_t)nb * 16], m.bvh.nodes.data(), m.bvh.nodes.size() * sizeof( float ) );
-			for (size_t k = 0; k < nn; k++)
-			{
-				int* refs = (int*)&nodes[((size_t)nb + k) * 16 + 12];
-				for (int c = 0; c < 2; c++)
-				{
-					if (refs[c] >= 0) refs[c] += nb;
-					else refs[c] = MAKE_LEAF( LEAF_FIRST( refs[c] ) + (uint32_t)tb, LEAF_COUNT( refs[c] ) );
-				}
-			}
-			for (size_t j = 0; j < m.bvh.perm.size(); j++)
-			{
-				const uint32_t ti = m.bvh.perm[j];
-				const lh2_CoreTri& t = m.tris[ti];
-				float* o = &tris48[((size_t)tb + j) * 12];
-				/* v0, e1 = v1 - v0, e2 = v2 - v0 in fp32, exactly as the oracle's intersect_tri */
-				o[0] = t.vertex0.x, o[1] = t.vertex0.y, o[2] = t.vertex0.z; memcpy( &o[3], &ti, 4 );
-				o[4] = t.vertex1.x - t.vertex0.x, o[5] = t.vertex1.y - t.vertex0.y, o[6] = t.vertex1.z - t.vertex0.z, o[7] = 0;
-				o[8] = t.vertex2.x - t.vertex0.x, o[9] = t.vertex2.y - t.vertex0.y, o[10] = t.vertex2.z - t.vertex0.z, o[11] = 0;
-			}
-		}
-		blasNodeCount = nodeTotal, blasTriCount = triTotal;
-		dNodes.upload( (const float4*)nodes.data(), nodes.size() / 4, stream );
-		dTris.upload( (const float4*)tris48.data(), tris48.size() / 4, stream );
-		sceneMaxDepth = maxBlasDepth;
-		for (auto* m : meshes) m->dirty = false;
-		geometryDirty = false;
-	}
-	/* TLAS: leaf first -> instance index, interior refs offset behind the BLAS nodes */
-	const size_t tn = tlas.nodes.size() / 16;
-	for (size_t k = 0; k < tn; k++)
-	{
-		int* refs = (int*)&tlas.nodes[k * 16 + 12];
-		for (int c = 0; c < 2; c++)
-		{
-			if (refs[c] >= 0) refs[c] += blasNodeCount;
-			else if (!prims.empty())
-			{
-				if (LEAF_COUNT( refs[c] ) != 1) FatalError( "TLAS leaf with %d instances", LEAF_COUNT( refs[c] ) );
-				refs[c] = MAKE_LEAF( (uint32_t)primInst[tlas.perm[LEAF_FIRST( refs[c] )]], 1 );
-			}
-		}
-	}
-	tlasRoot = blasNodeCount;
-	CHK_HIP( hipMemcpyAsync( dNodes.ptr + (size_t)blasNodeCount * 4, tlas.nodes.data(), tlas.nodes.size() * sizeof( float ), hipMemcpyHostToDevice, stream ) );
-	int maxBlasDepth = 0;
-	for (auto* m : meshes) maxBlasDepth = std::max( maxBlasDepth, m->bvh.maxDepth );
-	sceneMaxDepth = tlas.maxDepth + maxBlasDepth;
-	if (sceneMaxDepth >= LH2_STACK_TOTAL - 1) FatalError( "BVH depth %d exceeds the traversal stack (%d)", sceneMaxDepth, LH2_STACK_TOTAL );
-	/* instance records for traversal and shading */
-	std::vector<DevInstance> di( std::max( ni, 1 ) );
-	std::vector<lh2_CoreInstanceDesc> desc( std::max( ni, 1 ) );
-	for (int i = 0; i < ni; i++)
-	{
-		const CoreInstanceHost& in = instances[i];
 		di[i].inv0 = make_float4( in.inv[0], in.inv[1], in.inv[2], in.inv[3] );
 		di[i].inv1 = make_float4( in.inv[4], in.inv[5], in.inv[6], in.inv[7] );
 		di[i].inv2 = make_float4( in.inv[8], in.inv[9], in.inv[10], in.inv[11] );
 		di[i].root = meshNodeBase[in.mesh], di[i].triBase = meshTriBase[in.mesh], di[i].mesh = in.mesh, di[i].pad = 0;
-		memset( &desc[i], 0, sizeof( desc[i] ) );
 		desc[i].triangles = meshes[in.mesh]->shadeTris.ptr;
 		desc[i].A = { in.inv[0], in.inv[1], in.inv[2], in.inv[3] };
 		desc[i].B = { in.inv[4], in.inv[5], in.inv[6], in.inv[7] };
 		desc[i].C = { in.inv[8], in.inv[9], in.inv[10], in.inv[11] };
 		desc[i].D = { in.inv[12], in.inv[13], in.inv[14], in.inv[15] };
+		memcpy( Ts + (size_t)i * 16, in.T, 64 );
+		meshIds[i] = in.mesh;
 	}
-	dInst.upload( (const uint8_t*)di.data(), di.size() * sizeof( DevInstance ), stream );
-	dInstDesc.upload( desc.data(), desc.size(), stream );
-	CHK_HIP( hipStreamSynchronize( stream ) );
+	dInst.resize( nRec * sizeof( DevInstance ) ), dInstDesc.resize( nRec ), dInstT.resize( nRec * 16 ), dInstMesh.resize( nRec );
+	dSceneError.resize( 1 ), dTlasDepth.resize( 1 );
+	CHK_HIP( hipMemcpyAsync( dInst.ptr, di, nRec * sizeof( DevInstance ), hipMemcpyHostToDevice, stream ) );
+	CHK_HIP( hipMemcpyAsync( dInstDesc.ptr, desc, nRec * sizeof( lh2_CoreInstanceDesc ), hipMemcpyHostToDevice, stream ) );
+	CHK_HIP( hipMemsetAsync( dSceneError.ptr, 0, sizeof( int ), stream ) );
+	if (ni >= 2 && gpuTlas)
+	{
+		/* TLAS built on the device from the instance transforms (bvh_gpu.h) */
+		CHK_HIP( hipMemcpyAsync( dInstT.ptr, Ts, nRec * 64, hipMemcpyHostToDevice, stream ) );
+		CHK_HIP( hipMemcpyAsync( dInstMesh.ptr, meshIds, nRec * 4, hipMemcpyHostToDevice, stream ) );
+		GpuTlasArgs ta;
+		ta.T = dInstT.ptr, ta.instMesh = dInstMesh.ptr, ta.meshBounds = dMeshBounds.ptr, ta.count = ni;
+		ta.nodeBase = blasNodeCount, ta.nodes = dNodes.ptr, ta.maxBlasDepth = maxBlasDepth;
+		ta.sceneError = dSceneError.ptr, ta.tlasDepth = dTlasDepth.ptr;
+		gpuBvh.BuildTlas( ta, stream );
+		tlasOnDevice = true;
+		sceneMaxDepth = -1;   /* known on the device; SceneInfo reads it */
+	}
+	else
+	{
+		/* host TLAS (binned SAH) over instance world bounds, 1 instance per leaf */
+		std::vector<Aabb> prims;
+		std::vector<int> primInst;
+		for (int i = 0; i < ni; i++)
+		{
+			const CoreInstanceHost& in = instances[i];
+			const CoreMeshHost& m = *meshes[in.mesh];
+			if (m.triCount == 0) continue;
+			Aabb b;
+			for (int k = 0; k < 3; k++) b.lo[k] = 1e30f, b.hi[k] = -1e30f;
+			for (int c = 0; c < 8; c++)
+			{
+				const float p[3] = { (c & 1) ? m.aabbHi[0] : m.aabbLo[0], (c & 2) ? m.aabbHi[1] : m.aabbLo[1], (c & 4) ? m.aabbHi[2] : m.aabbLo[2] };
+				for (int k = 0; k < 3; k++)
+				{
+					const float* r = in.T + k * 4;
+					const float v = r[0] * p[0] + r[1] * p[1] + r[2] * p[2] + r[3];
+					b.lo[k] = std::min( b.lo[k], v ), b.hi[k] = std::max( b.hi[k], v );
+				}
+			}
+			/* pad by a relative epsilon: the ray is transformed in fp32 on the device */
+			for (int k = 0; k < 3; k++)
+			{
+				const float e = 1e-5f * std::max( std::fabs( b.lo[k] ), std::fabs( b.hi[k] ) ) + 1e-30f;
+				b.lo[k] -= e, b.hi[k] += e;
+			}
+			prims.push_back( b ), primInst.push_back( i );
+		}
+		BvhOutput tlas;
+		BuildBvh2( prims, 1, 1, tlas );
+		const size_t tn = tlas.nodes.size() / 16;
+		if (tn > (size_t)tlasCapacity) FatalError( "TLAS of %zu nodes exceeds its capacity %d", tn, tlasCapacity );
+		for (size_t k = 0; k < tn; k++)
+		{
+			int* refs = (int*)&tlas.nodes[k * 16 + 12];
+			for (int c = 0; c < 2; c++)
+			{
+				if (refs[c] >= 0) refs[c] += blasNodeCount;
+				else if (!prims.empty())
+				{
+					if (LEAF_COUNT( refs[c] ) != 1) FatalError( "TLAS leaf with %d instances", LEAF_COUNT( refs[c] ) );
+					refs[c] = MAKE_LEAF( (uint32_t)primInst[tlas.perm[LEAF_FIRST( refs[c] )]], 1 );
+				}
+			}
+		}
+		if (tlas.nodes.size() * sizeof( float ) > need - offNodes) FatalError( "TLAS staging overflow" );
+		memcpy( sb + offNodes, tlas.nodes.data(), tlas.nodes.size() * sizeof( float ) );
+		CHK_HIP( hipMemcpyAsync( dNodes.ptr + (size_t)blasNodeCount * 4, sb + offNodes, tlas.nodes.size() * sizeof( float ), hipMemcpyHostToDevice, stream ) );
+		sceneMaxDepth = tlas.maxDepth + maxBlasDepth;
+		tlasOnDevice = false;
+		if (sceneMaxDepth >= LH2_STACK_TOTAL - 1) FatalError( "BVH depth %d exceeds the traversal stack (%d)", sceneMaxDepth, LH2_STACK_TOTAL );
+	}
+	CHK_HIP( hipEventRecord( evStage[slot], stream ) );
 	instancesDirty = false;
+}
+
+/* device-side scene errors (TLAS deeper than the traversal stack): the trace kernels skip the
+   frame, and the host reports it here */
+void RenderCore::CheckSceneError()
+{
+	if (!dSceneError.ptr) return;
+	int e = 0;
+	CHK_HIP( hipMemcpyAsync( &hostStats->sceneError, dSceneError.ptr, sizeof( int ), hipMemcpyDeviceToHost, stream ) );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	e = hostStats->sceneError;
+	if (e) FatalError( "BVH depth exceeds the traversal stack (%d levels)", LH2_STACK_TOTAL );
 }
 
 SceneDev RenderCore::MakeSceneDev() const
 {
 	SceneDev s;
 	s.nodes = dNodes.ptr, s.tris = dTris.ptr, s.inst = (const DevInstance*)dInst.ptr;
+	s.sceneError = dSceneError.ptr;
 	s.tlasRoot = tlasRoot, s.instCount = (int)instances.size();
 	s.instDesc = dInstDesc.ptr, s.materials = dMaterials.ptr;
 	s.areaLights = dArea.ptr, s.pointLights = dPoint.ptr, s.spotLights = dSpot.ptr, s.dirLights = dDir.ptr;
@@ -475,6 +552,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, stream );
 	CHK_HIP( hipMemcpyAsync( &hostStats->counters, c, sizeof( Counters ), hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipMemcpyAsync( hostStats->rayCount + 1, rayLog.ptr + 1, sizeof( uint32_t ) * 16, hipMemcpyDeviceToHost, stream ) );
+	CHK_HIP( hipMemcpyAsync( &hostStats->sceneError, dSceneError.ptr, sizeof( int ), hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipEventRecord( evFrame[1], stream ) );
 	hostStats->rayCount[0] = pathCount;
 	framePathLengths = pl;
@@ -502,6 +580,7 @@ void RenderCore::Synchronize()
 		statsPending = false;
 		const Counters& cnt = hostStats->counters;
 		if (cnt.shadowOverflow) FatalError( "shadow ray buffer overflow" );
+		if (hostStats->sceneError) FatalError( "BVH depth exceeds the traversal stack (%d levels): frame skipped", LH2_STACK_TOTAL );
 		uint32_t* rc = hostStats->rayCount;   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
 		auto ms = [&]( hipEvent_t a, hipEvent_t b ) { float t = 0; (void)hipEventElapsedTime( &t, a, b ); return t * 1e-3f; };
 		coreStats.primaryRayCount = rc[0];
@@ -577,6 +656,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
+	CheckSceneError();
 }
 
 void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* occluded )
@@ -597,6 +677,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	memcpy( occluded, tmp.data(), ((size_t)n + 31) / 32 * 4 );
+	CheckSceneError();
 }
 
 void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void* hitsOut, int iterations, float* msOut )
@@ -623,6 +704,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 	float t = 0;
 	CHK_HIP( hipEventElapsedTime( &t, a, b ) );
 	if (msOut) *msOut = t / std::max( 1, iterations );
+	CheckSceneError();
 	(void)hipEventDestroy( a ); (void)hipEventDestroy( b );
 }
 
@@ -653,6 +735,13 @@ void RenderCore::SceneInfo( int* nodeCount, int* triCount, int* maxDepth, int* i
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	if (nodeCount) *nodeCount = blasNodeCount;
 	if (triCount) *triCount = blasTriCount;
+	if (tlasOnDevice)
+	{
+		int d = 0;
+		CHK_HIP( hipMemcpyAsync( &d, dTlasDepth.ptr, sizeof( int ), hipMemcpyDeviceToHost, stream ) );
+		CHK_HIP( hipStreamSynchronize( stream ) );
+		sceneMaxDepth = d + maxBlasDepth;
+	}
 	if (maxDepth) *maxDepth = sceneMaxDepth;
 	if (instCount) *instCount = (int)instances.size();
 }
@@ -669,6 +758,8 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto& e : evShadow) (void)hipEventDestroy( e );
 	for (auto& e : evFrame) (void)hipEventDestroy( e );
 	for (auto& e : evCount) (void)hipEventDestroy( e );
+	for (auto& e : evStage) (void)hipEventDestroy( e );
+	for (int i = 0; i < 2; i++) { if (stage[i]) (void)hipHostFree( stage[i] ); stage[i] = nullptr, stageBytes[i] = 0; }
 	if (activeLog) (void)hipHostFree( activeLog );
 	activeLog = nullptr;
 	if (hostStats) (void)hipHostFree( hostStats );

@@ -8,6 +8,7 @@
 
 #include "../../include/lh2_core_types.h"
 #include "bvh_build.h"
+#include "bvh_gpu.h"
 #include "lh2_kernels.h"
 #include "lh2_device.h"
 
@@ -32,6 +33,7 @@ template <class T> struct DevBuf
 		if (hipMalloc( (void**)&ptr, n * sizeof( T ) ) != hipSuccess) FatalError( "hipMalloc of %zu bytes failed", n * sizeof( T ) );
 		count = n;
 	}
+	void adopt( T* p, size_t n ) { free(); ptr = p, count = n; }   /* takes ownership of a hipMalloc'ed block */
 	void upload( const T* src, size_t n, hipStream_t st )
 	{
 		resize( n );
@@ -39,13 +41,13 @@ template <class T> struct DevBuf
 	}
 };
 
-struct CoreMeshHost
+struct CoreMeshHost   /* RenderCore always copies what it needs (rendercore.h:57): all of it on the device */
 {
-	std::vector<lh2_CoreTri> tris;       /* RenderCore always copies what it needs (rendercore.h:57) */
-	BvhOutput bvh;
-	float aabbLo[3], aabbHi[3];
+	int triCount = 0;
+	float aabbLo[3], aabbHi[3];          /* lo.x > hi.x: empty mesh */
 	DevBuf<float4> shadeTris;            /* CoreTri4[] in original order, for shading */
-	bool dirty = true;
+	DevBuf<float4> bvhNodes, bvhTris;    /* BLAS with mesh-local refs; relocated into the scene arrays by UpdateToplevel */
+	int nodeCount = 0, maxDepth = 0;
 };
 
 struct CoreInstanceHost { int mesh; float T[16]; float inv[16]; };
@@ -54,6 +56,7 @@ struct FrameStats   /* per-frame values read back from the device */
 {
 	uint32_t rayCount[17];
 	Counters counters;
+	int sceneError;
 };
 
 class RenderCore
@@ -99,7 +102,8 @@ public:
 
 private:
 	void EnsureBuffers();
-	void UploadScene();
+	void ConcatenateBlas( int instanceCount );
+	void CheckSceneError();
 	SceneDev MakeSceneDev() const;
 	int TraceGrid() const { return smCount * blocksPerCU; }
 
@@ -114,6 +118,17 @@ private:
 	DevBuf<lh2_CoreInstanceDesc> dInstDesc;
 	int tlasRoot = 0, blasNodeCount = 0, blasTriCount = 0, sceneMaxDepth = 0;
 	std::vector<int> meshNodeBase, meshTriBase;
+	int tlasCapacity = 0, maxBlasDepth = 0;
+	bool tlasOnDevice = false;           /* TLAS of the last UpdateToplevel built by the GPU (depth in dTlasDepth) */
+	GpuBvhBuilder gpuBvh;
+	DevBuf<float> dMeshBounds;           /* 6 per mesh */
+	DevBuf<float> dInstT;                /* 16 per instance */
+	DevBuf<int> dInstMesh;
+	DevBuf<int> dSceneError, dTlasDepth;
+	uint8_t* stage[2] = {};              /* pinned staging of UpdateToplevel (double-buffered) */
+	size_t stageBytes[2] = {};
+	hipEvent_t evStage[2] = {};
+	int stageSlot = 0;
 	DevBuf<uint4> dMaterials;
 	DevBuf<lh2_CoreLightTri> dArea; DevBuf<lh2_CorePointLight> dPoint; DevBuf<lh2_CoreSpotLight> dSpot; DevBuf<lh2_CoreDirectionalLight> dDir;
 	int nArea = 0, nPoint = 0, nSpot = 0, nDir = 0;
@@ -144,6 +159,7 @@ private:
 	int tiledRays = 1;
 	int refillPrimary = 64, refillOther = 16, leafBatch = 16, leafBatchPrimary = 0;
 	int bvhMaxLeaf = 2;
+	int gpuBuild = 0, gpuTlas = 1;       /* BLAS builder (1: GPU PLOC, 0: CPU binned SAH); TLAS on the GPU */
 	float bvhTraversalCost = 1.0f;
 	int framePathLengths = 0;
 	double frameHostMs = 0;

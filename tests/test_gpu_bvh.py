@@ -1,0 +1,154 @@
+"""GPU acceleration-structure builds: BLAS by GPU PLOC (setting gpuBuild) and
+the per-frame TLAS on the device (setting gpuTlas, default on), checked against the CPU oracle.
+
+Hit results must not depend on the tree: the closest hit is unique under the (t, instance,
+triangle) tie rule and box tests only cull.  So the bar is the same as for the CPU-built tree:
+bit-exact hit records, identical occlusion bits, frame rel-L2 <= 1e-4 with identical ray counts.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from lighthouse2_amd import abi, scene
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _rays(n, seed, radius=14.0, spread=4.0, tmin=1e-4):
+    rng = np.random.default_rng(seed)
+    o = rng.normal(size=(n, 3)).astype(np.float32)
+    o = o / np.linalg.norm(o, axis=1, keepdims=True) * np.float32(radius)
+    d = rng.uniform(-spread, spread, size=(n, 3)).astype(np.float32) - o
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    O4 = np.concatenate([o, np.full((n, 1), tmin, np.float32)], 1)
+    D4 = np.concatenate([d, np.full((n, 1), 1e34, np.float32)], 1)
+    return O4, D4
+
+
+def _oracle(sc, w=64, h=36):
+    o = Oracle()
+    sc.load_into(o)
+    o.set_target(w, h, 1)
+    return o
+
+
+def _gpu(core, sc, w=64, h=36, **settings):
+    for k, v in settings.items():
+        core.setting(k, v)
+    sc.load_into(core)
+    core.set_target(w, h, 1)
+
+
+@pytest.mark.parametrize("max_leaf,radius", [(2, 16), (1, 4), (8, 32)])
+def test_gpu_blas_hits_bitexact(fresh_core, max_leaf, radius):
+    sc = scene.config2_scene(n=30000, width=64, height=36)
+    _gpu(fresh_core, sc, gpuBuild=1, bvhMaxLeaf=max_leaf, plocRadius=radius)
+    o = _oracle(sc)
+    info = fresh_core.scene_info()
+    assert 0 < info["nodes"] < 2 * 30000 and 0 < info["max_depth"] < 90
+    O4, D4 = _rays(60000, 11)
+    hg, ho = fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4)
+    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.3
+    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+    D4[:, 3] = np.random.default_rng(12).uniform(1.0, 20.0, len(D4)).astype(np.float32)
+    O4[:, 3] = 0
+    assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
+
+
+def _tri_array(v0, v1, v2):
+    n = len(v0)
+    tris = np.zeros((n, abi.TRI_WORDS), np.float32)
+    tris[:, 32:35], tris[:, 36:39], tris[:, 40:43] = v0, v1, v2
+    return tris
+
+
+def test_gpu_blas_degenerate_inputs(fresh_core):
+    """Identical triangles (all Morton codes and areas tie), a 2-triangle mesh, collinear slivers and
+    zero-area triangles: the build must terminate and the hits must still match."""
+    one = _tri_array(np.array([[-1, -1, 0]], np.float32), np.array([[1, -1, 0]], np.float32), np.array([[0, 1, 0]], np.float32))
+    dup = np.repeat(one, 500, axis=0)                           # 500 copies of one triangle
+    two = _tri_array(np.array([[-1, -1, 0], [1, 1, 0]], np.float32), np.array([[1, -1, 0], [-1, 1, 0]], np.float32),
+                     np.array([[1, 1, 0], [-1, -1, 0]], np.float32))
+    t = np.linspace(-1, 1, 300, dtype=np.float32)[:, None]
+    sliver = _tri_array(np.concatenate([t, t * 0 - 1, t * 0], 1), np.concatenate([t + 0.01, t * 0 - 1, t * 0], 1),
+                        np.concatenate([t + 0.005, t * 0 + 1, t * 0], 1))
+    point = _tri_array(np.zeros((50, 3), np.float32), np.zeros((50, 3), np.float32), np.zeros((50, 3), np.float32))
+    meshes = [dup, two, sliver, point]
+    inst = []
+    for k in range(len(meshes)):
+        T = np.eye(4, dtype=np.float32)
+        T[0, 3] = (k - 1.5) * 8.0
+        inst.append((k, T))
+    sc = scene.Scene(meshes=meshes, instances=inst, materials=[abi.make_material((0.8, 0.8, 0.8), roughness=1.0)])
+    sc.view = scene.camera_view((0, 0, -20), (0, 0, 1), pixel_height=36)
+    _gpu(fresh_core, sc, gpuBuild=1)
+    o = _oracle(sc)
+    rng = np.random.default_rng(13)
+    n = 40000
+    O4 = np.zeros((n, 4), np.float32)
+    O4[:, 0], O4[:, 1], O4[:, 2], O4[:, 3] = rng.uniform(-16, 16, n), rng.uniform(-2, 2, n), -20, 1e-4
+    d = np.stack([rng.uniform(-0.05, 0.05, n), rng.uniform(-0.05, 0.05, n), np.ones(n)], 1).astype(np.float32)
+    D4 = np.concatenate([d / np.linalg.norm(d, axis=1, keepdims=True), np.full((n, 1), 1e34, np.float32)], 1).astype(np.float32)
+    hg, ho = fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4)
+    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.05
+    assert np.array_equal(hg, ho)
+
+
+@pytest.mark.parametrize("count", [2, 300, 5000])
+def test_gpu_tlas_many_instances(fresh_core, count):
+    """TLAS on the device: one workgroup up to 4096 instances, the kernel sequence beyond; random
+    rotations and scales, and instances of an empty mesh (excluded from the TLAS)."""
+    rng = np.random.default_rng(count)
+    meshes = [scene.random_triangles(200, seed=0x12345678 + k, spread=2.0) for k in range(8)]
+    meshes.append(np.zeros((0, abi.TRI_WORDS), np.float32))
+    inst = []
+    for k in range(count):
+        a = float(rng.uniform(0, 2 * math.pi))
+        T = scene.rotation_y(a) * np.float32(rng.uniform(0.5, 1.5))
+        T[3, 3] = 1
+        T[:3, 3] = rng.uniform(-1, 1, 3).astype(np.float32) * np.float32(30 if count > 10 else 2)
+        inst.append((int(rng.integers(0, len(meshes))) if k % 17 else len(meshes) - 1, T.astype(np.float32)))
+    sc = scene.Scene(meshes=meshes, instances=inst, materials=[abi.make_material((0.8, 0.8, 0.8), roughness=1.0)])
+    sc.view = scene.camera_view((0, 0, -60), (0, 0, 1), pixel_height=36)
+    _gpu(fresh_core, sc, gpuTlas=1)
+    o = _oracle(sc)
+    O4, D4 = _rays(20000, 14, radius=50.0, spread=30.0 if count > 10 else 2.0)
+    hg, ho = fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4)
+    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.01
+    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+    assert fresh_core.scene_info()["max_depth"] > 0
+
+
+def test_gpu_build_frame_parity(fresh_core):
+    """A whole frame of the room scene (config 3 in miniature) on a GPU-built BLAS."""
+    w, h = 128, 72
+    sc = scene.room_scene(40000, w, h)
+    _gpu(fresh_core, sc, w, h, gpuBuild=1, maxPathLength=4)
+    o = _oracle(sc, w, h)
+    o.setting("maxPathLength", 4)
+    sc.render_frame(fresh_core)
+    sc.render_frame(o)
+    assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
+    ag, ao = fresh_core.accumulator(), o.accumulator()
+    rel = float(np.linalg.norm(ag[..., :3] - ao[..., :3]) / np.linalg.norm(ao[..., :3]))
+    assert rel <= 1e-4, rel
+
+
+def test_host_and_device_tlas_agree(fresh_core):
+    """gpuTlas 0 (host SAH TLAS, synchronous) and 1 (device PLOC TLAS) give the same hits on an
+    animated instanced scene."""
+    sc = scene.instanced_scene(meshes=6, tris_per_mesh=2000, width=64, height=36, grid=3, spacing=12.0)
+    _gpu(fresh_core, sc)
+    O4, D4 = _rays(30000, 15, radius=40.0, spread=18.0)
+    res = []
+    for f, flag in enumerate((0, 1, 0, 1)):
+        scene.animate_instances(sc, f // 2)
+        fresh_core.setting("gpuTlas", flag)
+        for k, (mesh, T) in enumerate(sc.instances):
+            fresh_core.set_instance(k, mesh, T)
+        fresh_core.update_toplevel()
+        res.append(fresh_core.trace_closest(O4, D4))
+    assert np.array_equal(res[0], res[1]) and np.array_equal(res[2], res[3])
+    assert not np.array_equal(res[0], res[2])
