@@ -63,6 +63,13 @@ class CoreDirectionalLight(C.Structure):
     _fields_ = [("direction", float3), ("energy", C.c_float), ("radiance", float3), ("dummy", C.c_int)]
 
 
+class CoreTexDesc(C.Structure):
+    """CoreTexDesc (common_classes.h:246-269, host layout): texel pointer + sizes; firstPixel is set by
+    the core (rendercore.cpp:328)."""
+    _fields_ = [("idata", C.c_void_p), ("width", C.c_uint32), ("height", C.c_uint32), ("flags", C.c_uint32),
+                ("pixelCount", C.c_uint32), ("firstPixel", C.c_uint32), ("MIPlevels", C.c_uint32), ("storage", C.c_int32)]
+
+
 class ViewPyramid(C.Structure):
     _fields_ = [("pos", float3), ("p1", float3), ("p2", float3), ("p3", float3), ("aperture", C.c_float),
                 ("spreadAngle", C.c_float), ("imagePlane", C.c_float), ("focalDistance", C.c_float),

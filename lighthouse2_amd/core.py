@@ -135,6 +135,14 @@ class RenderCore:
     def set_probe(self, x: int, y: int) -> None:
         self._chk(self.lib.lh2_core_set_probe(self.h, int(x), int(y)))
 
+    def set_textures(self, textures) -> None:
+        """textures: scene.Texture list (RenderSystem order: before set_materials)."""
+        self._tex_keep = [np.ascontiguousarray(t.pixels) for t in textures]
+        arr = (abi.CoreTexDesc * max(1, len(textures)))()
+        for i, t in enumerate(textures):
+            arr[i] = t.desc(self._tex_keep[i])
+        self._chk(self.lib.lh2_core_set_textures(self.h, C.cast(arr, _P), len(textures)))
+
     def set_materials(self, mats) -> None:
         arr = abi.material_array(mats)
         self._chk(self.lib.lh2_core_set_materials(self.h, arr, len(mats)))

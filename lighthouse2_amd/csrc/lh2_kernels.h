@@ -37,6 +37,9 @@ struct SceneDev       /* everything the traversal and shading kernels read, by v
 	const uint8_t* blueNoise;
 	float geometryEpsilon, clampValue;
 	const int* sceneError;           /* nonzero: the scene is unsafe to traverse (TLAS too deep); trace kernels exit */
+	const uint32_t* argb32;          /* texel storage (rendercore.cpp:296-336): ARGB32 / NRM32 u32 texels */
+	const uint32_t* nrm32;
+	uint32_t argb32Count, nrm32Count;
 };
 
 struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path state */
@@ -49,6 +52,7 @@ struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path st
 	Counters* counters;
 	int w, h, pass, pathLength, maxPathLength, probePixel;
 	uint32_t R0;
+	float spreadAngle;               /* ViewPyramid::spreadAngle: ray cone width per unit distance (texture LOD) */
 };
 
 struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (any) out */

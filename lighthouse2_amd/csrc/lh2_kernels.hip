@@ -510,11 +510,70 @@ LH2_DEV v3 ConsistentNormal( const v3 D, const v3 iN, const float alpha ) /* too
 	return normalize3( add3( D, Rc ) );
 }
 
-/* GetShadingData, material_shared.h:35-98 (OPTIXPRIMEBUILD, CONSISTENTNORMALS; texture maps are
-   out of scope this round) */
-LH2_DEV void GetShadingData( const SceneDev& s, const v3 D, const float u, const float v, const float4* __restrict__ tri,
+/* ---- texture maps: sampling_shared.h:35-86 (BILINEAR), MIPLEVELCOUNT 5 (common_settings.h:49) ----
+   Texels are u32 in HBM (one gather per tap).  Defined where the reference is undefined: float->int
+   conversions saturate (lh2_f2i), MIP levels narrower than one texel count as one texel (the
+   reference divides by zero there), and indices are clamped to the texel array. */
+#define MIPLEVELCOUNT 5
+#define HASDIFFUSEMAP (1 << 2)
+#define HASNORMALMAP (1 << 3)
+#define HASSPECULARITYMAP (1 << 4)
+#define HASROUGHNESSMAP (1 << 5)
+#define HAS2NDNORMALMAP (1 << 7)
+#define HAS2NDDIFFUSEMAP (1 << 9)
+#define HASALPHA (1 << 12)
+LH2_DEV float4 uchar4_to_float4( const uint32_t v )
+{
+	const float r = 1.0f / 256.0f;
+	return make_float4( (float)(v & 255u) * r, (float)((v >> 8) & 255u) * r, (float)((v >> 16) & 255u) * r, (float)(v >> 24) * r );
+}
+LH2_DEV float4 FetchTexel( const uint32_t* __restrict__ tex, const uint32_t count, const float tcu, const float tcv, const int o, int w, int h )
+{
+	w = max( w, 1 ), h = max( h, 1 );
+	const float tcx = (fmaxf( tcu + 1000, 0.0f ) * (float)w) - 0.5f, tcy = (fmaxf( tcv + 1000, 0.0f ) * (float)h) - 0.5f;
+	const int iu = lh2_f2i( tcx ) % w, iv = lh2_f2i( tcy ) % h;
+	const float fu = tcx - floorf( tcx ), fv = tcy - floorf( tcy );
+	const float w0 = (1 - fu) * (1 - fv), w1 = fu * (1 - fv), w2 = (1 - fu) * fv, w3 = 1 - (w0 + w1 + w2);
+	const uint32_t iu1 = (uint32_t)((iu + 1) % w), iv1 = (uint32_t)((iv + 1) % h);
+	const uint32_t last = count - 1;
+	const float4 p0 = uchar4_to_float4( tex[min( (uint32_t)o + (uint32_t)iu + (uint32_t)iv * (uint32_t)w, last )] );
+	const float4 p1 = uchar4_to_float4( tex[min( (uint32_t)o + iu1 + (uint32_t)iv * (uint32_t)w, last )] );
+	const float4 p2 = uchar4_to_float4( tex[min( (uint32_t)o + (uint32_t)iu + iv1 * (uint32_t)w, last )] );
+	const float4 p3 = uchar4_to_float4( tex[min( (uint32_t)o + iu1 + iv1 * (uint32_t)w, last )] );
+	return make_float4( p0.x * w0 + p1.x * w1 + p2.x * w2 + p3.x * w3, p0.y * w0 + p1.y * w1 + p2.y * w2 + p3.y * w3,
+		p0.z * w0 + p1.z * w1 + p2.z * w2 + p3.z * w3, p0.w * w0 + p1.w * w1 + p2.w * w2 + p3.w * w3 );
+}
+LH2_DEV float4 FetchTexelTrilinear( const uint32_t* __restrict__ tex, const uint32_t count, const float lambda, const float tcu, const float tcv,
+	const int offset, const int width, const int height )
+{
+	const int level0 = min( MIPLEVELCOUNT - 1, lh2_f2i( lambda ) );
+	const int level1 = min( MIPLEVELCOUNT - 1, level0 + 1 );
+	const float f = lambda - floorf( lambda );
+	int o0 = offset, w0 = width, h0 = height;
+	for (int i = 0; i < level0; i++) o0 += w0 * h0, w0 >>= 1, h0 >>= 1;
+	int o1 = offset, w1 = width, h1 = height;
+	for (int i = 0; i < level1; i++) o1 += w1 * h1, w1 >>= 1, h1 >>= 1;
+	const float4 p0 = FetchTexel( tex, count, tcu, tcv, o0, w0, h0 );
+	const float4 p1 = FetchTexel( tex, count, tcu, tcv, o1, w1, h1 );
+	return make_float4( (1 - f) * p0.x + f * p1.x, (1 - f) * p0.y + f * p1.y, (1 - f) * p0.z + f * p1.z, (1 - f) * p0.w + f * p1.w );
+}
+/* texture coordinate of a map record: uvscale * (uvoffs + (tu, tv)), halves in y / z (CUDAMaterial::Map) */
+LH2_DEV void map_coord( const uint4 data, const float tu, const float tv, float& cu, float& cv )
+{
+	cu = h2f( data.y & 0xffff ) * (h2f( data.z & 0xffff ) + tu);
+	cv = h2f( data.y >> 16 ) * (h2f( data.z >> 16 ) + tv);
+}
+LH2_DEV float normal_scale( const uint32_t byte, const bool absArg )   /* material_shared.h:135, :142 */
+{
+	const float b = (float)byte - 128.0f;
+	return copysignf( -0.0001f + 0.0001f * lh2_expf( 0.1f * (absArg ? fabsf( b ) : b) ), b );
+}
+
+/* GetShadingData, material_shared.h:35-178 (OPTIXPRIMEBUILD, CONSISTENTNORMALS, BILINEAR) */
+LH2_DEV void GetShadingData( const SceneDev& s, const v3 D, const float u, const float v, const float coneWidth, const float4* __restrict__ tri,
 	const int instIdx, ShadingData& sd, v3& N, v3& iN, v3& fN, v3& T )
 {
+
 	const float4 tdata1 = tri[1], tdata2 = tri[2], tdata3 = tri[3], tdata4 = tri[4], tdata5 = tri[5], alpha4 = tri[7];
 	const uint4* mat = s.materials + (size_t)__float_as_int( tdata1.w ) * 8;
 	const uint4 baseData = mat[0];
@@ -540,7 +599,64 @@ LH2_DEV void GetShadingData( const SceneDev& s, const v3 D, const float u, const
 	const float alpha = u * alpha4.x + v * alpha4.y + w * alpha4.z;
 	iN = smul( backSide ? -1.0f : 1.0f, ConsistentNormal( muls( D, -1.0f ), backSide ? muls( iN, -1.0f ) : iN, alpha ) );
 	fN = iN;
+	if (!(flags & (HASDIFFUSEMAP | HAS2NDDIFFUSEMAP | HASSPECULARITYMAP | HASNORMALMAP | HAS2NDNORMALMAP | HASROUGHNESSMAP))) return;
+	/* texturing (material_shared.h:99-171) */
+	const float4 tdata0 = tri[0];
+	const float tu = u * tdata0.x + v * tdata0.y + w * tdata0.z;
+	const float tv = u * tdata1.x + v * tdata1.y + w * tdata1.z;
+	float cu, cv;
+	if (flags & HASDIFFUSEMAP)
+	{
+		const float lambda = alpha4.w + lh2_log2f( coneWidth * (1.0f / fabsf( dot3( D, N ) )) );   /* eq. 26 */
+		const uint4 data = mat[2];
+		map_coord( data, tu, tv, cu, cv );
+		const float4 texel = FetchTexelTrilinear( s.argb32, s.argb32Count, lambda, cu, cv, (int)data.w, (int)(data.x & 0xffff), (int)(data.x >> 16) );
+		if ((flags & HASALPHA) && texel.w < 0.5f)
+		{
+			sd.flags |= 1;
+			return;
+		}
+		sd.color = mul3( sd.color, mk3( texel.x, texel.y, texel.z ) );
+		if (flags & HAS2NDDIFFUSEMAP)
+		{
+			const uint4 d1 = mat[3];
+			map_coord( d1, tu, tv, cu, cv );
+			const float4 t1 = FetchTexel( s.argb32, s.argb32Count, cu, cv, (int)d1.w, (int)(d1.x & 0xffff), (int)(d1.x >> 16) );
+			sd.color = add3( sd.color, sub3( mk3( t1.x, t1.y, t1.z ), s3( 0.5f ) ) );
+		}
+	}
+	if (flags & HASNORMALMAP)
+	{
+		const v3 Bt = xyz( tri[6] );
+		const uint4 data = mat[4];
+		const uint32_t part3 = baseData.z;
+		const float n0scale = normal_scale( (part3 >> 8) & 255, true );
+		map_coord( data, tu, tv, cu, cv );
+		const float4 t0 = FetchTexel( s.nrm32, s.nrm32Count, cu, cv, (int)data.w, (int)(data.x & 0xffff), (int)(data.x >> 16) );
+		v3 sN = mk3( (t0.x - 0.5f) * 2.0f, (t0.y - 0.5f) * 2.0f, (t0.z - 0.5f) * 2.0f );
+		sN.x *= n0scale, sN.y *= n0scale;
+		if (flags & HAS2NDNORMALMAP)
+		{
+			const uint4 d1 = mat[5];
+			const float n1scale = normal_scale( (part3 >> 16) & 255, false );
+			map_coord( d1, tu, tv, cu, cv );
+			const float4 t1 = FetchTexel( s.nrm32, s.nrm32Count, cu, cv, (int)d1.w, (int)(d1.x & 0xffff), (int)(d1.x >> 16) );
+			v3 l1 = mk3( (t1.x - 0.5f) * 2.0f, (t1.y - 0.5f) * 2.0f, (t1.z - 0.5f) * 2.0f );
+			l1.x *= n1scale, l1.y *= n1scale;
+			sN = add3( sN, l1 );
+		}
+		sN = normalize3( sN );
+		fN = normalize3( add3( add3( smul( sN.x, T ), smul( sN.y, Bt ) ), smul( sN.z, iN ) ) );
+	}
+	if (flags & HASROUGHNESSMAP)
+	{
+		const uint4 data = mat[7];
+		map_coord( data, tu, tv, cu, cv );
+		const float4 t = FetchTexel( s.argb32, s.argb32Count, cu, cv, (int)data.w, (int)(data.x & 0xffff), (int)(data.x >> 16) );
+		sd.params.x = (sd.params.x & 0xffffff) + (lh2_f2u( t.x * 255.0f ) << 24);
+	}
 }
+
 
 /* ---- lights (lights_shared.h:36-261) ------------------------------------------------------ */
 LH2_DEV float PotentialArea( const SceneDev& s, int idx, v3 O, v3 N, v3 I, v3 bary )
@@ -1126,7 +1242,7 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const Scen
 				v3 N, iN, fN, T;
 				const v3 I = add3( RAY_O, smul( HIT_T, D ) );
 				const float4* tri = (const float4*)s.instDesc[INSTANCEIDX].triangles + (size_t)PRIMIDX * 11;
-				GetShadingData( s, D, HIT_U, HIT_V, tri, INSTANCEIDX, sd, N, iN, fN, T );
+				GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, INSTANCEIDX, sd, N, iN, fN, T );
 				if (sd.flags & 1)
 				{
 					if (p.pathLength < p.maxPathLength)

@@ -172,10 +172,36 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* other names ("clampDirect", "filter", "TAA", ...) are ignored, as in the reference */
 }
 
-void RenderCore::SetTextures( const lh2_CoreTexDesc*, int textureCount )
+void RenderCore::SetTextures( const lh2_CoreTexDesc* tex, int textureCount )   /* rendercore.cpp:276-292 */
 {
-	coreStats.argb32TexelCount = coreStats.argb128TexelCount = coreStats.nrm32TexelCount = 0;
-	(void)textureCount;   /* texture maps: SURVEY §8f row 2 (next round) */
+	texDescs.assign( tex, tex + std::max( 0, textureCount ) );
+	/* SyncStorageType (rendercore.cpp:299-336) for ARGB32, ARGB128 and NRM32: one continuous array per
+	   storage type, textures in descriptor order, at least 16 texels.  ARGB128 texels are copied whole
+	   (the reference copies pixelCount * 4 bytes of each 16-byte texel there; this core never reads
+	   ARGB128 texels while shading, so only CoreStats sees the difference). */
+	for (int storage = 0; storage < 3; storage++)
+	{
+		uint32_t total = 0;
+		for (auto& t : texDescs) if (t.storage == storage) total += t.pixelCount;
+		const uint32_t alloc = std::max( 16u, total );
+		if (storage == 1)
+		{
+			std::vector<float4> buf( alloc, make_float4( 0, 0, 0, 0 ) );
+			uint32_t at = 0;
+			for (auto& t : texDescs) if (t.storage == storage) { memcpy( buf.data() + at, t.idata, (size_t)t.pixelCount * 16 ); t.firstPixel = at; at += t.pixelCount; }
+			dArgb128.upload( buf.data(), buf.size(), stream );
+			coreStats.argb128TexelCount = alloc;
+		}
+		else
+		{
+			std::vector<uint32_t> buf( alloc, 0u );
+			uint32_t at = 0;
+			for (auto& t : texDescs) if (t.storage == storage) { memcpy( buf.data() + at, t.idata, (size_t)t.pixelCount * 4 ); t.firstPixel = at; at += t.pixelCount; }
+			(storage == 0 ? dArgb32 : dNrm32).upload( buf.data(), buf.size(), stream );
+			(storage == 0 ? coreStats.argb32TexelCount : coreStats.nrm32TexelCount) = alloc;
+		}
+	}
+	CHK_HIP( hipStreamSynchronize( stream ) );   /* texel pointers are borrowed for this call only */
 }
 
 #define TOCHAR(a) lh2_f2u( (a) * 255.0f )
@@ -194,6 +220,25 @@ void RenderCore::SetMaterials( const lh2_CoreMaterial* mat, int n )   /* renderc
 		recs[i * 8 + 1] = make_uint4( TOUINT4( m.metallic.value, m.subsurface.value, m.specular.value, m.roughness.value ),
 			TOUINT4( m.specularTint.value, m.anisotropic.value, m.sheen.value, m.sheenTint.value ),
 			TOUINT4( m.clearcoat.value, m.clearcoatGloss.value, m.transmission.value, 0 ), lh2_f2b( m.eta.value ) );
+		/* texture / normal map records (rendercore.cpp:379-384, RenderCore::Map rendercore.h:79-86):
+		   x = width | height << 16 (shorts), y / z = uvscale / uvoffset (halves), w = first texel */
+		auto map = [&]( int tid, lh2_float2 uvscale, lh2_float2 uvoffs ) {
+			if (tid < 0 || tid >= (int)texDescs.size()) FatalError( "SetMaterials: material %d uses texture %d of %d (call SetTextures first)", i, tid, (int)texDescs.size() );
+			const lh2_CoreTexDesc& t = texDescs[tid];
+			return make_uint4( (t.width & 0xffffu) | ((t.height & 0xffffu) << 16), lh2_f2h( uvscale.x ) | ((uint32_t)lh2_f2h( uvscale.y ) << 16),
+				lh2_f2h( uvoffs.x ) | ((uint32_t)lh2_f2h( uvoffs.y ) << 16), t.firstPixel );
+		};
+		uint32_t texFlags = 0;
+		if (m.color.textureID != -1) recs[i * 8 + 2] = map( m.color.textureID, m.color.uvscale, m.color.uvoffset ), texFlags |= 1u << 2;
+		if (m.detailColor.textureID != -1) recs[i * 8 + 3] = map( m.detailColor.textureID, m.detailColor.uvscale, m.detailColor.uvoffset ), texFlags |= 1u << 9;
+		if (m.normals.textureID != -1) recs[i * 8 + 4] = map( m.normals.textureID, m.normals.uvscale, m.normals.uvoffset ), texFlags |= 1u << 3;
+		if (m.detailNormals.textureID != -1) recs[i * 8 + 5] = map( m.detailNormals.textureID, m.detailNormals.uvscale, m.detailNormals.uvoffset ), texFlags |= 1u << 7;
+		if (m.specular.textureID != -1) recs[i * 8 + 6] = map( m.specular.textureID, m.specular.uvscale, m.specular.uvoffset ), texFlags |= 1u << 4;
+		if (m.roughness.textureID != -1) recs[i * 8 + 7] = map( m.roughness.textureID, m.roughness.uvscale, m.roughness.uvoffset ), texFlags |= 1u << 5;
+		/* DIFFUSEMAPISHDR: the reference tests textureID != 1 and so reads texDescs[-1] for untextured
+		   materials (rendercore.cpp:386); here only a valid diffuse map can set it.  Not read by shading. */
+		if (m.color.textureID >= 0 && (texDescs[m.color.textureID].flags & 8)) texFlags |= 1u << 1;
+		recs[i * 8 + 0].w |= texFlags;
 	}
 	dMaterials.upload( recs.data(), recs.size(), stream );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -456,6 +501,8 @@ SceneDev RenderCore::MakeSceneDev() const
 	SceneDev s;
 	s.nodes = dNodes.ptr, s.tris = dTris.ptr, s.inst = (const DevInstance*)dInst.ptr;
 	s.sceneError = dSceneError.ptr;
+	s.argb32 = dArgb32.ptr, s.nrm32 = dNrm32.ptr;
+	s.argb32Count = (uint32_t)dArgb32.count, s.nrm32Count = (uint32_t)dNrm32.count;
 	s.tlasRoot = tlasRoot, s.instCount = (int)instances.size();
 	s.instDesc = dInstDesc.ptr, s.materials = dMaterials.ptr;
 	s.areaLights = dArea.ptr, s.pointLights = dPoint.ptr, s.spotLights = dSpot.ptr, s.dirLights = dDir.ptr;
@@ -523,6 +570,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPathLength;
 		sp.probePixel = probeX + scrwidth * probeY;
 		sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
+		sp.spreadAngle = view.spreadAngle;
 		CHK_HIP( hipEventRecord( evShade[2 * pathLength], stream ) );
 		lh2_launch_shade( &sd, &sp, grid, stream );
 		CHK_HIP( hipEventRecord( evShade[2 * pathLength + 1], stream ) );

@@ -130,6 +130,9 @@ private:
 	hipEvent_t evStage[2] = {};
 	int stageSlot = 0;
 	DevBuf<uint4> dMaterials;
+	std::vector<lh2_CoreTexDesc> texDescs;   /* copies, firstPixel assigned per storage (rendercore.cpp:276-292) */
+	DevBuf<uint32_t> dArgb32, dNrm32;        /* continuous texel arrays (rendercore.cpp:299-336) */
+	DevBuf<float4> dArgb128;
 	DevBuf<lh2_CoreLightTri> dArea; DevBuf<lh2_CorePointLight> dPoint; DevBuf<lh2_CoreSpotLight> dSpot; DevBuf<lh2_CoreDirectionalLight> dDir;
 	int nArea = 0, nPoint = 0, nSpot = 0, nDir = 0;
 	DevBuf<float> dSky; int skyW = 0, skyH = 0;

@@ -146,6 +146,7 @@ class Scene:
     spot_lights: list = dataclasses.field(default_factory=list)
     dir_lights: list = dataclasses.field(default_factory=list)
     sky: np.ndarray | None = None      # (h, w, 3) float32
+    textures: list = dataclasses.field(default_factory=list)   # Texture
     view: abi.ViewPyramid | None = None
     name: str = "scene"
 
@@ -157,6 +158,8 @@ class Scene:
         """RenderSystem::SynchronizeSceneData order (rendersystem.cpp:214-222)."""
         if self.sky is not None:
             core.set_sky(self.sky)
+        if self.textures:
+            core.set_textures(self.textures)
         core.set_materials(self.materials)
         for i, m in enumerate(self.meshes):
             core.set_geometry(i, m)
@@ -457,3 +460,188 @@ def animate_instances(sc: Scene, frame: int, seed: int = 7) -> None:
         M[:, 3] = T[:, 3]
         new.append((mesh, M.astype(np.float32)))
     sc.instances = new
+
+
+# ---------------------------------------------------------------------------------------------
+# texture maps: HostTexture-equivalent texel preparation + a textured scene
+# ---------------------------------------------------------------------------------------------
+MIPLEVELCOUNT = 5          # common_settings.h:49
+TEX_NORMALMAP, TEX_HDR = 2, 8   # HostTexture flags (host_texture.h:42-44)
+
+
+def pixels_needed(w: int, h: int, levels: int) -> int:
+    """HostTexture::PixelsNeeded (host_texture.cpp:117-122)."""
+    n = 0
+    for _ in range(levels):
+        n += w * h
+        w >>= 1
+        h >>= 1
+    return n
+
+
+def construct_mipmaps(base: np.ndarray) -> np.ndarray:
+    """HostTexture::ConstructMIPmaps (host_texture.cpp:128-151) on uint32 texels (h, w): each level
+    averages 2x2 blocks of bytes 0..2 (>> 2 of the sum) and keeps the minimum of byte 3."""
+    h, w = base.shape
+    out = [base.reshape(-1).astype(np.uint32)]
+    src = base.astype(np.uint32)
+    for _ in range(1, MIPLEVELCOUNT):
+        h2, w2 = src.shape[0] >> 1, src.shape[1] >> 1
+        if h2 == 0 or w2 == 0:
+            out.append(np.zeros(0, np.uint32))
+            src = np.zeros((h2, w2), np.uint32)
+            continue
+        q = [src[0:2 * h2:2, 0:2 * w2:2], src[0:2 * h2:2, 1:2 * w2:2], src[1:2 * h2:2, 0:2 * w2:2], src[1:2 * h2:2, 1:2 * w2:2]]
+        a = np.minimum(np.minimum(q[0] >> 24, q[1] >> 24), np.minimum(q[2] >> 24, q[3] >> 24))
+        ch = [sum(((x >> s) & 255) for x in q) >> 2 for s in (16, 8, 0)]
+        dst = (a << 24) + (ch[0] << 16) + (ch[1] << 8) + ch[2]
+        out.append(dst.reshape(-1).astype(np.uint32))
+        src = dst
+    return np.concatenate(out).astype(np.uint32)
+
+
+@dataclasses.dataclass
+class Texture:
+    """Texel data as RenderSystem hands it to the core (HostTexture::ConvertToCoreTexDesc,
+    host_texture.cpp:43-67): LDR textures carry all MIPLEVELCOUNT levels; normal maps use NRM32."""
+    pixels: np.ndarray        # uint32 texels, levels concatenated
+    width: int
+    height: int
+    flags: int = 0
+    storage: int = 0          # 0 ARGB32, 1 ARGB128, 2 NRM32
+    mips: int = MIPLEVELCOUNT
+
+    def desc(self, keep: np.ndarray) -> abi.CoreTexDesc:
+        d = abi.CoreTexDesc()
+        d.idata = keep.ctypes.data
+        d.width, d.height, d.flags = self.width, self.height, self.flags
+        d.pixelCount = int(keep.size if self.storage != 1 else keep.size // 4)
+        d.firstPixel, d.MIPlevels, d.storage = 0, self.mips, self.storage
+        return d
+
+
+def make_texture(rgba: np.ndarray, normal_map: bool = False) -> Texture:
+    """rgba: (h, w, 4) uint8, bytes in texel order (byte 0 = the texel's x component)."""
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    h, w = rgba.shape[:2]
+    base = rgba.view(np.uint32).reshape(h, w)
+    px = construct_mipmaps(base)
+    assert px.size == pixels_needed(w, h, MIPLEVELCOUNT)
+    return Texture(px, w, h, TEX_NORMALMAP if normal_map else 0, 2 if normal_map else 0)
+
+
+def _tex_pattern(w: int, h: int, seed: int, kind: str) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    if kind == "checker":
+        c = ((x // 8 + y // 8) % 2).astype(np.float32)
+        rgb = np.stack([0.25 + 0.7 * c, 0.3 + 0.4 * c, 0.8 - 0.6 * c], -1)
+        rgb = rgb + rng.uniform(-0.1, 0.1, rgb.shape)
+        a = np.ones((h, w))
+    elif kind == "detail":
+        rgb = 0.5 + 0.2 * np.stack([np.sin(x * 0.7), np.cos(y * 0.9), np.sin((x + y) * 0.4)], -1)
+        a = np.ones((h, w))
+    elif kind == "cutout":
+        rgb = np.stack([0.9 * np.ones((h, w)), 0.6 + 0.3 * (x / w), 0.2 + 0.5 * (y / h)], -1)
+        a = (((x - w / 2) ** 2 + (y - h / 2) ** 2) > (0.3 * w) ** 2).astype(np.float32) * ((x // 4) % 3 != 0)
+    elif kind == "gray":
+        rgb = np.repeat((0.2 + 0.8 * rng.uniform(0, 1, (h, w, 1))), 3, -1)
+        a = np.ones((h, w))
+    else:  # normal map: tilted bumps, z up, mapped to [0, 1]
+        nx = 0.5 * np.sin(x * 2 * np.pi / 16) + rng.uniform(-0.1, 0.1, (h, w))
+        ny = 0.5 * np.cos(y * 2 * np.pi / 16)
+        nz = np.sqrt(np.maximum(0.05, 1 - nx * nx - ny * ny))
+        rgb = np.stack([nx, ny, nz], -1) * 0.5 + 0.5
+        a = np.ones((h, w))
+    px = np.concatenate([np.clip(rgb, 0, 1), a[..., None]], -1)
+    return np.ascontiguousarray((px * 255.999).astype(np.uint8))
+
+
+def _uv_tris(v0, v1, v2, uv0, uv1, uv2, material, vertex_normals=None, tex_area: float = 64 * 64) -> np.ndarray:
+    """CoreTri records with texture coordinates, tangent frame and LOD: T / B from the UV gradient
+    (HostMesh::BuildFromIndexedData convention), triLOD = 0.5 log2(texel area / triangle area)."""
+    t = abi.tris_from_vertices(v0, v1, v2, material, vertex_normals=vertex_normals)
+    uv0, uv1, uv2 = (np.asarray(a, np.float32) for a in (uv0, uv1, uv2))
+    t[:, abi.TRI["u"]:abi.TRI["u"] + 3] = np.stack([uv0[:, 0], uv1[:, 0], uv2[:, 0]], 1)
+    t[:, abi.TRI["v"]:abi.TRI["v"] + 3] = np.stack([uv0[:, 1], uv1[:, 1], uv2[:, 1]], 1)
+    e1, e2 = (v1 - v0).astype(np.float32), (v2 - v0).astype(np.float32)
+    d1, d2 = uv1 - uv0, uv2 - uv0
+    det = d1[:, 0] * d2[:, 1] - d2[:, 0] * d1[:, 1]
+    det = np.where(np.abs(det) < 1e-12, 1.0, det)[:, None]
+    T = (e1 * d2[:, 1:2] - e2 * d1[:, 1:2]) / det
+    B = (e2 * d1[:, 0:1] - e1 * d2[:, 0:1]) / det
+    T = T / np.maximum(np.linalg.norm(T, axis=1, keepdims=True), 1e-12)
+    B = B / np.maximum(np.linalg.norm(B, axis=1, keepdims=True), 1e-12)
+    t[:, abi.TRI["T"]:abi.TRI["T"] + 3] = T
+    t[:, abi.TRI["B"]:abi.TRI["B"] + 3] = B
+    area = 0.5 * np.linalg.norm(np.cross(e1, e2), axis=1)
+    tarea = 0.5 * np.abs(det[:, 0]) * tex_area
+    t[:, abi.TRI["LOD"]] = (0.5 * np.log2(np.maximum(tarea, 1e-12) / np.maximum(area, 1e-12))).astype(np.float32)
+    t[:, abi.TRI["alpha"]:abi.TRI["alpha"] + 3] = 0.0
+    return t.astype(np.float32)
+
+
+def _grid_uv(origin, du, dv, nu, nv, repeat):
+    a, b, c = _grid_quads(origin, du, dv, nu, nv)
+    o, du, dv = (np.asarray(x, np.float32) for x in (origin, du, dv))
+    def uv(p):
+        rel = p - o
+        return np.stack([rel @ du / (du @ du), rel @ dv / (dv @ dv)], 1).astype(np.float32) * np.float32(repeat)
+    return a, b, c, uv(a), uv(b), uv(c)
+
+
+def textured_scene(width: int = 1920, height: int = 1080, tess: int = 24, instances: int = 2) -> Scene:
+    """Every texture path of GetShadingData (material_shared.h:99-171): trilinear diffuse map + detail
+    map, alpha cut-out, normal map + detail normal map (NRM32), roughness map, UV scale / offset;
+    smooth sphere with a diffuse map; an area light; mesh instanced with rotations and scale."""
+    tex = [make_texture(_tex_pattern(64, 64, 1, "checker")), make_texture(_tex_pattern(32, 32, 2, "detail")),
+           make_texture(_tex_pattern(64, 64, 3, "gray")), make_texture(_tex_pattern(32, 32, 4, "normal"), normal_map=True),
+           make_texture(_tex_pattern(16, 16, 5, "normal"), normal_map=True), make_texture(_tex_pattern(64, 64, 6, "cutout"))]
+    def mat(color, tid=None, detail=None, nrm=None, nrm2=None, rough=None, alpha=False, uvs=(1, 1), uvo=(0, 0), **kw):
+        m = abi.make_material(color, **kw)
+        for field, t in (("color", tid), ("detailColor", detail), ("normals", nrm), ("detailNormals", nrm2)):
+            if t is not None:
+                f = getattr(m, field)
+                f.textureID = t
+                f.uvscale[0], f.uvscale[1] = uvs
+                f.uvoffset[0], f.uvoffset[1] = uvo
+        if rough is not None:
+            m.roughness.textureID = rough
+        if alpha:
+            m.flags |= 2
+        return m
+    mats = [mat((0.9, 0.9, 0.9), tid=0, detail=1, rough=2, roughness=0.6, uvs=(1.5, 1.25), uvo=(0.25, 0.1)),   # 0 floor
+            mat((0.8, 0.7, 0.6), tid=0, nrm=3, nrm2=4, roughness=1.0),                                          # 1 wall
+            mat((1.0, 1.0, 1.0), tid=5, alpha=True, roughness=1.0),                                             # 2 cut-out
+            abi.make_material((30.0, 30.0, 26.0)),                                                              # 3 light
+            mat((0.9, 0.8, 0.7), tid=0, nrm=3, roughness=0.8, metallic=0.2, uvs=(4, 2)),                       # 4 sphere
+            mat((0.7, 0.8, 0.9), tid=1, roughness=0.0)]                                                         # 5 specular textured
+    parts = []
+    a, b, c, ua, ub, uc = _grid_uv((-6, 0, -6), (12, 0, 0), (0, 0, 12), tess, tess, 3.0)
+    parts.append(_uv_tris(a, b, c, ua, ub, uc, 0))
+    a, b, c, ua, ub, uc = _grid_uv((-6, 0, 6), (12, 0, 0), (0, 8, 0), tess, tess // 2, 2.0)
+    parts.append(_uv_tris(a, c, b, ua, uc, ub, 1))
+    a, b, c, ua, ub, uc = _grid_uv((-2.5, 0.2, 1.5), (5, 0, 0), (0, 4, 0), 4, 4, 1.0)
+    parts.append(_uv_tris(a, c, b, ua, uc, ub, 2))
+    a, b, c, ua, ub, uc = _grid_uv((3.0, 0.2, -1.0), (0, 0, 3), (0, 3, 0), 3, 3, 1.0)
+    parts.append(_uv_tris(a, c, b, ua, uc, ub, 5))
+    s0, s1, s2, vn = _sphere((-3.0, 1.4, -1.0), 1.3, 2 * tess, tess)
+    def suv(n):
+        return np.stack([np.arctan2(n[:, 2], n[:, 0]) / (2 * np.pi) + 0.5, np.arccos(np.clip(n[:, 1], -1, 1)) / np.pi], 1)
+    parts.append(_uv_tris(s0, s1, s2, suv(vn[0]), suv(vn[1]), suv(vn[2]), 4, vertex_normals=vn))
+    tris = np.concatenate(parts).astype(np.float32)
+    light = quad_tris((0, -1, 0), (0, 7.5, 0), 3, 3, 3)
+    base = len(tris)
+    light.view(np.int32)[:, abi.TRI["ltriIdx"]] = np.arange(2)
+    tris = np.concatenate([tris, light])
+    area = [light_from_tri(tris[base + i], base + i, 0, (30.0, 30.0, 26.0)) for i in range(2)]
+    inst = [(0, np.eye(4, dtype=np.float32))]
+    for k in range(1, instances):
+        T = rotation_y(0.6 * k) * np.float32(0.5)
+        T[3, 3] = 1
+        T[:3, 3] = (14.0 * k, 0.0, 3.0)
+        inst.append((0, T.astype(np.float32)))
+    sc = Scene(meshes=[tris], instances=inst, materials=mats, area_lights=area, textures=tex, name="textured")
+    sc.sky = gradient_sky(64, 32)
+    sc.view = camera_view((2, 5, -12), (0.25, -0.3, 1), fov_deg=60, aspect=width / height, focal=5, pixel_height=height)
+    return sc

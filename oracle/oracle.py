@@ -49,7 +49,8 @@ def lib() -> C.CDLL:
             "orc_set_geometry": [_P, C.c_int, _P, C.c_int], "orc_set_instance": [_P, C.c_int, C.c_int, _F],
             "orc_update_toplevel": [_P], "orc_set_materials": [_P, _P, C.c_int],
             "orc_set_lights": [_P, _P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int],
-            "orc_set_sky": [_P, _F, C.c_int, C.c_int], "orc_setting": [_P, C.c_char_p, C.c_float],
+            "orc_set_sky": [_P, _F, C.c_int, C.c_int], "orc_set_textures": [_P, _P, C.c_int],
+            "orc_fetch_texel": [_P, C.c_int, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, C.c_float, C.c_int, _F], "orc_setting": [_P, C.c_char_p, C.c_float],
             "orc_set_target": [_P, C.c_int, C.c_int, C.c_int], "orc_set_probe": [_P, C.c_int, C.c_int],
             "orc_set_tile": [_P, C.c_int, C.c_int], "orc_set_tile_bands": [_P, C.c_int, C.c_int, C.c_int],
             "orc_render": [_P, C.POINTER(abi.ViewPyramid), C.c_int, C.c_int], "orc_get_accumulator": [_P, _F],
@@ -62,6 +63,7 @@ def lib() -> C.CDLL:
         for k, v in sig.items():
             getattr(L, k).argtypes = v
             getattr(L, k).restype = None
+        L.orc_fetch_texel.restype = C.c_int
         L.orc_samples_taken.argtypes = [_P]
         L.orc_samples_taken.restype = C.c_int
         for k in ("orc_wanghash", "orc_xorshift"):
@@ -139,6 +141,18 @@ class Oracle:
             carr(abi.CoreDirectionalLight, directional)
         self.L.orc_set_lights(self.o, C.cast(a, _P), len(area), C.cast(p, _P), len(point), C.cast(s, _P), len(spot),
                               C.cast(d, _P), len(directional))
+
+    def set_textures(self, textures):
+        self._tex_keep = [np.ascontiguousarray(t.pixels) for t in textures]
+        arr = (abi.CoreTexDesc * max(1, len(textures)))()
+        for i, t in enumerate(textures):
+            arr[i] = t.desc(self._tex_keep[i])
+        self.L.orc_set_textures(self.o, C.cast(arr, _P), len(textures))
+
+    def fetch_texel(self, storage, u, v, offset, w, h, lam=0.0, trilinear=False):
+        out = np.zeros(4, np.float32)
+        assert self.L.orc_fetch_texel(self.o, storage, u, v, offset, w, h, lam, int(trilinear), _fp(out)) == 0
+        return out
 
     def set_sky(self, rgb):
         rgb = np.ascontiguousarray(rgb, np.float32)

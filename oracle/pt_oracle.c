@@ -100,6 +100,7 @@ typedef struct
 	/* CUDAMaterial-equivalent (core_settings.h:94-104) after the host conversion */
 	uint16_t diffuse[3], transmittance[3]; uint32_t flags;
 	uint32_t params[4];
+	uint32_t maps[6][4];   /* tex0, tex1, nmap0, nmap1, smap, rmap: {w | h << 16, half uvscale, half uvoffs, firstPixel} */
 } Mat;
 
 struct Oracle
@@ -114,6 +115,10 @@ struct Oracle
 	lh2_CoreSpotLight* spot; int nSpot;
 	lh2_CoreDirectionalLight* dirl; int nDir;
 	float* sky; int skyW, skyH;
+	lh2_CoreTexDesc* tex; int texCount;    /* copies; firstPixel assigned per storage type */
+	uint32_t* argb32; uint32_t argb32Count;
+	uint32_t* nrm32; uint32_t nrm32Count;
+	float spreadAngle;                    /* of the view being rendered (texture LOD cone) */
 	float geometryEpsilon, clampValue;
 	int w, h, spp;
 	float* acc;          /* float4 per pixel */
@@ -149,6 +154,7 @@ void orc_destroy( Oracle* o )
 	for (int i = 0; i < o->meshCount; i++) free_mesh( &o->meshes[i] );
 	free( o->meshes ); free( o->inst ); free( o->mats ); free( o->area ); free( o->point ); free( o->spot );
 	free( o->dirl ); free( o->sky ); free( o->acc ); free( o->blueNoise );
+	free( o->tex ); free( o->argb32 ); free( o->nrm32 );
 	free( o );
 }
 
@@ -553,9 +559,61 @@ void orc_set_materials( Oracle* o, const lh2_CoreMaterial* mat, int n )
 		g->params[1] = TOUINT4( m->specularTint.value, m->anisotropic.value, m->sheen.value, m->sheenTint.value );
 		g->params[2] = TOUINT4( m->clearcoat.value, m->clearcoatGloss.value, m->transmission.value, 0 );
 		g->params[3] = fbits( m->eta.value );
-		/* texture maps are out of scope this round; the HDR lookup at
-		   rendercore.cpp:386 indexes texDescs[-1] for untextured materials and is dropped */
-		g->flags = (m->eta.value < 1 ? ISDIELECTRIC : 0) + ((m->flags & 1) ? HASSMOOTHNORMALS : 0) + ((m->flags & 2) ? HASALPHA : 0);
+		/* maps: RenderCore::Map (rendercore.h:79-86) for each textured field (rendercore.cpp:379-384) */
+		const struct { int id; lh2_float2 sc, of; int slot; uint32_t flag; } F[6] = {
+			{ m->color.textureID, m->color.uvscale, m->color.uvoffset, 0, 1u << 2 },
+			{ m->detailColor.textureID, m->detailColor.uvscale, m->detailColor.uvoffset, 1, 1u << 9 },
+			{ m->normals.textureID, m->normals.uvscale, m->normals.uvoffset, 2, 1u << 3 },
+			{ m->detailNormals.textureID, m->detailNormals.uvscale, m->detailNormals.uvoffset, 3, 1u << 7 },
+			{ m->specular.textureID, m->specular.uvscale, m->specular.uvoffset, 4, 1u << 4 },
+			{ m->roughness.textureID, m->roughness.uvscale, m->roughness.uvoffset, 5, 1u << 5 } };
+		uint32_t tf = 0;
+		for (int k = 0; k < 6; k++)
+		{
+			if (F[k].id == -1) continue;
+			if (F[k].id < 0 || F[k].id >= o->texCount) continue;   /* the core rejects this (FatalError) */
+			const lh2_CoreTexDesc* t = &o->tex[F[k].id];
+			uint32_t* r = g->maps[F[k].slot];
+			r[0] = (t->width & 0xffffu) | ((t->height & 0xffffu) << 16);
+			r[1] = (uint32_t)lh2_f2h( F[k].sc.x ) | ((uint32_t)lh2_f2h( F[k].sc.y ) << 16);
+			r[2] = (uint32_t)lh2_f2h( F[k].of.x ) | ((uint32_t)lh2_f2h( F[k].of.y ) << 16);
+			r[3] = t->firstPixel;
+			tf |= F[k].flag;
+		}
+		/* DIFFUSEMAPISHDR (bit 1) is never read while shading; the reference's test at
+		   rendercore.cpp:386 indexes texDescs[-1] for untextured materials */
+		if (m->color.textureID >= 0 && m->color.textureID < o->texCount && (o->tex[m->color.textureID].flags & 8)) tf |= 1u << 1;
+		g->flags = (m->eta.value < 1 ? ISDIELECTRIC : 0) + ((m->flags & 1) ? HASSMOOTHNORMALS : 0) + ((m->flags & 2) ? HASALPHA : 0) + tf;
+	}
+}
+
+/* RenderCore::SetTextures + SyncStorageType (rendercore.cpp:276-336): per storage type, one
+   continuous texel array in descriptor order (at least 16 texels); ARGB128 texels are not read
+   by this core's shading and are not kept */
+void orc_set_textures( Oracle* o, const lh2_CoreTexDesc* t, int n )
+{
+	free( o->tex ); free( o->argb32 ); free( o->nrm32 );
+	o->tex = (lh2_CoreTexDesc*)calloc( n > 0 ? n : 1, sizeof( lh2_CoreTexDesc ) );
+	if (n > 0) memcpy( o->tex, t, sizeof( lh2_CoreTexDesc ) * n );
+	o->texCount = n > 0 ? n : 0;
+	for (int storage = 0; storage < 3; storage += 2)
+	{
+		uint32_t total = 0, at = 0;
+		for (int i = 0; i < o->texCount; i++) if (o->tex[i].storage == storage) total += o->tex[i].pixelCount;
+		const uint32_t cnt = total < 16 ? 16 : total;
+		uint32_t* buf = (uint32_t*)calloc( cnt, 4 );
+		for (int i = 0; i < o->texCount; i++) if (o->tex[i].storage == storage)
+		{
+			memcpy( buf + at, o->tex[i].idata, (size_t)o->tex[i].pixelCount * 4 );
+			o->tex[i].firstPixel = at, at += o->tex[i].pixelCount;
+		}
+		if (storage == 0) o->argb32 = buf, o->argb32Count = cnt; else o->nrm32 = buf, o->nrm32Count = cnt;
+	}
+	for (int i = 0; i < o->texCount; i++) if (o->tex[i].storage == 1)
+	{
+		uint32_t at = 0;
+		for (int j = 0; j < i; j++) if (o->tex[j].storage == 1) at += o->tex[j].pixelCount;
+		o->tex[i].firstPixel = at;
 	}
 }
 
@@ -682,7 +740,78 @@ static inline f3 ciexyz_to_linear_rgb( f3 xyz )
 		fmaxf( 0.0f, 0.055648f * xyz.x - 0.204043f * xyz.y + 1.057311f * xyz.z ) );
 }
 
-static void GetShadingData( const Oracle* o, f3 D, float u, float v, const lh2_CoreTri* tri, int instIdx,
+/* texel fetch: sampling_shared.h:35-86 with BILINEAR (core_settings.h:31), MIPLEVELCOUNT 5
+   (common_settings.h:49).  The reference leaves three cases undefined; here (and in the core):
+   float->int conversions saturate (lh2_f2i), a MIP level narrower than one texel counts as one
+   texel (the reference takes % 0 there), and texel indices are clamped to the array. */
+#define MIPLEVELCOUNT 5
+static inline f4 texel_u8( uint32_t v )   /* __uchar4_to_float4: x = lowest byte */
+{
+	const float r = 1.0f / 256.0f;
+	f4 t;
+	t.x = (float)(v & 255u) * r, t.y = (float)((v >> 8) & 255u) * r, t.z = (float)((v >> 16) & 255u) * r, t.w = (float)(v >> 24) * r;
+	return t;
+}
+static f4 FetchTexel( const uint32_t* tex, uint32_t count, f2 tc, int o, int w, int h )
+{
+	if (w < 1) w = 1;
+	if (h < 1) h = 1;
+	const float tcx = (fmaxf( tc.x + 1000, 0.0f ) * (float)w) - 0.5f;
+	const float tcy = (fmaxf( tc.y + 1000, 0.0f ) * (float)h) - 0.5f;
+	const int iu = lh2_f2i( tcx ) % w, iv = lh2_f2i( tcy ) % h;
+	const float fu = tcx - floorf( tcx ), fv = tcy - floorf( tcy );
+	const float w0 = (1 - fu) * (1 - fv), w1 = fu * (1 - fv), w2 = (1 - fu) * fv, w3 = 1 - (w0 + w1 + w2);
+	const uint32_t iu1 = (uint32_t)((iu + 1) % w), iv1 = (uint32_t)((iv + 1) % h);
+	uint32_t a[4] = { (uint32_t)o + (uint32_t)iu + (uint32_t)iv * (uint32_t)w, (uint32_t)o + iu1 + (uint32_t)iv * (uint32_t)w,
+		(uint32_t)o + (uint32_t)iu + iv1 * (uint32_t)w, (uint32_t)o + iu1 + iv1 * (uint32_t)w };
+	f4 p[4];
+	for (int k = 0; k < 4; k++) p[k] = texel_u8( tex[a[k] < count ? a[k] : count - 1] );
+	f4 r;
+	r.x = p[0].x * w0 + p[1].x * w1 + p[2].x * w2 + p[3].x * w3;
+	r.y = p[0].y * w0 + p[1].y * w1 + p[2].y * w2 + p[3].y * w3;
+	r.z = p[0].z * w0 + p[1].z * w1 + p[2].z * w2 + p[3].z * w3;
+	r.w = p[0].w * w0 + p[1].w * w1 + p[2].w * w2 + p[3].w * w3;
+	return r;
+}
+static f4 FetchTexelTrilinear( const uint32_t* tex, uint32_t count, float lambda, f2 tc, int offset, int width, int height )
+{
+	int level0 = lh2_f2i( lambda );
+	if (level0 > MIPLEVELCOUNT - 1) level0 = MIPLEVELCOUNT - 1;
+	const int level1 = level0 + 1 > MIPLEVELCOUNT - 1 ? MIPLEVELCOUNT - 1 : level0 + 1;
+	const float f = lambda - floorf( lambda );
+	int o0 = offset, w0 = width, h0 = height;
+	for (int i = 0; i < level0; i++) o0 += w0 * h0, w0 >>= 1, h0 >>= 1;
+	int o1 = offset, w1 = width, h1 = height;
+	for (int i = 0; i < level1; i++) o1 += w1 * h1, w1 >>= 1, h1 >>= 1;
+	const f4 p0 = FetchTexel( tex, count, tc, o0, w0, h0 ), p1 = FetchTexel( tex, count, tc, o1, w1, h1 );
+	f4 r;
+	r.x = (1 - f) * p0.x + f * p1.x, r.y = (1 - f) * p0.y + f * p1.y, r.z = (1 - f) * p0.z + f * p1.z, r.w = (1 - f) * p0.w + f * p1.w;
+	return r;
+}
+/* uvscale * (uvoffs + (tu, tv)) with the halves of a map record */
+static inline f2 MapCoord( const uint32_t* m, float tu, float tv )
+{
+	f2 c;
+	c.x = lh2_h2f( (uint16_t)(m[1] & 0xffff) ) * (lh2_h2f( (uint16_t)(m[2] & 0xffff) ) + tu);
+	c.y = lh2_h2f( (uint16_t)(m[1] >> 16) ) * (lh2_h2f( (uint16_t)(m[2] >> 16) ) + tv);
+	return c;
+}
+static inline f4 MapFetch( const uint32_t* tex, uint32_t count, const uint32_t* m, float tu, float tv )
+{
+	return FetchTexel( tex, count, MapCoord( m, tu, tv ), (int)m[3], (int)(m[0] & 0xffff), (int)(m[0] >> 16) );
+}
+int orc_fetch_texel( const Oracle* o, int storage, float u, float v, int offset, int w, int h, float lambda, int trilinear, float* out4 )
+{
+	const uint32_t* tex = storage == 2 ? o->nrm32 : o->argb32;
+	const uint32_t cnt = storage == 2 ? o->nrm32Count : o->argb32Count;
+	if (!tex) return -1;
+	f2 tc; tc.x = u, tc.y = v;
+	const f4 r = trilinear ? FetchTexelTrilinear( tex, cnt, lambda, tc, offset, w, h ) : FetchTexel( tex, cnt, tc, offset, w, h );
+	out4[0] = r.x, out4[1] = r.y, out4[2] = r.z, out4[3] = r.w;
+	return 0;
+}
+
+static void GetShadingData( const Oracle* o, f3 D, float u, float v, float coneWidth, const lh2_CoreTri* tri, int instIdx,
 	ShadingData* sd, f3* N, f3* iN, f3* fN, f3* T )
 {
 	const Mat* mat = &o->mats[tri->material];
@@ -709,6 +838,54 @@ static void GetShadingData( const Oracle* o, f3 D, float u, float v, const lh2_C
 	const float alpha = u * tri->alpha.x + v * tri->alpha.y + w * tri->alpha.z;
 	*iN = smul( backSide ? -1.0f : 1.0f, ConsistentNormal( muls( D, -1.0f ), backSide ? muls( *iN, -1.0f ) : *iN, alpha ) );
 	*fN = *iN;
+	/* texturing: material_shared.h:99-171 (OPTIXPRIMEBUILD barycentrics) */
+	if (!(flags & ((1u << 2) | (1u << 9) | (1u << 4) | (1u << 3) | (1u << 7) | (1u << 5)))) return;
+	const float tu = u * tri->u0 + v * tri->u1 + w * tri->u2;
+	const float tv = u * tri->v0 + v * tri->v1 + w * tri->v2;
+	if (flags & (1u << 2))   /* HASDIFFUSEMAP */
+	{
+		const float lambda = tri->LOD + lh2_log2f( coneWidth * (1.0f / fabsf( dot3( D, *N ) )) );   /* eq. 26 */
+		const uint32_t* m = mat->maps[0];
+		const f4 texel = FetchTexelTrilinear( o->argb32, o->argb32Count, lambda, MapCoord( m, tu, tv ), (int)m[3], (int)(m[0] & 0xffff), (int)(m[0] >> 16) );
+		if ((flags & HASALPHA) && texel.w < 0.5f)
+		{
+			sd->flags |= 1;
+			return;
+		}
+		sd->color = mul3( sd->color, mk3( texel.x, texel.y, texel.z ) );
+		if (flags & (1u << 9))   /* HAS2NDDIFFUSEMAP */
+		{
+			const f4 t1 = MapFetch( o->argb32, o->argb32Count, mat->maps[1], tu, tv );
+			sd->color = add3( sd->color, sub3( mk3( t1.x, t1.y, t1.z ), s3( 0.5f ) ) );
+		}
+	}
+	if (flags & (1u << 3))   /* HASNORMALMAP */
+	{
+		const f3 Bt = lf3( tri->B );
+		/* part3 = baseData.z = transmittance_g | transmittance_b << 16 (CUDAMaterial layout) */
+		const uint32_t part3 = (uint32_t)mat->transmittance[1] | ((uint32_t)mat->transmittance[2] << 16);
+		const float b0 = (float)((part3 >> 8) & 255) - 128.0f;
+		const float n0scale = copysignf( -0.0001f + 0.0001f * lh2_expf( 0.1f * fabsf( b0 ) ), b0 );
+		const f4 t0 = MapFetch( o->nrm32, o->nrm32Count, mat->maps[2], tu, tv );
+		f3 sN = mk3( (t0.x - 0.5f) * 2.0f, (t0.y - 0.5f) * 2.0f, (t0.z - 0.5f) * 2.0f );
+		sN.x *= n0scale, sN.y *= n0scale;
+		if (flags & (1u << 7))   /* HAS2NDNORMALMAP */
+		{
+			const float b1 = (float)((part3 >> 16) & 255) - 128.0f;
+			const float n1scale = copysignf( -0.0001f + 0.0001f * lh2_expf( 0.1f * b1 ), b1 );
+			const f4 t1 = MapFetch( o->nrm32, o->nrm32Count, mat->maps[3], tu, tv );
+			f3 l1 = mk3( (t1.x - 0.5f) * 2.0f, (t1.y - 0.5f) * 2.0f, (t1.z - 0.5f) * 2.0f );
+			l1.x *= n1scale, l1.y *= n1scale;
+			sN = add3( sN, l1 );
+		}
+		sN = normalize3( sN );
+		*fN = normalize3( add3( add3( smul( sN.x, *T ), smul( sN.y, Bt ) ), smul( sN.z, *iN ) ) );
+	}
+	if (flags & (1u << 5))   /* HASROUGHNESSMAP */
+	{
+		const f4 t = MapFetch( o->argb32, o->argb32Count, mat->maps[5], tu, tv );
+		sd->params[0] = (sd->params[0] & 0xffffff) + (lh2_f2u( t.x * 255.0f ) << 24);
+	}
 }
 
 /* ------------------------------------------------------------------------------------- */
@@ -1346,7 +1523,7 @@ static int shade_one( const Oracle* o, ThreadCtx* ctx, const PathSeg* in, const 
 	f3 N, iN, fN, T;
 	const f3 I = add3( in->O, smul( HIT_T, D ) );
 	const lh2_CoreTri* tri = &o->meshes[o->inst[INSTANCEIDX].mesh].tris[PRIMIDX];
-	GetShadingData( o, D, HIT_U, HIT_V, tri, INSTANCEIDX, sd, &N, &iN, &fN, &T );
+	GetShadingData( o, D, HIT_U, HIT_V, o->spreadAngle * HIT_T, tri, INSTANCEIDX, sd, &N, &iN, &fN, &T );
 	if (sd->flags & 1) /* alpha pass-through (never set without textures) */
 	{
 		if (pathLength < MAXPL)
@@ -1497,6 +1674,7 @@ void orc_render( Oracle* o, const lh2_ViewPyramid* view, int converge, int nthre
 		o->camRNGseed = 0x12345678;
 	}
 	if (converge == LH2_CONVERGE) o->firstConvergingFrame = 0;
+	o->spreadAngle = view->spreadAngle;
 	const uint32_t camR0 = RandomInt( &o->camRNGseed );
 	if (nthreads < 1) nthreads = 1;
 	const int np = o->w * o->h;

@@ -41,6 +41,9 @@ void orc_set_materials( Oracle* o, const lh2_CoreMaterial* mats, int count );
 void orc_set_lights( Oracle* o, const lh2_CoreLightTri* area, int nArea, const lh2_CorePointLight* point, int nPoint,
 	const lh2_CoreSpotLight* spot, int nSpot, const lh2_CoreDirectionalLight* dir, int nDir );
 void orc_set_sky( Oracle* o, const float* rgb, int w, int h );
+void orc_set_textures( Oracle* o, const lh2_CoreTexDesc* tex, int count );   /* before orc_set_materials */
+/* one texel fetch (sampling_shared.h FetchTexel / FetchTexelTrilinear); storage 0 = ARGB32, 2 = NRM32 */
+int orc_fetch_texel( const Oracle* o, int storage, float u, float v, int offset, int w, int h, float lambda, int trilinear, float* out4 );
 void orc_setting( Oracle* o, const char* name, float value );
 void orc_set_target( Oracle* o, int w, int h, int spp );
 void orc_set_probe( Oracle* o, int x, int y );

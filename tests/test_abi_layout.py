@@ -30,7 +30,7 @@ FIELDS = {   # (struct, field) -> offset, from the reference layout (SURVEY.md Â
 PY_TYPES = {"CoreMaterial": abi.CoreMaterial, "CoreStats": abi.CoreStats, "CoreLightTri": abi.CoreLightTri,
             "ViewPyramid": abi.ViewPyramid, "CorePointLight": abi.CorePointLight, "CoreSpotLight": abi.CoreSpotLight,
             "CoreDirectionalLight": abi.CoreDirectionalLight, "Vec3Value": abi.Vec3Value,
-            "ScalarValue": abi.ScalarValue, "GLTexture": abi.GLTexture}
+            "ScalarValue": abi.ScalarValue, "GLTexture": abi.GLTexture, "CoreTexDesc": abi.CoreTexDesc}
 
 
 def test_python_mirror_sizes_and_offsets():

@@ -91,7 +91,8 @@ def test_oracle_matches_compiled_reference_on_random_rays():
 
 @pytest.mark.parametrize("name,make", [
     ("config2_light_96x54", lambda: scene.config2_scene(n=5000, width=96, height=54, sky=True, light=True)),
-    ("room_96x54", lambda: scene.room_scene(8000, 96, 54))])
+    ("room_96x54", lambda: scene.room_scene(8000, 96, 54)),
+    ("textured_96x54", lambda: scene.textured_scene(96, 54, tess=8))])
 def test_oracle_frame_regression(name, make):
     g = np.load(GOLD / "oracle_frames.npz")
     sc = make()

@@ -159,3 +159,52 @@ def test_hit_barycentrics_follow_prime_convention():
     P = u[:, None] * V[0] + v[:, None] * V[1] + (1 - u - v)[:, None] * V[2]
     Q = org[hit] + h[:, 0].view(np.float32)[:, None].astype(np.float64) * d[hit]
     assert np.max(np.linalg.norm(P - Q, axis=1)) < 2e-3 * 2.0
+
+
+def _np_fetch(tex, u, v, o, w, h):
+    """sampling_shared.h:35-64 (BILINEAR) restated in numpy float32, for one texel fetch."""
+    f = np.float32
+    w, h = max(w, 1), max(h, 1)
+    tcx = f(f(max(f(u + f(1000)), f(0)) * f(w)) - f(0.5))
+    tcy = f(f(max(f(v + f(1000)), f(0)) * f(h)) - f(0.5))
+    iu, iv = int(tcx) % w, int(tcy) % h
+    fu, fv = f(tcx - np.floor(tcx)), f(tcy - np.floor(tcy))
+    w0, w1, w2 = f(f(1) - fu) * f(f(1) - fv), fu * f(f(1) - fv), f(f(1) - fu) * fv
+    w3 = f(f(1) - f(f(w0 + w1) + w2))
+    iu1, iv1 = (iu + 1) % w, (iv + 1) % h
+    p = [tex[o + iu + iv * w], tex[o + iu1 + iv * w], tex[o + iu + iv1 * w], tex[o + iu1 + iv1 * w]]
+    c = [np.array([(t >> s) & 255 for s in (0, 8, 16, 24)], np.float32) * f(1.0 / 256.0) for t in p]
+    return ((c[0] * w0 + c[1] * w1) + c[2] * w2) + c[3] * w3
+
+
+def test_fetch_texel_matches_numpy_restatement():
+    """Oracle FetchTexel / FetchTexelTrilinear (sampling_shared.h:35-86) against an independent numpy
+    restatement; mipmaps against a loop restatement of HostTexture::ConstructMIPmaps."""
+    from lighthouse2_amd import scene
+    from oracle.oracle import Oracle
+    rng = np.random.default_rng(3)
+    rgba = rng.integers(0, 256, (16, 32, 4), dtype=np.uint8)
+    t = scene.make_texture(rgba)
+    # mip level 1 by loops (host_texture.cpp:136-147)
+    src = rgba.view(np.uint32).reshape(16, 32)
+    lvl1 = t.pixels[32 * 16:32 * 16 + 16 * 8].reshape(8, 16)
+    for y in range(8):
+        for x in range(16):
+            q = [int(src[2 * y, 2 * x]), int(src[2 * y, 2 * x + 1]), int(src[2 * y + 1, 2 * x]), int(src[2 * y + 1, 2 * x + 1])]
+            a = min(s >> 24 for s in q)
+            r, g, b = (sum((s >> k) & 255 for s in q) >> 2 for k in (16, 8, 0))
+            assert lvl1[y, x] == (a << 24) + (r << 16) + (g << 8) + b
+    o = Oracle()
+    o.set_textures([t])
+    for k in range(300):
+        u, v = rng.uniform(-3, 3, 2).astype(np.float32)
+        got = o.fetch_texel(0, float(u), float(v), 0, 32, 16)
+        want = _np_fetch(t.pixels, np.float32(u), np.float32(v), 0, 32, 16)
+        assert np.array_equal(got, want), (u, v, got, want)
+    # trilinear: lambda between levels 1 and 2 = mix of the two bilinear fetches
+    lam = np.float32(1.25)
+    got = o.fetch_texel(0, 0.3, 0.7, 0, 32, 16, float(lam), True)
+    p0 = _np_fetch(t.pixels, np.float32(0.3), np.float32(0.7), 32 * 16, 16, 8)
+    p1 = _np_fetch(t.pixels, np.float32(0.3), np.float32(0.7), 32 * 16 + 16 * 8, 8, 4)
+    f = np.float32(0.25)
+    assert np.array_equal(got, (np.float32(1) - f) * p0 + f * p1)

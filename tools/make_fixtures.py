@@ -78,7 +78,8 @@ def bart_fixture():
 def oracle_frames():
     frames = {}
     for name, sc in (("config2_light_96x54", scene.config2_scene(n=5000, width=96, height=54, sky=True, light=True)),
-                     ("room_96x54", scene.room_scene(8000, 96, 54))):
+                     ("room_96x54", scene.room_scene(8000, 96, 54)),
+                     ("textured_96x54", scene.textured_scene(96, 54, tess=8))):
         o = Oracle(threads=8)
         sc.load_into(o)
         o.set_target(96, 54, 1)
