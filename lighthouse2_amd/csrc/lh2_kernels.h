@@ -66,6 +66,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	int* gstack;                                      /* stack entries past LH2_STACK_LDS */
 	uint32_t refill;                                  /* refill idle lanes once >= refill are idle (1..64) */
 	uint32_t leafBatch;                               /* run triangle tests once >= leafBatch lanes parked a leaf */
+	int version;                                      /* traversal loop: 1 (trace_stream) or 2 (lh2_trace2.inc) */
 };
 
 extern "C" {

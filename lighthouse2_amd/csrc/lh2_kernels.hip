@@ -447,18 +447,22 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 	}
 }
 
-template <bool PARK>
+#include "lh2_trace2.inc"
+
+template <bool PARK, int V>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_closest( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	trace_stream<0, PARK>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	if (V == 2) trace_stream2<0, PARK>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	else trace_stream<0, PARK>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 }
 
-template <int MODE>
+template <int MODE, int V>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_any( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	trace_stream<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	if (V == 2) trace_stream2<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	else trace_stream<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 }
 
 /* =====================================================================================
@@ -1417,19 +1421,36 @@ void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, 
 }
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, hipStream_t st )
 {
-	if (a->leafBatch) k_trace_closest<true><<<grid, 256, 0, st>>>( *s, *a );   /* incoherent rays: parked leaves */
-	else k_trace_closest<false><<<grid, 256, 0, st>>>( *s, *a );
+	/* incoherent rays: parked leaves (leafBatch > 0); traversal loop version 1 or 2 (lh2_trace2.inc) */
+	if (a->version == 2)
+	{
+		if (a->leafBatch) k_trace_closest<true, 2><<<grid, 256, 0, st>>>( *s, *a );
+		else k_trace_closest<false, 2><<<grid, 256, 0, st>>>( *s, *a );
+	}
+	else
+	{
+		if (a->leafBatch) k_trace_closest<true, 1><<<grid, 256, 0, st>>>( *s, *a );
+		else k_trace_closest<false, 1><<<grid, 256, 0, st>>>( *s, *a );
+	}
 }
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, hipStream_t st )
 {
-	if (fused) k_trace_any<1><<<grid, 256, 0, st>>>( *s, *a );
-	else k_trace_any<0><<<grid, 256, 0, st>>>( *s, *a );
+	if (a->version == 2)
+	{
+		if (fused) k_trace_any<1, 2><<<grid, 256, 0, st>>>( *s, *a );
+		else k_trace_any<0, 2><<<grid, 256, 0, st>>>( *s, *a );
+	}
+	else
+	{
+		if (fused) k_trace_any<1, 1><<<grid, 256, 0, st>>>( *s, *a );
+		else k_trace_any<0, 1><<<grid, 256, 0, st>>>( *s, *a );
+	}
 }
 int lh2_trace_blocks_per_cu( void )
 {
 	int n1 = 0, n2 = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest<true>, 256, 0 ) != hipSuccess) n1 = 4;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_any<1>, 256, 0 ) != hipSuccess) n2 = 4;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest<true, 1>, 256, 0 ) != hipSuccess) n1 = 4;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_any<1, 1>, 256, 0 ) != hipSuccess) n2 = 4;
 	return n1 > n2 ? n1 : n2;
 }
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, hipStream_t st ) { k_shade<<<grid, 256, 0, st>>>( *s, *p ); }

@@ -119,6 +119,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipMemsetAsync( dSceneError.ptr, 0, sizeof( int ), stream ) );
 	CHK_HIP( hipMemsetAsync( dTlasDepth.ptr, 0, sizeof( int ), stream ) );
 	CHK_HIP( hipHostMalloc( (void**)&activeLog, sizeof( uint32_t ) * 20, hipHostMallocDefault ) );
+	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 2, std::max( 1, atoi( tv ) ) );   /* A/B runs */
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
 }
@@ -165,6 +166,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
+	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 2, std::max( 1, (int)value ) );   /* traversal loop (lh2_trace2.inc) */
 	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
 	else if (!strcmp( name, "gpuTlas" )) { gpuTlas = value != 0; instancesDirty = true; }
 	else if (!strcmp( name, "plocRadius" )) gpuBvh.radius = std::min( 32, std::max( 1, (int)value ) );
@@ -555,6 +557,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		pl = pathLength;
 		CHK_HIP( hipEventRecord( evTrace[2 * pathLength], stream ) );
 		TraceArgs ta{};
+		ta.version = traceVersion;
 		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.countPtr = &c->activePaths, ta.cursor = fetchCursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
 		ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
@@ -591,6 +594,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	CHK_HIP( hipEventRecord( evShadow[0], stream ) );
 	{
 		TraceArgs ta{};
+		ta.version = traceVersion;
 		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = fetchCursors.ptr + (size_t)20 * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
 		lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
@@ -700,6 +704,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
+	ta.version = traceVersion;
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
@@ -719,6 +724,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	CHK_HIP( hipMemsetAsync( m.ptr, 0, words * 4, stream ) );
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
+	ta.version = traceVersion;
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, stream );
 	std::vector<uint32_t> tmp( words );
@@ -743,6 +749,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 	for (int i = 0; i < iterations; i++)
 	{
 		TraceArgs ta{};
+		ta.version = traceVersion;
 		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.cursor = cursors.ptr + (size_t)i * LH2_CURSOR_WORDS;
 		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );

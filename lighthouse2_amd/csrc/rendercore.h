@@ -162,6 +162,7 @@ private:
 	int tiledRays = 1;
 	int refillPrimary = 64, refillOther = 16, leafBatch = 16, leafBatchPrimary = 0;
 	int bvhMaxLeaf = 2;
+	int traceVersion = 1;                /* traversal loop version (setting "traceVersion") */
 	int gpuBuild = 0, gpuTlas = 1;       /* BLAS builder (1: GPU PLOC, 0: CPU binned SAH); TLAS on the GPU */
 	float bvhTraversalCost = 1.0f;
 	int framePathLengths = 0;
