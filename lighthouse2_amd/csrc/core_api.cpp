@@ -42,7 +42,12 @@ public:
 	lh2_CoreStats GetCoreStats() override { lh2_CoreStats s{}; guard( [&] { s = core->GetCoreStats(); } ); return s; }
 	void Init() override { guard( [&] { if (!core) { core = new RenderCore(); core->Init(); } } ); }
 	void SetProbePos( const lh2_int2 pos ) override { core->SetProbePos( pos.x, pos.y ); }
-	void SetTarget( lh2abi::GLTextureView* t, const uint32_t spp ) override { guard( [&] { core->SetTarget( t->width, t->height, spp ); } ); }
+	void SetTarget( lh2abi::GLTextureView* t, const uint32_t spp ) override
+	{
+		/* a GL texture (ID != 0, GL context current) receives every finalized frame through HIP-GL
+		   interop, as InteropTexture does for the CUDA cores (interoptexture.cpp:51-71) */
+		guard( [&] { core->SetTarget( t->width, t->height, spp ); core->SetInteropTexture( t->ID ); } );
+	}
 	void Setting( const char* name, float value ) override { guard( [&] { core->Setting( name, value ); } ); }
 	void Render( const lh2_ViewPyramid& view, const int converge ) override { guard( [&] { core->Render( view, converge ); } ); }
 	void Shutdown() override { guard( [&] { if (core) { core->Shutdown(); delete core; core = nullptr; } } ); }

@@ -12,6 +12,8 @@
 */
 #include "rendercore.h"
 
+#include <hip/hip_gl_interop.h>
+
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -132,6 +134,19 @@ void RenderCore::SetTarget( uint32_t w, uint32_t h, uint32_t spp )  /* rendercor
 	EnsureBuffers();
 	CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)w * h, stream ) );
 	samplesTaken = 0;
+}
+
+/* display output (interoptexture.cpp:25-71): register the app's GL_RGBA32F texture with HIP once per
+   SetTarget; Render copies the finalized frame into it.  Needs the app's GL context to be current,
+   as the reference's interop does; ID 0 (headless RenderSystem, tests, bench) skips it. */
+void RenderCore::SetInteropTexture( uint32_t glTextureId )
+{
+	if (glTextureId == glTexture && (glResource || !glTextureId)) return;
+	if (glResource) { CHK_HIP( hipStreamSynchronize( stream ) ); (void)hipGraphicsUnregisterResource( glResource ); glResource = nullptr; }
+	glTexture = glTextureId;
+	if (!glTextureId) return;
+	const unsigned GL_TEXTURE_2D_ = 0x0DE1;
+	CHK_HIP( hipGraphicsGLRegisterImage( &glResource, glTextureId, GL_TEXTURE_2D_, hipGraphicsRegisterFlagsWriteDiscard ) );
 }
 
 void RenderCore::EnsureBuffers()
@@ -524,6 +539,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	if (!dMaterials.ptr) FatalError( "Render before SetMaterials" );
 	const auto t0 = std::chrono::high_resolution_clock::now();
+	CHK_HIP( hipEventRecord( evFrame[0], stream ) );
 	if (converge == LH2_RESTART || firstConvergingFrame)
 	{
 		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
@@ -602,6 +618,14 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	CHK_HIP( hipEventRecord( evShadow[1], stream ) );
 	samplesTaken += scrspp;
 	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, stream );
+	if (glResource)
+	{
+		hipArray_t arr = nullptr;
+		CHK_HIP( hipGraphicsMapResources( 1, &glResource, stream ) );
+		CHK_HIP( hipGraphicsSubResourceGetMappedArray( &arr, glResource, 0, 0 ) );
+		CHK_HIP( hipMemcpy2DToArrayAsync( arr, 0, 0, frame.ptr, sizeof( float4 ) * scrwidth, sizeof( float4 ) * scrwidth, scrheight, hipMemcpyDeviceToDevice, stream ) );
+		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, stream ) );
+	}
 	CHK_HIP( hipMemcpyAsync( &hostStats->counters, c, sizeof( Counters ), hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipMemcpyAsync( hostStats->rayCount + 1, rayLog.ptr + 1, sizeof( uint32_t ) * 16, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipMemcpyAsync( &hostStats->sceneError, dSceneError.ptr, sizeof( int ), hipMemcpyDeviceToHost, stream ) );
@@ -649,7 +673,7 @@ void RenderCore::Synchronize()
 		coreStats.totalShadowRays = cnt.shadowRays;
 		coreStats.totalExtensionRays = cnt.totalExtensionRays;
 		coreStats.totalRays = coreStats.totalExtensionRays + coreStats.totalShadowRays;
-		coreStats.renderTime = (float)(frameHostMs * 1e-3);
+		coreStats.renderTime = ms( evFrame[0], evFrame[1] );   /* device time of the whole frame (the reference's Render blocks) */
 		coreStats.probedInstid = cnt.probedInstid, coreStats.probedTriid = cnt.probedTriid, coreStats.probedDist = cnt.probedDist;
 	}
 }
@@ -815,6 +839,8 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto& e : evCount) (void)hipEventDestroy( e );
 	for (auto& e : evStage) (void)hipEventDestroy( e );
 	for (int i = 0; i < 2; i++) { if (stage[i]) (void)hipHostFree( stage[i] ); stage[i] = nullptr, stageBytes[i] = 0; }
+	if (glResource) (void)hipGraphicsUnregisterResource( glResource );
+	glResource = nullptr, glTexture = 0;
 	if (activeLog) (void)hipHostFree( activeLog );
 	activeLog = nullptr;
 	if (hostStats) (void)hipHostFree( hostStats );

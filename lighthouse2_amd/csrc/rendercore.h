@@ -65,6 +65,7 @@ public:
 	void Init();
 	void SetProbePos( int x, int y ) { probeX = x, probeY = y; }
 	void SetTarget( uint32_t w, uint32_t h, uint32_t spp );
+	void SetInteropTexture( uint32_t glTextureId );   /* 0: headless (frame stays in the device buffer) */
 	void Setting( const char* name, float value );
 	void Render( const lh2_ViewPyramid& view, int converge );
 	void Shutdown();
@@ -129,6 +130,8 @@ private:
 	size_t stageBytes[2] = {};
 	hipEvent_t evStage[2] = {};
 	int stageSlot = 0;
+	hipGraphicsResource_t glResource = nullptr;   /* registered GL_RGBA32F target texture */
+	uint32_t glTexture = 0;
 	DevBuf<uint4> dMaterials;
 	std::vector<lh2_CoreTexDesc> texDescs;   /* copies, firstPixel assigned per storage (rendercore.cpp:276-292) */
 	DevBuf<uint32_t> dArgb32, dNrm32;        /* continuous texel arrays (rendercore.cpp:299-336) */
@@ -162,7 +165,7 @@ private:
 	int tiledRays = 1;
 	int refillPrimary = 64, refillOther = 16, leafBatch = 16, leafBatchPrimary = 0;
 	int bvhMaxLeaf = 2;
-	int traceVersion = 1;                /* traversal loop version (setting "traceVersion") */
+	int traceVersion = 2;                /* traversal loop version (setting "traceVersion") */
 	int gpuBuild = 0, gpuTlas = 1;       /* BLAS builder (1: GPU PLOC, 0: CPU binned SAH); TLAS on the GPU */
 	float bvhTraversalCost = 1.0f;
 	int framePathLengths = 0;
