@@ -17,6 +17,7 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	   y0 + (lr / band) * bandStride + lr % band  (contiguous tile: band = rows) */
 	int y0, band, bandStride, tileRows;
 	int tiled;   /* store rays in 8x8 pixel blocks per wave (coherent traversal); 0 = row-major */
+	int primeRef;  /* RenderCore_PrimeRef camera: uniform random numbers, no distortion (camera.h:57-60) */
 };
 
 struct SceneDev       /* everything the traversal and shading kernels read, by value (kernarg) */
@@ -53,6 +54,7 @@ struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path st
 	int w, h, pass, pathLength, maxPathLength, probePixel;
 	uint32_t R0;
 	float spreadAngle;               /* ViewPyramid::spreadAngle: ray cone width per unit distance (texture LOD) */
+	int primeRef;                    /* RenderCore_PrimeRef shading (k_shade_ref) */
 };
 
 struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (any) out */
@@ -71,7 +73,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 
 extern "C" {
 void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t* cursors, int cursorWords, hipStream_t st );
-void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, hipStream_t st );
+void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, hipStream_t st );
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, hipStream_t st );
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, hipStream_t st );
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, hipStream_t st );
@@ -88,7 +90,9 @@ void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, hi
 #endif
 #define LH2_CURSOR_STRIDE 32
 #define LH2_CURSOR_WORDS (LH2_CHUNKS * LH2_CURSOR_STRIDE)   /* per trace launch */
-#define LH2_CURSOR_SLOTS 24                                  /* launches per frame: [L] bounce L, [20] shadow */
+#define LH2_MAX_BOUNCES 64                                   /* RenderCore_PrimeRef MAXPATHLENGTH (core_settings.h:25) */
+#define LH2_CURSOR_SLOTS (2 * LH2_MAX_BOUNCES + 4)           /* launches per frame: [L] bounce L, [64 + L] shadow after bounce L, [130] shadow */
+#define LH2_SHADOW_SLOT (2 * LH2_MAX_BOUNCES + 2)
 #ifndef LH2_STACK_LDS
 #define LH2_STACK_LDS 16
 #endif

@@ -107,7 +107,7 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 	const uint32_t sampleIndex = (uint32_t)p.pass + y / h;
 	y %= h;
 	float r0, r1, r2, r3;
-	if (sampleIndex < 256)
+	if (sampleIndex < 256 && !p.primeRef)
 	{
 		r0 = blueNoiseSampler( bn, x, y, sampleIndex, 0 );
 		r1 = blueNoiseSampler( bn, x, y, sampleIndex, 1 );
@@ -122,7 +122,7 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 	}
 	const v3 p1 = mk3( p.p1.x, p.p1.y, p.p1.z ), right = mk3( p.right.x, p.right.y, p.right.z ), up = mk3( p.up.x, p.up.y, p.up.z );
 	v3 posOnPixel;
-	if (p.distortion == 0)
+	if (p.distortion == 0 || p.primeRef)
 	{
 		posOnPixel = add3( add3( p1, smul( (float)x + r0, divs( right, (float)w ) ) ), smul( (float)y + r1, divs( up, (float)h ) ) );
 	}
@@ -1369,6 +1369,181 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const Scen
 }
 
 /* counters: .cuda.cu:64-84 */
+/* =====================================================================================
+   PrimeRef validation mode: RenderCore_PrimeRef/kernels/pathtracer.h:44-165 with its Lambert
+   BSDF (kernels/bsdf.h:18-101): uniform random numbers, NEE without MIS, Russian roulette at
+   every vertex, MAXPATHLENGTH 64, no clamping.  Defined where the reference is undefined: a
+   total-internal-reflection sample leaves the direction (0,0,0) (bsdf.h:75 returns before
+   writing wi), and alpha cut-outs are shaded as hits (this pathtracer never tests the flag).
+   ===================================================================================== */
+LH2_DEV float Fr_Lambert( const float VDotN, const float eio )   /* bsdf.h:18-26 */
+{
+	const float SinThetaT2 = sqrf( eio ) * (1.0f - VDotN * VDotN);
+	if (SinThetaT2 > 1.0f) return 1.0f;
+	const float LDotN = sqrtf( 1.0f - SinThetaT2 );
+	const float r1 = (VDotN - eio * LDotN) / (VDotN + eio * LDotN);
+	const float r2 = (LDotN - eio * VDotN) / (LDotN + eio * VDotN);
+	return 0.5f * (sqrf( r1 ) + sqrf( r2 ));
+}
+LH2_DEV v3 Tangent2World1( const v3 V, const v3 N )   /* tools_shared.h:211-220, "Building an Orthonormal Basis, Revisited" */
+{
+	const float sign = copysignf( 1.0f, N.z );
+	const float a = -1.0f / (sign + N.z);
+	const float b = N.x * N.y * a;
+	const v3 B = mk3( 1.0f + sign * N.x * N.x * a, sign * b, -sign * N.x );
+	const v3 T = mk3( b, sign + N.y * N.y * a, -N.y );
+	return add3( add3( smul( V.x, T ), smul( V.y, B ) ), smul( V.z, N ) );
+}
+LH2_DEV v3 EvaluateBSDF_Lambert( const ShadingData& sd, const v3 iN, const v3 wi, float& pdf )   /* bsdf.h:40-51 */
+{
+	if (TRANSMISSION > 0.999f || ROUGHNESS <= 0.001f) { pdf = 0; return s3( 0 ); }
+	pdf = fabsf( dot3( wi, iN ) ) * INVPI;
+	return muls( muls( sd.color, INVPI ), ROUGHNESS );
+}
+LH2_DEV v3 SampleBSDF_Lambert( const ShadingData& sd, v3 iN, const v3 N, const v3 wo, const float distance, const float r3, const float r4,
+	v3& wi, float& pdf, bool& specular )   /* bsdf.h:53-101 */
+{
+	const float flip = (dot3( wo, N ) < 0) ? -1 : 1;
+	iN = muls( iN, flip );
+	specular = true, pdf = 1;
+	v3 bsdf;
+	if (r4 < TRANSMISSION)
+	{
+		const float eio = flip < 0 ? (1.0f / ETA) : ETA, F = Fr_Lambert( dot3( iN, wo ), eio );
+		const v3 beer = mk3( lh2_expf( -sd.transmittance.x * distance * 2.0f ), lh2_expf( -sd.transmittance.y * distance * 2.0f ),
+			lh2_expf( -sd.transmittance.z * distance * 2.0f ) );
+		if (r3 < F)
+		{
+			wi = reflect3( muls( wo, -1.0f ), iN );
+			bsdf = muls( mul3( sd.color, beer ), 1 / fabsf( dot3( iN, wi ) ) );
+		}
+		else
+		{
+			if (!Refract_L( wo, iN, eio, wi )) return s3( 0 );
+			return muls( mul3( sd.color, beer ), 1 / fabsf( dot3( iN, wi ) ) );
+		}
+	}
+	else
+	{
+		const float pReflect = 1 - ROUGHNESS;
+		if (r3 < pReflect)
+		{
+			wi = reflect3( muls( wo, -1.0f ), iN );
+			bsdf = muls( sd.color, 1.0f / fabsf( dot3( iN, wi ) ) );
+		}
+		else
+		{
+			const float r5 = (r3 - pReflect) / (1 - pReflect);
+			const float r6 = (r4 - TRANSMISSION) / (1 - TRANSMISSION);
+			wi = normalize3( Tangent2World1( DiffuseReflectionCosWeighted( r5, r6 ), iN ) );
+			pdf = fmaxf( 0.0f, dot3( wi, iN ) ) * INVPI;
+			specular = false;
+			bsdf = muls( sd.color, INVPI );
+		}
+	}
+	if (dot3( muls( N, flip ), wi ) <= 0) pdf = 0;   /* APPLYSAFENORMALS */
+	return bsdf;
+}
+
+__global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const SceneDev s, const ShadeParams p )
+{
+	const uint32_t count = *p.pathCount;
+	const uint32_t gstride = gridDim.x * 256u;
+	const int w = p.w, h = p.h;
+	for (uint32_t base = blockIdx.x * 256u; base < count; base += gstride)
+	{
+		const uint32_t jobIndex = base + threadIdx.x;
+		bool doExt = false, doShadow = false;
+		float4 eO, eD, eT, eQ, sO, sD, sP;
+		if (jobIndex < count)
+		{
+			const float4 O4 = p.rayO[jobIndex], D4 = p.rayD[jobIndex], T4 = p.T4[jobIndex];
+			const uint4 hd = p.hits[jobIndex];
+			const float HIT_T = __uint_as_float( hd.x );
+			const int PRIMIDX = (int)hd.y;
+			const int INSTANCEIDX = PRIMIDX == -1 ? 0 : (int)hd.z;
+			const float HIT_U = (float)(hd.w & 65535) * (1.0f / 65535.0f);
+			const float HIT_V = (float)(hd.w >> 16) * (1.0f / 65535.0f);
+			uint32_t data = fbits( T4.w );
+			const v3 D = xyz( D4 ), RAY_O = xyz( O4 );
+			v3 throughput = xyz( T4 );
+			const uint32_t pathIdx = data >> 8;
+			const uint32_t pixelIdx = pathIdx % (uint32_t)(w * h);
+			const uint32_t sampleIdx = pathIdx / (uint32_t)(w * h) + (uint32_t)p.pass;
+			if (p.pathLength == 1) unsafeAtomicAdd( &p.acc[pixelIdx].w, PRIMIDX == NOHIT ? 10000.0f : HIT_T );
+			if (PRIMIDX == NOHIT)
+			{
+				acc_add( p.acc, pixelIdx, mul3( throughput, SampleSkydome( s, D ) ) );
+				goto compact;
+			}
+			if ((int)pixelIdx == p.probePixel && p.pathLength == 1 && sampleIdx == 0)
+				p.counters->probedInstid = INSTANCEIDX, p.counters->probedTriid = PRIMIDX, p.counters->probedDist = HIT_T;
+			{
+				ShadingData sd;
+				v3 N, iN, fN, T;
+				const v3 I = add3( RAY_O, smul( HIT_T, D ) );
+				const float4* tri = (const float4*)s.instDesc[INSTANCEIDX].triangles + (size_t)PRIMIDX * 11;
+				GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, INSTANCEIDX, sd, N, iN, fN, T );
+				if (sd.color.x > 1.0f || sd.color.y > 1.0f || sd.color.z > 1.0f)
+				{
+					if (-dot3( D, N ) > 0 && (p.pathLength == 1 || (data & S_SPECULAR))) acc_add( p.acc, pixelIdx, mul3( throughput, sd.color ) );
+					goto compact;
+				}
+				if (ROUGHNESS <= 0.001f || TRANSMISSION > 0.999f) data |= S_SPECULAR; else data &= ~S_SPECULAR;
+				uint32_t seed = WangHash( pathIdx * 17 + p.R0 );
+				const float faceDir = (dot3( D, N ) > 0) ? -1 : 1;
+				if (faceDir == 1) sd.transmittance = s3( 0 );
+				if (!(data & S_SPECULAR))
+				{
+					const float r0 = RandomFloat( seed ), r1 = RandomFloat( seed );
+					float pickProb = 0, lightPdf = 0;
+					v3 lightColor = s3( 0 );
+					v3 L = sub3( RandomPointOnLight( s, r0, r1, I, muls( fN, faceDir ), pickProb, lightPdf, lightColor ), I );
+					const float dist = length3( L );
+					L = muls( L, 1.0f / dist );
+					const float NdotL = dot3( L, muls( fN, faceDir ) );
+					if (NdotL > 0 && lightPdf > 0 && p.pathLength < p.maxPathLength)   /* the last bounce's shadow rays are never traced (rendercore.cpp loop break) */
+					{
+						float bsdfPdf;
+						const v3 sampledBSDF = EvaluateBSDF_Lambert( sd, fN, L, bsdfPdf );
+						const v3 contribution = muls( mul3( mul3( throughput, sampledBSDF ), lightColor ), NdotL / (pickProb * lightPdf) );
+						const v3 so = SafeOrigin( I, L, muls( N, faceDir ), s.geometryEpsilon );
+						doShadow = true;
+						sO = make_float4( so.x, so.y, so.z, 0 );
+						sD = make_float4( L.x, L.y, L.z, dist - 2 * s.geometryEpsilon );
+						sP = make_float4( contribution.x, contribution.y, contribution.z, __uint_as_float( pixelIdx ) );
+					}
+				}
+				const float r3 = RandomFloat( seed ), r4 = RandomFloat( seed ), r5 = RandomFloat( seed );
+				v3 R = s3( 0 );
+				float newBsdfPdf = 0;
+				bool specular = false;
+				const v3 bsdf = SampleBSDF_Lambert( sd, fN, N, muls( D, -1.0f ), HIT_T, r3, r4, R, newBsdfPdf, specular );
+				if (newBsdfPdf < EPSILON || newBsdfPdf != newBsdfPdf) goto compact;
+				if (specular) data |= S_SPECULAR;
+				const float pr = p.pathLength == p.maxPathLength ? 0 : ((data & S_SPECULAR) ? 1 : SurvivalProbability( bsdf ));
+				if (pr <= r5) goto compact;
+				throughput = mul3( throughput, divs( muls( bsdf, fabsf( dot3( fN, R ) ) ), pr * newBsdfPdf ) );
+				const v3 eo = SafeOrigin( I, R, muls( N, faceDir ), s.geometryEpsilon );
+				doExt = true;
+				eO = make_float4( eo.x, eo.y, eo.z, 0 ), eD = make_float4( R.x, R.y, R.z, 1e34f );
+				eT = make_float4( throughput.x, throughput.y, throughput.z, bitsf( data ) ), eQ = make_float4( 1, 0, 0, 0 );
+			}
+		}
+	compact:
+		{
+			const uint32_t es = wave_alloc( doExt, &p.counters->extensionRays );
+			if (doExt) { p.rayOut[es] = eO; p.rayDOut[es] = eD; p.T4Out[es] = eT; p.Q4Out[es] = eQ; }
+			const uint32_t ss = wave_alloc( doShadow, &p.counters->shadowRays );
+			if (doShadow)
+			{
+				if (ss < p.shadowCap) { p.shO[ss] = sO; p.shD[ss] = sD; p.shP[ss] = sP; }
+				else atomicOr( &p.counters->shadowOverflow, 1u );
+			}
+		}
+	}
+}
+
 __global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t* cursors, int cursorWords )
 {
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1379,13 +1554,14 @@ __global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t* curs
 	c->probedInstid = -1, c->probedTriid = -1, c->probedDist = 0;
 	c->reserved0 = 0, c->shadowOverflow = 0;
 }
-__global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength )
+__global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength, int resetShadow )
 {
 	if (threadIdx.x != 0) return;
 	rayCountLog[pathLength] = c->extensionRays;     /* rays traced at pathLength + 1 */
 	c->totalExtensionRays += c->extensionRays;
 	c->activePaths = c->extensionRays;
 	c->extensionRays = 0;
+	if (resetShadow) c->totalShadowRays += c->shadowRays, c->shadowRays = 0;   /* InitCountersSubsequent (.cuda.cu:76-84) */
 }
 __global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale )
 {
@@ -1413,7 +1589,7 @@ void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t* cursor
 {
 	k_init_counters<<<(cursorWords + 255) / 256 + 1, 256, 0, st>>>( c, pathCount, cursors, cursorWords );
 }
-void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, hipStream_t st ) { k_counters_next<<<1, 64, 0, st>>>( c, log, pathLength ); }
+void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, hipStream_t st ) { k_counters_next<<<1, 64, 0, st>>>( c, log, pathLength, resetShadow ); }
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, hipStream_t st )
 {
 	if (jobCount <= 0) return;
@@ -1453,7 +1629,11 @@ int lh2_trace_blocks_per_cu( void )
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_any<1, 1>, 256, 0 ) != hipSuccess) n2 = 4;
 	return n1 > n2 ? n1 : n2;
 }
-void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, hipStream_t st ) { k_shade<<<grid, 256, 0, st>>>( *s, *p ); }
+void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, hipStream_t st )
+{
+	if (p->primeRef) k_shade_ref<<<grid, 256, 0, st>>>( *s, *p );
+	else k_shade<<<grid, 256, 0, st>>>( *s, *p );
+}
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, hipStream_t st )
 {
 	if (rows * w <= 0) return;

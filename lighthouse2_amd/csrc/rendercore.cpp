@@ -107,13 +107,14 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	dBlueNoise.upload( bn.data(), bn.size(), stream );
 	counters.resize( 1 );
 	fetchCursors.resize( (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
-	rayLog.resize( 32 );
+	rayLog.resize( LH2_MAX_BOUNCES + 8 );
 	blocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocDefault ) );
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evTrace) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evShade) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evShadow) CHK_HIP( hipEventCreate( &e ) );
+	for (auto& e : evShadowB) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evCount) CHK_HIP( hipEventCreateWithFlags( &e, hipEventDisableTiming ) );
 	for (auto& e : evStage) CHK_HIP( hipEventCreateWithFlags( &e, hipEventDisableTiming ) );
@@ -170,6 +171,9 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	if (!strcmp( name, "epsilon" )) geometryEpsilon = value;
 	else if (!strcmp( name, "clampValue" )) clampValue = value;
 	else if (!strcmp( name, "maxPathLength" )) maxPathLength = std::min( 16, std::max( 1, (int)value ) );
+	/* PrimeRef validation mode: the RenderCore_PrimeRef path tracer (uniform random numbers, Lambert
+	   BSDF, NEE without MIS, Russian roulette, MAXPATHLENGTH 64) on the same scene data */
+	else if (!strcmp( name, "primeRef" )) primeRef = value != 0;
 	else if (!strcmp( name, "tiledRays" )) tiledRays = value != 0;
 	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle (64 = whole batches);
 	   coherent 8x8-tiled primary rays trace best in batches, incoherent bounce rays with refills */
@@ -555,7 +559,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	Counters* c = counters.ptr;
 	lh2_launch_init_counters( c, pathCount, fetchCursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, stream );
 	/* primary rays (camera.h) for every sample of the tile */
-	CameraParams cp;
+	CameraParams cp{};
 	cp.pos = view.pos, cp.p1 = view.p1;
 	cp.right = { view.p2.x - view.p1.x, view.p2.y - view.p1.y, view.p2.z - view.p1.z };
 	cp.up = { view.p3.x - view.p1.x, view.p3.y - view.p1.y, view.p3.z - view.p1.z };
@@ -565,10 +569,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	cp.y0 = std::max( 0, tileY0 ), cp.tileRows = tileRows;
 	cp.band = tileBand > 0 ? tileBand : std::max( 1, tileRows ), cp.bandStride = tileBand > 0 ? tileStride : std::max( 1, tileRows );
 	cp.tiled = tiledRays;
+	cp.primeRef = primeRef;
 	lh2_launch_camera( &cp, dBlueNoise.ptr, rayO[0].ptr, rayD[0].ptr, T4[0].ptr, Q4[0].ptr, (int)pathCount, stream );
 	int in = 0, pl = 0;
 	const int grid = TraceGrid();
-	for (int pathLength = 1; pathLength <= maxPathLength; pathLength++)
+	const int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
+	for (int pathLength = 1; pathLength <= maxPL; pathLength++)
 	{
 		pl = pathLength;
 		CHK_HIP( hipEventRecord( evTrace[2 * pathLength], stream ) );
@@ -580,21 +586,35 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.hits = hits.ptr, ta.gstack = gstack.ptr;
 		lh2_launch_trace_closest( &sd, &ta, grid, stream );
 		CHK_HIP( hipEventRecord( evTrace[2 * pathLength + 1], stream ) );
-		ShadeParams sp;
+		ShadeParams sp{};
 		sp.pathCount = &c->activePaths;
 		sp.rayO = rayO[in].ptr, sp.rayD = rayD[in].ptr, sp.T4 = T4[in].ptr, sp.Q4 = Q4[in].ptr, sp.hits = hits.ptr;
 		sp.rayOut = rayO[1 - in].ptr, sp.rayDOut = rayD[1 - in].ptr, sp.T4Out = T4[1 - in].ptr, sp.Q4Out = Q4[1 - in].ptr;
 		sp.shO = shO.ptr, sp.shD = shD.ptr, sp.shP = shP.ptr, sp.shadowCap = (uint32_t)shO.count;
 		sp.acc = accumulator.ptr, sp.counters = c;
-		sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPathLength;
+		sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
+		sp.primeRef = primeRef;
 		sp.probePixel = probeX + scrwidth * probeY;
 		sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
 		sp.spreadAngle = view.spreadAngle;
 		CHK_HIP( hipEventRecord( evShade[2 * pathLength], stream ) );
 		lh2_launch_shade( &sd, &sp, grid, stream );
 		CHK_HIP( hipEventRecord( evShade[2 * pathLength + 1], stream ) );
-		if (pathLength == maxPathLength) break;
-		lh2_launch_counters_next( c, rayLog.ptr, pathLength, stream );
+		if (pathLength == maxPL) break;
+		if (primeRef)
+		{
+			/* RenderCore_PrimeRef traces the shadow rays of every bounce right after it
+			   (rendercore.cpp connect step), fused with finalizeConnections */
+			CHK_HIP( hipEventRecord( evShadowB[2 * pathLength], stream ) );
+			TraceArgs ta{};
+			ta.version = traceVersion;
+			ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = fetchCursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
+			ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+			ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
+			lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
+			CHK_HIP( hipEventRecord( evShadowB[2 * pathLength + 1], stream ) );
+		}
+		lh2_launch_counters_next( c, rayLog.ptr, pathLength, primeRef, stream );
 		CHK_HIP( hipMemcpyAsync( activeLog + pathLength, &c->activePaths, sizeof( uint32_t ), hipMemcpyDeviceToHost, stream ) );
 		CHK_HIP( hipEventRecord( evCount[pathLength], stream ) );
 		/* early exit without stalling the GPU: wait for the count of the previous bounce while this
@@ -608,10 +628,11 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	}
 	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
 	CHK_HIP( hipEventRecord( evShadow[0], stream ) );
+	if (!primeRef)
 	{
 		TraceArgs ta{};
 		ta.version = traceVersion;
-		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = fetchCursors.ptr + (size_t)20 * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = fetchCursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
 		lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
 	}
@@ -627,11 +648,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, stream ) );
 	}
 	CHK_HIP( hipMemcpyAsync( &hostStats->counters, c, sizeof( Counters ), hipMemcpyDeviceToHost, stream ) );
-	CHK_HIP( hipMemcpyAsync( hostStats->rayCount + 1, rayLog.ptr + 1, sizeof( uint32_t ) * 16, hipMemcpyDeviceToHost, stream ) );
+	CHK_HIP( hipMemcpyAsync( hostStats->rayCount + 1, rayLog.ptr + 1, sizeof( uint32_t ) * LH2_MAX_BOUNCES, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipMemcpyAsync( &hostStats->sceneError, dSceneError.ptr, sizeof( int ), hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipEventRecord( evFrame[1], stream ) );
 	hostStats->rayCount[0] = pathCount;
 	framePathLengths = pl;
+	framePrimeRef = primeRef;
 	statsPending = true;
 	frameHostMs = std::chrono::duration<double, std::milli>( std::chrono::high_resolution_clock::now() - t0 ).count();
 }
@@ -666,11 +688,12 @@ void RenderCore::Synchronize()
 		coreStats.deepRayCount = 0, coreStats.traceTimeX = 0;
 		for (int L = 3; L <= framePathLengths; L++) coreStats.deepRayCount = rc[L - 1], coreStats.traceTimeX = ms( evTrace[2 * L], evTrace[2 * L + 1] );
 		coreStats.shadowTraceTime = ms( evShadow[0], evShadow[1] );
+		if (framePrimeRef) for (int L = 1; L < framePathLengths; L++) coreStats.shadowTraceTime += ms( evShadowB[2 * L], evShadowB[2 * L + 1] );
 		float shade = 0;
 		for (int L = 1; L <= framePathLengths; L++) shade += ms( evShade[2 * L], evShade[2 * L + 1] );
 		coreStats.shadeTime = shade;
 		for (int L = 1; L <= framePathLengths && L <= 8; L++) lastKernelMs[L - 1] = ms( evTrace[2 * L], evTrace[2 * L + 1] ) * 1e3f;
-		coreStats.totalShadowRays = cnt.shadowRays;
+		coreStats.totalShadowRays = framePrimeRef ? cnt.totalShadowRays : cnt.shadowRays;
 		coreStats.totalExtensionRays = cnt.totalExtensionRays;
 		coreStats.totalRays = coreStats.totalExtensionRays + coreStats.totalShadowRays;
 		coreStats.renderTime = ms( evFrame[0], evFrame[1] );   /* device time of the whole frame (the reference's Render blocks) */
@@ -688,7 +711,7 @@ void RenderCore::GetRayCounts( uint32_t* out17 )
 {
 	Synchronize();
 	for (int i = 0; i < 17; i++) out17[i] = i < framePathLengths ? hostStats->rayCount[i] : 0;
-	out17[16] = hostStats->counters.shadowRays;
+	out17[16] = framePrimeRef ? hostStats->counters.totalShadowRays : hostStats->counters.shadowRays;
 }
 
 void RenderCore::GetAccumulator( float* hostOut4 )
@@ -792,13 +815,13 @@ void RenderCore::GenerateEyeRays( const lh2_ViewPyramid& view, uint32_t R0, int 
 	const int n = scrwidth * scrheight * scrspp;
 	DevBuf<float4> o, d, t4, q4;
 	o.resize( n ), d.resize( n ), t4.resize( n ), q4.resize( n );
-	CameraParams cp;
+	CameraParams cp{};
 	cp.pos = view.pos, cp.p1 = view.p1;
 	cp.right = { view.p2.x - view.p1.x, view.p2.y - view.p1.y, view.p2.z - view.p1.z };
 	cp.up = { view.p3.x - view.p1.x, view.p3.y - view.p1.y, view.p3.z - view.p1.z };
 	cp.aperture = view.aperture, cp.distortion = view.distortion, cp.geometryEpsilon = geometryEpsilon;
 	cp.w = scrwidth, cp.h = scrheight, cp.pass = pass, cp.R0 = R0;
-	cp.y0 = 0, cp.tileRows = scrheight, cp.band = scrheight, cp.bandStride = scrheight, cp.tiled = 0;
+	cp.y0 = 0, cp.tileRows = scrheight, cp.band = scrheight, cp.bandStride = scrheight, cp.tiled = 0, cp.primeRef = primeRef;
 	lh2_launch_camera( &cp, dBlueNoise.ptr, o.ptr, d.ptr, t4.ptr, q4.ptr, n, stream );
 	std::vector<float4> T( n ), Q( n );
 	CHK_HIP( hipMemcpyAsync( ot, o.ptr, sizeof( float4 ) * n, hipMemcpyDeviceToHost, stream ) );
@@ -835,6 +858,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto& e : evTrace) (void)hipEventDestroy( e );
 	for (auto& e : evShade) (void)hipEventDestroy( e );
 	for (auto& e : evShadow) (void)hipEventDestroy( e );
+	for (auto& e : evShadowB) (void)hipEventDestroy( e );
 	for (auto& e : evFrame) (void)hipEventDestroy( e );
 	for (auto& e : evCount) (void)hipEventDestroy( e );
 	for (auto& e : evStage) (void)hipEventDestroy( e );

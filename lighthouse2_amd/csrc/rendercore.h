@@ -54,7 +54,7 @@ struct CoreInstanceHost { int mesh; float T[16]; float inv[16]; };
 
 struct FrameStats   /* per-frame values read back from the device */
 {
-	uint32_t rayCount[17];
+	uint32_t rayCount[LH2_MAX_BOUNCES + 1];
 	Counters counters;
 	int sceneError;
 };
@@ -143,6 +143,7 @@ private:
 	/* settings (rendercore.h DeviceVars; constant-memory defaults: .cuda.cu:38-39) */
 	float geometryEpsilon = 0.0f, clampValue = 10.0f;
 	int maxPathLength = 16;
+	int primeRef = 0;                    /* RenderCore_PrimeRef validation mode (setting "primeRef") */
 	int probeX = 0, probeY = 0;
 	/* target + frame buffers */
 	int scrwidth = 0, scrheight = 0, scrspp = 1;
@@ -159,8 +160,9 @@ private:
 	DevBuf<uint32_t> rayLog;
 	FrameStats* hostStats = nullptr;     /* pinned */
 	bool statsPending = false;
-	hipEvent_t evTrace[2 * 17] = {}, evShade[2 * 17] = {}, evShadow[2] = {}, evFrame[2] = {};
-	hipEvent_t evCount[18] = {};
+	hipEvent_t evTrace[2 * (LH2_MAX_BOUNCES + 1)] = {}, evShade[2 * (LH2_MAX_BOUNCES + 1)] = {}, evShadow[2] = {}, evFrame[2] = {};
+	hipEvent_t evShadowB[2 * (LH2_MAX_BOUNCES + 1)] = {};   /* per-bounce shadow passes (PrimeRef mode) */
+	hipEvent_t evCount[LH2_MAX_BOUNCES + 2] = {};
 	uint32_t* activeLog = nullptr;     /* pinned: active paths after each bounce */
 	int tiledRays = 1;
 	int refillPrimary = 64, refillOther = 16, leafBatch = 16, leafBatchPrimary = 0;
@@ -168,7 +170,7 @@ private:
 	int traceVersion = 2;                /* traversal loop version (setting "traceVersion") */
 	int gpuBuild = 0, gpuTlas = 1;       /* BLAS builder (1: GPU PLOC, 0: CPU binned SAH); TLAS on the GPU */
 	float bvhTraversalCost = 1.0f;
-	int framePathLengths = 0;
+	int framePathLengths = 0, framePrimeRef = 0;
 	double frameHostMs = 0;
 	int samplesTaken = 0;
 	bool firstConvergingFrame = false;

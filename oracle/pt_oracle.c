@@ -119,6 +119,7 @@ struct Oracle
 	uint32_t* argb32; uint32_t argb32Count;
 	uint32_t* nrm32; uint32_t nrm32Count;
 	float spreadAngle;                    /* of the view being rendered (texture LOD cone) */
+	int primeRef;                         /* RenderCore_PrimeRef validation mode */
 	float geometryEpsilon, clampValue;
 	int w, h, spp;
 	float* acc;          /* float4 per pixel */
@@ -640,6 +641,7 @@ void orc_setting( Oracle* o, const char* name, float value ) /* rendercore.cpp:4
 	if (!strcmp( name, "epsilon" )) o->geometryEpsilon = value;
 	else if (!strcmp( name, "clampValue" )) o->clampValue = value;
 	else if (!strcmp( name, "maxPathLength" )) orc_set_max_path_length( o, (int)value );
+	else if (!strcmp( name, "primeRef" )) o->primeRef = value != 0;
 }
 
 void orc_set_target( Oracle* o, int w, int h, int spp ) /* rendercore.cpp:149-209 */
@@ -1420,7 +1422,7 @@ static void eye_ray( const Oracle* o, const lh2_ViewPyramid* view, uint32_t R0, 
 	const uint32_t sampleIndex = (uint32_t)pass + y / (uint32_t)h;
 	y %= (uint32_t)h;
 	float r0, r1, r2, r3;
-	if (sampleIndex < 256)
+	if (sampleIndex < 256 && !o->primeRef)   /* PrimeRef camera: uniform random numbers (camera.h:57-59) */
 	{
 		r0 = blueNoiseSampler( o->blueNoise, x, y, sampleIndex, 0 );
 		r1 = blueNoiseSampler( o->blueNoise, x, y, sampleIndex, 1 );
@@ -1434,7 +1436,7 @@ static void eye_ray( const Oracle* o, const lh2_ViewPyramid* view, uint32_t R0, 
 		r2 = RandomFloat( &seed ), r3 = RandomFloat( &seed );
 	}
 	f3 posOnPixel;
-	if (view->distortion == 0)
+	if (view->distortion == 0 || o->primeRef)
 	{
 		posOnPixel = add3( add3( p1, smul( (float)x + r0, divs( right, (float)w ) ) ), smul( (float)y + r1, divs( up, (float)h ) ) );
 	}
@@ -1638,6 +1640,155 @@ typedef struct
 	int px0, px1; ThreadCtx ctx;
 } RenderJob;
 
+
+/* ------------------------------------------------------------------------------------- */
+/* PrimeRef validation mode: RenderCore_PrimeRef/kernels/pathtracer.h:44-165 + bsdf.h:18-101 */
+/* (uniform random numbers, Lambert BSDF, NEE without MIS, Russian roulette every vertex,    */
+/* MAXPATHLENGTH 64; the last bounce's shadow rays are never traced; a TIR refraction       */
+/* sample leaves the direction (0,0,0); alpha cut-outs are shaded as hits)                 */
+/* ------------------------------------------------------------------------------------- */
+static inline float FrLambert( float VDotN, float eio )
+{
+	const float SinThetaT2 = sqrf( eio ) * (1.0f - VDotN * VDotN);
+	if (SinThetaT2 > 1.0f) return 1.0f;
+	const float LDotN = sqrtf( 1.0f - SinThetaT2 );
+	const float r1 = (VDotN - eio * LDotN) / (VDotN + eio * LDotN);
+	const float r2 = (LDotN - eio * VDotN) / (LDotN + eio * VDotN);
+	return 0.5f * (sqrf( r1 ) + sqrf( r2 ));
+}
+static inline f3 Tangent2WorldN( f3 V, f3 N )   /* tools_shared.h:211-220 */
+{
+	const float sign = copysignf( 1.0f, N.z );
+	const float a = -1.0f / (sign + N.z);
+	const float b = N.x * N.y * a;
+	const f3 B = mk3( 1.0f + sign * N.x * N.x * a, sign * b, -sign * N.x );
+	const f3 T = mk3( b, sign + N.y * N.y * a, -N.y );
+	return add3( add3( smul( V.x, T ), smul( V.y, B ) ), smul( V.z, N ) );
+}
+static f3 LambertEvaluate( const ShadingData* sd, f3 iN, f3 wi, float* pdf )
+{
+	if (TRANSMISSION > 0.999f || ROUGHNESS <= 0.001f) { *pdf = 0; return s3( 0 ); }
+	*pdf = fabsf( dot3( wi, iN ) ) * INVPI;
+	return muls( muls( sd->color, INVPI ), ROUGHNESS );
+}
+static f3 LambertSample( const ShadingData* sd, f3 iN, f3 N, f3 wo, float distance, float r3, float r4, f3* wi, float* pdf, int* specular )
+{
+	const float flip = (dot3( wo, N ) < 0) ? -1 : 1;
+	iN = muls( iN, flip );
+	*specular = 1, *pdf = 1;
+	f3 bsdf;
+	if (r4 < TRANSMISSION)
+	{
+		const float eio = flip < 0 ? (1.0f / ETA) : ETA, F = FrLambert( dot3( iN, wo ), eio );
+		const f3 beer = mk3( lh2_expf( -sd->transmittance.x * distance * 2.0f ), lh2_expf( -sd->transmittance.y * distance * 2.0f ),
+			lh2_expf( -sd->transmittance.z * distance * 2.0f ) );
+		if (r3 < F)
+		{
+			*wi = reflect3( muls( wo, -1.0f ), iN );
+			bsdf = muls( mul3( sd->color, beer ), 1 / fabsf( dot3( iN, *wi ) ) );
+		}
+		else
+		{
+			if (!Refract_L( wo, iN, eio, wi )) return s3( 0 );
+			return muls( mul3( sd->color, beer ), 1 / fabsf( dot3( iN, *wi ) ) );
+		}
+	}
+	else
+	{
+		const float pReflect = 1 - ROUGHNESS;
+		if (r3 < pReflect)
+		{
+			*wi = reflect3( muls( wo, -1.0f ), iN );
+			bsdf = muls( sd->color, 1.0f / fabsf( dot3( iN, *wi ) ) );
+		}
+		else
+		{
+			const float r5 = (r3 - pReflect) / (1 - pReflect);
+			const float r6 = (r4 - TRANSMISSION) / (1 - TRANSMISSION);
+			*wi = normalize3( Tangent2WorldN( DiffuseReflectionCosWeighted( r5, r6 ), iN ) );
+			*pdf = fmaxf( 0.0f, dot3( *wi, iN ) ) * INVPI;
+			*specular = 0;
+			bsdf = muls( sd->color, INVPI );
+		}
+	}
+	if (dot3( muls( N, flip ), *wi ) <= 0) *pdf = 0;
+	return bsdf;
+}
+static int shade_one_ref( const Oracle* o, ThreadCtx* ctx, const PathSeg* in, const THit* hd, uint32_t R0, int pass, int pathLength, int MAXPL, PathSeg* next )
+{
+	const int w = o->w, h = o->h;
+	const uint32_t uvbits = lh2_f2u( 65535.0f * hd->u ) + (lh2_f2u( 65535.0f * hd->v ) << 16);
+	const int PRIMIDX = hd->tri;
+	const int INSTANCEIDX = hd->tri == -1 ? 0 : hd->inst;
+	const float HIT_U = (float)(uvbits & 65535) * (1.0f / 65535.0f);
+	const float HIT_V = (float)(uvbits >> 16) * (1.0f / 65535.0f);
+	const float HIT_T = hd->t;
+	uint32_t data = fbits( in->T4.w );
+	const f3 D = in->D;
+	f3 throughput = f4xyz( in->T4 );
+	const uint32_t pathIdx = data >> 8;
+	const uint32_t pixelIdx = pathIdx % (uint32_t)(w * h);
+	const uint32_t sampleIdx = pathIdx / (uint32_t)(w * h) + (uint32_t)pass;
+	if (pathLength == 1) ctx->acc[pixelIdx * 4 + 3] += PRIMIDX == NOHIT ? 10000 : HIT_T;
+	if (PRIMIDX == NOHIT)
+	{
+		acc_add( ctx->acc, pixelIdx, mul3( throughput, SampleSkydome( o, D ) ), 0 );
+		return 0;
+	}
+	if ((int)pixelIdx == o->probeX + w * o->probeY && pathLength == 1 && sampleIdx == 0)
+		ctx->st.probedInstid = INSTANCEIDX, ctx->st.probedTriid = PRIMIDX, ctx->st.probedDist = HIT_T;
+	ShadingData sdv, * sd = &sdv;
+	f3 N, iN, fN, T;
+	const f3 I = add3( in->O, smul( HIT_T, D ) );
+	const lh2_CoreTri* tri = &o->meshes[o->inst[INSTANCEIDX].mesh].tris[PRIMIDX];
+	GetShadingData( o, D, HIT_U, HIT_V, o->spreadAngle * HIT_T, tri, INSTANCEIDX, sd, &N, &iN, &fN, &T );
+	if (sd->color.x > 1.0f || sd->color.y > 1.0f || sd->color.z > 1.0f)
+	{
+		if (-dot3( D, N ) > 0 && (pathLength == 1 || (data & S_SPECULAR))) acc_add( ctx->acc, pixelIdx, mul3( throughput, sd->color ), 0 );
+		return 0;
+	}
+	if (ROUGHNESS <= 0.001f || TRANSMISSION > 0.999f) data |= S_SPECULAR; else data &= ~S_SPECULAR;
+	uint32_t seed = WangHash( pathIdx * 17 + R0 );
+	const float faceDir = (dot3( D, N ) > 0) ? -1 : 1;
+	if (faceDir == 1) sd->transmittance = s3( 0 );
+	if (!(data & S_SPECULAR))
+	{
+		const float r0 = RandomFloat( &seed ), r1 = RandomFloat( &seed );
+		float pickProb = 0, lightPdf = 0;
+		f3 lightColor = s3( 0 );
+		f3 L = sub3( RandomPointOnLight( o, r0, r1, I, muls( fN, faceDir ), &pickProb, &lightPdf, &lightColor ), I );
+		const float dist = length3( L );
+		L = muls( L, 1.0f / dist );
+		const float NdotL = dot3( L, muls( fN, faceDir ) );
+		if (NdotL > 0 && lightPdf > 0 && pathLength < MAXPL)
+		{
+			float bsdfPdf;
+			const f3 sampledBSDF = LambertEvaluate( sd, fN, L, &bsdfPdf );
+			const f3 contribution = muls( mul3( mul3( throughput, sampledBSDF ), lightColor ), NdotL / (pickProb * lightPdf) );
+			ctx->st.shadowRays++;
+			const f3 SO = SafeOrigin( I, L, muls( N, faceDir ), o->geometryEpsilon );
+			THit sh; uint32_t nn = 0, tt = 0; int occluded;
+			trace_ray( o, SO, L, 0.0f, dist - 2 * o->geometryEpsilon, 1, &sh, &nn, &tt, &occluded );
+			if (!occluded) acc_add( ctx->acc, pixelIdx, contribution, 0 );
+		}
+	}
+	const float r3 = RandomFloat( &seed ), r4 = RandomFloat( &seed ), r5 = RandomFloat( &seed );
+	f3 R = s3( 0 );
+	float newBsdfPdf = 0;
+	int specular = 0;
+	const f3 bsdf = LambertSample( sd, fN, N, muls( D, -1.0f ), HIT_T, r3, r4, &R, &newBsdfPdf, &specular );
+	if (newBsdfPdf < EPSILON || newBsdfPdf != newBsdfPdf) return 0;
+	if (specular) data |= S_SPECULAR;
+	const float p = pathLength == MAXPL ? 0 : ((data & S_SPECULAR) ? 1 : SurvivalProbability( bsdf ));
+	if (p <= r5) return 0;
+	throughput = mul3( throughput, divs( muls( bsdf, fabsf( dot3( fN, R ) ) ), p * newBsdfPdf ) );
+	next->O = SafeOrigin( I, R, muls( N, faceDir ), o->geometryEpsilon ), next->tmin = 0;
+	next->D = R, next->tmax = 1e34f;
+	next->T4.x = throughput.x, next->T4.y = throughput.y, next->T4.z = throughput.z, next->T4.w = bitsf( data );
+	next->Q4.x = 1, next->Q4.y = 0, next->Q4.z = 0, next->Q4.w = 0;
+	return 1;
+}
+
 static void* render_worker( void* arg )
 {
 	RenderJob* j = (RenderJob*)arg;
@@ -1649,15 +1800,17 @@ static void* render_worker( void* arg )
 		const int jobIndex = px + s * np;
 		PathSeg cur, nxt;
 		eye_ray( o, j->view, j->camR0, j->pass, jobIndex, &cur );
-		for (int pathLength = 1; pathLength <= o->maxPathLength; pathLength++)
+		const int MAXPL = o->primeRef ? 64 : o->maxPathLength;   /* PrimeRef: MAXPATHLENGTH 64 */
+		for (int pathLength = 1; pathLength <= MAXPL; pathLength++)
 		{
 			THit hit; uint32_t nn = 0, tt = 0; int occ;
 			trace_ray( o, cur.O, cur.D, cur.tmin, cur.tmax, 0, &hit, &nn, &tt, &occ );
 			if (hit.tri == -1) hit.t = -1.0f, hit.inst = -1;
-			j->ctx.st.rayCount[pathLength - 1]++;
+			if (pathLength <= 16) j->ctx.st.rayCount[pathLength - 1]++;
 			if (pathLength > (int)j->ctx.st.maxPathLength) j->ctx.st.maxPathLength = pathLength;
 			const uint32_t R0 = (uint32_t)j->pass * 7907u + (uint32_t)pathLength * 91771u;
-			if (!shade_one( o, &j->ctx, &cur, &hit, R0, j->pass, pathLength, &nxt )) break;
+			if (o->primeRef ? !shade_one_ref( o, &j->ctx, &cur, &hit, R0, j->pass, pathLength, MAXPL, &nxt )
+				: !shade_one( o, &j->ctx, &cur, &hit, R0, j->pass, pathLength, &nxt )) break;
 			cur = nxt;
 		}
 	}
