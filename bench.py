@@ -177,12 +177,10 @@ def main():
         rd = torch.from_numpy(d4).to(dev)
         hits = torch.empty((n, 4), dtype=torch.int32, device=dev)
         torch.cuda.synchronize()
-        core.setting("refill", 64)            # the primary-ray launch settings (refillPrimary, leafBatchPrimary)
-        core.setting("leafBatch", 0)
+        core.setting("unitCoherent", 1)       # launched exactly as the frame launches its primary rays
         core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), 2)
         ms = core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), args.kernel_iters)
-        core.setting("refill", 16)
-        core.setting("leafBatch", 16)
+        core.setting("unitCoherent", 0)
         fix = json.load(open(ROOT / "tests" / "golden" / "config2_visits.json"))
         bpr = 32 + 20 + 32 * fix["mean_node_records"] + 36 * fix["mean_tri_tests"]
         algo = bpr * n

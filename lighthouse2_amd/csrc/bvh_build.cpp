@@ -12,7 +12,10 @@ namespace lh2 {
 
 namespace {
 
-constexpr int BINS = 16;
+#ifndef LH2_SAH_BINS
+#define LH2_SAH_BINS 32   /* A/B 8/16/32/64 bins: 32 best by 1-3 % (profiles/r01b_ab_sah_bins.jsonl) */
+#endif
+constexpr int BINS = LH2_SAH_BINS;
 constexpr float C_ISECT = 1.0f;   /* node-visit cost C_TRAV is a build parameter (relative to one triangle test) */
 constexpr uint32_t PAR_THRESHOLD = 16384;
 

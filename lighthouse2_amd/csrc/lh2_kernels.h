@@ -69,6 +69,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	uint32_t refill;                                  /* refill idle lanes once >= refill are idle (1..64) */
 	uint32_t leafBatch;                               /* run triangle tests once >= leafBatch lanes parked a leaf */
 	int version;                                      /* traversal loop: 1 (trace_stream) or 2 (lh2_trace2.inc) */
+	int packet;                                       /* 1: wave-uniform packet traversal (coherent rays, closest hit) */
 };
 
 extern "C" {

@@ -448,6 +448,10 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 }
 
 #include "lh2_trace2.inc"
+#include "lh2_trace_packet.inc"
+
+/* packet traversal of coherent (8x8-tiled primary) rays: wave-uniform, no LDS stack */
+__global__ __launch_bounds__( 256 ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet<0>( s, a ); }
 
 template <bool PARK, int V>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_closest( const SceneDev s, const TraceArgs a )
@@ -1597,8 +1601,10 @@ void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, 
 }
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, hipStream_t st )
 {
-	/* incoherent rays: parked leaves (leafBatch > 0); traversal loop version 1 or 2 (lh2_trace2.inc) */
-	if (a->version == 2)
+	/* incoherent rays: parked leaves (leafBatch > 0); traversal loop version 1 or 2 (lh2_trace2.inc);
+	   coherent primary rays: packet traversal (lh2_trace_packet.inc) */
+	if (a->packet) k_trace_closest_packet<<<grid, 256, 0, st>>>( *s, *a );
+	else if (a->version == 2)
 	{
 		if (a->leafBatch) k_trace_closest<true, 2><<<grid, 256, 0, st>>>( *s, *a );
 		else k_trace_closest<false, 2><<<grid, 256, 0, st>>>( *s, *a );

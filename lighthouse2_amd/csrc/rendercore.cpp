@@ -185,6 +185,8 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
+	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value != 0;   /* packet traversal of tiled primary rays */
+	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice uses the primary-ray launch */
 	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 2, std::max( 1, (int)value ) );   /* traversal loop (lh2_trace2.inc) */
 	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
 	else if (!strcmp( name, "gpuTlas" )) { gpuTlas = value != 0; instancesDirty = true; }
@@ -582,6 +584,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.version = traceVersion;
 		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.countPtr = &c->activePaths, ta.cursor = fetchCursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
+		ta.packet = pathLength == 1 && tiledRays && packetPrimary;
 		ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
 		ta.hits = hits.ptr, ta.gstack = gstack.ptr;
 		lh2_launch_trace_closest( &sd, &ta, grid, stream );
@@ -752,7 +755,9 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
 	ta.version = traceVersion;
-	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
+	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
+	ta.packet = unitCoherent && packetPrimary;
 	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -798,7 +803,10 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 		TraceArgs ta{};
 		ta.version = traceVersion;
 		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.cursor = cursors.ptr + (size_t)i * LH2_CURSOR_WORDS;
-		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr;
+		/* unitCoherent: trace as the frame traces its (tiled) primary rays */
+		ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
+		ta.packet = unitCoherent && packetPrimary;
 		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	}
 	CHK_HIP( hipEventRecord( b, stream ) );

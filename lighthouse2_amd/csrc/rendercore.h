@@ -165,9 +165,11 @@ private:
 	hipEvent_t evCount[LH2_MAX_BOUNCES + 2] = {};
 	uint32_t* activeLog = nullptr;     /* pinned: active paths after each bounce */
 	int tiledRays = 1;
-	int refillPrimary = 64, refillOther = 16, leafBatch = 16, leafBatchPrimary = 0;
+	int refillPrimary = 48, refillOther = 32, leafBatch = 16, leafBatchPrimary = 8;   /* v2 sweep: profiles/r01b_refill_sweep.jsonl */
 	int bvhMaxLeaf = 2;
-	int traceVersion = 2;                /* traversal loop version (setting "traceVersion") */
+	int traceVersion = 2;
+	int unitCoherent = 0;
+	int packetPrimary = 1;               /* wave-uniform packet traversal for 8x8-tiled primary rays */                /* traversal loop version (setting "traceVersion") */
 	int gpuBuild = 0, gpuTlas = 1;       /* BLAS builder (1: GPU PLOC, 0: CPU binned SAH); TLAS on the GPU */
 	float bvhTraversalCost = 1.0f;
 	int framePathLengths = 0, framePrimeRef = 0;

@@ -233,3 +233,29 @@ def test_room_depth4_parity(core):
     ag, ao = core.accumulator(), o.accumulator()
     assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
     core.setting("maxPathLength", 16)
+
+
+@pytest.mark.parametrize("kind", ["random", "primary", "instanced"])
+def test_packet_traversal_bitexact(fresh_core, kind):
+    """Packet traversal (wave-uniform path for 64 rays, lh2_trace_packet.inc) gives every ray exactly
+    the per-ray traversal's hit record, also for incoherent rays and through instances."""
+    if kind == "instanced":
+        sc = scene.instanced_scene(meshes=6, tris_per_mesh=3000, width=64, height=36, grid=3, spacing=12.0)
+        scene.animate_instances(sc, 2)
+    else:
+        sc = scene.config2_scene(n=20000, width=192, height=108)
+    o = _load_both(fresh_core, sc, 192, 108)
+    fresh_core.setting("epsilon", 1e-4)
+    o.setting("epsilon", 1e-4)
+    if kind == "primary":
+        O4, D4, _ = o.generate_eye_rays(sc.view, 0, 0)
+        perm = scene.tiled_order(192, 108)
+        O4, D4 = np.ascontiguousarray(O4[perm]), np.ascontiguousarray(D4[perm])
+    else:
+        O4, D4 = _random_rays(30001, 7, radius=40.0 if kind == "instanced" else 14.0)
+    fresh_core.setting("unitCoherent", 1)
+    hp = fresh_core.trace_closest(O4, D4)
+    fresh_core.setting("unitCoherent", 0)
+    ho = o.trace_closest(O4, D4)
+    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.05
+    assert np.array_equal(hp, ho), np.argwhere((hp != ho).any(1))[:10]

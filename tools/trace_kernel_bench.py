@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--leaf-batch-primary", type=int, default=0)
     ap.add_argument("--pre-setting", action="append", default=[], help="name=value set before loading (BVH build)")
     ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
+    ap.add_argument("--sweep", action="store_true", help="refill x leafBatch grid")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     sc = scene.config2_scene(n=args.tris)
@@ -75,6 +76,21 @@ def main():
     if args.set in ("both", "bounce"):
         hits = core.trace_closest(O4, D4)
         sets["bounce"] = bounce_rays(sc.meshes[0], O4[perm], D4[perm], hits[perm])   # compacted, in-frame order
+    if args.sweep:
+        # refill x leafBatch grid per ray set, one process (scene loaded once)
+        for name, (o, d) in sets.items():
+            n = len(o)
+            ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
+            h = torch.empty((n, 4), dtype=torch.int32, device=dev)
+            for rf in (4, 8, 16, 32, 48, 64):
+                for lb in (0, 4, 8, 16, 32):
+                    core.setting("refill", rf)
+                    core.setting("leafBatch", lb)
+                    core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, h.data_ptr(), 1)
+                    ms = core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, h.data_ptr(), args.iters)
+                    print(json.dumps({"set": name, "refill": rf, "leafBatch": lb, "ms": round(ms, 4)}), flush=True)
+        core.close()
+        return
     res = {}
     for name, (o, d) in sets.items():
         if args.set not in ("both", name):
