@@ -451,7 +451,12 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 #include "lh2_trace_packet.inc"
 
 /* packet traversal of coherent (8x8-tiled primary) rays: wave-uniform, no LDS stack */
-__global__ __launch_bounds__( 256 ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet<0>( s, a ); }
+#ifndef LH2_PACKET_MINWAVES
+#define LH2_PACKET_MINWAVES 1
+#endif
+__global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet<0>( s, a ); }
+template <int MODE>
+__global__ __launch_bounds__( 256 ) void k_trace_any_packet( const SceneDev s, const TraceArgs a ) { trace_packet<MODE == 0 ? 1 : 2>( s, a ); }
 
 template <bool PARK, int V>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_closest( const SceneDev s, const TraceArgs a )
@@ -1617,7 +1622,12 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
 }
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, hipStream_t st )
 {
-	if (a->version == 2)
+	if (a->packet)
+	{
+		if (fused) k_trace_any_packet<1><<<grid, 256, 0, st>>>( *s, *a );
+		else k_trace_any_packet<0><<<grid, 256, 0, st>>>( *s, *a );
+	}
+	else if (a->version == 2)
 	{
 		if (fused) k_trace_any<1, 2><<<grid, 256, 0, st>>>( *s, *a );
 		else k_trace_any<0, 2><<<grid, 256, 0, st>>>( *s, *a );

@@ -150,6 +150,18 @@ void RenderCore::SetInteropTexture( uint32_t glTextureId )
 	CHK_HIP( hipGraphicsGLRegisterImage( &glResource, glTextureId, GL_TEXTURE_2D_, hipGraphicsRegisterFlagsWriteDiscard ) );
 }
 
+/* Packets share one node fetch per wave (scalar loads, one path for 64 rays): a win while the BVH
+   and triangles stay in L2 / Infinity Cache, a loss when node fetches go to DRAM, where the
+   per-ray loop's 64 independent loads per wave hide latency better (config 2: 8.6 MB, packets
+   1.6x faster; 1M-tri room 81 MB: 12 % slower; 10M-tri instanced 1 GB: 1.5x slower;
+   profiles/r01b_ab_packets.jsonl) */
+bool RenderCore::UsePackets() const
+{
+	if (packetPrimary >= 0) return packetPrimary != 0;
+	const double bytes = ((double)blasNodeCount + tlasCapacity) * 64.0 + (double)blasTriCount * 48.0;
+	return bytes <= (double)packetMaxMB * 1048576.0;
+}
+
 void RenderCore::EnsureBuffers()
 {
 	const size_t paths = (size_t)scrwidth * scrheight * scrspp;
@@ -185,7 +197,10 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
-	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value != 0;   /* packet traversal of tiled primary rays */
+	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
+	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
+	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
+	else if (!strcmp( name, "packetShadow" )) packetShadow = value != 0;     /* packet traversal of the shadow rays */
 	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice uses the primary-ray launch */
 	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 2, std::max( 1, (int)value ) );   /* traversal loop (lh2_trace2.inc) */
 	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
@@ -584,7 +599,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.version = traceVersion;
 		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.countPtr = &c->activePaths, ta.cursor = fetchCursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
-		ta.packet = pathLength == 1 && tiledRays && packetPrimary;
+		ta.packet = pathLength == 1 && tiledRays && UsePackets();
 		ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
 		ta.hits = hits.ptr, ta.gstack = gstack.ptr;
 		lh2_launch_trace_closest( &sd, &ta, grid, stream );
@@ -614,6 +629,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = fetchCursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
 			ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 			ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
+			ta.packet = packetShadow;
 			lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
 			CHK_HIP( hipEventRecord( evShadowB[2 * pathLength + 1], stream ) );
 		}
@@ -637,6 +653,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.version = traceVersion;
 		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = fetchCursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
+		ta.packet = packetShadow;
 		lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
 	}
 	CHK_HIP( hipEventRecord( evShadow[1], stream ) );
@@ -757,7 +774,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	ta.version = traceVersion;
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
 	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
-	ta.packet = unitCoherent && packetPrimary;
+	ta.packet = unitCoherent && UsePackets();
 	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -778,6 +795,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	TraceArgs ta{};
 	ta.version = traceVersion;
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+	ta.packet = unitCoherent && packetShadow;
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, stream );
 	std::vector<uint32_t> tmp( words );
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
@@ -806,7 +824,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr;
 		/* unitCoherent: trace as the frame traces its (tiled) primary rays */
 		ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
-		ta.packet = unitCoherent && packetPrimary;
+		ta.packet = unitCoherent && UsePackets();
 		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
 	}
 	CHK_HIP( hipEventRecord( b, stream ) );

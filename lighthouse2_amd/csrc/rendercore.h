@@ -105,6 +105,7 @@ private:
 	void EnsureBuffers();
 	void ConcatenateBlas( int instanceCount );
 	void CheckSceneError();
+	bool UsePackets() const;
 	SceneDev MakeSceneDev() const;
 	int TraceGrid() const { return smCount * blocksPerCU; }
 
@@ -169,7 +170,9 @@ private:
 	int bvhMaxLeaf = 2;
 	int traceVersion = 2;
 	int unitCoherent = 0;
-	int packetPrimary = 1;               /* wave-uniform packet traversal for 8x8-tiled primary rays */                /* traversal loop version (setting "traceVersion") */
+	int packetPrimary = -1;              /* wave-uniform packet traversal for 8x8-tiled primary rays (-1: by scene size) */
+	float packetMaxMB = 16.0f;
+	int packetShadow = 0;                /* the same for shadow rays (setting "packetShadow") */                /* traversal loop version (setting "traceVersion") */
 	int gpuBuild = 0, gpuTlas = 1;       /* BLAS builder (1: GPU PLOC, 0: CPU binned SAH); TLAS on the GPU */
 	float bvhTraversalCost = 1.0f;
 	int framePathLengths = 0, framePrimeRef = 0;

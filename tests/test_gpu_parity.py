@@ -253,9 +253,38 @@ def test_packet_traversal_bitexact(fresh_core, kind):
         O4, D4 = np.ascontiguousarray(O4[perm]), np.ascontiguousarray(D4[perm])
     else:
         O4, D4 = _random_rays(30001, 7, radius=40.0 if kind == "instanced" else 14.0)
+    fresh_core.setting("packetPrimary", 1)
     fresh_core.setting("unitCoherent", 1)
     hp = fresh_core.trace_closest(O4, D4)
     fresh_core.setting("unitCoherent", 0)
     ho = o.trace_closest(O4, D4)
     assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.05
     assert np.array_equal(hp, ho), np.argwhere((hp != ho).any(1))[:10]
+
+
+def test_packet_shadow_rays_match(fresh_core):
+    """Packet any-hit (fused finalizeConnection path and occlusion bits) equals the per-ray result."""
+    sc = scene.config2_scene(n=20000, width=64, height=36)
+    o = _load_both(fresh_core, sc, 64, 36)
+    O4, D4 = _random_rays(30001, 4, tmin=0.0)
+    rng = np.random.default_rng(5)
+    D4[:, 3] = rng.uniform(1.0, 20.0, len(D4)).astype(np.float32)
+    fresh_core.setting("packetShadow", 1)
+    fresh_core.setting("unitCoherent", 1)
+    mg = fresh_core.trace_any(O4, D4)
+    fresh_core.setting("unitCoherent", 0)
+    assert np.array_equal(mg, o.trace_any(O4, D4))
+
+
+def test_packet_shadow_frame_parity(fresh_core):
+    w, h = 128, 72
+    sc = scene.room_scene(40000, w, h)
+    o = _load_both(fresh_core, sc, w, h)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", 4)
+    fresh_core.setting("packetShadow", 1)
+    sc.render_frame(fresh_core)
+    sc.render_frame(o)
+    assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
+    ag, ao = fresh_core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL

@@ -58,6 +58,8 @@ def config3(args):
     sc = scene.room_scene(args.room_tris, args.width, args.height)
     core = RenderCore(device=0)
     core.setting("maxPathLength", 4)
+    for kv in args.setting:
+        core.setting(kv.split("=")[0], float(kv.split("=")[1]))
     sc.load_into(core)
     core.set_target(args.width, args.height, 1)
     setup = time.perf_counter() - t0
@@ -72,6 +74,8 @@ def config5(args):
     t0 = time.perf_counter()
     sc = scene.instanced_scene(meshes=args.meshes, tris_per_mesh=args.mesh_tris, width=args.width, height=args.height)
     core = RenderCore(device=0)
+    for kv in args.setting:
+        core.setting(kv.split("=")[0], float(kv.split("=")[1]))
     sc.load_into(core)
     core.set_target(args.width, args.height, 8)
     setup = time.perf_counter() - t0
@@ -100,6 +104,7 @@ def main():
     ap.add_argument("--room-tris", type=int, default=1_000_000)
     ap.add_argument("--meshes", type=int, default=100)
     ap.add_argument("--mesh-tris", type=int, default=100_000)
+    ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
     args = ap.parse_args()
     for c in args.configs.split(","):
         r = config3(args) if c.strip() == "3" else config5(args)

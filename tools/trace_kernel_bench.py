@@ -73,9 +73,23 @@ def main():
     O4, D4, _ = core.generate_eye_rays(sc.view, 0, 0)
     perm = scene.tiled_order(1920, 1080)    # in-frame order of the primary rays (k_camera, tiledRays)
     sets = {"primary": (np.ascontiguousarray(O4[perm]), np.ascontiguousarray(D4[perm]))}
-    if args.set in ("both", "bounce"):
+    if args.set in ("both", "bounce", "bounce_sorted"):
         hits = core.trace_closest(O4, D4)
         sets["bounce"] = bounce_rays(sc.meshes[0], O4[perm], D4[perm], hits[perm])   # compacted, in-frame order
+        if args.set in ("both", "bounce_sorted"):
+            # sorted by (direction octant, Morton code of the origin): coherent groups of 64 rays
+            bo, bd = sets["bounce"]
+            lo, hi = bo[:, :3].min(0), bo[:, :3].max(0)
+            q = np.clip(((bo[:, :3] - lo) / np.maximum(hi - lo, 1e-9) * 1023).astype(np.int64), 0, 1023)
+            def spread(x):
+                x = (x | (x << 16)) & 0x030000FF; x = (x | (x << 8)) & 0x0300F00F
+                x = (x | (x << 4)) & 0x030C30C3; return (x | (x << 2)) & 0x09249249
+            m = (spread(q[:, 0]) << 2) | (spread(q[:, 1]) << 1) | spread(q[:, 2])
+            octant = ((bd[:, 0] < 0).astype(np.int64) << 2) | ((bd[:, 1] < 0).astype(np.int64) << 1) | (bd[:, 2] < 0)
+            order = np.argsort((octant << 30) | m, kind="stable")
+            sets["bounce_sorted"] = (np.ascontiguousarray(bo[order]), np.ascontiguousarray(bd[order]))
+            if args.set == "bounce_sorted":
+                del sets["bounce"]
     if args.sweep:
         # refill x leafBatch grid per ray set, one process (scene loaded once)
         for name, (o, d) in sets.items():
@@ -93,7 +107,7 @@ def main():
         return
     res = {}
     for name, (o, d) in sets.items():
-        if args.set not in ("both", name):
+        if args.set not in ("both", name) and not (args.set == "bounce_sorted" and name == "bounce_sorted"):
             continue
         n = len(o)
         core.setting("refill", args.refill_primary if name == "primary" else args.refill)
