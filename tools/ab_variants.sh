@@ -8,7 +8,7 @@ mkdir -p "$ROOT/gpurun_out"
 vs=("$@"); [ ${#vs[@]} -eq 0 ] && vs=($(ls "$ROOT/gpuvar"))
 for v in "${vs[@]}"; do
   for rep in 1 2; do
-    out=$(LH2_CORE_LIB="$ROOT/gpuvar/$v/libRenderCore_MI355X.so" timeout -k 10 120 python3 "$ROOT/tools/trace_kernel_bench.py" 2>/dev/null)
+    out=$(LH2_CORE_LIB="$ROOT/gpuvar/$v/libRenderCore_MI355X.so" timeout -k 10 120 python3 "$ROOT/tools/trace_kernel_bench.py" ${TKB_ARGS:-} 2>/dev/null)
     rc=$?
     echo "{\"variant\": \"$v\", \"rep\": $rep, \"rc\": $rc, \"res\": ${out:-null}}" | tee -a "$ROOT/gpurun_out/ab.jsonl"
     [ $rc -ne 0 ] && exit $rc
