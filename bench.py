@@ -78,15 +78,16 @@ def cpu_baseline(sc, width, height, seconds):
             orc.trace_closest(np.concatenate([o, np.full((len(o), 1), 1e-4, np.float32)], 1),
                               np.concatenate([d, np.full((len(d), 1), 1e34, np.float32)], 1))
     done, t0, batch = 0, time.perf_counter(), 4096
-    while time.perf_counter() - t0 < seconds and done < len(perm):
-        idx = perm[done:done + batch]
+    while time.perf_counter() - t0 < seconds:       # bounded sample: passes over the frame's rays, in random order
+        start = done % len(perm)
+        idx = perm[start:start + batch]
         trace(np.ascontiguousarray(O4[idx, :3]), np.ascontiguousarray(D4[idx, :3]))
         done += len(idx)
         batch = min(batch * 2, 262144)
     el = time.perf_counter() - t0
     return {"value": done / el / 1e6, "unit": "Mrays/s", "cores": threads, "kind": kind,
-            "sample": f"{done} of the {len(O4)} config-2 primary rays (1080p), closest hit, "
-                      f"{'RenderCore_Bart BVH2::Traverse' if kind == 'reference' else 'oracle trace_closest'}, "
+            "sample": f"{done} rays ({done / len(O4):.2f} passes over the {len(O4)} config-2 primary rays, 1080p), "
+                      f"closest hit, {'RenderCore_Bart BVH2::Traverse' if kind == 'reference' else 'oracle trace_closest'}, "
                       f"{threads} threads, {el:.1f} s"}
 
 
@@ -168,25 +169,38 @@ def main():
     value = rays_total * args.steps / elapsed / 1e6
 
     if rank == 0:
-        # ---- roofline of the dominant kernel: closest hit on the primary rays of this frame ----
+        # ---- roofline of the dominant kernel: closest hit on the frame's bounce rays (per-ray traversal,
+        # ~half the frame), and beside it the primary-ray launch (packet traversal when auto-selected) ----
         o4, d4, _ = core.generate_eye_rays(sc.view, 0, 0)
         perm = scene.tiled_order(W, H)        # the in-frame ray order (8x8 pixel block per wave)
         o4, d4 = np.ascontiguousarray(o4[perm]), np.ascontiguousarray(d4[perm])
-        n = len(o4)
-        ro = torch.from_numpy(o4).to(dev)
-        rd = torch.from_numpy(d4).to(dev)
-        hits = torch.empty((n, 4), dtype=torch.int32, device=dev)
-        torch.cuda.synchronize()
-        core.setting("unitCoherent", 1)       # launched exactly as the frame launches its primary rays
-        core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), 2)
-        ms = core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), args.kernel_iters)
-        core.setting("unitCoherent", 0)
-        fix = json.load(open(ROOT / "tests" / "golden" / "config2_visits.json"))
-        bpr = 32 + 20 + 32 * fix["mean_node_records"] + 36 * fix["mean_tri_tests"]
-        algo = bpr * n
-        achieved = algo / (ms * 1e-3) / 1e9
+
+        def launch(o, d, coherent):
+            n = len(o)
+            ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
+            hits = torch.empty((n, 4), dtype=torch.int32, device=dev)
+            torch.cuda.synchronize()
+            core.setting("unitCoherent", 1 if coherent else 0)   # launched exactly as the frame launches it
+            core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), 2)
+            ms = core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), args.kernel_iters)
+            core.setting("unitCoherent", 0)
+            return ms, hits.cpu().numpy().view(np.uint32)
+
+        def bytes_per_ray(name):
+            fix = json.load(open(ROOT / "tests" / "golden" / name))
+            return 32 + 20 + 32 * fix["mean_node_records"] + 36 * fix["mean_tri_tests"]
+
+        ms_p, hits_p = launch(o4, d4, True)
+        bo, bd = scene.bounce_rays(sc.meshes[0], o4, d4, hits_p)
+        ms, _ = launch(bo, bd, False)
+        n, n_p = len(bo), len(o4)
+        bpr, bpr_p = bytes_per_ray("config2_bounce_visits.json"), bytes_per_ray("config2_visits.json")
+        achieved = bpr * n / (ms * 1e-3) / 1e9
+        achieved_p = bpr_p * n_p / (ms_p * 1e-3) / 1e9
         traffic = latest_pmc_traffic()
         info = core.scene_info()
+        # RenderCore::UsePackets (auto): BVH + triangle footprint <= packetMaxMB (16 MiB)
+        packets = (info["nodes"] * 64 + info["tris"] * 48) <= 16 * 1048576
         out = {
             "metric": "Mrays/s (primary+secondary) at 1080p 1spp",
             "value": round(value, 3),
@@ -207,11 +221,24 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "k_trace_closest (primary rays, in-frame order and settings)", "kernel_ms": round(ms, 4),
-                         "bytes_per_ray": round(bpr, 1), "rays_per_launch": n},
+                         "kernel": "k_trace_closest<PARK=true,v2> (per-ray traversal) on the frame's diffuse bounce "
+                                   "rays, in-frame order and settings", "kernel_ms": round(ms, 4),
+                         "bytes_per_ray": round(bpr, 1), "rays_per_launch": n,
+                         "bytes_model": "32 ray + 20 hit + 32 x node records + 36 x triangle tests of the reference "
+                                        "traversal (tests/golden/config2_bounce_visits.json)"},
+            "roofline_primary": {"bound": "hbm", "achieved": round(achieved_p, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(achieved_p / HBM_PEAK_GBS, 4),
+                                 "kernel": ("k_trace_closest_packet (wave-uniform packet traversal)" if packets
+                                            else "k_trace_closest<PARK=true,v2>") + " on the 1080p primary rays",
+                                 "kernel_ms": round(ms_p, 4), "bytes_per_ray": round(bpr_p, 1), "rays_per_launch": n_p,
+                                 "note": "per-ray byte model; a packet fetches each node once per 64 rays (scalar "
+                                         "loads), so frac > 1 is possible and means the kernel is not HBM-bound"},
             "detail": {"primary_rays": int(counts[0]), "secondary_rays": int(counts[1]),
                        "deep_rays": int(counts[2:16].sum()), "shadow_rays": int(counts[16]),
-                       "trace_Mrays_s_primary": round(n / (ms * 1e-3) / 1e6, 1),
+                       "trace_Mrays_s_bounce": round(n / (ms * 1e-3) / 1e6, 1),
+                       "trace_Mrays_s_primary": round(n_p / (ms_p * 1e-3) / 1e6, 1),
+                       "trace_Mrays_s_frame": round(rays_total / world / ((st.traceTime0 + st.traceTime1) * 1e6), 1)
+                       if st.traceTime0 + st.traceTime1 > 0 else None,
                        "traceTime0_ms": round(st.traceTime0 * 1e3, 4), "traceTime1_ms": round(st.traceTime1 * 1e3, 4),
                        "shadeTime_ms": round(st.shadeTime * 1e3, 4), "bvh_nodes": info["nodes"],
                        "bvh_depth": info["max_depth"], "setup_s": round(build_s, 3)},

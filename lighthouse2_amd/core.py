@@ -220,9 +220,13 @@ class RenderCore:
         """Pack the owned accumulator rows into device memory (asynchronously, on the core stream).
         With order_torch, torch's current stream is made to wait for it (no host synchronisation), so
         torch ops and collectives on the tile see the finished rows."""
+        if order_torch:
+            # the previous frame's gather may still read this tile on torch's / RCCL's stream: the core
+            # stream waits for it (GPU-side wait, so that gather overlaps this frame's rendering)
+            import torch
+            torch.cuda.ExternalStream(self.stream_ptr()).wait_stream(torch.cuda.current_stream())
         self._chk(self.lib.lh2_core_pack_tile(self.h, C.c_void_p(device_ptr)))
         if order_torch:
-            import torch
             torch.cuda.current_stream().wait_stream(torch.cuda.ExternalStream(self.stream_ptr()))
 
     def stream_ptr(self) -> int:

@@ -645,3 +645,30 @@ def textured_scene(width: int = 1920, height: int = 1080, tess: int = 24, instan
     sc.sky = gradient_sky(64, 32)
     sc.view = camera_view((2, 5, -12), (0.25, -0.3, 1), fov_deg=60, aspect=width / height, focal=5, pixel_height=height)
     return sc
+
+
+def bounce_rays(tris, O4, D4, hits, seed=1):
+    """Diffuse 'bounce' rays from primary hits, as the first shade pass emits them (bench.py's roofline
+    launch, tools/trace_kernel_bench.py, the bounce-visits fixture): cosine-weighted around the face
+    normal of each hit (flipped toward the viewer), origin offset 1e-4 along it.  Misses are dropped
+    (compacted, input order kept).  Returns O (tmin 0), D (tmax 1e34) as float32 [n, 4]."""
+    hit = hits[:, 1] != 0xFFFFFFFF
+    idx = np.nonzero(hit)[0]
+    tri = hits[idx, 1].astype(np.int64)
+    t = hits[idx, 0].view(np.float32)
+    P = O4[idx, :3] + t[:, None] * D4[idx, :3]
+    N = np.stack([tris[tri, abi.TRI["Nx"]], tris[tri, abi.TRI["Ny"]], tris[tri, abi.TRI["Nz"]]], 1)
+    N = np.where(((N * D4[idx, :3]).sum(1) > 0)[:, None], -N, N)
+    rng = np.random.default_rng(seed)
+    r0, r1 = rng.random(len(idx)), rng.random(len(idx))
+    phi = 2 * np.pi * r0
+    local = np.stack([np.cos(phi) * np.sqrt(1 - r1), np.sin(phi) * np.sqrt(1 - r1), np.sqrt(r1)], 1)
+    a = np.where(np.abs(N[:, 0:1]) > 0.9, np.array([[0, 1, 0]]), np.array([[1, 0, 0]]))
+    T = np.cross(N, a)
+    T /= np.linalg.norm(T, axis=1, keepdims=True)
+    B = np.cross(N, T)
+    d = local[:, 0:1] * T + local[:, 1:2] * B + local[:, 2:3] * N
+    o = P + 1e-4 * N
+    O = np.concatenate([o, np.zeros((len(o), 1))], 1).astype(np.float32)
+    D = np.concatenate([d, np.full((len(d), 1), 1e34)], 1).astype(np.float32)
+    return O, D

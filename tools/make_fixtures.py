@@ -45,6 +45,23 @@ def visits_fixture():
     }
     (GOLD / "config2_visits.json").write_text(json.dumps(d, indent=1))
     print(d)
+    # the frame's first bounce: diffuse rays from the primary hits (scene.bounce_rays, in-frame order)
+    perm = scene.tiled_order(1920, 1080)
+    O4, D4, hits = O4[perm], D4[perm], hits[perm]
+    bo, bd = scene.bounce_rays(sc.meshes[0], O4, D4, hits)
+    bhits, bvis = o.trace_closest(bo, bd, visits=True)
+    b = {
+        "scene": "config2 100k random tris; diffuse bounce rays (lighthouse2_amd.scene.bounce_rays, seed 1) "
+                 "from the hits of the 1920x1080 primary rays",
+        "rays": int(len(bo)),
+        "hit_fraction": float((bhits[:, 1] != 0xFFFFFFFF).mean()),
+        "mean_node_records": float(bvis[:, 0].mean()),
+        "mean_tri_tests": float(bvis[:, 1].mean()),
+        "node_record_bytes": 32, "tri_bytes": 36,
+        "generator": d["generator"],
+    }
+    (GOLD / "config2_bounce_visits.json").write_text(json.dumps(b, indent=1))
+    print(b)
 
 
 def bart_fixture():

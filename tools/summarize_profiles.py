@@ -3,7 +3,8 @@ under profiles/ for one round:
 
   profiles/<tag>_rocprof_kernel_stats.csv   rocprofv3 --kernel-trace --stats of bench.py
   profiles/<tag>_bench.json                 the bench.py JSON line of the same call
-  profiles/<tag>_pmc_traffic.json           HBM bytes per k_trace_closest launch (primary rays):
+  profiles/<tag>_pmc_traffic.json           HBM bytes per k_trace_closest<true, 2> launch (the frame's
+                                            diffuse bounce rays, bench.py's roofline kernel):
                                             2 x FETCH_SIZE (gfx950 calibration, MI355X_MICROARCH.md
                                             §HBM) + WRITE_SIZE, each from its own --pmc pass
 
@@ -41,7 +42,7 @@ def main():
     bench = json.loads((src / "bench.json").read_text().strip().splitlines()[-1])
     (dst / f"{a.tag}_bench.json").write_text(json.dumps(bench, indent=1) + "\n")
 
-    kernel = "k_trace_closest"
+    kernel = "k_trace_closest<true, 2>"      # per-ray traversal (the packet kernel is k_trace_closest_packet)
     fetch, fd = _pmc(src / "pmc_fetch" / "run_counter_collection.csv", kernel)
     write, wd = _pmc(src / "pmc_write" / "run_counter_collection.csv", kernel)
     # kernel-trace durations of the roofline launches in the profiled bench run (the last kernel_iters)
@@ -52,7 +53,7 @@ def main():
     fetch_b = 2.0 * statistics.median(fetch) * 1024.0      # FETCH_SIZE is in KiB; x2 per the gfx950 calibration
     write_b = statistics.median(write) * 1024.0
     out = {
-        "kernel": f"{kernel} (config-2 1080p primary rays, tools/trace_kernel_bench.py --set primary)",
+        "kernel": f"{kernel} (config-2 bounce rays from the 1080p primary hits, tools/trace_kernel_bench.py --set bounce)",
         "rays_per_launch": rays,
         "fetch_size_kib_raw_median": statistics.median(fetch),
         "write_size_kib_median": statistics.median(write),

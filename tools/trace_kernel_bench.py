@@ -22,27 +22,7 @@ from lighthouse2_amd import abi, scene  # noqa: E402
 from lighthouse2_amd.core import RenderCore  # noqa: E402
 
 
-def bounce_rays(tris, O4, D4, hits, seed=1):
-    hit = hits[:, 1] != 0xFFFFFFFF
-    idx = np.nonzero(hit)[0]
-    tri = hits[idx, 1].astype(np.int64)
-    t = hits[idx, 0].view(np.float32)
-    P = O4[idx, :3] + t[:, None] * D4[idx, :3]
-    N = np.stack([tris[tri, abi.TRI["Nx"]], tris[tri, abi.TRI["Ny"]], tris[tri, abi.TRI["Nz"]]], 1)
-    N = np.where(((N * D4[idx, :3]).sum(1) > 0)[:, None], -N, N)
-    rng = np.random.default_rng(seed)
-    r0, r1 = rng.random(len(idx)), rng.random(len(idx))
-    phi = 2 * np.pi * r0
-    local = np.stack([np.cos(phi) * np.sqrt(1 - r1), np.sin(phi) * np.sqrt(1 - r1), np.sqrt(r1)], 1)
-    a = np.where(np.abs(N[:, 0:1]) > 0.9, np.array([[0, 1, 0]]), np.array([[1, 0, 0]]))
-    T = np.cross(N, a)
-    T /= np.linalg.norm(T, axis=1, keepdims=True)
-    B = np.cross(N, T)
-    d = local[:, 0:1] * T + local[:, 1:2] * B + local[:, 2:3] * N
-    o = P + 1e-4 * N
-    O = np.concatenate([o, np.zeros((len(o), 1))], 1).astype(np.float32)
-    D = np.concatenate([d, np.full((len(d), 1), 1e34)], 1).astype(np.float32)
-    return O, D
+bounce_rays = scene.bounce_rays   # shared with bench.py and tools/make_fixtures.py
 
 
 def main():
@@ -50,10 +30,13 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tris", type=int, default=100_000)
     ap.add_argument("--set", default="both")
-    ap.add_argument("--refill", type=int, default=16)
-    ap.add_argument("--refill-primary", type=int, default=64)
+    # defaults = the core's (RenderCore refillOther / refillPrimary / leafBatch / leafBatchPrimary)
+    ap.add_argument("--refill", type=int, default=32)
+    ap.add_argument("--refill-primary", type=int, default=48)
     ap.add_argument("--leaf-batch", type=int, default=16)
-    ap.add_argument("--leaf-batch-primary", type=int, default=0)
+    ap.add_argument("--leaf-batch-primary", type=int, default=8)
+    ap.add_argument("--no-frame-launch", action="store_true",
+                    help="do not set unitCoherent=1 for the primary set (the frame's launch: packets when auto-selected)")
     ap.add_argument("--pre-setting", action="append", default=[], help="name=value set before loading (BVH build)")
     ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
     ap.add_argument("--sweep", action="store_true", help="refill x leafBatch grid")
@@ -112,6 +95,8 @@ def main():
         n = len(o)
         core.setting("refill", args.refill_primary if name == "primary" else args.refill)
         core.setting("leafBatch", args.leaf_batch_primary if name == "primary" else args.leaf_batch)
+        if not args.no_frame_launch:
+            core.setting("unitCoherent", 1 if name == "primary" else 0)
         ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
         h = torch.empty((n, 4), dtype=torch.int32, device=dev)
         torch.cuda.synchronize()
