@@ -45,10 +45,11 @@ struct SceneDev       /* everything the traversal and shading kernels read, by v
 
 struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path state */
 {
-	const uint32_t* pathCount;
+	const uint32_t* segCounts; uint32_t segStride;     /* input paths: a segmented stream (see LH2_SEGS) */
+	uint32_t shadowStride;                             /* shadow-ray segments: capacity of each */
 	const float4* rayO; const float4* rayD; const float4* T4; const float4* Q4; const uint4* hits;
 	float4* rayOut; float4* rayDOut; float4* T4Out; float4* Q4Out;
-	float4* shO; float4* shD; float4* shP; uint32_t shadowCap;
+	float4* shO; float4* shD; float4* shP;
 	float4* acc;
 	Counters* counters;
 	int w, h, pass, pathLength, maxPathLength, probePixel;
@@ -60,8 +61,10 @@ struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path st
 struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (any) out */
 {
 	const float4* rayO; const float4* rayD;
-	const uint32_t* countPtr; uint32_t countFixed;   /* count from device memory, or fixed */
-	uint32_t* cursor;                                 /* LH2_CHUNKS zeroed work-queue heads, LH2_CURSOR_STRIDE apart */
+	/* the rays: a segmented stream (see LH2_SEGS), counts from device memory (segCounts), or, with
+	   segCounts null, countFixed rays stored densely (segments of segStride) */
+	const uint32_t* segCounts; uint32_t segStride; uint32_t countFixed;
+	uint32_t* cursor;                                 /* LH2_SEGS zeroed work-queue heads, LH2_CURSOR_STRIDE apart */
 	uint4* hits;                                      /* closest: {t, triid, instid, uv16} */
 	uint32_t* mask;                                   /* any, mode 0: occlusion bits */
 	const float4* potentials; float4* acc;            /* any, mode 1: fused finalizeConnection */
@@ -73,7 +76,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 };
 
 extern "C" {
-void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t* cursors, int cursorWords, hipStream_t st );
+void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, hipStream_t st );
 void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, hipStream_t st );
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, hipStream_t st );
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, hipStream_t st );
@@ -84,11 +87,18 @@ void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int ba
 void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, hipStream_t st );
 }
 
-/* ray-fetch work queue: the ray range is split into LH2_CHUNKS contiguous chunks with one cursor
-   each (128 B apart), so the per-wave atomics of a launch spread over 8 addresses instead of one */
+/* Segmented ray streams.  A stream of paths or rays lives in LH2_SEGS segments of one buffer:
+   segment c holds count[c] records from index c * segStride (counters LH2_SEGCOUNT_STRIDE words
+   apart, each on its own 128-B line).  Producers (the camera: densely; shade: extension and shadow
+   rays) and consumers (trace, shade) take segment blockIdx % LH2_SEGS first - blocks go round-robin
+   over the 8 XCDs, so that is the XCD's own segment - and every segment has its own work-queue head
+   and its own compaction counter: the per-wave atomics of a launch spread over 8 words, where one
+   word sustains only ~88 returning atomics per microsecond (MI355X_MICROARCH.md, 'dequeue'). */
 #ifndef LH2_CHUNKS
 #define LH2_CHUNKS 8
 #endif
+#define LH2_SEGS LH2_CHUNKS
+#define LH2_SEGCOUNT_STRIDE 32
 #define LH2_CURSOR_STRIDE 32
 #define LH2_CURSOR_WORDS (LH2_CHUNKS * LH2_CURSOR_STRIDE)   /* per trace launch */
 #define LH2_MAX_BOUNCES 64                                   /* RenderCore_PrimeRef MAXPATHLENGTH (core_settings.h:25) */

@@ -44,6 +44,32 @@ LH2_DEV uint32_t wave_alloc( bool want, uint32_t* counter )
 	return want ? base + lanes_below( m ) : 0xffffffffu;
 }
 
+static_assert( sizeof( ((Counters*)0)->segActive ) == LH2_SEGS * LH2_SEGCOUNT_STRIDE * 4, "Counters segment layout" );
+
+/* [lo, hi): segment c of a trace launch's ray stream (lh2_kernels.h, LH2_SEGS).  Wave-uniform, and
+   said so (readfirstlane): kept in SGPRs, they cost the traversal loop no VGPRs (which it has none
+   to spare: with two more live VGPRs the compiler spilled the stack pointers next to the LDS push) */
+LH2_DEV void seg_range( const TraceArgs& a, uint32_t c, uint32_t& lo, uint32_t& hi )
+{
+	c = __builtin_amdgcn_readfirstlane( c );
+	lo = c * a.segStride;
+	uint32_t n;
+	if (a.segCounts) n = a.segCounts[c * LH2_SEGCOUNT_STRIDE];
+	else n = a.countFixed > lo ? min( a.countFixed - lo, a.segStride ) : 0u;
+	lo = __builtin_amdgcn_readfirstlane( lo );
+	hi = __builtin_amdgcn_readfirstlane( lo + n );
+}
+
+/* no rays in any segment: the launch returns at once (a bounce after the last one, or no shadow rays) */
+LH2_DEV bool stream_empty( const TraceArgs& a )
+{
+	if (!a.segCounts) return a.countFixed == 0;
+	uint32_t any = 0;
+#pragma unroll
+	for (int k = 0; k < LH2_SEGS; k++) any |= a.segCounts[k * LH2_SEGCOUNT_STRIDE];
+	return any == 0;
+}
+
 LH2_DEV void acc_add( float4* acc, uint32_t px, v3 c )
 {
 	float* a = (float*)(acc + px);
@@ -62,6 +88,31 @@ LH2_DEV float blueNoiseSampler( const uint8_t* bn, int x, int y, int sampleIndex
 	int value = (int)bn[sampleDimension + rankedSampleIndex * 256];
 	value ^= (int)bn[(sampleDimension & 7) + (x + y * 128) * 8 + 65536];
 	return (0.5f + (float)value) * (1.0f / 256.0f);
+}
+/* blueNoiseSampler for the four dimensions dim0 .. dim0 + 3 (dim0 a multiple of 4, as every caller's
+   4 + 4 * pathLength), in two steps so that callers can put other loads between them: the four ranking
+   bytes and the four scrambling bytes of a pixel are adjacent and 4-aligned (one dword each), then the
+   four sample bytes; the values are those of four blueNoiseSampler calls */
+struct BlueNoise4 { uint32_t rank, scr; int d0, sampleIndex; };
+LH2_DEV BlueNoise4 blueNoiseFetch4( const uint8_t* bn, int x, int y, const int sampleIndex, const int dim0 )
+{
+	x &= 127, y &= 127;
+	BlueNoise4 q;
+	q.d0 = dim0 & 255, q.sampleIndex = sampleIndex & 255;
+	const int pix = (x + y * 128) * 8;
+	q.rank = *(const uint32_t*)(bn + q.d0 + pix + 65536 * 3);
+	q.scr = *(const uint32_t*)(bn + (q.d0 & 7) + pix + 65536);
+	return q;
+}
+LH2_DEV void blueNoiseFinish4( const uint8_t* bn, const BlueNoise4& q, float r[4] )
+{
+#pragma unroll
+	for (int k = 0; k < 4; k++)
+	{
+		const int ranked = (q.sampleIndex ^ (int)((q.rank >> (8 * k)) & 255)) & 255;
+		const int value = (int)bn[q.d0 + k + ranked * 256] ^ (int)((q.scr >> (8 * k)) & 255);
+		r[k] = (0.5f + (float)value) * (1.0f / 256.0f);
+	}
 }
 LH2_DEV uint32_t WangHash( uint32_t s ) { s = (s ^ 61) ^ (s >> 16), s *= 9, s = s ^ (s >> 4), s *= 0x27d4eb2d, s = s ^ (s >> 15); return s; }
 LH2_DEV uint32_t RandomInt( uint32_t& s ) { s ^= s << 13, s ^= s >> 17, s ^= s << 5; return s; }
@@ -335,15 +386,14 @@ template <int KIND, bool PARK>
 LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restrict__ lst, int* __restrict__ gst, const uint32_t gstride )
 {
 	constexpr bool ANY = KIND != 0;
-	const uint32_t count = a.countPtr ? *a.countPtr : a.countFixed;
-	if (count == 0 || *s.sceneError) return;
+	if (stream_empty( a ) || *s.sceneError) return;
 	const uint32_t refill = a.refill ? a.refill : 64u;
 	const uint32_t leafBatch = a.leafBatch ? a.leafBatch : 1u;
 	bool active = false, exhausted = false;
-	/* this wave's chunk of the ray range: blocks go round-robin over the 8 XCDs, so blockIdx % 8
-	   gives each XCD its own chunk and cursor; a dry chunk moves the wave on to the next one */
-	uint32_t chunk = blockIdx.x % LH2_CHUNKS, tried = 0;
-	uint32_t lo = (uint32_t)(((uint64_t)count * chunk) / LH2_CHUNKS), hi = (uint32_t)(((uint64_t)count * (chunk + 1)) / LH2_CHUNKS);
+	/* this wave's segment of the ray stream: blocks go round-robin over the 8 XCDs, so blockIdx % 8
+	   gives each XCD its own segment and cursor; a dry segment moves the wave on to the next one */
+	uint32_t chunk = blockIdx.x % LH2_CHUNKS, tried = 0, lo, hi;
+	seg_range( a, chunk, lo, hi );
 	TraceState q;
 	q.idx = 0, q.tmin = 0, q.sp = 0, q.blasSp = -1, q.cur = 0, q.curInst = -1, q.leaf = 0;
 	while (true)
@@ -372,7 +422,7 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 			{
 				if (++tried == LH2_CHUNKS) exhausted = true;
 				chunk = (chunk + 1) % LH2_CHUNKS;
-				lo = (uint32_t)(((uint64_t)count * chunk) / LH2_CHUNKS), hi = (uint32_t)(((uint64_t)count * (chunk + 1)) / LH2_CHUNKS);
+				seg_range( a, chunk, lo, hi );
 			}
 		}
 		if (__ballot( active ) == 0)
@@ -513,7 +563,8 @@ LH2_DEV v3 ciexyz_to_linear_rgb( const v3 x )
 		fmaxf( 0.0f, -0.969256f * x.x + 1.875992f * x.y + 0.041556f * x.z ),
 		fmaxf( 0.0f, 0.055648f * x.x - 0.204043f * x.y + 1.057311f * x.z ) );
 }
-LH2_DEV float h2f( uint32_t bits16 ) { return lh2_h2f( (uint16_t)bits16 ); }
+/* half -> float is exact for every non-NaN half (lh2_h2f, the host restatement): one v_cvt_f32_f16 */
+LH2_DEV float h2f( uint32_t bits16 ) { return (float)__builtin_bit_cast( _Float16, (uint16_t)bits16 ); }
 
 LH2_DEV v3 ConsistentNormal( const v3 D, const v3 iN, const float alpha ) /* tools_shared.h:296-310 */
 {
@@ -584,7 +635,7 @@ LH2_DEV float normal_scale( const uint32_t byte, const bool absArg )   /* materi
 
 /* GetShadingData, material_shared.h:35-178 (OPTIXPRIMEBUILD, CONSISTENTNORMALS, BILINEAR) */
 LH2_DEV void GetShadingData( const SceneDev& s, const v3 D, const float u, const float v, const float coneWidth, const float4* __restrict__ tri,
-	const int instIdx, ShadingData& sd, v3& N, v3& iN, v3& fN, v3& T )
+	const v3 A, const v3 B, const v3 C, ShadingData& sd, v3& N, v3& iN, v3& fN, v3& T )
 {
 
 	const float4 tdata1 = tri[1], tdata2 = tri[2], tdata3 = tri[3], tdata4 = tri[4], tdata5 = tri[5], alpha4 = tri[7];
@@ -603,8 +654,7 @@ LH2_DEV void GetShadingData( const SceneDev& s, const v3 D, const float u, const
 	T = xyz( tdata5 );
 	const float w = 1 - (u + v);
 	if (flags & HASSMOOTHNORMALS) iN = normalize3( add3( add3( smul( u, xyz( tdata2 ) ), smul( v, xyz( tdata3 ) ) ), smul( w, xyz( tdata4 ) ) ) );
-	const lh2_CoreInstanceDesc* id = s.instDesc + instIdx;
-	const v3 A = mk3( id->A.x, id->A.y, id->A.z ), B = mk3( id->B.x, id->B.y, id->B.z ), C = mk3( id->C.x, id->C.y, id->C.z );
+	/* A, B, C: rows of the instance's inverse transform (lh2_CoreInstanceDesc, fetched by the caller) */
 	const v3 n0 = N, i0 = iN;
 	N = add3( add3( smul( n0.x, A ), smul( n0.y, B ) ), smul( n0.z, C ) );
 	iN = add3( add3( smul( i0.x, A ), smul( i0.y, B ) ), smul( i0.z, C ) );
@@ -1208,25 +1258,40 @@ LH2_DEV v3 clampintensity( const float clampValue, v3 c )
 LH2_DEV v3 fixnan( v3 a ) { if (!isfinite_( a.x + a.y + a.z )) a = s3( 0 ); return a; }
 LH2_DEV float SurvivalProbability( const v3 a ) { return fminf( 1.0f, fmaxf( fmaxf( a.x, a.y ), a.z ) ); }
 
+/* the hit's instance record (lh2_CoreInstanceDesc: triangle pointer, inverse-transform rows A, B, C),
+   read in one step of the dependent load chain right after the hit record; none for a miss */
+LH2_DEV const float4* HitInstance( const SceneDev& s, const int primIdx, const int instIdx, v3& A, v3& B, v3& C )
+{
+	/* branch-free (a miss reads record 0, which always exists: RenderCore::Init allocates it), so the
+	   loads stay in flight with the caller's other loads instead of being waited for inside a branch */
+	const lh2_CoreInstanceDesc* id = s.instDesc + (primIdx == NOHIT ? 0 : instIdx);
+	const float4 a = *(const float4*)&id->A, b = *(const float4*)&id->B, c = *(const float4*)&id->C;
+	A = xyz( a ), B = xyz( b ), C = xyz( c );
+	return (const float4*)id->triangles + (size_t)primIdx * 11;
+}
+
 /* ---- shade kernel: pathtracer.h:54-245 --------------------------------------------------- */
 #ifndef LH2_SHADE_MINWAVES
 #define LH2_SHADE_MINWAVES 1
 #endif
 __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const SceneDev s, const ShadeParams p )
 {
-	const uint32_t count = *p.pathCount;
-	const uint32_t gstride = gridDim.x * 256u;
+	/* the block's segment of the path stream (its XCD's), and the segment's share of the grid */
+	const uint32_t seg = blockIdx.x % LH2_SEGS;
+	const uint32_t count = p.segCounts[seg * LH2_SEGCOUNT_STRIDE], segBase = seg * p.segStride;
+	const uint32_t gstride = ((gridDim.x - seg + LH2_SEGS - 1) / LH2_SEGS) * 256u;
 	const int w = p.w, h = p.h;
-	for (uint32_t base = blockIdx.x * 256u; base < count; base += gstride)
+	for (uint32_t base = (blockIdx.x / LH2_SEGS) * 256u; base < count; base += gstride)
 	{
-		const uint32_t jobIndex = base + threadIdx.x;
+		const uint32_t jobIndex = segBase + base + threadIdx.x;
 		bool doExt = false, doShadow = false;
 		float4 eO, eD, eT, eQ, sO, sD, sP;
-		if (jobIndex < count)
+		if (base + threadIdx.x < count)
 		{
-			const float4 O4 = p.rayO[jobIndex], D4 = p.rayD[jobIndex];
-			const float4 T4 = p.T4[jobIndex], Q4 = p.Q4[jobIndex];
+			/* the five input records first, all in flight together (the hit starts the dependent chain) */
 			const uint4 hd = p.hits[jobIndex];
+			const float4 T4 = p.T4[jobIndex], O4 = p.rayO[jobIndex], D4 = p.rayD[jobIndex], Q4 = p.Q4[jobIndex];
+			__builtin_amdgcn_sched_barrier( 0 );
 			const float HIT_T = __uint_as_float( hd.x );
 			const int PRIMIDX = (int)hd.y;
 			const int INSTANCEIDX = PRIMIDX == -1 ? 0 : (int)hd.z;
@@ -1239,6 +1304,16 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const Scen
 			const uint32_t pathIdx = data >> 8;
 			const uint32_t pixelIdx = pathIdx % (uint32_t)(w * h);
 			const uint32_t sampleIdx = pathIdx / (uint32_t)(w * h) + (uint32_t)p.pass;
+			/* this vertex's blue-noise samples (dimensions 4..7 + 4 pathLength: r0, r1 for the light, r3, r4
+			   for the BSDF) and the hit's instance record are fetched together, and the sample bytes with
+			   the triangle: the dependent chain is inputs -> (ranking bytes, instance) -> (samples,
+			   triangle) -> material, instead of the table lookups following the material */
+			const BlueNoise4 bnq = blueNoiseFetch4( s.blueNoise, (int)(pixelIdx % (uint32_t)w), (int)(pixelIdx / (uint32_t)w), (int)sampleIdx, 4 + 4 * p.pathLength );
+			v3 instA, instB, instC;
+			const float4* tri = HitInstance( s, PRIMIDX, INSTANCEIDX, instA, instB, instC );
+			__builtin_amdgcn_sched_barrier( 0 );
+			float bnv[4];
+			blueNoiseFinish4( s.blueNoise, bnq, bnv );
 			if (p.pathLength == 1) unsafeAtomicAdd( &p.acc[pixelIdx].w, PRIMIDX == NOHIT ? 10000.0f : HIT_T );
 			if (PRIMIDX == NOHIT)
 			{
@@ -1254,8 +1329,7 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const Scen
 				ShadingData sd;
 				v3 N, iN, fN, T;
 				const v3 I = add3( RAY_O, smul( HIT_T, D ) );
-				const float4* tri = (const float4*)s.instDesc[INSTANCEIDX].triangles + (size_t)PRIMIDX * 11;
-				GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, INSTANCEIDX, sd, N, iN, fN, T );
+				GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, instA, instB, instC, sd, N, iN, fN, T );
 				if (sd.flags & 1)
 				{
 					if (p.pathLength < p.maxPathLength)
@@ -1296,12 +1370,7 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const Scen
 				if (!(data & S_SPECULAR))
 				{
 					float r0, r1, pickProb = 0, lightPdf = 0;
-					if (sampleIdx < 2)
-					{
-						const uint32_t x = (pixelIdx % (uint32_t)w) & 127, y = (pixelIdx / (uint32_t)w) & 127;
-						r0 = blueNoiseSampler( s.blueNoise, x, y, sampleIdx, 4 + 4 * p.pathLength );
-						r1 = blueNoiseSampler( s.blueNoise, x, y, sampleIdx, 5 + 4 * p.pathLength );
-					}
+					if (sampleIdx < 2) r0 = bnv[0], r1 = bnv[1];
 					else
 					{
 						r0 = RandomFloat( seed );
@@ -1333,12 +1402,7 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const Scen
 				{
 					v3 R = s3( 0 );
 					float newBsdfPdf = 0, r3, r4;
-					if (sampleIdx < 256)
-					{
-						const uint32_t x = (pixelIdx % (uint32_t)w) & 127, y = (pixelIdx / (uint32_t)w) & 127;
-						r3 = blueNoiseSampler( s.blueNoise, x, y, sampleIdx, 6 + 4 * p.pathLength );
-						r4 = blueNoiseSampler( s.blueNoise, x, y, sampleIdx, 7 + 4 * p.pathLength );
-					}
+					if (sampleIdx < 256) r3 = bnv[2], r4 = bnv[3];
 					else
 					{
 						r3 = RandomFloat( seed );
@@ -1363,14 +1427,15 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const Scen
 			}
 		}
 	compact:
-		/* wave-level compaction of extension and shadow rays (one atomicAdd per wave each) */
+		/* wave-level compaction of extension and shadow rays into this block's segment of the output
+		   streams (one atomicAdd per wave each, on the segment's own counter) */
 		{
-			const uint32_t es = wave_alloc( doExt, &p.counters->extensionRays );
-			if (doExt) { p.rayOut[es] = eO; p.rayDOut[es] = eD; p.T4Out[es] = eT; p.Q4Out[es] = eQ; }
-			const uint32_t ss = wave_alloc( doShadow, &p.counters->shadowRays );
+			const uint32_t es = wave_alloc( doExt, &p.counters->segExt[seg * LH2_SEGCOUNT_STRIDE] );
+			if (doExt) { const uint32_t o = segBase + es; p.rayOut[o] = eO; p.rayDOut[o] = eD; p.T4Out[o] = eT; p.Q4Out[o] = eQ; }
+			const uint32_t ss = wave_alloc( doShadow, &p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE] );
 			if (doShadow)
 			{
-				if (ss < p.shadowCap) { p.shO[ss] = sO; p.shD[ss] = sD; p.shP[ss] = sP; }
+				if (ss < p.shadowStride) { const uint32_t o = seg * p.shadowStride + ss; p.shO[o] = sO; p.shD[o] = sD; p.shP[o] = sP; }
 				else atomicOr( &p.counters->shadowOverflow, 1u );
 			}
 		}
@@ -1456,23 +1521,28 @@ LH2_DEV v3 SampleBSDF_Lambert( const ShadingData& sd, v3 iN, const v3 N, const v
 
 __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const SceneDev s, const ShadeParams p )
 {
-	const uint32_t count = *p.pathCount;
-	const uint32_t gstride = gridDim.x * 256u;
+	/* the block's segment of the path stream (its XCD's), and the segment's share of the grid */
+	const uint32_t seg = blockIdx.x % LH2_SEGS;
+	const uint32_t count = p.segCounts[seg * LH2_SEGCOUNT_STRIDE], segBase = seg * p.segStride;
+	const uint32_t gstride = ((gridDim.x - seg + LH2_SEGS - 1) / LH2_SEGS) * 256u;
 	const int w = p.w, h = p.h;
-	for (uint32_t base = blockIdx.x * 256u; base < count; base += gstride)
+	for (uint32_t base = (blockIdx.x / LH2_SEGS) * 256u; base < count; base += gstride)
 	{
-		const uint32_t jobIndex = base + threadIdx.x;
+		const uint32_t jobIndex = segBase + base + threadIdx.x;
 		bool doExt = false, doShadow = false;
 		float4 eO, eD, eT, eQ, sO, sD, sP;
-		if (jobIndex < count)
+		if (base + threadIdx.x < count)
 		{
-			const float4 O4 = p.rayO[jobIndex], D4 = p.rayD[jobIndex], T4 = p.T4[jobIndex];
 			const uint4 hd = p.hits[jobIndex];
+			const float4 T4 = p.T4[jobIndex], O4 = p.rayO[jobIndex], D4 = p.rayD[jobIndex];
+			__builtin_amdgcn_sched_barrier( 0 );
 			const float HIT_T = __uint_as_float( hd.x );
 			const int PRIMIDX = (int)hd.y;
 			const int INSTANCEIDX = PRIMIDX == -1 ? 0 : (int)hd.z;
 			const float HIT_U = (float)(hd.w & 65535) * (1.0f / 65535.0f);
 			const float HIT_V = (float)(hd.w >> 16) * (1.0f / 65535.0f);
+			v3 instA, instB, instC;
+			const float4* tri = HitInstance( s, PRIMIDX, INSTANCEIDX, instA, instB, instC );
 			uint32_t data = fbits( T4.w );
 			const v3 D = xyz( D4 ), RAY_O = xyz( O4 );
 			v3 throughput = xyz( T4 );
@@ -1491,8 +1561,7 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const 
 				ShadingData sd;
 				v3 N, iN, fN, T;
 				const v3 I = add3( RAY_O, smul( HIT_T, D ) );
-				const float4* tri = (const float4*)s.instDesc[INSTANCEIDX].triangles + (size_t)PRIMIDX * 11;
-				GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, INSTANCEIDX, sd, N, iN, fN, T );
+				GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, instA, instB, instC, sd, N, iN, fN, T );
 				if (sd.color.x > 1.0f || sd.color.y > 1.0f || sd.color.z > 1.0f)
 				{
 					if (-dot3( D, N ) > 0 && (p.pathLength == 1 || (data & S_SPECULAR))) acc_add( p.acc, pixelIdx, mul3( throughput, sd.color ) );
@@ -1541,22 +1610,29 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const 
 		}
 	compact:
 		{
-			const uint32_t es = wave_alloc( doExt, &p.counters->extensionRays );
-			if (doExt) { p.rayOut[es] = eO; p.rayDOut[es] = eD; p.T4Out[es] = eT; p.Q4Out[es] = eQ; }
-			const uint32_t ss = wave_alloc( doShadow, &p.counters->shadowRays );
+			const uint32_t es = wave_alloc( doExt, &p.counters->segExt[seg * LH2_SEGCOUNT_STRIDE] );
+			if (doExt) { const uint32_t o = segBase + es; p.rayOut[o] = eO; p.rayDOut[o] = eD; p.T4Out[o] = eT; p.Q4Out[o] = eQ; }
+			const uint32_t ss = wave_alloc( doShadow, &p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE] );
 			if (doShadow)
 			{
-				if (ss < p.shadowCap) { p.shO[ss] = sO; p.shD[ss] = sD; p.shP[ss] = sP; }
+				if (ss < p.shadowStride) { const uint32_t o = seg * p.shadowStride + ss; p.shO[o] = sO; p.shD[o] = sD; p.shP[o] = sP; }
 				else atomicOr( &p.counters->shadowOverflow, 1u );
 			}
 		}
 	}
 }
 
-__global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t* cursors, int cursorWords )
+__global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords )
 {
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i < cursorWords) cursors[i] = 0;
+	if (i < LH2_SEGS)
+	{
+		/* the camera writes the paths densely: segment i is [i * segStride, (i + 1) * segStride) */
+		const uint32_t lo = (uint32_t)i * segStride;
+		c->segActive[i * LH2_SEGCOUNT_STRIDE] = pathCount > lo ? min( pathCount - lo, segStride ) : 0u;
+		c->segExt[i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadow[i * LH2_SEGCOUNT_STRIDE] = 0;
+	}
 	if (i != 0) return;
 	c->activePaths = pathCount, c->extensionRays = 0, c->shadowRays = 0;
 	c->totalExtensionRays = pathCount, c->totalShadowRays = 0;
@@ -1566,11 +1642,19 @@ __global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t* curs
 __global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength, int resetShadow )
 {
 	if (threadIdx.x != 0) return;
-	rayCountLog[pathLength] = c->extensionRays;     /* rays traced at pathLength + 1 */
-	c->totalExtensionRays += c->extensionRays;
-	c->activePaths = c->extensionRays;
-	c->extensionRays = 0;
-	if (resetShadow) c->totalShadowRays += c->shadowRays, c->shadowRays = 0;   /* InitCountersSubsequent (.cuda.cu:76-84) */
+	/* the extension rays become the next bounce's paths, segment by segment */
+	uint32_t ext = 0, sh = 0;
+	for (int k = 0; k < LH2_SEGS; k++)
+	{
+		const uint32_t e = c->segExt[k * LH2_SEGCOUNT_STRIDE];
+		ext += e, c->segActive[k * LH2_SEGCOUNT_STRIDE] = e, c->segExt[k * LH2_SEGCOUNT_STRIDE] = 0;
+		sh += c->segShadow[k * LH2_SEGCOUNT_STRIDE];
+		if (resetShadow) c->segShadow[k * LH2_SEGCOUNT_STRIDE] = 0;
+	}
+	rayCountLog[pathLength] = ext;     /* rays traced at pathLength + 1 */
+	c->totalExtensionRays += ext;
+	c->activePaths = ext;
+	if (resetShadow) c->totalShadowRays += sh;   /* InitCountersSubsequent (.cuda.cu:76-84) */
 }
 __global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale )
 {
@@ -1594,9 +1678,9 @@ __global__ void k_pack_rows( const float4* __restrict__ acc, float4* __restrict_
 
 /* ---- host-side launchers (extern "C", no torch / no HIP types beyond the stream) ---------- */
 extern "C" {
-void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t* cursors, int cursorWords, hipStream_t st )
+void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, hipStream_t st )
 {
-	k_init_counters<<<(cursorWords + 255) / 256 + 1, 256, 0, st>>>( c, pathCount, cursors, cursorWords );
+	k_init_counters<<<(cursorWords + 255) / 256 + 1, 256, 0, st>>>( c, pathCount, segStride, cursors, cursorWords );
 }
 void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, hipStream_t st ) { k_counters_next<<<1, 64, 0, st>>>( c, log, pathLength, resetShadow ); }
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, hipStream_t st )
@@ -1647,6 +1731,7 @@ int lh2_trace_blocks_per_cu( void )
 }
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, hipStream_t st )
 {
+	grid = grid < LH2_SEGS ? LH2_SEGS : grid;   /* every segment needs a block */
 	if (p->primeRef) k_shade_ref<<<grid, 256, 0, st>>>( *s, *p );
 	else k_shade<<<grid, 256, 0, st>>>( *s, *p );
 }

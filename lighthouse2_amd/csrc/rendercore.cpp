@@ -121,7 +121,9 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	dSceneError.resize( 1 ), dTlasDepth.resize( 1 );
 	CHK_HIP( hipMemsetAsync( dSceneError.ptr, 0, sizeof( int ), stream ) );
 	CHK_HIP( hipMemsetAsync( dTlasDepth.ptr, 0, sizeof( int ), stream ) );
-	CHK_HIP( hipHostMalloc( (void**)&activeLog, sizeof( uint32_t ) * 20, hipHostMallocDefault ) );
+	dInstDesc.resize( 1 );   /* shading reads record 0 for a miss (HitInstance): it always exists */
+	CHK_HIP( hipMemsetAsync( dInstDesc.ptr, 0, sizeof( lh2_CoreInstanceDesc ), stream ) );
+	CHK_HIP( hipHostMalloc( (void**)&activeLog, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), hipHostMallocDefault ) );   /* indexed by pathLength */
 	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 2, std::max( 1, atoi( tv ) ) );   /* A/B runs */
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
@@ -167,7 +169,7 @@ void RenderCore::EnsureBuffers()
 	const size_t paths = (size_t)scrwidth * scrheight * scrspp;
 	if (paths > maxPaths)
 	{
-		maxPaths = paths + (paths >> 4);   /* reserve a bit extra, as the reference does */
+		maxPaths = paths + (paths >> 4) + 64;   /* reserve a bit extra, as the reference does (and >= LH2_SEGS segments of ceil(paths / LH2_SEGS)) */
 		for (int i = 0; i < 2; i++) rayO[i].resize( maxPaths ), rayD[i].resize( maxPaths ), T4[i].resize( maxPaths ), Q4[i].resize( maxPaths );
 		hits.resize( maxPaths );
 		shO.resize( 2 * maxPaths ), shD.resize( 2 * maxPaths ), shP.resize( 2 * maxPaths );
@@ -574,7 +576,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const uint32_t pathCount = (uint32_t)tilePix * (uint32_t)scrspp;
 	const SceneDev sd = MakeSceneDev();
 	Counters* c = counters.ptr;
-	lh2_launch_init_counters( c, pathCount, fetchCursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, stream );
+	/* segmented path / ray streams (lh2_kernels.h): LH2_SEGS segments of segStride records; shadow rays
+	   in segments of shadowStride */
+	const uint32_t segStride = (pathCount + LH2_SEGS - 1) / LH2_SEGS;
+	const uint32_t shadowStride = (uint32_t)(shO.count / LH2_SEGS);
+	if ((size_t)segStride * LH2_SEGS > maxPaths) FatalError( "path buffers too small for %u segments of %u", LH2_SEGS, segStride );
+	lh2_launch_init_counters( c, pathCount, segStride, fetchCursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, stream );
 	/* primary rays (camera.h) for every sample of the tile */
 	CameraParams cp{};
 	cp.pos = view.pos, cp.p1 = view.p1;
@@ -597,7 +604,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipEventRecord( evTrace[2 * pathLength], stream ) );
 		TraceArgs ta{};
 		ta.version = traceVersion;
-		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.countPtr = &c->activePaths, ta.cursor = fetchCursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
+		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.segCounts = c->segActive, ta.segStride = segStride, ta.cursor = fetchCursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
 		ta.packet = pathLength == 1 && tiledRays && UsePackets();
 		ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
@@ -605,10 +612,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		lh2_launch_trace_closest( &sd, &ta, grid, stream );
 		CHK_HIP( hipEventRecord( evTrace[2 * pathLength + 1], stream ) );
 		ShadeParams sp{};
-		sp.pathCount = &c->activePaths;
+		sp.segCounts = c->segActive, sp.segStride = segStride, sp.shadowStride = shadowStride;
 		sp.rayO = rayO[in].ptr, sp.rayD = rayD[in].ptr, sp.T4 = T4[in].ptr, sp.Q4 = Q4[in].ptr, sp.hits = hits.ptr;
 		sp.rayOut = rayO[1 - in].ptr, sp.rayDOut = rayD[1 - in].ptr, sp.T4Out = T4[1 - in].ptr, sp.Q4Out = Q4[1 - in].ptr;
-		sp.shO = shO.ptr, sp.shD = shD.ptr, sp.shP = shP.ptr, sp.shadowCap = (uint32_t)shO.count;
+		sp.shO = shO.ptr, sp.shD = shD.ptr, sp.shP = shP.ptr;
 		sp.acc = accumulator.ptr, sp.counters = c;
 		sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
 		sp.primeRef = primeRef;
@@ -626,7 +633,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			CHK_HIP( hipEventRecord( evShadowB[2 * pathLength], stream ) );
 			TraceArgs ta{};
 			ta.version = traceVersion;
-			ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = fetchCursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
+			ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.segCounts = c->segShadow, ta.segStride = shadowStride, ta.cursor = fetchCursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
 			ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 			ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
 			ta.packet = packetShadow;
@@ -651,7 +658,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	{
 		TraceArgs ta{};
 		ta.version = traceVersion;
-		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.countPtr = &c->shadowRays, ta.cursor = fetchCursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.segCounts = c->segShadow, ta.segStride = shadowStride, ta.cursor = fetchCursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
 		ta.packet = packetShadow;
 		lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
@@ -690,6 +697,14 @@ int RenderCore::TileRows() const
 	return std::max( 0, y1 - y0 );
 }
 
+/* shadow rays queued in the segments of the shadow stream (the final shadow pass traces them all) */
+static uint32_t QueuedShadowRays( const Counters& c )
+{
+	uint32_t n = 0;
+	for (int k = 0; k < LH2_SEGS; k++) n += c.segShadow[k * LH2_SEGCOUNT_STRIDE];
+	return n;
+}
+
 void RenderCore::Synchronize()
 {
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -713,7 +728,7 @@ void RenderCore::Synchronize()
 		for (int L = 1; L <= framePathLengths; L++) shade += ms( evShade[2 * L], evShade[2 * L + 1] );
 		coreStats.shadeTime = shade;
 		for (int L = 1; L <= framePathLengths && L <= 8; L++) lastKernelMs[L - 1] = ms( evTrace[2 * L], evTrace[2 * L + 1] ) * 1e3f;
-		coreStats.totalShadowRays = framePrimeRef ? cnt.totalShadowRays : cnt.shadowRays;
+		coreStats.totalShadowRays = framePrimeRef ? cnt.totalShadowRays : QueuedShadowRays( cnt );
 		coreStats.totalExtensionRays = cnt.totalExtensionRays;
 		coreStats.totalRays = coreStats.totalExtensionRays + coreStats.totalShadowRays;
 		coreStats.renderTime = ms( evFrame[0], evFrame[1] );   /* device time of the whole frame (the reference's Render blocks) */
@@ -731,7 +746,7 @@ void RenderCore::GetRayCounts( uint32_t* out17 )
 {
 	Synchronize();
 	for (int i = 0; i < 17; i++) out17[i] = i < framePathLengths ? hostStats->rayCount[i] : 0;
-	out17[16] = framePrimeRef ? hostStats->counters.totalShadowRays : hostStats->counters.shadowRays;
+	out17[16] = framePrimeRef ? hostStats->counters.totalShadowRays : QueuedShadowRays( hostStats->counters );
 }
 
 void RenderCore::GetAccumulator( float* hostOut4 )
@@ -772,7 +787,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
 	ta.version = traceVersion;
-	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
+	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
 	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
 	ta.packet = unitCoherent && UsePackets();
 	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
@@ -794,7 +809,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
 	ta.version = traceVersion;
-	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 	ta.packet = unitCoherent && packetShadow;
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, stream );
 	std::vector<uint32_t> tmp( words );
@@ -820,7 +835,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 	{
 		TraceArgs ta{};
 		ta.version = traceVersion;
-		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.cursor = cursors.ptr + (size_t)i * LH2_CURSOR_WORDS;
+		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = cursors.ptr + (size_t)i * LH2_CURSOR_WORDS;
 		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr;
 		/* unitCoherent: trace as the frame traces its (tiled) primary rays */
 		ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
