@@ -75,16 +75,27 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	int packet;                                       /* 1: wave-uniform packet traversal (coherent rays, closest hit) */
 };
 
+/* start / stop events of one launch, recorded by the dispatch itself (hipExtLaunchKernelGGL); null: none */
+struct LaunchEvents { hipEvent_t start, stop; };
+
+/* where k_finalize delivers the frame's statistics: the device counters / ray-count log / scene error,
+   and the host's pinned FrameStats fields (hostCounters null: nothing is delivered) */
+struct FrameStatsDev
+{
+	const Counters* counters; const uint32_t* rayLog; const int* sceneError;
+	Counters* hostCounters; uint32_t* hostRayCount; int* hostSceneError;
+};
+
 extern "C" {
-void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, hipStream_t st );
-void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, hipStream_t st );
-void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, hipStream_t st );
-void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, hipStream_t st );
-void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, hipStream_t st );
+void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, LaunchEvents ev, hipStream_t st );
+void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, uint32_t* hostActiveLog, LaunchEvents ev, hipStream_t st );
+void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, LaunchEvents ev, hipStream_t st );
+void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st );
+void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st );
 int lh2_trace_blocks_per_cu( void );
-void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, hipStream_t st );
+void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, hipStream_t st );
-void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, hipStream_t st );
+void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st );
 }
 
 /* Segmented ray streams.  A stream of paths or rays lives in LH2_SEGS segments of one buffer:

@@ -14,6 +14,7 @@
    Numerics: compiled with -ffp-contract=off and correctly rounded div/sqrt; every expression
    keeps the reference's evaluation order so results are bit-comparable with oracle/pt_oracle.c.
 */
+#include <hip/hip_ext.h>
 #include "lh2_device.h"
 #include "../../include/lh2_core_types.h"
 #include "lh2_kernels.h"
@@ -1271,8 +1272,11 @@ LH2_DEV const float4* HitInstance( const SceneDev& s, const int primIdx, const i
 }
 
 /* ---- shade kernel: pathtracer.h:54-245 --------------------------------------------------- */
+/* 3 waves per SIMD (<= 168 VGPRs, 4 spilled): the kernel is load-latency bound (a dependent chain of
+   hit -> instance -> triangle -> material loads per path), 0.285 -> 0.244 ms per frame on config 2
+   over the unbounded 171-VGPR build (2 waves); 4 waves spill ~100 VGPRs */
 #ifndef LH2_SHADE_MINWAVES
-#define LH2_SHADE_MINWAVES 1
+#define LH2_SHADE_MINWAVES 3
 #endif
 __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const SceneDev s, const ShadeParams p )
 {
@@ -1639,7 +1643,7 @@ __global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t segSt
 	c->probedInstid = -1, c->probedTriid = -1, c->probedDist = 0;
 	c->reserved0 = 0, c->shadowOverflow = 0;
 }
-__global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength, int resetShadow )
+__global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength, int resetShadow, uint32_t* hostActiveLog )
 {
 	if (threadIdx.x != 0) return;
 	/* the extension rays become the next bounce's paths, segment by segment */
@@ -1655,10 +1659,24 @@ __global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLen
 	c->totalExtensionRays += ext;
 	c->activePaths = ext;
 	if (resetShadow) c->totalShadowRays += sh;   /* InitCountersSubsequent (.cuda.cu:76-84) */
+	/* the host's early exit reads this after the launch's stop event (no copy launch) */
+	if (hostActiveLog) __hip_atomic_store( hostActiveLog + pathLength, ext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
 }
-__global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale )
+__global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale, const FrameStatsDev fs )
 {
 	const int i = threadIdx.x + blockIdx.x * blockDim.x;
+	if (blockIdx.x == 0 && fs.hostCounters)
+	{
+		/* block 0 also hands the frame's counters, ray-count log and scene error to the host's pinned
+		   FrameStats (system-scope stores: no device-to-host copy launches at the end of the frame) */
+		const uint32_t* src = (const uint32_t*)fs.counters;
+		uint32_t* dst = (uint32_t*)fs.hostCounters;
+		for (int k = threadIdx.x; k < (int)(sizeof( Counters ) / 4); k += blockDim.x)
+			__hip_atomic_store( dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+		for (int k = threadIdx.x; k < LH2_MAX_BOUNCES; k += blockDim.x)
+			__hip_atomic_store( fs.hostRayCount + k, fs.rayLog[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+		if (threadIdx.x == 0) __hip_atomic_store( fs.hostSceneError, *fs.sceneError, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+	}
 	if (i >= n) return;
 	const float4 a = acc[i];
 	out[i] = make_float4( a.x * scale, a.y * scale, a.z * scale, a.w * scale );
@@ -1677,49 +1695,57 @@ __global__ void k_pack_rows( const float4* __restrict__ acc, float4* __restrict_
 }
 
 /* ---- host-side launchers (extern "C", no torch / no HIP types beyond the stream) ---------- */
+/* Launches go through hipExtLaunchKernelGGL: its start / stop events are recorded by the kernel's own
+   dispatch packet, where a hipEventRecord between two launches costs a barrier packet and ~5 us of
+   idle GPU per event (rocprofv3 kernel trace of the config-2 frame); null events: a plain launch. */
+#define LH2_LAUNCH( kernel, grid, block, st, ev, ... ) \
+	hipExtLaunchKernelGGL( kernel, dim3( grid ), dim3( block ), 0, st, (ev).start, (ev).stop, 0, __VA_ARGS__ )
+
 extern "C" {
-void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, hipStream_t st )
+void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, LaunchEvents ev, hipStream_t st )
 {
-	k_init_counters<<<(cursorWords + 255) / 256 + 1, 256, 0, st>>>( c, pathCount, segStride, cursors, cursorWords );
+	LH2_LAUNCH( k_init_counters, (cursorWords + 255) / 256 + 1, 256, st, ev, c, pathCount, segStride, cursors, cursorWords );
 }
-void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, hipStream_t st ) { k_counters_next<<<1, 64, 0, st>>>( c, log, pathLength, resetShadow ); }
-void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, hipStream_t st )
+void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, uint32_t* hostActiveLog, LaunchEvents ev, hipStream_t st )
 {
-	if (jobCount <= 0) return;
-	k_camera<<<(jobCount + 255) / 256, 256, 0, st>>>( *p, bn, rayO, rayD, T4, Q4, jobCount );
+	LH2_LAUNCH( k_counters_next, 1, 64, st, ev, c, log, pathLength, resetShadow, hostActiveLog );
 }
-void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, hipStream_t st )
+void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, LaunchEvents ev, hipStream_t st )
+{
+	LH2_LAUNCH( k_camera, jobCount > 0 ? (jobCount + 255) / 256 : 1, 256, st, ev, *p, bn, rayO, rayD, T4, Q4, jobCount );
+}
+void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st )
 {
 	/* incoherent rays: parked leaves (leafBatch > 0); traversal loop version 1 or 2 (lh2_trace2.inc);
 	   coherent primary rays: packet traversal (lh2_trace_packet.inc) */
-	if (a->packet) k_trace_closest_packet<<<grid, 256, 0, st>>>( *s, *a );
+	if (a->packet) LH2_LAUNCH( k_trace_closest_packet, grid, 256, st, ev, *s, *a );
 	else if (a->version == 2)
 	{
-		if (a->leafBatch) k_trace_closest<true, 2><<<grid, 256, 0, st>>>( *s, *a );
-		else k_trace_closest<false, 2><<<grid, 256, 0, st>>>( *s, *a );
+		if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 2>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_closest<false, 2>), grid, 256, st, ev, *s, *a );
 	}
 	else
 	{
-		if (a->leafBatch) k_trace_closest<true, 1><<<grid, 256, 0, st>>>( *s, *a );
-		else k_trace_closest<false, 1><<<grid, 256, 0, st>>>( *s, *a );
+		if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 1>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_closest<false, 1>), grid, 256, st, ev, *s, *a );
 	}
 }
-void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, hipStream_t st )
+void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st )
 {
 	if (a->packet)
 	{
-		if (fused) k_trace_any_packet<1><<<grid, 256, 0, st>>>( *s, *a );
-		else k_trace_any_packet<0><<<grid, 256, 0, st>>>( *s, *a );
+		if (fused) LH2_LAUNCH( k_trace_any_packet<1>, grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( k_trace_any_packet<0>, grid, 256, st, ev, *s, *a );
 	}
 	else if (a->version == 2)
 	{
-		if (fused) k_trace_any<1, 2><<<grid, 256, 0, st>>>( *s, *a );
-		else k_trace_any<0, 2><<<grid, 256, 0, st>>>( *s, *a );
+		if (fused) LH2_LAUNCH( (k_trace_any<1, 2>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_any<0, 2>), grid, 256, st, ev, *s, *a );
 	}
 	else
 	{
-		if (fused) k_trace_any<1, 1><<<grid, 256, 0, st>>>( *s, *a );
-		else k_trace_any<0, 1><<<grid, 256, 0, st>>>( *s, *a );
+		if (fused) LH2_LAUNCH( (k_trace_any<1, 1>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_any<0, 1>), grid, 256, st, ev, *s, *a );
 	}
 }
 int lh2_trace_blocks_per_cu( void )
@@ -1729,20 +1755,20 @@ int lh2_trace_blocks_per_cu( void )
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_any<1, 1>, 256, 0 ) != hipSuccess) n2 = 4;
 	return n1 > n2 ? n1 : n2;
 }
-void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, hipStream_t st )
+void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st )
 {
 	grid = grid < LH2_SEGS ? LH2_SEGS : grid;   /* every segment needs a block */
-	if (p->primeRef) k_shade_ref<<<grid, 256, 0, st>>>( *s, *p );
-	else k_shade<<<grid, 256, 0, st>>>( *s, *p );
+	if (p->primeRef) LH2_LAUNCH( k_shade_ref, grid, 256, st, ev, *s, *p );
+	else LH2_LAUNCH( k_shade, grid, 256, st, ev, *s, *p );
 }
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, hipStream_t st )
 {
 	if (rows * w <= 0) return;
 	k_pack_rows<<<(rows * w + 255) / 256, 256, 0, st>>>( acc, dst, w, y0, band, bandStride, rows );
 }
-void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, hipStream_t st )
+void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st )
 {
-	if (n <= 0) return;
-	k_finalize<<<(n + 255) / 256, 256, 0, st>>>( acc, out, n, scale );
+	const FrameStatsDev none{};
+	LH2_LAUNCH( k_finalize, n > 0 ? (n + 255) / 256 : 1, 256, st, ev, acc, out, n, scale, fs ? *fs : none );
 }
 }

@@ -109,21 +109,22 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	fetchCursors.resize( (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
 	rayLog.resize( LH2_MAX_BOUNCES + 8 );
 	blocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
-	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocDefault ) );
+	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evTrace) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evShade) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evShadow) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evShadowB) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
-	for (auto& e : evCount) CHK_HIP( hipEventCreateWithFlags( &e, hipEventDisableTiming ) );
+	for (auto& e : evCount) CHK_HIP( hipEventCreate( &e ) );   /* stop events of launches (LaunchEvents) */
+	CHK_HIP( hipEventCreate( &evCamera ) );
 	for (auto& e : evStage) CHK_HIP( hipEventCreateWithFlags( &e, hipEventDisableTiming ) );
 	dSceneError.resize( 1 ), dTlasDepth.resize( 1 );
 	CHK_HIP( hipMemsetAsync( dSceneError.ptr, 0, sizeof( int ), stream ) );
 	CHK_HIP( hipMemsetAsync( dTlasDepth.ptr, 0, sizeof( int ), stream ) );
 	dInstDesc.resize( 1 );   /* shading reads record 0 for a miss (HitInstance): it always exists */
 	CHK_HIP( hipMemsetAsync( dInstDesc.ptr, 0, sizeof( lh2_CoreInstanceDesc ), stream ) );
-	CHK_HIP( hipHostMalloc( (void**)&activeLog, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), hipHostMallocDefault ) );   /* indexed by pathLength */
+	CHK_HIP( hipHostMalloc( (void**)&activeLog, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), hipHostMallocCoherent ) );   /* indexed by pathLength; written by k_counters_next */
 	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 2, std::max( 1, atoi( tv ) ) );   /* A/B runs */
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
@@ -562,7 +563,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	if (!dMaterials.ptr) FatalError( "Render before SetMaterials" );
 	const auto t0 = std::chrono::high_resolution_clock::now();
-	CHK_HIP( hipEventRecord( evFrame[0], stream ) );
+	/* CoreStats timings come from the start / stop events of the launches themselves (LaunchEvents,
+	   recorded by the dispatch packets): no hipEventRecord between kernels */
 	if (converge == LH2_RESTART || firstConvergingFrame)
 	{
 		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
@@ -581,7 +583,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const uint32_t segStride = (pathCount + LH2_SEGS - 1) / LH2_SEGS;
 	const uint32_t shadowStride = (uint32_t)(shO.count / LH2_SEGS);
 	if ((size_t)segStride * LH2_SEGS > maxPaths) FatalError( "path buffers too small for %u segments of %u", LH2_SEGS, segStride );
-	lh2_launch_init_counters( c, pathCount, segStride, fetchCursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, stream );
+	lh2_launch_init_counters( c, pathCount, segStride, fetchCursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, { nullptr, evFrame[0] }, stream );
 	/* primary rays (camera.h) for every sample of the tile */
 	CameraParams cp{};
 	cp.pos = view.pos, cp.p1 = view.p1;
@@ -594,14 +596,14 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	cp.band = tileBand > 0 ? tileBand : std::max( 1, tileRows ), cp.bandStride = tileBand > 0 ? tileStride : std::max( 1, tileRows );
 	cp.tiled = tiledRays;
 	cp.primeRef = primeRef;
-	lh2_launch_camera( &cp, dBlueNoise.ptr, rayO[0].ptr, rayD[0].ptr, T4[0].ptr, Q4[0].ptr, (int)pathCount, stream );
+	lh2_launch_camera( &cp, dBlueNoise.ptr, rayO[0].ptr, rayD[0].ptr, T4[0].ptr, Q4[0].ptr, (int)pathCount, { nullptr, evCamera }, stream );
+	hipEvent_t prevStop = evCamera;   /* timed intervals: previous launch's stop -> this launch's stop */
 	int in = 0, pl = 0;
 	const int grid = TraceGrid();
 	const int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
 	for (int pathLength = 1; pathLength <= maxPL; pathLength++)
 	{
 		pl = pathLength;
-		CHK_HIP( hipEventRecord( evTrace[2 * pathLength], stream ) );
 		TraceArgs ta{};
 		ta.version = traceVersion;
 		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.segCounts = c->segActive, ta.segStride = segStride, ta.cursor = fetchCursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
@@ -609,8 +611,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.packet = pathLength == 1 && tiledRays && UsePackets();
 		ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
 		ta.hits = hits.ptr, ta.gstack = gstack.ptr;
-		lh2_launch_trace_closest( &sd, &ta, grid, stream );
-		CHK_HIP( hipEventRecord( evTrace[2 * pathLength + 1], stream ) );
+		lh2_launch_trace_closest( &sd, &ta, grid, { nullptr, evTrace[2 * pathLength + 1] }, stream );
+		fromTrace[pathLength] = prevStop, prevStop = evTrace[2 * pathLength + 1];
 		ShadeParams sp{};
 		sp.segCounts = c->segActive, sp.segStride = segStride, sp.shadowStride = shadowStride;
 		sp.rayO = rayO[in].ptr, sp.rayD = rayD[in].ptr, sp.T4 = T4[in].ptr, sp.Q4 = Q4[in].ptr, sp.hits = hits.ptr;
@@ -622,27 +624,25 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		sp.probePixel = probeX + scrwidth * probeY;
 		sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
 		sp.spreadAngle = view.spreadAngle;
-		CHK_HIP( hipEventRecord( evShade[2 * pathLength], stream ) );
-		lh2_launch_shade( &sd, &sp, grid, stream );
-		CHK_HIP( hipEventRecord( evShade[2 * pathLength + 1], stream ) );
+		lh2_launch_shade( &sd, &sp, grid, { nullptr, evShade[2 * pathLength + 1] }, stream );
+		fromShade[pathLength] = prevStop, prevStop = evShade[2 * pathLength + 1];
 		if (pathLength == maxPL) break;
 		if (primeRef)
 		{
 			/* RenderCore_PrimeRef traces the shadow rays of every bounce right after it
 			   (rendercore.cpp connect step), fused with finalizeConnections */
-			CHK_HIP( hipEventRecord( evShadowB[2 * pathLength], stream ) );
 			TraceArgs ta{};
 			ta.version = traceVersion;
 			ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.segCounts = c->segShadow, ta.segStride = shadowStride, ta.cursor = fetchCursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
 			ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 			ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
 			ta.packet = packetShadow;
-			lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
-			CHK_HIP( hipEventRecord( evShadowB[2 * pathLength + 1], stream ) );
+			lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, evShadowB[2 * pathLength + 1] }, stream );
+			fromShadowB[pathLength] = prevStop, prevStop = evShadowB[2 * pathLength + 1];
 		}
-		lh2_launch_counters_next( c, rayLog.ptr, pathLength, primeRef, stream );
-		CHK_HIP( hipMemcpyAsync( activeLog + pathLength, &c->activePaths, sizeof( uint32_t ), hipMemcpyDeviceToHost, stream ) );
-		CHK_HIP( hipEventRecord( evCount[pathLength], stream ) );
+		/* the kernel writes this bounce's extension-ray count into the pinned activeLog itself */
+		lh2_launch_counters_next( c, rayLog.ptr, pathLength, primeRef, activeLog, { nullptr, evCount[pathLength] }, stream );
+		prevStop = evCount[pathLength];
 		/* early exit without stalling the GPU: wait for the count of the previous bounce while this
 		   bounce is queued; when it was 0, this bounce is empty and so is everything after it */
 		if (pathLength >= 2)
@@ -653,7 +653,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		in = 1 - in;
 	}
 	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
-	CHK_HIP( hipEventRecord( evShadow[0], stream ) );
 	if (!primeRef)
 	{
 		TraceArgs ta{};
@@ -661,11 +660,15 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.segCounts = c->segShadow, ta.segStride = shadowStride, ta.cursor = fetchCursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
 		ta.packet = packetShadow;
-		lh2_launch_trace_any( &sd, &ta, grid, 1, stream );
+		lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, evShadow[1] }, stream );
+		fromShadow = prevStop;
 	}
-	CHK_HIP( hipEventRecord( evShadow[1], stream ) );
 	samplesTaken += scrspp;
-	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, stream );
+	/* finalize also delivers the frame's counters, ray-count log and scene error to hostStats */
+	FrameStatsDev fs{};
+	fs.counters = c, fs.rayLog = rayLog.ptr + 1, fs.sceneError = dSceneError.ptr;
+	fs.hostCounters = &hostStats->counters, fs.hostRayCount = hostStats->rayCount + 1, fs.hostSceneError = &hostStats->sceneError;
+	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, &fs, { nullptr, evFrame[1] }, stream );
 	if (glResource)
 	{
 		hipArray_t arr = nullptr;
@@ -674,10 +677,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipMemcpy2DToArrayAsync( arr, 0, 0, frame.ptr, sizeof( float4 ) * scrwidth, sizeof( float4 ) * scrwidth, scrheight, hipMemcpyDeviceToDevice, stream ) );
 		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, stream ) );
 	}
-	CHK_HIP( hipMemcpyAsync( &hostStats->counters, c, sizeof( Counters ), hipMemcpyDeviceToHost, stream ) );
-	CHK_HIP( hipMemcpyAsync( hostStats->rayCount + 1, rayLog.ptr + 1, sizeof( uint32_t ) * LH2_MAX_BOUNCES, hipMemcpyDeviceToHost, stream ) );
-	CHK_HIP( hipMemcpyAsync( &hostStats->sceneError, dSceneError.ptr, sizeof( int ), hipMemcpyDeviceToHost, stream ) );
-	CHK_HIP( hipEventRecord( evFrame[1], stream ) );
 	hostStats->rayCount[0] = pathCount;
 	framePathLengths = pl;
 	framePrimeRef = primeRef;
@@ -717,17 +716,18 @@ void RenderCore::Synchronize()
 		uint32_t* rc = hostStats->rayCount;   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
 		auto ms = [&]( hipEvent_t a, hipEvent_t b ) { float t = 0; (void)hipEventElapsedTime( &t, a, b ); return t * 1e-3f; };
 		coreStats.primaryRayCount = rc[0];
-		coreStats.traceTime0 = ms( evTrace[2], evTrace[3] );
+		/* each interval: previous launch's stop event -> this launch's stop event (kernel + launch gap) */
+		coreStats.traceTime0 = ms( fromTrace[1], evTrace[3] );
 		coreStats.bounce1RayCount = framePathLengths >= 2 ? rc[1] : 0;
-		coreStats.traceTime1 = framePathLengths >= 2 ? ms( evTrace[4], evTrace[5] ) : 0;
+		coreStats.traceTime1 = framePathLengths >= 2 ? ms( fromTrace[2], evTrace[5] ) : 0;
 		coreStats.deepRayCount = 0, coreStats.traceTimeX = 0;
-		for (int L = 3; L <= framePathLengths; L++) coreStats.deepRayCount = rc[L - 1], coreStats.traceTimeX = ms( evTrace[2 * L], evTrace[2 * L + 1] );
-		coreStats.shadowTraceTime = ms( evShadow[0], evShadow[1] );
-		if (framePrimeRef) for (int L = 1; L < framePathLengths; L++) coreStats.shadowTraceTime += ms( evShadowB[2 * L], evShadowB[2 * L + 1] );
+		for (int L = 3; L <= framePathLengths; L++) coreStats.deepRayCount = rc[L - 1], coreStats.traceTimeX = ms( fromTrace[L], evTrace[2 * L + 1] );
+		coreStats.shadowTraceTime = framePrimeRef ? 0.0f : ms( fromShadow, evShadow[1] );
+		if (framePrimeRef) for (int L = 1; L < framePathLengths; L++) coreStats.shadowTraceTime += ms( fromShadowB[L], evShadowB[2 * L + 1] );
 		float shade = 0;
-		for (int L = 1; L <= framePathLengths; L++) shade += ms( evShade[2 * L], evShade[2 * L + 1] );
+		for (int L = 1; L <= framePathLengths; L++) shade += ms( fromShade[L], evShade[2 * L + 1] );
 		coreStats.shadeTime = shade;
-		for (int L = 1; L <= framePathLengths && L <= 8; L++) lastKernelMs[L - 1] = ms( evTrace[2 * L], evTrace[2 * L + 1] ) * 1e3f;
+		for (int L = 1; L <= framePathLengths && L <= 8; L++) lastKernelMs[L - 1] = ms( fromTrace[L], evTrace[2 * L + 1] ) * 1e3f;
 		coreStats.totalShadowRays = framePrimeRef ? cnt.totalShadowRays : QueuedShadowRays( cnt );
 		coreStats.totalExtensionRays = cnt.totalExtensionRays;
 		coreStats.totalRays = coreStats.totalExtensionRays + coreStats.totalShadowRays;
@@ -790,7 +790,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
 	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
 	ta.packet = unitCoherent && UsePackets();
-	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
+	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), {}, stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	CheckSceneError();
@@ -811,7 +811,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	ta.version = traceVersion;
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 	ta.packet = unitCoherent && packetShadow;
-	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, stream );
+	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, {}, stream );
 	std::vector<uint32_t> tmp( words );
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -828,9 +828,10 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 	DevBuf<uint32_t> cursors;
 	cursors.resize( (size_t)std::max( 1, iterations ) * LH2_CURSOR_WORDS );
 	CHK_HIP( hipMemsetAsync( cursors.ptr, 0, sizeof( uint32_t ) * (size_t)std::max( 1, iterations ) * LH2_CURSOR_WORDS, stream ) );
-	hipEvent_t a, b;
-	CHK_HIP( hipEventCreate( &a ) ); CHK_HIP( hipEventCreate( &b ) );
-	CHK_HIP( hipEventRecord( a, stream ) );
+	/* each launch timed by its own dispatch-recorded start / stop events: msOut is the mean kernel
+	   duration, launch gaps excluded (as rocprofv3 --kernel-trace reports it) */
+	std::vector<hipEvent_t> ev( 2 * (size_t)std::max( 1, iterations ) );
+	for (auto& e : ev) CHK_HIP( hipEventCreate( &e ) );
 	for (int i = 0; i < iterations; i++)
 	{
 		TraceArgs ta{};
@@ -840,15 +841,14 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 		/* unitCoherent: trace as the frame traces its (tiled) primary rays */
 		ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
 		ta.packet = unitCoherent && UsePackets();
-		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), stream );
+		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), { ev[2 * i], ev[2 * i + 1] }, stream );
 	}
-	CHK_HIP( hipEventRecord( b, stream ) );
-	CHK_HIP( hipEventSynchronize( b ) );
-	float t = 0;
-	CHK_HIP( hipEventElapsedTime( &t, a, b ) );
-	if (msOut) *msOut = t / std::max( 1, iterations );
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	double total = 0;
+	for (int i = 0; i < iterations; i++) { float t = 0; CHK_HIP( hipEventElapsedTime( &t, ev[2 * i], ev[2 * i + 1] ) ); total += t; }
+	if (msOut) *msOut = (float)(total / std::max( 1, iterations ));
 	CheckSceneError();
-	(void)hipEventDestroy( a ); (void)hipEventDestroy( b );
+	for (auto& e : ev) (void)hipEventDestroy( e );
 }
 
 void RenderCore::GenerateEyeRays( const lh2_ViewPyramid& view, uint32_t R0, int pass, float* ot, float* dt, float* st )
@@ -863,7 +863,7 @@ void RenderCore::GenerateEyeRays( const lh2_ViewPyramid& view, uint32_t R0, int 
 	cp.aperture = view.aperture, cp.distortion = view.distortion, cp.geometryEpsilon = geometryEpsilon;
 	cp.w = scrwidth, cp.h = scrheight, cp.pass = pass, cp.R0 = R0;
 	cp.y0 = 0, cp.tileRows = scrheight, cp.band = scrheight, cp.bandStride = scrheight, cp.tiled = 0, cp.primeRef = primeRef;
-	lh2_launch_camera( &cp, dBlueNoise.ptr, o.ptr, d.ptr, t4.ptr, q4.ptr, n, stream );
+	lh2_launch_camera( &cp, dBlueNoise.ptr, o.ptr, d.ptr, t4.ptr, q4.ptr, n, {}, stream );
 	std::vector<float4> T( n ), Q( n );
 	CHK_HIP( hipMemcpyAsync( ot, o.ptr, sizeof( float4 ) * n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipMemcpyAsync( dt, d.ptr, sizeof( float4 ) * n, hipMemcpyDeviceToHost, stream ) );
@@ -902,6 +902,8 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto& e : evShadowB) (void)hipEventDestroy( e );
 	for (auto& e : evFrame) (void)hipEventDestroy( e );
 	for (auto& e : evCount) (void)hipEventDestroy( e );
+	if (evCamera) (void)hipEventDestroy( evCamera );
+	evCamera = nullptr;
 	for (auto& e : evStage) (void)hipEventDestroy( e );
 	for (int i = 0; i < 2; i++) { if (stage[i]) (void)hipHostFree( stage[i] ); stage[i] = nullptr, stageBytes[i] = 0; }
 	if (glResource) (void)hipGraphicsUnregisterResource( glResource );

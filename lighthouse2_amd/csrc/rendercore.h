@@ -164,6 +164,11 @@ private:
 	hipEvent_t evTrace[2 * (LH2_MAX_BOUNCES + 1)] = {}, evShade[2 * (LH2_MAX_BOUNCES + 1)] = {}, evShadow[2] = {}, evFrame[2] = {};
 	hipEvent_t evShadowB[2 * (LH2_MAX_BOUNCES + 1)] = {};   /* per-bounce shadow passes (PrimeRef mode) */
 	hipEvent_t evCount[LH2_MAX_BOUNCES + 2] = {};
+	hipEvent_t evCamera = nullptr;
+	/* a launch carries only a stop event (a start event costs its dispatch ~5 us of idle GPU); a timed
+	   interval runs from the previous launch's stop event, so it includes the launch gap: these hold
+	   the previous stop event of each interval (handles owned by the arrays above) */
+	hipEvent_t fromTrace[LH2_MAX_BOUNCES + 1] = {}, fromShade[LH2_MAX_BOUNCES + 1] = {}, fromShadowB[LH2_MAX_BOUNCES + 1] = {}, fromShadow = nullptr;
 	uint32_t* activeLog = nullptr;     /* pinned: active paths after each bounce */
 	int tiledRays = 1;
 	int refillPrimary = 48, refillOther = 32, leafBatch = 16, leafBatchPrimary = 8;   /* v2 sweep: profiles/r01b_refill_sweep.jsonl */
