@@ -115,6 +115,7 @@ def main():
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--setting", action="append", default=[], help="name=value core setting before loading (A/B runs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -130,6 +131,9 @@ def main():
     sc.view = scene.camera_view((0, 0, -12), (0, 0, 1), fov_deg=40, aspect=args.width / args.height, focal=5,
                                 pixel_height=H)
     core = RenderCore(device=local)
+    for kv in args.setting:
+        k, v = kv.split("=")
+        core.setting(k, float(v))
     t0 = time.perf_counter()
     sc.load_into(core)
     core.set_target(W, H, 1)
@@ -221,15 +225,15 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "k_trace_closest<PARK=true,v2> (per-ray traversal) on the frame's diffuse bounce "
-                                   "rays, in-frame order and settings", "kernel_ms": round(ms, 4),
+                         "kernel": "k_trace_closest<false, 4> (per-ray BVH4 traversal, the core's default settings) on "
+                                   "the frame's diffuse bounce rays, in-frame order", "kernel_ms": round(ms, 4),
                          "bytes_per_ray": round(bpr, 1), "rays_per_launch": n,
                          "bytes_model": "32 ray + 20 hit + 32 x node records + 36 x triangle tests of the reference "
                                         "traversal (tests/golden/config2_bounce_visits.json)"},
             "roofline_primary": {"bound": "hbm", "achieved": round(achieved_p, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": round(achieved_p / HBM_PEAK_GBS, 4),
                                  "kernel": ("k_trace_closest_packet (wave-uniform packet traversal)" if packets
-                                            else "k_trace_closest<PARK=true,v2>") + " on the 1080p primary rays",
+                                            else "k_trace_closest<true, 4>") + " on the 1080p primary rays",
                                  "kernel_ms": round(ms_p, 4), "bytes_per_ray": round(bpr_p, 1), "rays_per_launch": n_p,
                                  "note": "per-ray byte model; a packet fetches each node once per 64 rays (scalar "
                                          "loads), so frac > 1 is possible and means the kernel is not HBM-bound"},

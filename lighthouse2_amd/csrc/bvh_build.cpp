@@ -242,4 +242,84 @@ void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOut
 	out.sah = sah;
 }
 
+/* ---- BVH2 -> BVH4 (greedy surface-area collapse) ------------------------------------------
+   A BVH4 node takes a BVH2 node's two children and, while it has fewer than four, replaces its
+   interior child of largest surface area by that child's two children; interior children left
+   become BVH4 nodes of their own (breadth-first).  Empty (NaN-box) children are dropped; unused
+   slots get NaN boxes, which no box test hits.  Leaves keep their references, so the triangle
+   array (and every hit) is that of the BVH2. */
+int CollapseBvh4( const float* nodes2, size_t nodeCount2, std::vector<float>& nodes4 )
+{
+	struct E { float lo[3], hi[3]; int ref; };
+	auto children = [&]( int k, E* out ) {
+		const float* n = nodes2 + (size_t)k * 16;
+		int refs[2];
+		memcpy( refs, n + 12, 8 );
+		int m = 0;
+		for (int c = 0; c < 2; c++)
+		{
+			E e;
+			e.lo[0] = n[c * 4 + 0], e.hi[0] = n[c * 4 + 1], e.lo[1] = n[c * 4 + 2], e.hi[1] = n[c * 4 + 3];
+			e.lo[2] = n[8 + c * 2], e.hi[2] = n[9 + c * 2], e.ref = refs[c];
+			if (e.lo[0] == e.lo[0]) out[m++] = e;   /* NaN box: empty child */
+		}
+		return m;
+	};
+	auto area4 = [&]( const E& e ) {
+		const float dx = std::max( 0.0f, e.hi[0] - e.lo[0] ), dy = std::max( 0.0f, e.hi[1] - e.lo[1] ), dz = std::max( 0.0f, e.hi[2] - e.lo[2] );
+		return dx * dy + dy * dz + dz * dx;
+	};
+	const float nanv = std::numeric_limits<float>::quiet_NaN();
+	nodes4.assign( 32, 0.0f );
+	if (nodeCount2 == 0) { for (int i = 0; i < 24; i++) nodes4[i] = nanv; return 1; }
+	struct Item { int node2, node4, depth; };
+	std::vector<Item> queue;
+	queue.push_back( { 0, 0, 1 } );
+	int depth = 1;
+	for (size_t qi = 0; qi < queue.size(); qi++)
+	{
+		const Item it = queue[qi];
+		depth = std::max( depth, it.depth );
+		E list[4];
+		int n = children( it.node2, list );
+		while (n < 4)
+		{
+			int best = -1;
+			float bestA = -1;
+			for (int i = 0; i < n; i++) if (list[i].ref >= 0 && area4( list[i] ) > bestA) best = i, bestA = area4( list[i] );
+			if (best < 0) break;
+			E c[2];
+			const int m = children( list[best].ref, c );
+			if (m == 0) { list[best] = list[--n]; continue; }
+			list[best] = c[0];
+			if (m == 2) list[n++] = c[1];
+		}
+		int refs[4] = { 0, 0, 0, 0 };
+		for (int i = 0; i < n; i++)
+		{
+			if (list[i].ref >= 0)
+			{
+				const int child4 = (int)(nodes4.size() / 32);
+				nodes4.resize( nodes4.size() + 32, 0.0f );
+				queue.push_back( { list[i].ref, child4, it.depth + 1 } );
+				refs[i] = child4;
+			}
+			else refs[i] = list[i].ref;
+		}
+		float* q = &nodes4[(size_t)it.node4 * 32];
+		for (int i = 0; i < 4; i++)
+		{
+			/* slots i = 0, 1 in q0..q2, slots 2, 3 in q3..q5: (lo.x, hi.x, lo.y, hi.y) per slot, z pairs */
+			float* b = q + (i >> 1) * 12;
+			const int j = i & 1;
+			const bool used = i < n;
+			b[j * 4 + 0] = used ? list[i].lo[0] : nanv, b[j * 4 + 1] = used ? list[i].hi[0] : nanv;
+			b[j * 4 + 2] = used ? list[i].lo[1] : nanv, b[j * 4 + 3] = used ? list[i].hi[1] : nanv;
+			b[8 + j * 2] = used ? list[i].lo[2] : nanv, b[9 + j * 2] = used ? list[i].hi[2] : nanv;
+		}
+		memcpy( q + 24, refs, 16 );
+	}
+	return depth;
+}
+
 }  // namespace lh2

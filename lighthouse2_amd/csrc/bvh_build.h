@@ -28,4 +28,8 @@ struct BvhOutput
    traversalCost: SAH cost of a node visit relative to one triangle test */
 void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost = 1.0f );
 
+/* BVH2 (16 floats per node, root 0) -> BVH4 (32 floats per node, root 0; layout: lh2_device.h) by
+   greedy surface-area collapse; returns the BVH4 depth (interior levels) */
+int CollapseBvh4( const float* nodes2, size_t nodeCount2, std::vector<float>& nodes4 );
+
 }  // namespace lh2

@@ -68,6 +68,10 @@ public:
 	/* copy a mesh's nodes into the scene node array, offsetting interior refs by nodeBase and
 	   leaf triangle indices by triBase (asynchronous) */
 	static void Relocate( const float4* src, int nodeCount, int nodeBase, uint32_t triBase, float4* dst, hipStream_t stream );
+	/* the same for BVH4 nodes (128 B) */
+	static void Relocate4( const float4* src, int nodeCount, int nodeBase, uint32_t triBase, float4* dst, hipStream_t stream );
+	/* TLAS BVH2 nodes [base2, base2 + count) as two-child BVH4 nodes at base4 (interior refs remapped) */
+	static void TlasToBvh4( const float4* nodes2, int base2, int count, int base4, float4* nodes4, hipStream_t stream );
 
 private:
 	void Reserve( int n );

@@ -514,6 +514,40 @@ __global__ __launch_bounds__( 256 ) void k_relocate( const float4* __restrict__ 
 	d[3] = make_float4( __int_as_float( ref[0] ), __int_as_float( ref[1] ), 0, 0 );
 }
 
+/* BVH4 relocation: interior references + nodeBase, leaf triangle ranges + triBase */
+__global__ __launch_bounds__( 256 ) void k_relocate4( const float4* __restrict__ src, int count, int nodeBase, uint32_t triBase, float4* __restrict__ dst )
+{
+	const int i = blockIdx.x * 256 + threadIdx.x;
+	if (i >= count) return;
+	const float4* s = src + (size_t)i * 8;
+	float4* d = dst + (size_t)(nodeBase + i) * 8;
+	for (int k = 0; k < 6; k++) d[k] = s[k];
+	const int4 r = *(const int4*)(s + 6);
+	int ref[4] = { r.x, r.y, r.z, r.w };
+	for (int c = 0; c < 4; c++) ref[c] = ref[c] >= 0 ? ref[c] + nodeBase : MAKE_LEAF( LEAF_FIRST( ref[c] ) + triBase, LEAF_COUNT( ref[c] ) );
+	*(int4*)(d + 6) = make_int4( ref[0], ref[1], ref[2], ref[3] );
+	d[7] = make_float4( 0, 0, 0, 0 );
+}
+
+/* TLAS (BVH2 at nodes2[base2 ...]) as BVH4 nodes of two children (slots 2, 3 empty) at
+   nodes4[base4 ...]: interior references move from the BVH2 to the BVH4 index space, instance
+   leaves stay; one node per thread, so per-frame TLAS updates cost one short launch */
+__global__ __launch_bounds__( 256 ) void k_tlas_to_bvh4( const float4* __restrict__ nodes2, int base2, int count, int base4, float4* __restrict__ nodes4 )
+{
+	const int i = blockIdx.x * 256 + threadIdx.x;
+	if (i >= count) return;
+	const float4* s = nodes2 + (size_t)(base2 + i) * 4;
+	float4* d = nodes4 + (size_t)(base4 + i) * 8;
+	const float nanv = __builtin_nanf( "" );
+	d[0] = s[0], d[1] = s[1], d[2] = s[2];
+	d[3] = d[4] = d[5] = make_float4( nanv, nanv, nanv, nanv );
+	const float4 r = s[3];
+	int ref[2] = { __float_as_int( r.x ), __float_as_int( r.y ) };
+	for (int c = 0; c < 2; c++) if (ref[c] >= 0) ref[c] = ref[c] - base2 + base4;
+	*(int4*)(d + 6) = make_int4( ref[0], ref[1], MAKE_LEAF( 0, 1 ), MAKE_LEAF( 0, 1 ) );
+	d[7] = make_float4( 0, 0, 0, 0 );
+}
+
 inline int blocks( long n, int bs = 256 ) { return (int)std::max<long>( 1, (n + bs - 1) / bs ); }
 
 }  // namespace
@@ -640,6 +674,16 @@ void GpuBvhBuilder::Relocate( const float4* src, int nodeCount, int nodeBase, ui
 {
 	if (nodeCount <= 0) return;
 	k_relocate<<<blocks( nodeCount ), 256, 0, st>>>( src, nodeCount, nodeBase, triBase, dst );
+}
+void GpuBvhBuilder::Relocate4( const float4* src, int nodeCount, int nodeBase, uint32_t triBase, float4* dst, hipStream_t st )
+{
+	if (nodeCount <= 0) return;
+	k_relocate4<<<blocks( nodeCount ), 256, 0, st>>>( src, nodeCount, nodeBase, triBase, dst );
+}
+void GpuBvhBuilder::TlasToBvh4( const float4* nodes2, int base2, int count, int base4, float4* nodes4, hipStream_t st )
+{
+	if (count <= 0) return;
+	k_tlas_to_bvh4<<<blocks( count ), 256, 0, st>>>( nodes2, base2, count, base4, nodes4 );
 }
 
 }  // namespace lh2

@@ -26,6 +26,8 @@ struct SceneDev       /* everything the traversal and shading kernels read, by v
 	const float4* tris;
 	const DevInstance* inst;
 	int tlasRoot, instCount;
+	const float4* nodes4;            /* BVH4 of the same scene (traceVersion 4; null when not built) */
+	int tlasRoot4;
 	const lh2_CoreInstanceDesc* instDesc;
 	const uint4* materials;          /* 128 B CUDAMaterial records (core_settings.h:94-104) */
 	const lh2_CoreLightTri* areaLights;
@@ -71,9 +73,15 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	int* gstack;                                      /* stack entries past LH2_STACK_LDS */
 	uint32_t refill;                                  /* refill idle lanes once >= refill are idle (1..64) */
 	uint32_t leafBatch;                               /* run triangle tests once >= leafBatch lanes parked a leaf */
-	int version;                                      /* traversal loop: 1 (trace_stream) or 2 (lh2_trace2.inc) */
+	int version;                                      /* traversal loop: 1 (trace_stream), 2 (lh2_trace2.inc), 4 (BVH4, lh2_trace4.inc) */
 	int packet;                                       /* 1: wave-uniform packet traversal (coherent rays, closest hit) */
+	unsigned long long* stats;                        /* LH2_TRACE_STATS builds: LH2_TSTAT_N per-launch counters */
 };
+/* traversal-loop statistics (diagnostic builds with -DLH2_TRACE_STATS; tools/trace_stats.py):
+   wave-iterations, active-lane sum, leaf-phase iterations / lanes, walk iterations / lanes,
+   triangle-test lane sum, triangle-loop iterations, refill events / lanes, iterations / active-lane
+   sum once the queue is exhausted, wave time before / after exhaustion (100 MHz ticks) */
+#define LH2_TSTAT_N 14
 
 /* start / stop events of one launch, recorded by the dispatch itself (hipExtLaunchKernelGGL); null: none */
 struct LaunchEvents { hipEvent_t start, stop; };

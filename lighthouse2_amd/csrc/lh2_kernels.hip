@@ -513,7 +513,8 @@ template <bool PARK, int V>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_closest( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	if (V == 2) trace_stream2<0, PARK>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	if (V == 4) trace_stream2<0, PARK, 4>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	else if (V == 2) trace_stream2<0, PARK>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 	else trace_stream<0, PARK>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 }
 
@@ -521,7 +522,8 @@ template <int MODE, int V>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_any( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	if (V == 2) trace_stream2<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	if (V == 4) trace_stream2<MODE == 0 ? 1 : 2, true, 4>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	else if (V == 2) trace_stream2<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 	else trace_stream<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 }
 
@@ -1719,7 +1721,12 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
 	/* incoherent rays: parked leaves (leafBatch > 0); traversal loop version 1 or 2 (lh2_trace2.inc);
 	   coherent primary rays: packet traversal (lh2_trace_packet.inc) */
 	if (a->packet) LH2_LAUNCH( k_trace_closest_packet, grid, 256, st, ev, *s, *a );
-	else if (a->version == 2)
+	else if (a->version == 4 && s->nodes4)
+	{
+		if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 4>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_closest<false, 4>), grid, 256, st, ev, *s, *a );
+	}
+	else if (a->version >= 2)
 	{
 		if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 2>), grid, 256, st, ev, *s, *a );
 		else LH2_LAUNCH( (k_trace_closest<false, 2>), grid, 256, st, ev, *s, *a );
@@ -1737,7 +1744,12 @@ void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int 
 		if (fused) LH2_LAUNCH( k_trace_any_packet<1>, grid, 256, st, ev, *s, *a );
 		else LH2_LAUNCH( k_trace_any_packet<0>, grid, 256, st, ev, *s, *a );
 	}
-	else if (a->version == 2)
+	else if (a->version == 4 && s->nodes4)
+	{
+		if (fused) LH2_LAUNCH( (k_trace_any<1, 4>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_any<0, 4>), grid, 256, st, ev, *s, *a );
+	}
+	else if (a->version >= 2)
 	{
 		if (fused) LH2_LAUNCH( (k_trace_any<1, 2>), grid, 256, st, ev, *s, *a );
 		else LH2_LAUNCH( (k_trace_any<0, 2>), grid, 256, st, ev, *s, *a );

@@ -108,7 +108,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	counters.resize( 1 );
 	fetchCursors.resize( (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
 	rayLog.resize( LH2_MAX_BOUNCES + 8 );
-	blocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
+	blocksPerCU = maxBlocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evTrace) CHK_HIP( hipEventCreate( &e ) );
@@ -125,7 +125,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	dInstDesc.resize( 1 );   /* shading reads record 0 for a miss (HitInstance): it always exists */
 	CHK_HIP( hipMemsetAsync( dInstDesc.ptr, 0, sizeof( lh2_CoreInstanceDesc ), stream ) );
 	CHK_HIP( hipHostMalloc( (void**)&activeLog, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), hipHostMallocCoherent ) );   /* indexed by pathLength; written by k_counters_next */
-	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 2, std::max( 1, atoi( tv ) ) );   /* A/B runs */
+	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 4, std::max( 1, atoi( tv ) ) );   /* A/B runs */
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
 }
@@ -203,9 +203,15 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
+	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (default: occupancy limit) */
+	{
+		blocksPerCU = value > 0 ? std::min( maxBlocksPerCU, std::max( 1, (int)value ) ) : maxBlocksPerCU;
+		gstack.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
+	}
 	else if (!strcmp( name, "packetShadow" )) packetShadow = value != 0;     /* packet traversal of the shadow rays */
 	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice uses the primary-ray launch */
-	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 2, std::max( 1, (int)value ) );   /* traversal loop (lh2_trace2.inc) */
+	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 4, std::max( 1, (int)value ) );   /* traversal loop: 1, 2 (BVH2), 4 (BVH4) */
+	else if (!strcmp( name, "bvh4" )) { bvh4 = value != 0; if (!bvh4 && traceVersion == 4) traceVersion = 2; }   /* before SetGeometry */
 	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
 	else if (!strcmp( name, "gpuTlas" )) { gpuTlas = value != 0; instancesDirty = true; }
 	else if (!strcmp( name, "plocRadius" )) gpuBvh.radius = std::min( 32, std::max( 1, (int)value ) );
@@ -359,10 +365,27 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 		m.bvhNodes.upload( (const float4*)bvh.nodes.data(), bvh.nodes.size() / 4, stream );
 		m.bvhTris.upload( (const float4*)tris48.data(), tris48.size() / 4, stream );
 		m.nodeCount = (int)(bvh.nodes.size() / 16), m.maxDepth = bvh.maxDepth;
+		if (bvh4) BuildBlas4( m, bvh.nodes.data() );
+	}
+	else if (bvh4)
+	{
+		/* GPU-built BLAS: collapse on the host (one download of the BVH2) */
+		std::vector<float> n2( (size_t)m.nodeCount * 16 );
+		CHK_HIP( hipMemcpyAsync( n2.data(), m.bvhNodes.ptr, n2.size() * sizeof( float ), hipMemcpyDeviceToHost, stream ) );
+		CHK_HIP( hipStreamSynchronize( stream ) );
+		BuildBlas4( m, n2.data() );
 	}
 	CHK_HIP( hipStreamSynchronize( stream ) );   /* the caller's triangle array is borrowed for this call only */
 	geometryDirty = true;
 	coreStats.bvhBuildTime += std::chrono::duration<float>( std::chrono::high_resolution_clock::now() - t0 ).count();
+}
+
+void RenderCore::BuildBlas4( CoreMeshHost& m, const float* nodes2 )
+{
+	std::vector<float> n4;
+	m.depth4 = CollapseBvh4( nodes2, (size_t)m.nodeCount, n4 );
+	m.bvh4Nodes.upload( (const float4*)n4.data(), n4.size() / 4, stream );
+	m.node4Count = (int)(n4.size() / 32);
 }
 
 void RenderCore::SetInstance( int instanceIdx, int meshIdx, const float* M )   /* rendercore.cpp:229-243 */
@@ -378,33 +401,35 @@ void RenderCore::SetInstance( int instanceIdx, int meshIdx, const float* M )   /
 /* scene node array = all BLAS (relocated, device to device) followed by room for the TLAS */
 void RenderCore::ConcatenateBlas( int ni )
 {
-	meshNodeBase.assign( meshes.size(), 0 ), meshTriBase.assign( meshes.size(), 0 );
-	int nodeTotal = 0, triTotal = 0;
-	maxBlasDepth = 0;
+	meshNodeBase.assign( meshes.size(), 0 ), meshTriBase.assign( meshes.size(), 0 ), meshNode4Base.assign( meshes.size(), 0 );
+	int nodeTotal = 0, triTotal = 0, node4Total = 0;
+	maxBlasDepth = 0, maxBlas4Depth = 0;
 	std::vector<float> bounds( std::max<size_t>( meshes.size(), 1 ) * 6, 0.0f );
 	for (size_t mi = 0; mi < meshes.size(); mi++)
 	{
 		const CoreMeshHost& m = *meshes[mi];
-		meshNodeBase[mi] = nodeTotal, meshTriBase[mi] = triTotal;
-		nodeTotal += m.nodeCount, triTotal += m.triCount;
-		maxBlasDepth = std::max( maxBlasDepth, m.maxDepth );
+		meshNodeBase[mi] = nodeTotal, meshTriBase[mi] = triTotal, meshNode4Base[mi] = node4Total;
+		nodeTotal += m.nodeCount, triTotal += m.triCount, node4Total += m.node4Count;
+		maxBlasDepth = std::max( maxBlasDepth, m.maxDepth ), maxBlas4Depth = std::max( maxBlas4Depth, m.depth4 );
 		for (int k = 0; k < 3; k++) bounds[mi * 6 + k] = m.aabbLo[k], bounds[mi * 6 + 3 + k] = m.aabbHi[k];
 		if (m.triCount == 0) bounds[mi * 6] = 1.0f, bounds[mi * 6 + 3] = 0.0f;   /* empty-mesh marker */
 	}
 	tlasCapacity = std::max( 64, 2 * ni + 16 );
 	CHK_HIP( hipStreamSynchronize( stream ) );   /* frames in flight may still read the old arrays */
-	dNodes.free(), dTris.free();
+	dNodes.free(), dTris.free(), dNodes4.free();
 	dNodes.resize( ((size_t)nodeTotal + tlasCapacity) * 4 );
+	if (bvh4) dNodes4.resize( ((size_t)node4Total + tlasCapacity) * 8 );
 	dTris.resize( (size_t)std::max( triTotal, 1 ) * 3 );
 	for (size_t mi = 0; mi < meshes.size(); mi++)
 	{
 		const CoreMeshHost& m = *meshes[mi];
 		GpuBvhBuilder::Relocate( m.bvhNodes.ptr, m.nodeCount, meshNodeBase[mi], (uint32_t)meshTriBase[mi], dNodes.ptr, stream );
+		if (bvh4) GpuBvhBuilder::Relocate4( m.bvh4Nodes.ptr, m.node4Count, meshNode4Base[mi], (uint32_t)meshTriBase[mi], dNodes4.ptr, stream );
 		if (m.triCount) CHK_HIP( hipMemcpyAsync( dTris.ptr + (size_t)meshTriBase[mi] * 3, m.bvhTris.ptr, sizeof( float4 ) * 3 * (size_t)m.triCount, hipMemcpyDeviceToDevice, stream ) );
 	}
 	dMeshBounds.upload( bounds.data(), bounds.size(), stream );
 	CHK_HIP( hipStreamSynchronize( stream ) );
-	blasNodeCount = nodeTotal, blasTriCount = triTotal;
+	blasNodeCount = nodeTotal, blasTriCount = triTotal, blasNode4Count = node4Total;
 	geometryDirty = false;
 }
 
@@ -440,7 +465,8 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		di[i].inv0 = make_float4( in.inv[0], in.inv[1], in.inv[2], in.inv[3] );
 		di[i].inv1 = make_float4( in.inv[4], in.inv[5], in.inv[6], in.inv[7] );
 		di[i].inv2 = make_float4( in.inv[8], in.inv[9], in.inv[10], in.inv[11] );
-		di[i].root = meshNodeBase[in.mesh], di[i].triBase = meshTriBase[in.mesh], di[i].mesh = in.mesh, di[i].pad = 0;
+		di[i].root = meshNodeBase[in.mesh], di[i].triBase = meshTriBase[in.mesh], di[i].mesh = in.mesh;
+		di[i].root4 = bvh4 ? meshNode4Base[in.mesh] : 0;
 		desc[i].triangles = meshes[in.mesh]->shadeTris.ptr;
 		desc[i].A = { in.inv[0], in.inv[1], in.inv[2], in.inv[3] };
 		desc[i].B = { in.inv[4], in.inv[5], in.inv[6], in.inv[7] };
@@ -461,7 +487,7 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		CHK_HIP( hipMemcpyAsync( dInstMesh.ptr, meshIds, nRec * 4, hipMemcpyHostToDevice, stream ) );
 		GpuTlasArgs ta;
 		ta.T = dInstT.ptr, ta.instMesh = dInstMesh.ptr, ta.meshBounds = dMeshBounds.ptr, ta.count = ni;
-		ta.nodeBase = blasNodeCount, ta.nodes = dNodes.ptr, ta.maxBlasDepth = maxBlasDepth;
+		ta.nodeBase = blasNodeCount, ta.nodes = dNodes.ptr, ta.maxBlasDepth = StackDepthBound();
 		ta.sceneError = dSceneError.ptr, ta.tlasDepth = dTlasDepth.ptr;
 		gpuBvh.BuildTlas( ta, stream );
 		tlasOnDevice = true;
@@ -517,10 +543,12 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		if (tlas.nodes.size() * sizeof( float ) > need - offNodes) FatalError( "TLAS staging overflow" );
 		memcpy( sb + offNodes, tlas.nodes.data(), tlas.nodes.size() * sizeof( float ) );
 		CHK_HIP( hipMemcpyAsync( dNodes.ptr + (size_t)blasNodeCount * 4, sb + offNodes, tlas.nodes.size() * sizeof( float ), hipMemcpyHostToDevice, stream ) );
-		sceneMaxDepth = tlas.maxDepth + maxBlasDepth;
+		sceneMaxDepth = tlas.maxDepth + StackDepthBound();
 		tlasOnDevice = false;
 		if (sceneMaxDepth >= LH2_STACK_TOTAL - 1) FatalError( "BVH depth %d exceeds the traversal stack (%d)", sceneMaxDepth, LH2_STACK_TOTAL );
 	}
+	/* the TLAS in the BVH4 array: its BVH2 nodes as two-child BVH4 nodes (one short launch) */
+	if (bvh4) GpuBvhBuilder::TlasToBvh4( dNodes.ptr, blasNodeCount, tlasCapacity, blasNode4Count, dNodes4.ptr, stream );
 	CHK_HIP( hipEventRecord( evStage[slot], stream ) );
 	instancesDirty = false;
 }
@@ -545,6 +573,7 @@ SceneDev RenderCore::MakeSceneDev() const
 	s.argb32 = dArgb32.ptr, s.nrm32 = dNrm32.ptr;
 	s.argb32Count = (uint32_t)dArgb32.count, s.nrm32Count = (uint32_t)dNrm32.count;
 	s.tlasRoot = tlasRoot, s.instCount = (int)instances.size();
+	s.nodes4 = dNodes4.ptr, s.tlasRoot4 = blasNode4Count;
 	s.instDesc = dInstDesc.ptr, s.materials = dMaterials.ptr;
 	s.areaLights = dArea.ptr, s.pointLights = dPoint.ptr, s.spotLights = dSpot.ptr, s.dirLights = dDir.ptr;
 	s.nArea = nArea, s.nPoint = nPoint, s.nSpot = nSpot, s.nDir = nDir;
@@ -828,6 +857,11 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 	DevBuf<uint32_t> cursors;
 	cursors.resize( (size_t)std::max( 1, iterations ) * LH2_CURSOR_WORDS );
 	CHK_HIP( hipMemsetAsync( cursors.ptr, 0, sizeof( uint32_t ) * (size_t)std::max( 1, iterations ) * LH2_CURSOR_WORDS, stream ) );
+#ifdef LH2_TRACE_STATS
+	DevBuf<unsigned long long> tstats;
+	tstats.resize( LH2_TSTAT_N );
+	CHK_HIP( hipMemsetAsync( tstats.ptr, 0, sizeof( unsigned long long ) * LH2_TSTAT_N, stream ) );
+#endif
 	/* each launch timed by its own dispatch-recorded start / stop events: msOut is the mean kernel
 	   duration, launch gaps excluded (as rocprofv3 --kernel-trace reports it) */
 	std::vector<hipEvent_t> ev( 2 * (size_t)std::max( 1, iterations ) );
@@ -841,9 +875,21 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 		/* unitCoherent: trace as the frame traces its (tiled) primary rays */
 		ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
 		ta.packet = unitCoherent && UsePackets();
+#ifdef LH2_TRACE_STATS
+		ta.stats = tstats.ptr;
+#endif
 		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), { ev[2 * i], ev[2 * i + 1] }, stream );
 	}
 	CHK_HIP( hipStreamSynchronize( stream ) );
+#ifdef LH2_TRACE_STATS
+	{
+		unsigned long long h[LH2_TSTAT_N];
+		CHK_HIP( hipMemcpy( h, tstats.ptr, sizeof( h ), hipMemcpyDeviceToHost ) );
+		fprintf( stderr, "LH2_TRACE_STATS {\"rays\": %d, \"launches\": %d, \"c\": [", n, iterations );
+		for (int i = 0; i < LH2_TSTAT_N; i++) fprintf( stderr, "%s%llu", i ? ", " : "", h[i] );
+		fprintf( stderr, "]}\n" );
+	}
+#endif
 	double total = 0;
 	for (int i = 0; i < iterations; i++) { float t = 0; CHK_HIP( hipEventElapsedTime( &t, ev[2 * i], ev[2 * i + 1] ) ); total += t; }
 	if (msOut) *msOut = (float)(total / std::max( 1, iterations ));

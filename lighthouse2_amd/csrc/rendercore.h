@@ -48,6 +48,8 @@ struct CoreMeshHost   /* RenderCore always copies what it needs (rendercore.h:57
 	DevBuf<float4> shadeTris;            /* CoreTri4[] in original order, for shading */
 	DevBuf<float4> bvhNodes, bvhTris;    /* BLAS with mesh-local refs; relocated into the scene arrays by UpdateToplevel */
 	int nodeCount = 0, maxDepth = 0;
+	DevBuf<float4> bvh4Nodes;            /* the same BLAS collapsed to BVH4 (CollapseBvh4), mesh-local refs */
+	int node4Count = 0, depth4 = 0;
 };
 
 struct CoreInstanceHost { int mesh; float T[16]; float inv[16]; };
@@ -104,23 +106,28 @@ public:
 private:
 	void EnsureBuffers();
 	void ConcatenateBlas( int instanceCount );
+	void BuildBlas4( CoreMeshHost& m, const float* nodes2 );
 	void CheckSceneError();
 	bool UsePackets() const;
 	SceneDev MakeSceneDev() const;
 	int TraceGrid() const { return smCount * blocksPerCU; }
 
-	int device = 0, smCount = 256, blocksPerCU = 5;
+	int device = 0, smCount = 256, blocksPerCU = 5, maxBlocksPerCU = 5;
 	bool initialized = false;
 	/* scene */
 	std::vector<CoreMeshHost*> meshes;
 	std::vector<CoreInstanceHost> instances;
 	bool geometryDirty = true, instancesDirty = true;
 	DevBuf<float4> dNodes, dTris;
+	DevBuf<float4> dNodes4;              /* BVH4: all BLAS (relocated), then the TLAS as two-child nodes */
 	DevBuf<uint8_t> dInst;                 /* DevInstance[] */
 	DevBuf<lh2_CoreInstanceDesc> dInstDesc;
 	int tlasRoot = 0, blasNodeCount = 0, blasTriCount = 0, sceneMaxDepth = 0;
-	std::vector<int> meshNodeBase, meshTriBase;
+	std::vector<int> meshNodeBase, meshTriBase, meshNode4Base;
 	int tlasCapacity = 0, maxBlasDepth = 0;
+	int blasNode4Count = 0, maxBlas4Depth = 0;
+	int bvh4 = 1;                        /* build BVH4 copies of the BLAS (traceVersion 4 needs them) */
+	int StackDepthBound() const { return bvh4 ? std::max( maxBlasDepth, 3 * maxBlas4Depth ) : maxBlasDepth; }
 	bool tlasOnDevice = false;           /* TLAS of the last UpdateToplevel built by the GPU (depth in dTlasDepth) */
 	GpuBvhBuilder gpuBvh;
 	DevBuf<float> dMeshBounds;           /* 6 per mesh */
@@ -171,9 +178,13 @@ private:
 	hipEvent_t fromTrace[LH2_MAX_BOUNCES + 1] = {}, fromShade[LH2_MAX_BOUNCES + 1] = {}, fromShadowB[LH2_MAX_BOUNCES + 1] = {}, fromShadow = nullptr;
 	uint32_t* activeLog = nullptr;     /* pinned: active paths after each bounce */
 	int tiledRays = 1;
-	int refillPrimary = 48, refillOther = 32, leafBatch = 16, leafBatchPrimary = 8;   /* v2 sweep: profiles/r01b_refill_sweep.jsonl */
-	int bvhMaxLeaf = 2;
-	int traceVersion = 2;
+	/* BVH4 per-ray traversal, 1-triangle leaves, no leaf parking, refill at 48 idle lanes: the best of
+	   the sweeps on the config-2 frame (profiles/r01c_sweep_bvh4.jsonl, r01c_ab_bvh4_settings.jsonl:
+	   1.89 ms vs 1.94 for BVH2 with 2-triangle leaves); config 3 (room) runs 4 % faster with
+	   bvhMaxLeaf 2 / leafBatch 16, config 5 2 % slower */
+	int refillPrimary = 48, refillOther = 48, leafBatch = 0, leafBatchPrimary = 8;
+	int bvhMaxLeaf = 1;
+	int traceVersion = 4;
 	int unitCoherent = 0;
 	int packetPrimary = -1;              /* wave-uniform packet traversal for 8x8-tiled primary rays (-1: by scene size) */
 	float packetMaxMB = 16.0f;

@@ -288,3 +288,54 @@ def test_packet_shadow_frame_parity(fresh_core):
     assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
     ag, ao = fresh_core.accumulator(), o.accumulator()
     assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+
+
+@pytest.mark.parametrize("version,leaf_batch,max_leaf", [(1, 0, 2), (1, 16, 2), (2, 0, 2), (2, 16, 1), (4, 0, 1), (4, 16, 2), (4, 8, 4)])
+def test_traversal_variants_bitexact(fresh_core, version, leaf_batch, max_leaf):
+    """Every per-ray traversal loop (trace_stream, lh2_trace2.inc over the BVH2 and over the BVH4
+    collapse), with and without leaf parking, over trees of different leaf sizes, returns the
+    oracle's hit records and occlusion bits: hits do not depend on the tree or the visiting order."""
+    fresh_core.setting("bvhMaxLeaf", max_leaf)
+    fresh_core.setting("traceVersion", version)
+    fresh_core.setting("leafBatch", leaf_batch)
+    sc = scene.instanced_scene(meshes=4, tris_per_mesh=4000, width=64, height=36, grid=2, spacing=10.0)
+    scene.animate_instances(sc, 1)
+    o = _load_both(fresh_core, sc, 64, 36)
+    O4, D4 = _random_rays(30001, 11, radius=30.0)
+    hg = fresh_core.trace_closest(O4, D4)
+    ho = o.trace_closest(O4, D4)
+    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.05
+    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+    D4[:, 3] = np.random.default_rng(12).uniform(1.0, 40.0, len(D4)).astype(np.float32)
+    assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
+
+
+def test_bvh4_deep_stack(fresh_core):
+    """A deep BLAS (triangles shrinking geometrically along a line: a chain-like SAH tree) next to the
+    random cloud: BVH4 nodes push up to three children per level, the LDS part of the traversal
+    stack spills into the global part, and hits stay exact."""
+    k = np.arange(120, dtype=np.float32)
+    x = (6.0 * 0.93 ** k).astype(np.float32)
+    s_ = (0.02 * 0.93 ** k).astype(np.float32)
+    z0 = np.zeros_like(x)
+    v0 = np.stack([x, -s_, z0], 1)
+    v1 = np.stack([x + s_, s_, z0], 1)
+    v2 = np.stack([x - s_, s_, s_], 1)
+    chain = abi.tris_from_vertices(v0, v1, v2, 0)
+    sc = scene.config2_scene(n=5000, width=64, height=36)
+    sc.meshes.append(chain)
+    sc.instances.append((1, np.eye(4, dtype=np.float32)))
+    fresh_core.setting("traceVersion", 4)
+    o = _load_both(fresh_core, sc, 64, 36)
+    info = fresh_core.scene_info()
+    assert info["max_depth"] >= 14, info
+    O4, D4 = _random_rays(20001, 13)
+    # half of the rays aimed at chain triangles (their centroids), from random directions
+    rng = np.random.default_rng(14)
+    j = rng.integers(0, len(x), 10000)
+    tgt = ((v0[j] + v1[j] + v2[j]) / 3).astype(np.float32)
+    d = tgt - O4[:10000, :3]
+    D4[:10000, :3] = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    hg, ho = fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4)
+    assert (ho[:10000, 2] == 1).mean() > 0.2   # instance 1 (the chain) is hit
+    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]

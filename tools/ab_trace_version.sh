@@ -1,12 +1,13 @@
-set -e
-mkdir -p gpurun_out/ab
-export LH2_TRACE_VERSION=2
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab/tests_v2.log 2>&1
-for v in 1 2 1 2; do
-  LH2_TRACE_VERSION=$v timeout -k 10 120 python tools/trace_kernel_bench.py --iters 20 > gpurun_out/ab/kb_v$v.json 2>/dev/null
-  cat gpurun_out/ab/kb_v$v.json >> gpurun_out/ab/kb_all.txt; echo " v$v" >> gpurun_out/ab/kb_all.txt
+#!/bin/bash
+# GPU suite with a forced traversal version, then the closest-hit microbenchmark for versions 2 and 4.
+# usage (on the GPU box): bash tools/ab_trace_version.sh   -> gpurun_out/tv/
+set -uo pipefail
+ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
+OUT="$ROOT/gpurun_out/tv"; mkdir -p "$OUT"; cd "$ROOT"
+LH2_TRACE_VERSION=4 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/gpu_tests_v4.log" 2>&1 || exit 1
+for rep in 1 2; do
+  for v in 2 4; do
+    timeout -k 10 120 python3 tools/trace_kernel_bench.py --set both --setting traceVersion=$v > "$OUT/kb_v${v}_$rep.json" 2>>"$OUT/err.log" || exit 1
+  done
 done
-for v in 1 2; do
-  LH2_TRACE_VERSION=$v timeout -k 10 200 python bench.py --steps 20 --no-cpu-baseline > gpurun_out/ab/bench_v$v.json 2>/dev/null
-done
-echo ok
+echo tv done

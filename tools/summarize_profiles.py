@@ -3,7 +3,7 @@ under profiles/ for one round:
 
   profiles/<tag>_rocprof_kernel_stats.csv   rocprofv3 --kernel-trace --stats of bench.py
   profiles/<tag>_bench.json                 the bench.py JSON line of the same call
-  profiles/<tag>_pmc_traffic.json           HBM bytes per k_trace_closest<true, 2> launch (the frame's
+  profiles/<tag>_pmc_traffic.json           HBM bytes per roofline-kernel launch (the frame's
                                             diffuse bounce rays, bench.py's roofline kernel):
                                             2 x FETCH_SIZE (gfx950 calibration, MI355X_MICROARCH.md
                                             §HBM) + WRITE_SIZE, each from its own --pmc pass
@@ -35,6 +35,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="r01")
     ap.add_argument("--src", default=str(ROOT / "gpurun_out" / "prof"))
+    ap.add_argument("--kernel", default="k_trace_closest<false, 4>", help="bench.py's roofline kernel (rocprof name)")
     a = ap.parse_args()
     src = pathlib.Path(a.src)
     dst = ROOT / "profiles"
@@ -42,7 +43,7 @@ def main():
     bench = json.loads((src / "bench.json").read_text().strip().splitlines()[-1])
     (dst / f"{a.tag}_bench.json").write_text(json.dumps(bench, indent=1) + "\n")
 
-    kernel = "k_trace_closest<true, 2>"      # per-ray traversal (the packet kernel is k_trace_closest_packet)
+    kernel = a.kernel      # per-ray traversal (the packet kernel is k_trace_closest_packet)
     fetch, fd = _pmc(src / "pmc_fetch" / "run_counter_collection.csv", kernel)
     write, wd = _pmc(src / "pmc_write" / "run_counter_collection.csv", kernel)
     # kernel-trace durations of the roofline launches in the profiled bench run (the last kernel_iters)
