@@ -76,6 +76,14 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	int version;                                      /* traversal loop: 1 (trace_stream), 2 (lh2_trace2.inc), 4 (BVH4, lh2_trace4.inc) */
 	int packet;                                       /* 1: wave-uniform packet traversal (coherent rays, closest hit) */
 	unsigned long long* stats;                        /* LH2_TRACE_STATS builds: LH2_TSTAT_N per-launch counters */
+	/* tail hand-off (lh2_trace2.inc): once the queue is exhausted, a wave with fewer than tailLanes
+	   active rays appends them to tailOut / tailOutUV {idx, bits(tbest), tri, inst} {u, v} - segment
+	   blockIdx % LH2_SEGS, counters tailCounts (LH2_SEGCOUNT_STRIDE apart), tailStride records per
+	   segment - and exits; a second launch of the same kernel (tail_args) continues them densely
+	   from those records (tailIn) with the closest hit found so far as tmax, which gives the ray the
+	   same closest hit (the hit does not depend on the visiting order) */
+	uint4* tailOut; float2* tailOutUV; uint32_t* tailCounts; uint32_t tailStride, tailLanes;
+	const uint4* tailIn; const float2* tailInUV;
 };
 /* traversal-loop statistics (diagnostic builds with -DLH2_TRACE_STATS; tools/trace_stats.py):
    wave-iterations, active-lane sum, leaf-phase iterations / lanes, walk iterations / lanes,
@@ -119,7 +127,10 @@ void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, co
 #define LH2_SEGS LH2_CHUNKS
 #define LH2_SEGCOUNT_STRIDE 32
 #define LH2_CURSOR_STRIDE 32
-#define LH2_CURSOR_WORDS (LH2_CHUNKS * LH2_CURSOR_STRIDE)   /* per trace launch */
+/* per trace launch: the segment heads, the heads of its tail launch, the tail segment counts */
+#define LH2_CURSOR_WORDS (3 * LH2_CHUNKS * LH2_CURSOR_STRIDE)
+#define LH2_TAIL_CURSOR (LH2_CHUNKS * LH2_CURSOR_STRIDE)
+#define LH2_TAIL_COUNT (2 * LH2_CHUNKS * LH2_CURSOR_STRIDE)
 #define LH2_MAX_BOUNCES 64                                   /* RenderCore_PrimeRef MAXPATHLENGTH (core_settings.h:25) */
 #define LH2_CURSOR_SLOTS (2 * LH2_MAX_BOUNCES + 4)           /* launches per frame: [L] bounce L, [64 + L] shadow after bounce L, [130] shadow */
 #define LH2_SHADOW_SLOT (2 * LH2_MAX_BOUNCES + 2)

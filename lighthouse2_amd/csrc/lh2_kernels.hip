@@ -53,8 +53,8 @@ static_assert( sizeof( ((Counters*)0)->segActive ) == LH2_SEGS * LH2_SEGCOUNT_ST
 LH2_DEV void seg_range( const TraceArgs& a, uint32_t c, uint32_t& lo, uint32_t& hi )
 {
 	c = __builtin_amdgcn_readfirstlane( c );
-	lo = c * a.segStride;
 	uint32_t n;
+	lo = c * a.segStride;
 	if (a.segCounts) n = a.segCounts[c * LH2_SEGCOUNT_STRIDE];
 	else n = a.countFixed > lo ? min( a.countFixed - lo, a.segStride ) : 0u;
 	lo = __builtin_amdgcn_readfirstlane( lo );
@@ -1700,6 +1700,17 @@ __global__ void k_pack_rows( const float4* __restrict__ acc, float4* __restrict_
 /* Launches go through hipExtLaunchKernelGGL: its start / stop events are recorded by the kernel's own
    dispatch packet, where a hipEventRecord between two launches costs a barrier packet and ~5 us of
    idle GPU per event (rocprofv3 kernel trace of the config-2 frame); null events: a plain launch. */
+/* the tail launch of a trace launch: same rays, hits and outputs; rays from the hand-off records */
+static TraceArgs tail_args( const TraceArgs& a )
+{
+	TraceArgs t = a;
+	t.tailIn = a.tailOut, t.tailInUV = a.tailOutUV;
+	t.tailOut = nullptr, t.tailOutUV = nullptr, t.tailLanes = 0;
+	t.segCounts = a.tailCounts, t.segStride = a.tailStride, t.countFixed = 0;
+	t.cursor = a.cursor + LH2_TAIL_CURSOR;
+	return t;
+}
+
 #define LH2_LAUNCH( kernel, grid, block, st, ev, ... ) \
 	hipExtLaunchKernelGGL( kernel, dim3( grid ), dim3( block ), 0, st, (ev).start, (ev).stop, 0, __VA_ARGS__ )
 
@@ -1721,15 +1732,27 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
 	/* incoherent rays: parked leaves (leafBatch > 0); traversal loop version 1 or 2 (lh2_trace2.inc);
 	   coherent primary rays: packet traversal (lh2_trace_packet.inc) */
 	if (a->packet) LH2_LAUNCH( k_trace_closest_packet, grid, 256, st, ev, *s, *a );
-	else if (a->version == 4 && s->nodes4)
-	{
-		if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 4>), grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( (k_trace_closest<false, 4>), grid, 256, st, ev, *s, *a );
-	}
 	else if (a->version >= 2)
 	{
-		if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 2>), grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( (k_trace_closest<false, 2>), grid, 256, st, ev, *s, *a );
+		/* with a tail hand-off: the main launch, then the tail launch over the handed-off rays;
+		   the start event goes with the first, the stop event with the second */
+		const bool tail = a->tailOut && a->tailLanes;
+		TraceArgs t = tail_args( *a );
+		const LaunchEvents e1 = { ev.start, tail ? nullptr : ev.stop }, e2 = { nullptr, ev.stop };
+		if (a->version == 4 && s->nodes4)
+		{
+			if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 4>), grid, 256, st, e1, *s, *a );
+			else LH2_LAUNCH( (k_trace_closest<false, 4>), grid, 256, st, e1, *s, *a );
+			if (tail && a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 4>), grid, 256, st, e2, *s, t );
+			else if (tail) LH2_LAUNCH( (k_trace_closest<false, 4>), grid, 256, st, e2, *s, t );
+		}
+		else
+		{
+			if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 2>), grid, 256, st, e1, *s, *a );
+			else LH2_LAUNCH( (k_trace_closest<false, 2>), grid, 256, st, e1, *s, *a );
+			if (tail && a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 2>), grid, 256, st, e2, *s, t );
+			else if (tail) LH2_LAUNCH( (k_trace_closest<false, 2>), grid, 256, st, e2, *s, t );
+		}
 	}
 	else
 	{
@@ -1744,15 +1767,21 @@ void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int 
 		if (fused) LH2_LAUNCH( k_trace_any_packet<1>, grid, 256, st, ev, *s, *a );
 		else LH2_LAUNCH( k_trace_any_packet<0>, grid, 256, st, ev, *s, *a );
 	}
-	else if (a->version == 4 && s->nodes4)
-	{
-		if (fused) LH2_LAUNCH( (k_trace_any<1, 4>), grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( (k_trace_any<0, 4>), grid, 256, st, ev, *s, *a );
-	}
 	else if (a->version >= 2)
 	{
-		if (fused) LH2_LAUNCH( (k_trace_any<1, 2>), grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( (k_trace_any<0, 2>), grid, 256, st, ev, *s, *a );
+		const bool tail = a->tailOut && a->tailLanes;
+		TraceArgs t = tail_args( *a );
+		const LaunchEvents e1 = { ev.start, tail ? nullptr : ev.stop }, e2 = { nullptr, ev.stop };
+		const bool v4 = a->version == 4 && s->nodes4;
+		for (int pass = 0; pass < (tail ? 2 : 1); pass++)
+		{
+			const TraceArgs& x = pass ? t : *a;
+			const LaunchEvents& e = pass ? e2 : e1;
+			if (v4 && fused) LH2_LAUNCH( (k_trace_any<1, 4>), grid, 256, st, e, *s, x );
+			else if (v4) LH2_LAUNCH( (k_trace_any<0, 4>), grid, 256, st, e, *s, x );
+			else if (fused) LH2_LAUNCH( (k_trace_any<1, 2>), grid, 256, st, e, *s, x );
+			else LH2_LAUNCH( (k_trace_any<0, 2>), grid, 256, st, e, *s, x );
+		}
 	}
 	else
 	{

@@ -203,6 +203,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
+	else if (!strcmp( name, "tailLanes" )) tailLanes = std::min( 64, std::max( 0, (int)value ) );   /* traversal tail hand-off (0: off) */
 	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (default: occupancy limit) */
 	{
 		blocksPerCU = value > 0 ? std::min( maxBlocksPerCU, std::max( 1, (int)value ) ) : maxBlocksPerCU;
@@ -378,6 +379,17 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 	CHK_HIP( hipStreamSynchronize( stream ) );   /* the caller's triangle array is borrowed for this call only */
 	geometryDirty = true;
 	coreStats.bvhBuildTime += std::chrono::duration<float>( std::chrono::high_resolution_clock::now() - t0 ).count();
+}
+
+void RenderCore::SetTail( TraceArgs& ta )
+{
+	if (!tailLanes || ta.packet) return;
+	const size_t threads = (size_t)TraceGrid() * 256;
+	if (tailRec.count < threads) tailRec.resize( threads ), tailUV.resize( threads );
+	ta.tailOut = tailRec.ptr, ta.tailOutUV = tailUV.ptr;
+	ta.tailCounts = ta.cursor + LH2_TAIL_COUNT;
+	ta.tailStride = (uint32_t)(((TraceGrid() + LH2_SEGS - 1) / LH2_SEGS) * 256);   /* one record per thread of the segment's blocks */
+	ta.tailLanes = (uint32_t)tailLanes;
 }
 
 void RenderCore::BuildBlas4( CoreMeshHost& m, const float* nodes2 )
@@ -640,6 +652,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.packet = pathLength == 1 && tiledRays && UsePackets();
 		ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
 		ta.hits = hits.ptr, ta.gstack = gstack.ptr;
+		SetTail( ta );
 		lh2_launch_trace_closest( &sd, &ta, grid, { nullptr, evTrace[2 * pathLength + 1] }, stream );
 		fromTrace[pathLength] = prevStop, prevStop = evTrace[2 * pathLength + 1];
 		ShadeParams sp{};
@@ -666,6 +679,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 			ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
 			ta.packet = packetShadow;
+			SetTail( ta );
 			lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, evShadowB[2 * pathLength + 1] }, stream );
 			fromShadowB[pathLength] = prevStop, prevStop = evShadowB[2 * pathLength + 1];
 		}
@@ -689,6 +703,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.segCounts = c->segShadow, ta.segStride = shadowStride, ta.cursor = fetchCursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
 		ta.packet = packetShadow;
+		SetTail( ta );
 		lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, evShadow[1] }, stream );
 		fromShadow = prevStop;
 	}
@@ -819,6 +834,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
 	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
 	ta.packet = unitCoherent && UsePackets();
+	SetTail( ta );
 	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), {}, stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -840,6 +856,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	ta.version = traceVersion;
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 	ta.packet = unitCoherent && packetShadow;
+	SetTail( ta );
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, {}, stream );
 	std::vector<uint32_t> tmp( words );
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
@@ -862,6 +879,10 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 	tstats.resize( LH2_TSTAT_N );
 	CHK_HIP( hipMemsetAsync( tstats.ptr, 0, sizeof( unsigned long long ) * LH2_TSTAT_N, stream ) );
 #endif
+#ifdef LH2_TRACE_TIMES
+	DevBuf<unsigned long long> ttimes;
+	ttimes.resize( (size_t)TraceGrid() * 4 * 4 );
+#endif
 	/* each launch timed by its own dispatch-recorded start / stop events: msOut is the mean kernel
 	   duration, launch gaps excluded (as rocprofv3 --kernel-trace reports it) */
 	std::vector<hipEvent_t> ev( 2 * (size_t)std::max( 1, iterations ) );
@@ -878,9 +899,22 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 #ifdef LH2_TRACE_STATS
 		ta.stats = tstats.ptr;
 #endif
+#ifdef LH2_TRACE_TIMES
+		ta.stats = ttimes.ptr;
+#endif
+		SetTail( ta );
 		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), { ev[2 * i], ev[2 * i + 1] }, stream );
 	}
 	CHK_HIP( hipStreamSynchronize( stream ) );
+#ifdef LH2_TRACE_TIMES
+	{
+		/* the last launch's per-wave times: tools/trace_times.py reads this binary dump */
+		std::vector<unsigned long long> h( ttimes.count );
+		CHK_HIP( hipMemcpy( h.data(), ttimes.ptr, h.size() * 8, hipMemcpyDeviceToHost ) );
+		if (const char* path = getenv( "LH2_TRACE_TIMES_OUT" ))
+			if (FILE* f = fopen( path, "wb" )) { fwrite( h.data(), 8, h.size(), f ); fclose( f ); }
+	}
+#endif
 #ifdef LH2_TRACE_STATS
 	{
 		unsigned long long h[LH2_TSTAT_N];

@@ -107,6 +107,7 @@ private:
 	void EnsureBuffers();
 	void ConcatenateBlas( int instanceCount );
 	void BuildBlas4( CoreMeshHost& m, const float* nodes2 );
+	void SetTail( TraceArgs& ta );       /* tail hand-off buffers of a trace launch (ta.cursor set) */
 	void CheckSceneError();
 	bool UsePackets() const;
 	SceneDev MakeSceneDev() const;
@@ -165,6 +166,9 @@ private:
 	DevBuf<int> gstack;
 	DevBuf<Counters> counters;
 	DevBuf<uint32_t> fetchCursors;    /* LH2_CURSOR_SLOTS x LH2_CURSOR_WORDS work-queue heads */
+	DevBuf<uint4> tailRec;             /* tail hand-off records, one per trace thread (TraceArgs::tailOut) */
+	DevBuf<float2> tailUV;
+	int tailLanes = 0;                   /* hand a dry wave's rays on when fewer are active (0: off; restarting them costs more than the tail, profiles/r01c_sweep_tail.txt) */
 	DevBuf<uint32_t> rayLog;
 	FrameStats* hostStats = nullptr;     /* pinned */
 	bool statsPending = false;

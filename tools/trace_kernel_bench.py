@@ -31,10 +31,10 @@ def main():
     ap.add_argument("--tris", type=int, default=100_000)
     ap.add_argument("--set", default="both")
     # defaults = the core's (RenderCore refillOther / refillPrimary / leafBatch / leafBatchPrimary)
-    ap.add_argument("--refill", type=int, default=32)
-    ap.add_argument("--refill-primary", type=int, default=48)
-    ap.add_argument("--leaf-batch", type=int, default=16)
-    ap.add_argument("--leaf-batch-primary", type=int, default=8)
+    ap.add_argument("--refill", type=int, default=None, help="default: the core's setting")
+    ap.add_argument("--refill-primary", type=int, default=None)
+    ap.add_argument("--leaf-batch", type=int, default=None)
+    ap.add_argument("--leaf-batch-primary", type=int, default=None)
     ap.add_argument("--no-frame-launch", action="store_true",
                     help="do not set unitCoherent=1 for the primary set (the frame's launch: packets when auto-selected)")
     ap.add_argument("--pre-setting", action="append", default=[], help="name=value set before loading (BVH build)")
@@ -93,8 +93,12 @@ def main():
         if args.set not in ("both", name) and not (args.set == "bounce_sorted" and name == "bounce_sorted"):
             continue
         n = len(o)
-        core.setting("refill", args.refill_primary if name == "primary" else args.refill)
-        core.setting("leafBatch", args.leaf_batch_primary if name == "primary" else args.leaf_batch)
+        rf = args.refill_primary if name == "primary" else args.refill
+        lb = args.leaf_batch_primary if name == "primary" else args.leaf_batch
+        if rf is not None:
+            core.setting("refillPrimary" if name == "primary" else "refill", rf)
+        if lb is not None:
+            core.setting("leafBatchPrimary" if name == "primary" else "leafBatch", lb)
         if not args.no_frame_launch:
             core.setting("unitCoherent", 1 if name == "primary" else 0)
         ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
