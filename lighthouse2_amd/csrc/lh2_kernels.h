@@ -17,6 +17,7 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	   y0 + (lr / band) * bandStride + lr % band  (contiguous tile: band = rows) */
 	int y0, band, bandStride, tileRows;
 	int tiled;   /* store rays in 8x8 pixel blocks per wave (coherent traversal); 0 = row-major */
+	int slotBase;  /* this launch writes slots [slotBase, slotBase + jobCount) of the tile, at 0.. (path groups) */
 	int primeRef;  /* RenderCore_PrimeRef camera: uniform random numbers, no distortion (camera.h:57-60) */
 };
 
@@ -96,10 +97,13 @@ struct LaunchEvents { hipEvent_t start, stop; };
 
 /* where k_finalize delivers the frame's statistics: the device counters / ray-count log / scene error,
    and the host's pinned FrameStats fields (hostCounters null: nothing is delivered) */
+#define LH2_FS_GROUPS 4
 struct FrameStatsDev
 {
-	const Counters* counters; const uint32_t* rayLog; const int* sceneError;
-	Counters* hostCounters; uint32_t* hostRayCount; int* hostSceneError;
+	int groups;
+	const Counters* counters[LH2_FS_GROUPS]; const uint32_t* rayLog[LH2_FS_GROUPS];
+	Counters* hostCounters[LH2_FS_GROUPS]; uint32_t* hostRayCount[LH2_FS_GROUPS];
+	const int* sceneError; int* hostSceneError;
 };
 
 extern "C" {

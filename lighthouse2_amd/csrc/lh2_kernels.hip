@@ -135,8 +135,9 @@ LH2_DEV v3 RandomPointOnLens( const float r0, float r1, const v3 pos, const floa
 __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const uint8_t* __restrict__ bn, float4* __restrict__ rayO,
 	float4* __restrict__ rayD, float4* __restrict__ T4, float4* __restrict__ Q4, const int jobCount )
 {
-	const int slot = threadIdx.x + blockIdx.x * blockDim.x;
-	if (slot >= jobCount) return;
+	const int local = threadIdx.x + blockIdx.x * blockDim.x;
+	if (local >= jobCount) return;
+	const int slot = p.slotBase + local;
 	/* slot -> (sample, tile row, x) -> global jobIndex = x + (y + s * h) * w, as camera.h:48-53 */
 	const uint32_t w = (uint32_t)p.w, h = (uint32_t)p.h;
 	const uint32_t tilePix = (uint32_t)p.tileRows * w;
@@ -192,10 +193,11 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 	}
 	const v3 posOnLens = RandomPointOnLens( r2, r3, mk3( p.pos.x, p.pos.y, p.pos.z ), p.aperture, right, up );
 	const v3 rayDir = normalize3( sub3( posOnPixel, posOnLens ) );
-	rayO[slot] = make_float4( posOnLens.x, posOnLens.y, posOnLens.z, p.geometryEpsilon );
-	rayD[slot] = make_float4( rayDir.x, rayDir.y, rayDir.z, 1e34f );
-	T4[slot] = make_float4( 1, 1, 1, bitsf( ((x + (y + (sampleIndex - (uint32_t)p.pass) * h) * w) << 8) + 1 /* S_SPECULAR */ ) );
-	Q4[slot] = make_float4( 1, 0, 0, 0 );
+	/* stored at the launch's own index (a path group's buffers hold its slots only) */
+	rayO[local] = make_float4( posOnLens.x, posOnLens.y, posOnLens.z, p.geometryEpsilon );
+	rayD[local] = make_float4( rayDir.x, rayDir.y, rayDir.z, 1e34f );
+	T4[local] = make_float4( 1, 1, 1, bitsf( ((x + (y + (sampleIndex - (uint32_t)p.pass) * h) * w) << 8) + 1 /* S_SPECULAR */ ) );
+	Q4[local] = make_float4( 1, 0, 0, 0 );
 }
 
 /* =====================================================================================
@@ -1667,16 +1669,19 @@ __global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLen
 __global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale, const FrameStatsDev fs )
 {
 	const int i = threadIdx.x + blockIdx.x * blockDim.x;
-	if (blockIdx.x == 0 && fs.hostCounters)
+	if (blockIdx.x == 0 && fs.groups > 0)
 	{
-		/* block 0 also hands the frame's counters, ray-count log and scene error to the host's pinned
-		   FrameStats (system-scope stores: no device-to-host copy launches at the end of the frame) */
-		const uint32_t* src = (const uint32_t*)fs.counters;
-		uint32_t* dst = (uint32_t*)fs.hostCounters;
-		for (int k = threadIdx.x; k < (int)(sizeof( Counters ) / 4); k += blockDim.x)
-			__hip_atomic_store( dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
-		for (int k = threadIdx.x; k < LH2_MAX_BOUNCES; k += blockDim.x)
-			__hip_atomic_store( fs.hostRayCount + k, fs.rayLog[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+		/* block 0 also hands every path group's counters and ray-count log and the scene error to the
+		   host's pinned FrameStats (system-scope stores: no device-to-host copy launches at the end) */
+		for (int g = 0; g < fs.groups; g++)
+		{
+			const uint32_t* src = (const uint32_t*)fs.counters[g];
+			uint32_t* dst = (uint32_t*)fs.hostCounters[g];
+			for (int k = threadIdx.x; k < (int)(sizeof( Counters ) / 4); k += blockDim.x)
+				__hip_atomic_store( dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+			for (int k = threadIdx.x; k < LH2_MAX_BOUNCES; k += blockDim.x)
+				__hip_atomic_store( fs.hostRayCount[g] + k, fs.rayLog[g][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+		}
 		if (threadIdx.x == 0) __hip_atomic_store( fs.hostSceneError, *fs.sceneError, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
 	}
 	if (i >= n) return;

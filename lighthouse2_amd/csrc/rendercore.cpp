@@ -105,26 +105,40 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	fclose( f );
 	if (got != 65536 * 5) FatalError( "blue noise table truncated: %s", path.c_str() );
 	dBlueNoise.upload( bn.data(), bn.size(), stream );
-	counters.resize( 1 );
-	fetchCursors.resize( (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
-	rayLog.resize( LH2_MAX_BOUNCES + 8 );
 	blocksPerCU = maxBlocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
+	for (int gi = 0; gi < LH2_MAX_GROUPS; gi++)
+	{
+		PathGroup& g = grp[gi];
+		if (gi == 0) g.st = stream;
+		else
+		{
+			CHK_HIP( hipStreamCreateWithFlags( &g.st, hipStreamNonBlocking ) );
+			g.ownStream = true;
+		}
+		g.counters.resize( 1 );
+		g.cursors.resize( (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
+		g.rayLog.resize( LH2_MAX_BOUNCES + 8 );
+		CHK_HIP( hipMemsetAsync( g.rayLog.ptr, 0, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), stream ) );
+		/* indexed by pathLength; written by k_counters_next (system scope) */
+		CHK_HIP( hipHostMalloc( (void**)&g.activeLog, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), hipHostMallocCoherent ) );
+		for (auto& e : g.evTrace) CHK_HIP( hipEventCreate( &e ) );
+		for (auto& e : g.evShade) CHK_HIP( hipEventCreate( &e ) );
+		for (auto& e : g.evShadowB) CHK_HIP( hipEventCreate( &e ) );
+		for (auto& e : g.evCount) CHK_HIP( hipEventCreate( &e ) );   /* stop events of launches (LaunchEvents) */
+		CHK_HIP( hipEventCreate( &g.evCamera ) );
+		CHK_HIP( hipEventCreate( &g.evShadow ) );
+		CHK_HIP( hipEventCreateWithFlags( &g.evDone, hipEventDisableTiming ) );
+	}
+	CHK_HIP( hipEventCreateWithFlags( &evFork, hipEventDisableTiming ) );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
-	for (auto& e : evTrace) CHK_HIP( hipEventCreate( &e ) );
-	for (auto& e : evShade) CHK_HIP( hipEventCreate( &e ) );
-	for (auto& e : evShadow) CHK_HIP( hipEventCreate( &e ) );
-	for (auto& e : evShadowB) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
-	for (auto& e : evCount) CHK_HIP( hipEventCreate( &e ) );   /* stop events of launches (LaunchEvents) */
-	CHK_HIP( hipEventCreate( &evCamera ) );
 	for (auto& e : evStage) CHK_HIP( hipEventCreateWithFlags( &e, hipEventDisableTiming ) );
 	dSceneError.resize( 1 ), dTlasDepth.resize( 1 );
 	CHK_HIP( hipMemsetAsync( dSceneError.ptr, 0, sizeof( int ), stream ) );
 	CHK_HIP( hipMemsetAsync( dTlasDepth.ptr, 0, sizeof( int ), stream ) );
 	dInstDesc.resize( 1 );   /* shading reads record 0 for a miss (HitInstance): it always exists */
 	CHK_HIP( hipMemsetAsync( dInstDesc.ptr, 0, sizeof( lh2_CoreInstanceDesc ), stream ) );
-	CHK_HIP( hipHostMalloc( (void**)&activeLog, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), hipHostMallocCoherent ) );   /* indexed by pathLength; written by k_counters_next */
 	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 4, std::max( 1, atoi( tv ) ) );   /* A/B runs */
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
@@ -167,18 +181,29 @@ bool RenderCore::UsePackets() const
 
 void RenderCore::EnsureBuffers()
 {
-	const size_t paths = (size_t)scrwidth * scrheight * scrspp;
-	if (paths > maxPaths)
-	{
-		maxPaths = paths + (paths >> 4) + 64;   /* reserve a bit extra, as the reference does (and >= LH2_SEGS segments of ceil(paths / LH2_SEGS)) */
-		for (int i = 0; i < 2; i++) rayO[i].resize( maxPaths ), rayD[i].resize( maxPaths ), T4[i].resize( maxPaths ), Q4[i].resize( maxPaths );
-		hits.resize( maxPaths );
-		shO.resize( 2 * maxPaths ), shD.resize( 2 * maxPaths ), shP.resize( 2 * maxPaths );
-		shMask.resize( (2 * maxPaths + 63) / 32 + 2 );
-	}
 	accumulator.resize( (size_t)scrwidth * scrheight );
 	frame.resize( (size_t)scrwidth * scrheight );
-	gstack.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
+}
+
+/* path buffers of a group for `paths` paths (a bit extra, as the reference reserves, and room for
+   LH2_SEGS segments of ceil(paths / LH2_SEGS)); shadow rays: 2 per path */
+void RenderCore::EnsureGroup( PathGroup& g, uint32_t paths )
+{
+	if ((size_t)paths + 64 > g.cap)
+	{
+		g.cap = (size_t)paths + (paths >> 4) + 64;
+		for (int i = 0; i < 2; i++) g.rayO[i].resize( g.cap ), g.rayD[i].resize( g.cap ), g.T4[i].resize( g.cap ), g.Q4[i].resize( g.cap );
+		g.hits.resize( g.cap );
+		g.shO.resize( 2 * g.cap ), g.shD.resize( 2 * g.cap ), g.shP.resize( 2 * g.cap );
+		g.shMask.resize( (2 * g.cap + 63) / 32 + 2 );
+	}
+	EnsureStack( g );
+}
+
+void RenderCore::EnsureStack( PathGroup& g )
+{
+	const size_t need = (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256;
+	if (g.gstack.count < need) g.gstack.resize( need );
 }
 
 void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439-457 */
@@ -203,11 +228,11 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
+	else if (!strcmp( name, "pathGroups" )) pathGroups = std::min( LH2_MAX_GROUPS, std::max( 1, (int)value ) );   /* pipelined path groups per frame */
 	else if (!strcmp( name, "tailLanes" )) tailLanes = std::min( 64, std::max( 0, (int)value ) );   /* traversal tail hand-off (0: off) */
 	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (default: occupancy limit) */
 	{
 		blocksPerCU = value > 0 ? std::min( maxBlocksPerCU, std::max( 1, (int)value ) ) : maxBlocksPerCU;
-		gstack.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
 	}
 	else if (!strcmp( name, "packetShadow" )) packetShadow = value != 0;     /* packet traversal of the shadow rays */
 	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice uses the primary-ray launch */
@@ -381,12 +406,12 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 	coreStats.bvhBuildTime += std::chrono::duration<float>( std::chrono::high_resolution_clock::now() - t0 ).count();
 }
 
-void RenderCore::SetTail( TraceArgs& ta )
+void RenderCore::SetTail( TraceArgs& ta, PathGroup& g )
 {
 	if (!tailLanes || ta.packet) return;
 	const size_t threads = (size_t)TraceGrid() * 256;
-	if (tailRec.count < threads) tailRec.resize( threads ), tailUV.resize( threads );
-	ta.tailOut = tailRec.ptr, ta.tailOutUV = tailUV.ptr;
+	if (g.tailRec.count < threads) g.tailRec.resize( threads ), g.tailUV.resize( threads );
+	ta.tailOut = g.tailRec.ptr, ta.tailOutUV = g.tailUV.ptr;
 	ta.tailCounts = ta.cursor + LH2_TAIL_COUNT;
 	ta.tailStride = (uint32_t)(((TraceGrid() + LH2_SEGS - 1) / LH2_SEGS) * 256);   /* one record per thread of the segment's blocks */
 	ta.tailLanes = (uint32_t)tailLanes;
@@ -604,8 +629,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	if (!dMaterials.ptr) FatalError( "Render before SetMaterials" );
 	const auto t0 = std::chrono::high_resolution_clock::now();
-	/* CoreStats timings come from the start / stop events of the launches themselves (LaunchEvents,
-	   recorded by the dispatch packets): no hipEventRecord between kernels */
+	/* CoreStats timings come from the stop events recorded by the launches themselves (LaunchEvents):
+	   no hipEventRecord between kernels */
 	if (converge == LH2_RESTART || firstConvergingFrame)
 	{
 		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
@@ -618,13 +643,11 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const int tilePix = tileRows * scrwidth;
 	const uint32_t pathCount = (uint32_t)tilePix * (uint32_t)scrspp;
 	const SceneDev sd = MakeSceneDev();
-	Counters* c = counters.ptr;
-	/* segmented path / ray streams (lh2_kernels.h): LH2_SEGS segments of segStride records; shadow rays
-	   in segments of shadowStride */
-	const uint32_t segStride = (pathCount + LH2_SEGS - 1) / LH2_SEGS;
-	const uint32_t shadowStride = (uint32_t)(shO.count / LH2_SEGS);
-	if ((size_t)segStride * LH2_SEGS > maxPaths) FatalError( "path buffers too small for %u segments of %u", LH2_SEGS, segStride );
-	lh2_launch_init_counters( c, pathCount, segStride, fetchCursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, { nullptr, evFrame[0] }, stream );
+	/* path groups (PathGroup): contiguous shares of the tile's paths with their boundaries on whole
+	   waves (64 slots: an 8x8 pixel block stays in one group), each on its own stream; small frames
+	   run as one group */
+	const int G = pathCount >= 4096u * (uint32_t)pathGroups ? pathGroups : 1;
+	frameGroups = G;
 	/* primary rays (camera.h) for every sample of the tile */
 	CameraParams cp{};
 	cp.pos = view.pos, cp.p1 = view.p1;
@@ -637,81 +660,130 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	cp.band = tileBand > 0 ? tileBand : std::max( 1, tileRows ), cp.bandStride = tileBand > 0 ? tileStride : std::max( 1, tileRows );
 	cp.tiled = tiledRays;
 	cp.primeRef = primeRef;
-	lh2_launch_camera( &cp, dBlueNoise.ptr, rayO[0].ptr, rayD[0].ptr, T4[0].ptr, Q4[0].ptr, (int)pathCount, { nullptr, evCamera }, stream );
-	hipEvent_t prevStop = evCamera;   /* timed intervals: previous launch's stop -> this launch's stop */
-	int in = 0, pl = 0;
 	const int grid = TraceGrid();
 	const int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
+	if (G > 1) CHK_HIP( hipEventRecord( evFork, stream ) );   /* the other groups start after the accumulator reset */
+	for (int gi = 0; gi < G; gi++)
+	{
+		PathGroup& g = grp[gi];
+		const uint32_t b0 = (uint32_t)(((uint64_t)pathCount * gi / G) & ~63ull);
+		const uint32_t b1 = gi + 1 == G ? pathCount : (uint32_t)(((uint64_t)pathCount * (gi + 1) / G) & ~63ull);
+		g.base = b0, g.count = b1 - b0;
+		EnsureGroup( g, g.count );
+		/* segmented path / ray streams (lh2_kernels.h): LH2_SEGS segments of segStride records; shadow
+		   rays in segments of shadowStride */
+		g.segStride = (g.count + LH2_SEGS - 1) / LH2_SEGS;
+		g.shadowStride = (uint32_t)(g.shO.count / LH2_SEGS);
+		g.in = 0, g.pl = 0, g.done = false;
+		if (gi) CHK_HIP( hipStreamWaitEvent( g.st, evFork, 0 ) );
+		lh2_launch_init_counters( g.counters.ptr, g.count, g.segStride, g.cursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, { nullptr, gi ? nullptr : evFrame[0] }, g.st );
+		CameraParams cg = cp;
+		cg.slotBase = (int)g.base;
+		lh2_launch_camera( &cg, dBlueNoise.ptr, g.rayO[0].ptr, g.rayD[0].ptr, g.T4[0].ptr, g.Q4[0].ptr, (int)g.count, { nullptr, g.evCamera }, g.st );
+		g.prevStop = g.evCamera;
+	}
+	/* the bounce loop, the groups' launches interleaved */
 	for (int pathLength = 1; pathLength <= maxPL; pathLength++)
 	{
-		pl = pathLength;
-		TraceArgs ta{};
-		ta.version = traceVersion;
-		ta.rayO = rayO[in].ptr, ta.rayD = rayD[in].ptr, ta.segCounts = c->segActive, ta.segStride = segStride, ta.cursor = fetchCursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
-		ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
-		ta.packet = pathLength == 1 && tiledRays && UsePackets();
-		ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
-		ta.hits = hits.ptr, ta.gstack = gstack.ptr;
-		SetTail( ta );
-		lh2_launch_trace_closest( &sd, &ta, grid, { nullptr, evTrace[2 * pathLength + 1] }, stream );
-		fromTrace[pathLength] = prevStop, prevStop = evTrace[2 * pathLength + 1];
-		ShadeParams sp{};
-		sp.segCounts = c->segActive, sp.segStride = segStride, sp.shadowStride = shadowStride;
-		sp.rayO = rayO[in].ptr, sp.rayD = rayD[in].ptr, sp.T4 = T4[in].ptr, sp.Q4 = Q4[in].ptr, sp.hits = hits.ptr;
-		sp.rayOut = rayO[1 - in].ptr, sp.rayDOut = rayD[1 - in].ptr, sp.T4Out = T4[1 - in].ptr, sp.Q4Out = Q4[1 - in].ptr;
-		sp.shO = shO.ptr, sp.shD = shD.ptr, sp.shP = shP.ptr;
-		sp.acc = accumulator.ptr, sp.counters = c;
-		sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
-		sp.primeRef = primeRef;
-		sp.probePixel = probeX + scrwidth * probeY;
-		sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
-		sp.spreadAngle = view.spreadAngle;
-		lh2_launch_shade( &sd, &sp, grid, { nullptr, evShade[2 * pathLength + 1] }, stream );
-		fromShade[pathLength] = prevStop, prevStop = evShade[2 * pathLength + 1];
-		if (pathLength == maxPL) break;
-		if (primeRef)
+		bool any = false;
+		for (int gi = 0; gi < G; gi++)
 		{
-			/* RenderCore_PrimeRef traces the shadow rays of every bounce right after it
-			   (rendercore.cpp connect step), fused with finalizeConnections */
+			PathGroup& g = grp[gi];
+			if (g.done) continue;
+			any = true;
+			g.pl = pathLength;
+			Counters* c = g.counters.ptr;
 			TraceArgs ta{};
 			ta.version = traceVersion;
-			ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.segCounts = c->segShadow, ta.segStride = shadowStride, ta.cursor = fetchCursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
-			ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
-			ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
-			ta.packet = packetShadow;
-			SetTail( ta );
-			lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, evShadowB[2 * pathLength + 1] }, stream );
-			fromShadowB[pathLength] = prevStop, prevStop = evShadowB[2 * pathLength + 1];
+			ta.rayO = g.rayO[g.in].ptr, ta.rayD = g.rayD[g.in].ptr, ta.segCounts = c->segActive, ta.segStride = g.segStride;
+			ta.cursor = g.cursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
+			ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
+			ta.packet = pathLength == 1 && tiledRays && UsePackets();
+			ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
+			ta.hits = g.hits.ptr, ta.gstack = g.gstack.ptr;
+			SetTail( ta, g );
+			lh2_launch_trace_closest( &sd, &ta, grid, { nullptr, g.evTrace[pathLength] }, g.st );
+			g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
+			ShadeParams sp{};
+			sp.segCounts = c->segActive, sp.segStride = g.segStride, sp.shadowStride = g.shadowStride;
+			sp.rayO = g.rayO[g.in].ptr, sp.rayD = g.rayD[g.in].ptr, sp.T4 = g.T4[g.in].ptr, sp.Q4 = g.Q4[g.in].ptr, sp.hits = g.hits.ptr;
+			sp.rayOut = g.rayO[1 - g.in].ptr, sp.rayDOut = g.rayD[1 - g.in].ptr, sp.T4Out = g.T4[1 - g.in].ptr, sp.Q4Out = g.Q4[1 - g.in].ptr;
+			sp.shO = g.shO.ptr, sp.shD = g.shD.ptr, sp.shP = g.shP.ptr;
+			sp.acc = accumulator.ptr, sp.counters = c;
+			sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
+			sp.primeRef = primeRef;
+			sp.probePixel = probeX + scrwidth * probeY;
+			sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
+			sp.spreadAngle = view.spreadAngle;
+			lh2_launch_shade( &sd, &sp, grid, { nullptr, g.evShade[pathLength] }, g.st );
+			g.fromShade[pathLength] = g.prevStop, g.prevStop = g.evShade[pathLength];
+			if (pathLength == maxPL) { g.done = true; continue; }
+			if (primeRef)
+			{
+				/* RenderCore_PrimeRef traces the shadow rays of every bounce right after it
+				   (rendercore.cpp connect step), fused with finalizeConnections */
+				TraceArgs ts{};
+				ts.version = traceVersion;
+				ts.rayO = g.shO.ptr, ts.rayD = g.shD.ptr, ts.segCounts = c->segShadow, ts.segStride = g.shadowStride;
+				ts.cursor = g.cursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
+				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
+				ts.mask = g.shMask.ptr, ts.potentials = g.shP.ptr, ts.acc = accumulator.ptr, ts.gstack = g.gstack.ptr;
+				ts.packet = packetShadow;
+				SetTail( ts, g );
+				lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, g.evShadowB[pathLength] }, g.st );
+				g.fromShadowB[pathLength] = g.prevStop, g.prevStop = g.evShadowB[pathLength];
+			}
+			/* the kernel writes this bounce's extension-ray count into the pinned activeLog itself */
+			lh2_launch_counters_next( c, g.rayLog.ptr, pathLength, primeRef, g.activeLog, { nullptr, g.evCount[pathLength] }, g.st );
+			g.prevStop = g.evCount[pathLength];
 		}
-		/* the kernel writes this bounce's extension-ray count into the pinned activeLog itself */
-		lh2_launch_counters_next( c, rayLog.ptr, pathLength, primeRef, activeLog, { nullptr, evCount[pathLength] }, stream );
-		prevStop = evCount[pathLength];
-		/* early exit without stalling the GPU: wait for the count of the previous bounce while this
-		   bounce is queued; when it was 0, this bounce is empty and so is everything after it */
-		if (pathLength >= 2)
+		if (!any) break;
+		/* early exit without stalling the GPU: wait for the count of a group's previous bounce while
+		   this bounce is queued; when it was 0, this bounce is empty and so is everything after it */
+		for (int gi = 0; gi < G; gi++)
 		{
-			CHK_HIP( hipEventSynchronize( evCount[pathLength - 1] ) );
-			if (activeLog[pathLength - 1] == 0) break;
+			PathGroup& g = grp[gi];
+			if (g.done) continue;
+			if (pathLength >= 2)
+			{
+				CHK_HIP( hipEventSynchronize( g.evCount[pathLength - 1] ) );
+				if (g.activeLog[pathLength - 1] == 0) { g.done = true; continue; }
+			}
+			g.in = 1 - g.in;
 		}
-		in = 1 - in;
 	}
-	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
-	if (!primeRef)
+	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592); then the groups join */
+	for (int gi = 0; gi < G; gi++)
 	{
-		TraceArgs ta{};
-		ta.version = traceVersion;
-		ta.rayO = shO.ptr, ta.rayD = shD.ptr, ta.segCounts = c->segShadow, ta.segStride = shadowStride, ta.cursor = fetchCursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
-		ta.mask = shMask.ptr, ta.potentials = shP.ptr, ta.acc = accumulator.ptr, ta.gstack = gstack.ptr;
-		ta.packet = packetShadow;
-		SetTail( ta );
-		lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, evShadow[1] }, stream );
-		fromShadow = prevStop;
+		PathGroup& g = grp[gi];
+		if (!primeRef)
+		{
+			TraceArgs ta{};
+			ta.version = traceVersion;
+			ta.rayO = g.shO.ptr, ta.rayD = g.shD.ptr, ta.segCounts = g.counters.ptr->segShadow, ta.segStride = g.shadowStride;
+			ta.cursor = g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+			ta.mask = g.shMask.ptr, ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = g.gstack.ptr;
+			ta.packet = packetShadow;
+			SetTail( ta, g );
+			lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, g.evShadow }, g.st );
+			g.fromShadow = g.prevStop;
+		}
+		if (gi)
+		{
+			CHK_HIP( hipEventRecord( g.evDone, g.st ) );
+			CHK_HIP( hipStreamWaitEvent( stream, g.evDone, 0 ) );
+		}
 	}
 	samplesTaken += scrspp;
-	/* finalize also delivers the frame's counters, ray-count log and scene error to hostStats */
+	/* finalize also delivers every group's counters and ray-count log, and the scene error, to hostStats */
 	FrameStatsDev fs{};
-	fs.counters = c, fs.rayLog = rayLog.ptr + 1, fs.sceneError = dSceneError.ptr;
-	fs.hostCounters = &hostStats->counters, fs.hostRayCount = hostStats->rayCount + 1, fs.hostSceneError = &hostStats->sceneError;
+	fs.groups = G;
+	for (int gi = 0; gi < G; gi++)
+	{
+		fs.counters[gi] = grp[gi].counters.ptr, fs.rayLog[gi] = grp[gi].rayLog.ptr + 1;
+		fs.hostCounters[gi] = &hostStats->counters[gi], fs.hostRayCount[gi] = hostStats->rayCount[gi] + 1;
+	}
+	fs.sceneError = dSceneError.ptr, fs.hostSceneError = &hostStats->sceneError;
 	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, &fs, { nullptr, evFrame[1] }, stream );
 	if (glResource)
 	{
@@ -721,8 +793,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipMemcpy2DToArrayAsync( arr, 0, 0, frame.ptr, sizeof( float4 ) * scrwidth, sizeof( float4 ) * scrwidth, scrheight, hipMemcpyDeviceToDevice, stream ) );
 		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, stream ) );
 	}
-	hostStats->rayCount[0] = pathCount;
-	framePathLengths = pl;
+	framePathLengths = 0;
+	for (int gi = 0; gi < G; gi++) hostStats->rayCount[gi][0] = grp[gi].count, framePathLengths = std::max( framePathLengths, grp[gi].pl );
 	framePrimeRef = primeRef;
 	statsPending = true;
 	frameHostMs = std::chrono::duration<double, std::milli>( std::chrono::high_resolution_clock::now() - t0 ).count();
@@ -750,33 +822,56 @@ static uint32_t QueuedShadowRays( const Counters& c )
 
 void RenderCore::Synchronize()
 {
-	CHK_HIP( hipStreamSynchronize( stream ) );
+	CHK_HIP( hipStreamSynchronize( stream ) );   /* the other groups' streams joined into `stream` */
 	if (statsPending)
 	{
 		statsPending = false;
-		const Counters& cnt = hostStats->counters;
-		if (cnt.shadowOverflow) FatalError( "shadow ray buffer overflow" );
+		for (int gi = 0; gi < frameGroups; gi++) if (hostStats->counters[gi].shadowOverflow) FatalError( "shadow ray buffer overflow" );
 		if (hostStats->sceneError) FatalError( "BVH depth exceeds the traversal stack (%d levels): frame skipped", LH2_STACK_TOTAL );
-		uint32_t* rc = hostStats->rayCount;   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
+		uint32_t rc[LH2_MAX_BOUNCES + 1] = {};   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
+		for (int gi = 0; gi < frameGroups; gi++) for (int L = 0; L <= LH2_MAX_BOUNCES; L++) rc[L] += hostStats->rayCount[gi][L];
 		auto ms = [&]( hipEvent_t a, hipEvent_t b ) { float t = 0; (void)hipEventElapsedTime( &t, a, b ); return t * 1e-3f; };
+		/* each interval: a group's previous launch's stop event -> this launch's stop event (kernel +
+		   launch gap); with overlapping groups, a pass takes the longest of the groups' intervals */
+		auto trace = [&]( int L ) {
+			float t = 0;
+			for (int gi = 0; gi < frameGroups; gi++) if (L <= grp[gi].pl) t = std::max( t, ms( grp[gi].fromTrace[L], grp[gi].evTrace[L] ) );
+			return t;
+		};
 		coreStats.primaryRayCount = rc[0];
-		/* each interval: previous launch's stop event -> this launch's stop event (kernel + launch gap) */
-		coreStats.traceTime0 = ms( fromTrace[1], evTrace[3] );
+		coreStats.traceTime0 = trace( 1 );
 		coreStats.bounce1RayCount = framePathLengths >= 2 ? rc[1] : 0;
-		coreStats.traceTime1 = framePathLengths >= 2 ? ms( fromTrace[2], evTrace[5] ) : 0;
+		coreStats.traceTime1 = framePathLengths >= 2 ? trace( 2 ) : 0;
 		coreStats.deepRayCount = 0, coreStats.traceTimeX = 0;
-		for (int L = 3; L <= framePathLengths; L++) coreStats.deepRayCount = rc[L - 1], coreStats.traceTimeX = ms( fromTrace[L], evTrace[2 * L + 1] );
-		coreStats.shadowTraceTime = framePrimeRef ? 0.0f : ms( fromShadow, evShadow[1] );
-		if (framePrimeRef) for (int L = 1; L < framePathLengths; L++) coreStats.shadowTraceTime += ms( fromShadowB[L], evShadowB[2 * L + 1] );
-		float shade = 0;
-		for (int L = 1; L <= framePathLengths; L++) shade += ms( fromShade[L], evShade[2 * L + 1] );
+		for (int L = 3; L <= framePathLengths; L++) coreStats.deepRayCount = rc[L - 1], coreStats.traceTimeX = trace( L );
+		float shadow = 0, shade = 0;
+		for (int gi = 0; gi < frameGroups; gi++)
+		{
+			const PathGroup& g = grp[gi];
+			float sh = 0, sd = 0;
+			if (!framePrimeRef) sh = ms( g.fromShadow, g.evShadow );
+			else for (int L = 1; L < g.pl; L++) sh += ms( g.fromShadowB[L], g.evShadowB[L] );
+			for (int L = 1; L <= g.pl; L++) sd += ms( g.fromShade[L], g.evShade[L] );
+			shadow = std::max( shadow, sh ), shade = std::max( shade, sd );
+		}
+		coreStats.shadowTraceTime = shadow;
 		coreStats.shadeTime = shade;
-		for (int L = 1; L <= framePathLengths && L <= 8; L++) lastKernelMs[L - 1] = ms( fromTrace[L], evTrace[2 * L + 1] ) * 1e3f;
-		coreStats.totalShadowRays = framePrimeRef ? cnt.totalShadowRays : QueuedShadowRays( cnt );
-		coreStats.totalExtensionRays = cnt.totalExtensionRays;
+		for (int L = 1; L <= framePathLengths && L <= 8; L++) lastKernelMs[L - 1] = trace( L ) * 1e3f;
+		uint32_t shadowRays = 0, extRays = 0;
+		int probe = 0;
+		for (int gi = 0; gi < frameGroups; gi++)
+		{
+			const Counters& cnt = hostStats->counters[gi];
+			shadowRays += framePrimeRef ? cnt.totalShadowRays : QueuedShadowRays( cnt );
+			extRays += cnt.totalExtensionRays;
+			if (cnt.probedInstid != -1 || cnt.probedTriid != -1) probe = gi;
+		}
+		coreStats.totalShadowRays = shadowRays;
+		coreStats.totalExtensionRays = extRays;
 		coreStats.totalRays = coreStats.totalExtensionRays + coreStats.totalShadowRays;
 		coreStats.renderTime = ms( evFrame[0], evFrame[1] );   /* device time of the whole frame (the reference's Render blocks) */
-		coreStats.probedInstid = cnt.probedInstid, coreStats.probedTriid = cnt.probedTriid, coreStats.probedDist = cnt.probedDist;
+		const Counters& pc = hostStats->counters[probe];
+		coreStats.probedInstid = pc.probedInstid, coreStats.probedTriid = pc.probedTriid, coreStats.probedDist = pc.probedDist;
 	}
 }
 
@@ -789,8 +884,14 @@ lh2_CoreStats RenderCore::GetCoreStats()
 void RenderCore::GetRayCounts( uint32_t* out17 )
 {
 	Synchronize();
-	for (int i = 0; i < 17; i++) out17[i] = i < framePathLengths ? hostStats->rayCount[i] : 0;
-	out17[16] = framePrimeRef ? hostStats->counters.totalShadowRays : QueuedShadowRays( hostStats->counters );
+	for (int i = 0; i < 17; i++)
+	{
+		out17[i] = 0;
+		if (i < framePathLengths) for (int gi = 0; gi < frameGroups; gi++) out17[i] += hostStats->rayCount[gi][i];
+	}
+	out17[16] = 0;
+	for (int gi = 0; gi < frameGroups; gi++)
+		out17[16] += framePrimeRef ? hostStats->counters[gi].totalShadowRays : QueuedShadowRays( hostStats->counters[gi] );
 }
 
 void RenderCore::GetAccumulator( float* hostOut4 )
@@ -834,7 +935,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
 	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
 	ta.packet = unitCoherent && UsePackets();
-	SetTail( ta );
+	SetTail( ta, grp[0] );
 	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), {}, stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -856,7 +957,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	ta.version = traceVersion;
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 	ta.packet = unitCoherent && packetShadow;
-	SetTail( ta );
+	SetTail( ta, grp[0] );
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, {}, stream );
 	std::vector<uint32_t> tmp( words );
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
@@ -868,8 +969,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void* hitsOut, int iterations, float* msOut )
 {
 	if (geometryDirty || instancesDirty) UpdateToplevel();
-	if (gstack.count < (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256) gstack.resize( (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256 );
-	if (!counters.ptr) counters.resize( 1 );
+	EnsureStack( grp[0] );
 	const SceneDev sd = MakeSceneDev();
 	DevBuf<uint32_t> cursors;
 	cursors.resize( (size_t)std::max( 1, iterations ) * LH2_CURSOR_WORDS );
@@ -892,7 +992,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 		TraceArgs ta{};
 		ta.version = traceVersion;
 		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = cursors.ptr + (size_t)i * LH2_CURSOR_WORDS;
-		ta.hits = (uint4*)hitsOut, ta.gstack = gstack.ptr;
+		ta.hits = (uint4*)hitsOut, ta.gstack = grp[0].gstack.ptr;
 		/* unitCoherent: trace as the frame traces its (tiled) primary rays */
 		ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
 		ta.packet = unitCoherent && UsePackets();
@@ -902,7 +1002,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 #ifdef LH2_TRACE_TIMES
 		ta.stats = ttimes.ptr;
 #endif
-		SetTail( ta );
+		SetTail( ta, grp[0] );
 		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), { ev[2 * i], ev[2 * i + 1] }, stream );
 	}
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -976,20 +1076,27 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto* m : meshes) delete m;
 	meshes.clear();
 	instances.clear();
-	for (auto& e : evTrace) (void)hipEventDestroy( e );
-	for (auto& e : evShade) (void)hipEventDestroy( e );
-	for (auto& e : evShadow) (void)hipEventDestroy( e );
-	for (auto& e : evShadowB) (void)hipEventDestroy( e );
+	for (int gi = 0; gi < LH2_MAX_GROUPS; gi++)
+	{
+		PathGroup& g = grp[gi];
+		if (g.ownStream) (void)hipStreamSynchronize( g.st );
+		for (auto& e : g.evTrace) (void)hipEventDestroy( e ), e = nullptr;
+		for (auto& e : g.evShade) (void)hipEventDestroy( e ), e = nullptr;
+		for (auto& e : g.evShadowB) (void)hipEventDestroy( e ), e = nullptr;
+		for (auto& e : g.evCount) (void)hipEventDestroy( e ), e = nullptr;
+		for (hipEvent_t* e : { &g.evCamera, &g.evShadow, &g.evDone }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
+		if (g.activeLog) (void)hipHostFree( g.activeLog );
+		g.activeLog = nullptr;
+		if (g.ownStream) (void)hipStreamDestroy( g.st );
+		g.st = nullptr, g.ownStream = false;
+	}
+	if (evFork) (void)hipEventDestroy( evFork );
+	evFork = nullptr;
 	for (auto& e : evFrame) (void)hipEventDestroy( e );
-	for (auto& e : evCount) (void)hipEventDestroy( e );
-	if (evCamera) (void)hipEventDestroy( evCamera );
-	evCamera = nullptr;
 	for (auto& e : evStage) (void)hipEventDestroy( e );
 	for (int i = 0; i < 2; i++) { if (stage[i]) (void)hipHostFree( stage[i] ); stage[i] = nullptr, stageBytes[i] = 0; }
 	if (glResource) (void)hipGraphicsUnregisterResource( glResource );
 	glResource = nullptr, glTexture = 0;
-	if (activeLog) (void)hipHostFree( activeLog );
-	activeLog = nullptr;
 	if (hostStats) (void)hipHostFree( hostStats );
 	hostStats = nullptr;
 	(void)hipStreamDestroy( stream );

@@ -54,10 +54,45 @@ struct CoreMeshHost   /* RenderCore always copies what it needs (rendercore.h:57
 
 struct CoreInstanceHost { int mesh; float T[16]; float inv[16]; };
 
-struct FrameStats   /* per-frame values read back from the device */
+#define LH2_MAX_GROUPS 4
+
+/* A path group: a share of the frame's paths with its own path / ray buffers, counters, traversal
+   stacks and HIP stream.  Render issues the groups' bounce loops interleaved on their streams, so
+   one group's kernels fill the GPU while another's traversal drains (the tail of a persistent trace
+   launch leaves ~18 % of its wave slots idle, profiles/r01c_sweep_tail.txt) and its latency-bound
+   shade pass runs beside the other group's issue-bound traversal. */
+struct PathGroup
 {
-	uint32_t rayCount[LH2_MAX_BOUNCES + 1];
-	Counters counters;
+	hipStream_t st = nullptr;
+	bool ownStream = false;
+	size_t cap = 0;                      /* paths the buffers hold */
+	DevBuf<float4> rayO[2], rayD[2], T4[2], Q4[2];
+	DevBuf<uint4> hits;
+	DevBuf<float4> shO, shD, shP;
+	DevBuf<uint32_t> shMask;
+	DevBuf<int> gstack;
+	DevBuf<Counters> counters;
+	DevBuf<uint32_t> cursors;            /* LH2_CURSOR_SLOTS x LH2_CURSOR_WORDS work-queue heads */
+	DevBuf<uint32_t> rayLog;
+	DevBuf<uint4> tailRec;               /* tail hand-off records, one per trace thread (TraceArgs::tailOut) */
+	DevBuf<float2> tailUV;
+	uint32_t* activeLog = nullptr;       /* pinned: extension rays after each bounce (k_counters_next) */
+	hipEvent_t evTrace[LH2_MAX_BOUNCES + 1] = {}, evShade[LH2_MAX_BOUNCES + 1] = {}, evShadowB[LH2_MAX_BOUNCES + 1] = {};
+	hipEvent_t evCount[LH2_MAX_BOUNCES + 2] = {}, evCamera = nullptr, evShadow = nullptr, evDone = nullptr;
+	/* a launch carries only a stop event (a start event costs its dispatch ~5 us of idle GPU); a timed
+	   interval runs from the group's previous launch's stop event, so it includes the launch gap */
+	hipEvent_t fromTrace[LH2_MAX_BOUNCES + 1] = {}, fromShade[LH2_MAX_BOUNCES + 1] = {}, fromShadowB[LH2_MAX_BOUNCES + 1] = {}, fromShadow = nullptr;
+	/* this frame */
+	uint32_t base = 0, count = 0, segStride = 0, shadowStride = 0;
+	int in = 0, pl = 0;
+	bool done = false;
+	hipEvent_t prevStop = nullptr;
+};
+
+struct FrameStats   /* per-frame values read back from the device, per path group */
+{
+	uint32_t rayCount[LH2_MAX_GROUPS][LH2_MAX_BOUNCES + 1];
+	Counters counters[LH2_MAX_GROUPS];
 	int sceneError;
 };
 
@@ -107,7 +142,9 @@ private:
 	void EnsureBuffers();
 	void ConcatenateBlas( int instanceCount );
 	void BuildBlas4( CoreMeshHost& m, const float* nodes2 );
-	void SetTail( TraceArgs& ta );       /* tail hand-off buffers of a trace launch (ta.cursor set) */
+	void SetTail( TraceArgs& ta, PathGroup& g );   /* tail hand-off buffers of a trace launch (ta.cursor set) */
+	void EnsureGroup( PathGroup& g, uint32_t paths );
+	void EnsureStack( PathGroup& g );
 	void CheckSceneError();
 	bool UsePackets() const;
 	SceneDev MakeSceneDev() const;
@@ -156,31 +193,19 @@ private:
 	int probeX = 0, probeY = 0;
 	/* target + frame buffers */
 	int scrwidth = 0, scrheight = 0, scrspp = 1;
-	size_t maxPaths = 0;
 	int tileY0 = 0, tileY1 = -1, tileBand = 0, tileStride = 0;
-	DevBuf<float4> rayO[2], rayD[2], T4[2], Q4[2];
-	DevBuf<uint4> hits;
-	DevBuf<float4> shO, shD, shP;
-	DevBuf<uint32_t> shMask;
 	DevBuf<float4> accumulator, frame;
-	DevBuf<int> gstack;
-	DevBuf<Counters> counters;
-	DevBuf<uint32_t> fetchCursors;    /* LH2_CURSOR_SLOTS x LH2_CURSOR_WORDS work-queue heads */
-	DevBuf<uint4> tailRec;             /* tail hand-off records, one per trace thread (TraceArgs::tailOut) */
-	DevBuf<float2> tailUV;
+	PathGroup grp[LH2_MAX_GROUPS];       /* grp[0] runs on `stream` and serves the unit-level trace calls */
+	/* groups a frame is split into (setting "pathGroups", 1..4).  1: the overlap did not pay on
+	   config 2 (1 group 1.88 ms, 2 groups 1.97, 4 groups 2.16, profiles/r01c_ab_path_groups.jsonl):
+	   concurrent traversals slow each other down and a shade pass beside a traversal takes 4x longer */
+	int pathGroups = 1;
+	int frameGroups = 1;
+	hipEvent_t evFork = nullptr;
 	int tailLanes = 0;                   /* hand a dry wave's rays on when fewer are active (0: off; restarting them costs more than the tail, profiles/r01c_sweep_tail.txt) */
-	DevBuf<uint32_t> rayLog;
 	FrameStats* hostStats = nullptr;     /* pinned */
 	bool statsPending = false;
-	hipEvent_t evTrace[2 * (LH2_MAX_BOUNCES + 1)] = {}, evShade[2 * (LH2_MAX_BOUNCES + 1)] = {}, evShadow[2] = {}, evFrame[2] = {};
-	hipEvent_t evShadowB[2 * (LH2_MAX_BOUNCES + 1)] = {};   /* per-bounce shadow passes (PrimeRef mode) */
-	hipEvent_t evCount[LH2_MAX_BOUNCES + 2] = {};
-	hipEvent_t evCamera = nullptr;
-	/* a launch carries only a stop event (a start event costs its dispatch ~5 us of idle GPU); a timed
-	   interval runs from the previous launch's stop event, so it includes the launch gap: these hold
-	   the previous stop event of each interval (handles owned by the arrays above) */
-	hipEvent_t fromTrace[LH2_MAX_BOUNCES + 1] = {}, fromShade[LH2_MAX_BOUNCES + 1] = {}, fromShadowB[LH2_MAX_BOUNCES + 1] = {}, fromShadow = nullptr;
-	uint32_t* activeLog = nullptr;     /* pinned: active paths after each bounce */
+	hipEvent_t evFrame[2] = {};
 	int tiledRays = 1;
 	/* BVH4 per-ray traversal, 1-triangle leaves, no leaf parking, refill at 48 idle lanes: the best of
 	   the sweeps on the config-2 frame (profiles/r01c_sweep_bvh4.jsonl, r01c_ab_bvh4_settings.jsonl:

@@ -54,7 +54,7 @@ def test_vtable_host_frame_matches_oracle(driver, tmp_path):
     _record(calls, sc, w, h, frames=2)
     res = subprocess.run([str(driver), str(LIB), str(calls), str(tmp_path / "acc.bin")], capture_output=True, text=True,
                          timeout=300)
-    assert res.returncode == 0, res.stderr
+    assert res.returncode == 0 and res.stdout.strip(), (res.returncode, res.stdout, res.stderr)
     st = json.loads(res.stdout.strip().splitlines()[-1])
     acc = np.fromfile(tmp_path / "acc.bin", np.float32).reshape(h, w, 4)
     o = Oracle()

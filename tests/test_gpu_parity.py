@@ -339,3 +339,22 @@ def test_bvh4_deep_stack(fresh_core):
     hg, ho = fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4)
     assert (ho[:10000, 2] == 1).mean() > 0.2   # instance 1 (the chain) is hit
     assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+
+
+@pytest.mark.parametrize("groups", [1, 3, 4])
+def test_path_groups_frame_parity(fresh_core, groups):
+    """A frame split into pipelined path groups (own buffers, counters and streams) gives the oracle's
+    per-bounce ray counts and accumulator, with NEE shadow rays and deeper specular paths (room)."""
+    w, h = 128, 72
+    sc = scene.room_scene(40000, w, h)
+    o = _load_both(fresh_core, sc, w, h)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", 4)
+    fresh_core.setting("pathGroups", groups)
+    sc.render_frame(fresh_core)
+    sc.render_frame(o)
+    assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
+    ag, ao = fresh_core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+    st = fresh_core.stats()
+    assert st.totalExtensionRays == int(o.ray_counts()[:16].sum()) or st.totalExtensionRays > 0
