@@ -345,7 +345,7 @@ def test_bvh4_deep_stack(fresh_core):
 def test_path_groups_frame_parity(fresh_core, groups):
     """A frame split into pipelined path groups (own buffers, counters and streams) gives the oracle's
     per-bounce ray counts and accumulator, with NEE shadow rays and deeper specular paths (room)."""
-    w, h = 128, 72
+    w, h = 192, 108          # 20736 paths: enough for 4 groups (>= 4096 paths each)
     sc = scene.room_scene(40000, w, h)
     o = _load_both(fresh_core, sc, w, h)
     for tgt in (fresh_core, o):
