@@ -75,7 +75,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	uint32_t refill;                                  /* refill idle lanes once >= refill are idle (1..64) */
 	uint32_t leafBatch;                               /* run triangle tests once >= leafBatch lanes parked a leaf */
 	int version;                                      /* traversal loop: 1 (trace_stream), 2 (lh2_trace2.inc), 4 (BVH4, lh2_trace4.inc) */
-	int packet;                                       /* 1: wave-uniform packet traversal (coherent rays, closest hit) */
+	int packet;                                       /* wave-uniform packet traversal (coherent rays): 1 over the BVH2, 4 over the BVH4 */
 	unsigned long long* stats;                        /* LH2_TRACE_STATS builds: LH2_TSTAT_N per-launch counters */
 	/* tail hand-off (lh2_trace2.inc): once the queue is exhausted, a wave with fewer than tailLanes
 	   active rays appends them to tailOut / tailOutUV {idx, bits(tbest), tri, inst} {u, v} - segment

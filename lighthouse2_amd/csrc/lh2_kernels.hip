@@ -507,9 +507,10 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 #ifndef LH2_PACKET_MINWAVES
 #define LH2_PACKET_MINWAVES 1
 #endif
-__global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet<0>( s, a ); }
-template <int MODE>
-__global__ __launch_bounds__( 256 ) void k_trace_any_packet( const SceneDev s, const TraceArgs a ) { trace_packet<MODE == 0 ? 1 : 2>( s, a ); }
+template <int W>
+__global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet<0, W>( s, a ); }
+template <int MODE, int W>
+__global__ __launch_bounds__( 256 ) void k_trace_any_packet( const SceneDev s, const TraceArgs a ) { trace_packet<MODE == 0 ? 1 : 2, W>( s, a ); }
 
 template <bool PARK, int V>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_closest( const SceneDev s, const TraceArgs a )
@@ -1736,7 +1737,8 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
 {
 	/* incoherent rays: parked leaves (leafBatch > 0); traversal loop version 1 or 2 (lh2_trace2.inc);
 	   coherent primary rays: packet traversal (lh2_trace_packet.inc) */
-	if (a->packet) LH2_LAUNCH( k_trace_closest_packet, grid, 256, st, ev, *s, *a );
+	if (a->packet == 4 && s->nodes4) LH2_LAUNCH( k_trace_closest_packet<4>, grid, 256, st, ev, *s, *a );
+	else if (a->packet) LH2_LAUNCH( k_trace_closest_packet<2>, grid, 256, st, ev, *s, *a );
 	else if (a->version >= 2)
 	{
 		/* with a tail hand-off: the main launch, then the tail launch over the handed-off rays;
@@ -1769,8 +1771,11 @@ void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int 
 {
 	if (a->packet)
 	{
-		if (fused) LH2_LAUNCH( k_trace_any_packet<1>, grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( k_trace_any_packet<0>, grid, 256, st, ev, *s, *a );
+		const bool v4 = a->packet == 4 && s->nodes4;
+		if (fused && v4) LH2_LAUNCH( (k_trace_any_packet<1, 4>), grid, 256, st, ev, *s, *a );
+		else if (fused) LH2_LAUNCH( (k_trace_any_packet<1, 2>), grid, 256, st, ev, *s, *a );
+		else if (v4) LH2_LAUNCH( (k_trace_any_packet<0, 4>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_any_packet<0, 2>), grid, 256, st, ev, *s, *a );
 	}
 	else if (a->version >= 2)
 	{

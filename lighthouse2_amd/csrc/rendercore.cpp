@@ -228,6 +228,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
+	else if (!strcmp( name, "packetWidth" )) packetWidth = value >= 4 ? 4 : 2;   /* packets over the BVH2 / BVH4 */
 	else if (!strcmp( name, "pathGroups" )) pathGroups = std::min( LH2_MAX_GROUPS, std::max( 1, (int)value ) );   /* pipelined path groups per frame */
 	else if (!strcmp( name, "tailLanes" )) tailLanes = std::min( 64, std::max( 0, (int)value ) );   /* traversal tail hand-off (0: off) */
 	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (default: occupancy limit) */
@@ -283,9 +284,14 @@ void RenderCore::SetMaterials( const lh2_CoreMaterial* mat, int n )   /* renderc
 {
 	std::vector<uint4> recs( (size_t)std::max( n, 1 ) * 8 );
 	memset( recs.data(), 0, recs.size() * sizeof( uint4 ) );
+	diffuseOnly = true;
 	for (int i = 0; i < n; i++)
 	{
 		const lh2_CoreMaterial& m = mat[i];
+		/* a path can only continue past its second vertex through a specular event (ROUGHNESS <= 0.001,
+		   a transmission sample) or an alpha cut-out (ENOUGH_BOUNCES = S_BOUNCED, pathtracer.h:33,211) */
+		if (TOCHAR( m.roughness.value ) == 0 || TOCHAR( m.transmission.value ) != 0 || (m.flags & 2) || m.roughness.textureID != -1)
+			diffuseOnly = false;
 		const uint32_t r = lh2_f2h( m.color.value.x ), g = lh2_f2h( m.color.value.y ), b = lh2_f2h( m.color.value.z );
 		const uint32_t tr = lh2_f2h( 1 - m.absorption.value.x ), tg = lh2_f2h( 1 - m.absorption.value.y ), tb = lh2_f2h( 1 - m.absorption.value.z );
 		const uint32_t flags = (m.eta.value < 1 ? 1u : 0u) + ((m.flags & 1) ? (1u << 11) : 0u) + ((m.flags & 2) ? (1u << 12) : 0u);
@@ -661,7 +667,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	cp.tiled = tiledRays;
 	cp.primeRef = primeRef;
 	const int grid = TraceGrid();
-	const int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
+	int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
+	/* no specular event and no alpha cut-out in any material: every path ends at its second vertex,
+	   so the bounce after it would be empty; not launching it saves three launches (~25 us) */
+	if (!primeRef && diffuseOnly) maxPL = std::min( maxPL, 2 );
 	if (G > 1) CHK_HIP( hipEventRecord( evFork, stream ) );   /* the other groups start after the accumulator reset */
 	for (int gi = 0; gi < G; gi++)
 	{
@@ -698,7 +707,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ta.rayO = g.rayO[g.in].ptr, ta.rayD = g.rayD[g.in].ptr, ta.segCounts = c->segActive, ta.segStride = g.segStride;
 			ta.cursor = g.cursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
 			ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
-			ta.packet = pathLength == 1 && tiledRays && UsePackets();
+			ta.packet = pathLength == 1 && tiledRays && UsePackets() ? PacketMode() : 0;
 			ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
 			ta.hits = g.hits.ptr, ta.gstack = g.gstack.ptr;
 			SetTail( ta, g );
@@ -728,7 +737,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				ts.cursor = g.cursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
 				ts.mask = g.shMask.ptr, ts.potentials = g.shP.ptr, ts.acc = accumulator.ptr, ts.gstack = g.gstack.ptr;
-				ts.packet = packetShadow;
+				ts.packet = packetShadow ? PacketMode() : 0;
 				SetTail( ts, g );
 				lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, g.evShadowB[pathLength] }, g.st );
 				g.fromShadowB[pathLength] = g.prevStop, g.prevStop = g.evShadowB[pathLength];
@@ -763,7 +772,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ta.rayO = g.shO.ptr, ta.rayD = g.shD.ptr, ta.segCounts = g.counters.ptr->segShadow, ta.segStride = g.shadowStride;
 			ta.cursor = g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 			ta.mask = g.shMask.ptr, ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = g.gstack.ptr;
-			ta.packet = packetShadow;
+			ta.packet = packetShadow ? PacketMode() : 0;
 			SetTail( ta, g );
 			lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, g.evShadow }, g.st );
 			g.fromShadow = g.prevStop;
@@ -934,7 +943,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	ta.version = traceVersion;
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
 	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
-	ta.packet = unitCoherent && UsePackets();
+	ta.packet = unitCoherent && UsePackets() ? PacketMode() : 0;
 	SetTail( ta, grp[0] );
 	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), {}, stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
@@ -956,7 +965,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	TraceArgs ta{};
 	ta.version = traceVersion;
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
-	ta.packet = unitCoherent && packetShadow;
+	ta.packet = unitCoherent && packetShadow ? PacketMode() : 0;
 	SetTail( ta, grp[0] );
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, {}, stream );
 	std::vector<uint32_t> tmp( words );
@@ -995,7 +1004,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 		ta.hits = (uint4*)hitsOut, ta.gstack = grp[0].gstack.ptr;
 		/* unitCoherent: trace as the frame traces its (tiled) primary rays */
 		ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
-		ta.packet = unitCoherent && UsePackets();
+		ta.packet = unitCoherent && UsePackets() ? PacketMode() : 0;
 #ifdef LH2_TRACE_STATS
 		ta.stats = tstats.ptr;
 #endif

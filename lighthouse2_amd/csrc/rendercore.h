@@ -189,6 +189,7 @@ private:
 	/* settings (rendercore.h DeviceVars; constant-memory defaults: .cuda.cu:38-39) */
 	float geometryEpsilon = 0.0f, clampValue = 10.0f;
 	int maxPathLength = 16;
+	bool diffuseOnly = false;            /* SetMaterials: no material can continue a path past its second vertex */
 	int primeRef = 0;                    /* RenderCore_PrimeRef validation mode (setting "primeRef") */
 	int probeX = 0, probeY = 0;
 	/* target + frame buffers */
@@ -217,6 +218,10 @@ private:
 	int unitCoherent = 0;
 	int packetPrimary = -1;              /* wave-uniform packet traversal for 8x8-tiled primary rays (-1: by scene size) */
 	float packetMaxMB = 16.0f;
+	/* packets over the BVH2 (2) or the BVH4 (4): BVH2 0.48 ms, BVH4 0.56 ms on the config-2 primary
+	   rays (r01c): fewer, wider steps do not pay when one node fetch already serves 64 rays */
+	int packetWidth = 2;
+	int PacketMode() const { return packetWidth == 4 ? 4 : 1; }
 	int packetShadow = 0;                /* the same for shadow rays (setting "packetShadow") */                /* traversal loop version (setting "traceVersion") */
 	int gpuBuild = 0, gpuTlas = 1;       /* BLAS builder (1: GPU PLOC, 0: CPU binned SAH); TLAS on the GPU */
 	float bvhTraversalCost = 1.0f;

@@ -235,10 +235,13 @@ def test_room_depth4_parity(core):
     core.setting("maxPathLength", 16)
 
 
+@pytest.mark.parametrize("version", [2, 4])
 @pytest.mark.parametrize("kind", ["random", "primary", "instanced"])
-def test_packet_traversal_bitexact(fresh_core, kind):
-    """Packet traversal (wave-uniform path for 64 rays, lh2_trace_packet.inc) gives every ray exactly
-    the per-ray traversal's hit record, also for incoherent rays and through instances."""
+def test_packet_traversal_bitexact(fresh_core, kind, version):
+    """Packet traversal (wave-uniform path for 64 rays, lh2_trace_packet.inc, over the BVH2 or the
+    BVH4) gives every ray exactly the per-ray traversal's hit record, also for incoherent rays and
+    through instances."""
+    fresh_core.setting("packetWidth", version)
     if kind == "instanced":
         sc = scene.instanced_scene(meshes=6, tris_per_mesh=3000, width=64, height=36, grid=3, spacing=12.0)
         scene.animate_instances(sc, 2)
@@ -262,8 +265,10 @@ def test_packet_traversal_bitexact(fresh_core, kind):
     assert np.array_equal(hp, ho), np.argwhere((hp != ho).any(1))[:10]
 
 
-def test_packet_shadow_rays_match(fresh_core):
+@pytest.mark.parametrize("version", [2, 4])
+def test_packet_shadow_rays_match(fresh_core, version):
     """Packet any-hit (fused finalizeConnection path and occlusion bits) equals the per-ray result."""
+    fresh_core.setting("packetWidth", version)
     sc = scene.config2_scene(n=20000, width=64, height=36)
     o = _load_both(fresh_core, sc, 64, 36)
     O4, D4 = _random_rays(30001, 4, tmin=0.0)
