@@ -504,8 +504,11 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 #include "lh2_trace_packet.inc"
 
 /* packet traversal of coherent (8x8-tiled primary) rays: wave-uniform, no LDS stack */
+/* 8 waves per SIMD (64 VGPRs, ~32 spilled outside the node loop): the packet loop is bound by the
+   latency of its dependent node fetches, and 8 waves hide more of it than the unbounded 94-VGPR
+   build's 5: 0.481 -> 0.437 ms on the config-2 primary rays (A/B 5/6/7/8 waves, r01c) */
 #ifndef LH2_PACKET_MINWAVES
-#define LH2_PACKET_MINWAVES 1
+#define LH2_PACKET_MINWAVES 8
 #endif
 template <int W>
 __global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet<0, W>( s, a ); }
@@ -1798,6 +1801,12 @@ void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int 
 		if (fused) LH2_LAUNCH( (k_trace_any<1, 1>), grid, 256, st, ev, *s, *a );
 		else LH2_LAUNCH( (k_trace_any<0, 1>), grid, 256, st, ev, *s, *a );
 	}
+}
+int lh2_packet_blocks_per_cu( void )
+{
+	int n = 0;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_closest_packet<2>, 256, 0 ) != hipSuccess) n = 4;
+	return n;
 }
 int lh2_trace_blocks_per_cu( void )
 {

@@ -106,6 +106,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	if (got != 65536 * 5) FatalError( "blue noise table truncated: %s", path.c_str() );
 	dBlueNoise.upload( bn.data(), bn.size(), stream );
 	blocksPerCU = maxBlocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
+	packetBlocksPerCU = std::max( 1, std::min( 8, lh2_packet_blocks_per_cu() ) );
 	for (int gi = 0; gi < LH2_MAX_GROUPS; gi++)
 	{
 		PathGroup& g = grp[gi];
@@ -711,7 +712,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
 			ta.hits = g.hits.ptr, ta.gstack = g.gstack.ptr;
 			SetTail( ta, g );
-			lh2_launch_trace_closest( &sd, &ta, grid, { nullptr, g.evTrace[pathLength] }, g.st );
+			lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : grid, { nullptr, g.evTrace[pathLength] }, g.st );
 			g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
 			ShadeParams sp{};
 			sp.segCounts = c->segActive, sp.segStride = g.segStride, sp.shadowStride = g.shadowStride;
@@ -945,7 +946,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
 	ta.packet = unitCoherent && UsePackets() ? PacketMode() : 0;
 	SetTail( ta, grp[0] );
-	lh2_launch_trace_closest( &sd, &ta, TraceGrid(), {}, stream );
+	lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : TraceGrid(), {}, stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	CheckSceneError();
@@ -1012,7 +1013,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 		ta.stats = ttimes.ptr;
 #endif
 		SetTail( ta, grp[0] );
-		lh2_launch_trace_closest( &sd, &ta, TraceGrid(), { ev[2 * i], ev[2 * i + 1] }, stream );
+		lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : TraceGrid(), { ev[2 * i], ev[2 * i + 1] }, stream );
 	}
 	CHK_HIP( hipStreamSynchronize( stream ) );
 #ifdef LH2_TRACE_TIMES

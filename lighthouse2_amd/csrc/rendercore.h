@@ -149,8 +149,9 @@ private:
 	bool UsePackets() const;
 	SceneDev MakeSceneDev() const;
 	int TraceGrid() const { return smCount * blocksPerCU; }
+	int PacketGrid() const { return smCount * packetBlocksPerCU; }   /* packet kernels: their own occupancy */
 
-	int device = 0, smCount = 256, blocksPerCU = 5, maxBlocksPerCU = 5;
+	int device = 0, smCount = 256, blocksPerCU = 5, maxBlocksPerCU = 5, packetBlocksPerCU = 5;
 	bool initialized = false;
 	/* scene */
 	std::vector<CoreMeshHost*> meshes;
