@@ -415,6 +415,10 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 
 void RenderCore::SetTail( TraceArgs& ta, PathGroup& g )
 {
+#ifndef LH2_TAIL_HANDOFF
+	(void)ta, (void)g;
+	return;   /* the traversal loop is compiled without the hand-off (lh2_trace2.inc) */
+#endif
 	if (!tailLanes || ta.packet) return;
 	const size_t threads = (size_t)TraceGrid() * 256;
 	if (g.tailRec.count < threads) g.tailRec.resize( threads ), g.tailUV.resize( threads );
