@@ -19,6 +19,11 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	int tiled;   /* store rays in 8x8 pixel blocks per wave (coherent traversal); 0 = row-major */
 	int slotBase;  /* this launch writes slots [slotBase, slotBase + jobCount) of the tile, at 0.. (path groups) */
 	int primeRef;  /* RenderCore_PrimeRef camera: uniform random numbers, no distortion (camera.h:57-60) */
+	/* folded into the camera launch (no launches of their own): the frame's counter / work-queue
+	   reset (initC non-null: what k_init_counters does), and the accumulator reset of a restart
+	   (clearAcc non-null: each pixel's first sample zeroes it; the memset of rendercore.cpp:465) */
+	Counters* initC; uint32_t* cursors; int cursorWords; uint32_t pathCount, segStride;
+	float4* clearAcc;
 };
 
 struct SceneDev       /* everything the traversal and shading kernels read, by value (kernarg) */
@@ -85,6 +90,10 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	   same closest hit (the hit does not depend on the visiting order) */
 	uint4* tailOut; float2* tailOutUV; uint32_t* tailCounts; uint32_t tailStride, tailLanes;
 	const uint4* tailIn; const float2* tailInUV;
+	/* tail pool (lh2_trace2.inc): once the queue is exhausted, a wave holding at most `pool` rays
+	   hands them, with their traversal state and stack, to another wave of its workgroup through
+	   LDS and exits (0: off) */
+	uint32_t pool;
 };
 /* traversal-loop statistics (diagnostic builds with -DLH2_TRACE_STATS; tools/trace_stats.py):
    wave-iterations, active-lane sum, leaf-phase iterations / lanes, walk iterations / lanes,

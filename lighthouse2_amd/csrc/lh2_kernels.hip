@@ -14,6 +14,7 @@
    Numerics: compiled with -ffp-contract=off and correctly rounded div/sqrt; every expression
    keeps the reference's evaluation order so results are bit-comparable with oracle/pt_oracle.c.
 */
+#include <algorithm>
 #include <hip/hip_ext.h>
 #include "lh2_device.h"
 #include "../../include/lh2_core_types.h"
@@ -132,10 +133,29 @@ LH2_DEV v3 RandomPointOnLens( const float r0, float r1, const v3 pos, const floa
 	return add3( pos, smul( aperture, add3( muls( right, xr ), muls( up, yr ) ) ) );
 }
 
+/* InitCountersForExtend (.cuda.cu:64-74) plus the frame's work-queue heads; thread i of the launch */
+LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_t segStride, uint32_t* cursors, const int cursorWords, const int i )
+{
+	if (i < cursorWords) cursors[i] = 0;
+	if (i < LH2_SEGS)
+	{
+		/* the camera writes the paths densely: segment i is [i * segStride, (i + 1) * segStride) */
+		const uint32_t lo = (uint32_t)i * segStride;
+		c->segActive[i * LH2_SEGCOUNT_STRIDE] = pathCount > lo ? min( pathCount - lo, segStride ) : 0u;
+		c->segExt[i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadow[i * LH2_SEGCOUNT_STRIDE] = 0;
+	}
+	if (i != 0) return;
+	c->activePaths = pathCount, c->extensionRays = 0, c->shadowRays = 0;
+	c->totalExtensionRays = pathCount, c->totalShadowRays = 0;
+	c->probedInstid = -1, c->probedTriid = -1, c->probedDist = 0;
+	c->reserved0 = 0, c->shadowOverflow = 0;
+}
+
 __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const uint8_t* __restrict__ bn, float4* __restrict__ rayO,
 	float4* __restrict__ rayD, float4* __restrict__ T4, float4* __restrict__ Q4, const int jobCount )
 {
 	const int local = threadIdx.x + blockIdx.x * blockDim.x;
+	if (p.initC) init_counters( p.initC, p.pathCount, p.segStride, p.cursors, p.cursorWords, local );
 	if (local >= jobCount) return;
 	const int slot = p.slotBase + local;
 	/* slot -> (sample, tile row, x) -> global jobIndex = x + (y + s * h) * w, as camera.h:48-53 */
@@ -198,6 +218,7 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 	rayD[local] = make_float4( rayDir.x, rayDir.y, rayDir.z, 1e34f );
 	T4[local] = make_float4( 1, 1, 1, bitsf( ((x + (y + (sampleIndex - (uint32_t)p.pass) * h) * w) << 8) + 1 /* S_SPECULAR */ ) );
 	Q4[local] = make_float4( 1, 0, 0, 0 );
+	if (p.clearAcc && sampleIndex == (uint32_t)p.pass) p.clearAcc[x + y * w] = make_float4( 0, 0, 0, 0 );
 }
 
 /* =====================================================================================
@@ -208,6 +229,13 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 #endif
 #define STACK_LDS LH2_STACK_LDS   /* entries per lane kept in LDS: 16 x 256 x 4 B = 16 KB / block */
 #define STACK_TOTAL LH2_STACK_TOTAL /* + global spill; the host checks the tree depth against it */
+
+/* tail pool of one workgroup (lh2_trace2.inc): rays handed between its waves once the work queue is
+   exhausted.  Field f of slot i at w[f * LH2_POOL_CAP + i] (a wave writes a field's 64 words
+   contiguously); lock / count / alive change only under the lock */
+#define LH2_POOL_CAP 64
+#define LH2_POOL_FIELDS 19
+struct TailPool { int lock, count, alive, pad; uint32_t w[LH2_POOL_FIELDS * LH2_POOL_CAP]; };
 
 LH2_DEV float safe_inv( float d ) { return (d > -1e-30f && d < 1e-30f) ? (d < 0 ? -1e30f : 1e30f) : 1.0f / d; }
 
@@ -519,8 +547,10 @@ template <bool PARK, int V>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_closest( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	if (V == 4) trace_stream2<0, PARK, 4>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
-	else if (V == 2) trace_stream2<0, PARK>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	__shared__ TailPool pool;
+	tail_pool_init( pool );
+	if (V == 4) trace_stream2<0, PARK, 4>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &pool );
+	else if (V == 2) trace_stream2<0, PARK>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &pool );
 	else trace_stream<0, PARK>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 }
 
@@ -528,8 +558,10 @@ template <int MODE, int V>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_any( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	if (V == 4) trace_stream2<MODE == 0 ? 1 : 2, true, 4>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
-	else if (V == 2) trace_stream2<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	__shared__ TailPool pool;
+	tail_pool_init( pool );
+	if (V == 4) trace_stream2<MODE == 0 ? 1 : 2, true, 4>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &pool );
+	else if (V == 2) trace_stream2<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &pool );
 	else trace_stream<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 }
 
@@ -1636,20 +1668,7 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const 
 
 __global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords )
 {
-	const int i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i < cursorWords) cursors[i] = 0;
-	if (i < LH2_SEGS)
-	{
-		/* the camera writes the paths densely: segment i is [i * segStride, (i + 1) * segStride) */
-		const uint32_t lo = (uint32_t)i * segStride;
-		c->segActive[i * LH2_SEGCOUNT_STRIDE] = pathCount > lo ? min( pathCount - lo, segStride ) : 0u;
-		c->segExt[i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadow[i * LH2_SEGCOUNT_STRIDE] = 0;
-	}
-	if (i != 0) return;
-	c->activePaths = pathCount, c->extensionRays = 0, c->shadowRays = 0;
-	c->totalExtensionRays = pathCount, c->totalShadowRays = 0;
-	c->probedInstid = -1, c->probedTriid = -1, c->probedDist = 0;
-	c->reserved0 = 0, c->shadowOverflow = 0;
+	init_counters( c, pathCount, segStride, cursors, cursorWords, blockIdx.x * blockDim.x + threadIdx.x );
 }
 __global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength, int resetShadow, uint32_t* hostActiveLog )
 {
@@ -1734,7 +1753,8 @@ void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int r
 }
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, LaunchEvents ev, hipStream_t st )
 {
-	LH2_LAUNCH( k_camera, jobCount > 0 ? (jobCount + 255) / 256 : 1, 256, st, ev, *p, bn, rayO, rayD, T4, Q4, jobCount );
+	const int threads = std::max( std::max( jobCount, 1 ), p->initC ? std::max( p->cursorWords, LH2_SEGS ) : 0 );
+	LH2_LAUNCH( k_camera, (threads + 255) / 256, 256, st, ev, *p, bn, rayO, rayD, T4, Q4, jobCount );
 }
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st )
 {

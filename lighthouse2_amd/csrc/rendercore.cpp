@@ -231,6 +231,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
 	else if (!strcmp( name, "packetWidth" )) packetWidth = value >= 4 ? 4 : 2;   /* packets over the BVH2 / BVH4 */
 	else if (!strcmp( name, "pathGroups" )) pathGroups = std::min( LH2_MAX_GROUPS, std::max( 1, (int)value ) );   /* pipelined path groups per frame */
+	else if (!strcmp( name, "tailPool" )) tailPool = std::min( 64, std::max( 0, (int)value ) );   /* hand a dry wave's rays to another wave of its workgroup (0: off) */
 	else if (!strcmp( name, "tailLanes" )) tailLanes = std::min( 64, std::max( 0, (int)value ) );   /* traversal tail hand-off (0: off) */
 	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (default: occupancy limit) */
 	{
@@ -415,6 +416,7 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 
 void RenderCore::SetTail( TraceArgs& ta, PathGroup& g )
 {
+	ta.pool = ta.packet ? 0u : (uint32_t)tailPool;
 #ifndef LH2_TAIL_HANDOFF
 	(void)ta, (void)g;
 	return;   /* the traversal loop is compiled without the hand-off (lh2_trace2.inc) */
@@ -642,9 +644,9 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const auto t0 = std::chrono::high_resolution_clock::now();
 	/* CoreStats timings come from the stop events recorded by the launches themselves (LaunchEvents):
 	   no hipEventRecord between kernels */
-	if (converge == LH2_RESTART || firstConvergingFrame)
+	const bool restart = converge == LH2_RESTART || firstConvergingFrame;
+	if (restart)
 	{
-		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
 		samplesTaken = 0;
 		firstConvergingFrame = true;
 		camRNGseed = 0x12345678;
@@ -659,6 +661,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	   run as one group */
 	const int G = pathCount >= 4096u * (uint32_t)pathGroups ? pathGroups : 1;
 	frameGroups = G;
+	/* the accumulator reset of a restart: one frame-wide memset when path groups run concurrently,
+	   else folded into the camera launch (each pixel's first sample zeroes it; rows outside this
+	   rank's tile stay zero from SetTarget / SetTileBands) */
+	if (restart && (G > 1 || tileChanged)) CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
 	/* primary rays (camera.h) for every sample of the tile */
 	CameraParams cp{};
 	cp.pos = view.pos, cp.p1 = view.p1;
@@ -690,12 +696,20 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		g.shadowStride = (uint32_t)(g.shO.count / LH2_SEGS);
 		g.in = 0, g.pl = 0, g.done = false;
 		if (gi) CHK_HIP( hipStreamWaitEvent( g.st, evFork, 0 ) );
-		lh2_launch_init_counters( g.counters.ptr, g.count, g.segStride, g.cursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, { nullptr, gi ? nullptr : evFrame[0] }, g.st );
+		/* the camera launch also resets the group's counters and work-queue heads (k_init_counters) */
 		CameraParams cg = cp;
 		cg.slotBase = (int)g.base;
-		lh2_launch_camera( &cg, dBlueNoise.ptr, g.rayO[0].ptr, g.rayD[0].ptr, g.T4[0].ptr, g.Q4[0].ptr, (int)g.count, { nullptr, g.evCamera }, g.st );
+		cg.initC = g.counters.ptr, cg.cursors = g.cursors.ptr, cg.cursorWords = LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS;
+		cg.pathCount = g.count, cg.segStride = g.segStride;
+		cg.clearAcc = restart && G == 1 && !tileChanged ? accumulator.ptr : nullptr;
+		lh2_launch_camera( &cg, dBlueNoise.ptr, g.rayO[0].ptr, g.rayD[0].ptr, g.T4[0].ptr, g.Q4[0].ptr, (int)g.count, { gi ? nullptr : evFrame[0], g.evCamera }, g.st );
 		g.prevStop = g.evCamera;
 	}
+	if (restart) tileChanged = false;
+	/* without lights no path samples one (RandomPointOnLight: lightPdf 0), so there are no shadow
+	   rays and their launches are not queued */
+	const bool shadows = nArea + nPoint + nSpot + nDir > 0;
+	frameShadows = shadows;
 	/* the bounce loop, the groups' launches interleaved */
 	for (int pathLength = 1; pathLength <= maxPL; pathLength++)
 	{
@@ -732,7 +746,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			lh2_launch_shade( &sd, &sp, grid, { nullptr, g.evShade[pathLength] }, g.st );
 			g.fromShade[pathLength] = g.prevStop, g.prevStop = g.evShade[pathLength];
 			if (pathLength == maxPL) { g.done = true; continue; }
-			if (primeRef)
+			if (primeRef && shadows)
 			{
 				/* RenderCore_PrimeRef traces the shadow rays of every bounce right after it
 				   (rendercore.cpp connect step), fused with finalizeConnections */
@@ -770,7 +784,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	for (int gi = 0; gi < G; gi++)
 	{
 		PathGroup& g = grp[gi];
-		if (!primeRef)
+		if (!primeRef && shadows)
 		{
 			TraceArgs ta{};
 			ta.version = traceVersion;
@@ -863,7 +877,8 @@ void RenderCore::Synchronize()
 		{
 			const PathGroup& g = grp[gi];
 			float sh = 0, sd = 0;
-			if (!framePrimeRef) sh = ms( g.fromShadow, g.evShadow );
+			if (!frameShadows) sh = 0;
+			else if (!framePrimeRef) sh = ms( g.fromShadow, g.evShadow );
 			else for (int L = 1; L < g.pl; L++) sh += ms( g.fromShadowB[L], g.evShadowB[L] );
 			for (int L = 1; L <= g.pl; L++) sd += ms( g.fromShade[L], g.evShade[L] );
 			shadow = std::max( shadow, sh ), shade = std::max( shade, sd );

@@ -117,9 +117,9 @@ public:
 	lh2_CoreStats GetCoreStats();
 
 	/* extensions beyond the reference ABI (tile partition, headless output, unit-level kernels) */
-	void SetTile( int y0, int y1 ) { tileY0 = y0, tileY1 = y1, tileBand = 0, tileStride = 0; }
+	void SetTile( int y0, int y1 ) { tileY0 = y0, tileY1 = y1, tileBand = 0, tileStride = 0, tileChanged = true; }
 	/* rank r of n owns the row bands [r*band + k*n*band, +band): balanced multi-GPU partition */
-	void SetTileBands( int rank, int nranks, int band ) { tileY0 = rank * band, tileY1 = -1, tileBand = band, tileStride = nranks * band; }
+	void SetTileBands( int rank, int nranks, int band ) { tileY0 = rank * band, tileY1 = -1, tileBand = band, tileStride = nranks * band, tileChanged = true; }
 	int TileRows() const;
 	void Synchronize();
 	void GetAccumulator( float* hostOut4 );                /* full frame, raw accumulator */
@@ -204,6 +204,9 @@ private:
 	int pathGroups = 1;
 	int frameGroups = 1;
 	hipEvent_t evFork = nullptr;
+	bool tileChanged = false;
+	bool frameShadows = true;            /* the last frame queued shadow-ray launches (the scene has lights) */            /* the next restart clears the whole accumulator, not only the tile's pixels */
+	int tailPool = 0;                    /* tail pool threshold: a dry wave with at most this many rays hands them to another wave of its workgroup (0: off) */
 	int tailLanes = 0;                   /* hand a dry wave's rays on when fewer are active (0: off; restarting them costs more than the tail, profiles/r01c_sweep_tail.txt) */
 	FrameStats* hostStats = nullptr;     /* pinned */
 	bool statsPending = false;

@@ -363,3 +363,66 @@ def test_path_groups_frame_parity(fresh_core, groups):
     assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
     st = fresh_core.stats()
     assert st.totalExtensionRays == int(o.ray_counts()[:16].sum()) or st.totalExtensionRays > 0
+
+
+@pytest.mark.parametrize("version,leaf_batch", [(2, 0), (4, 0), (4, 16)])
+@pytest.mark.parametrize("pool", [1, 16, 64])
+def test_tail_pool_bitexact(fresh_core, version, leaf_batch, pool):
+    """Rays handed between the waves of a workgroup through the LDS tail pool (setting tailPool)
+    resume with their traversal state and stack where they were: hit records and occlusion bits
+    stay the oracle's.  One block per CU makes each wave trace many rays, so pooling happens."""
+    fresh_core.setting("traceVersion", version)
+    fresh_core.setting("leafBatch", leaf_batch)
+    fresh_core.setting("traceBlocksPerCU", 1)
+    fresh_core.setting("tailPool", pool)
+    sc = scene.instanced_scene(meshes=4, tris_per_mesh=4000, width=64, height=36, grid=2, spacing=10.0)
+    scene.animate_instances(sc, 1)
+    o = _load_both(fresh_core, sc, 64, 36)
+    O4, D4 = _random_rays(200001, 21, radius=30.0)
+    hg = fresh_core.trace_closest(O4, D4)
+    ho = o.trace_closest(O4, D4)
+    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.05
+    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+    D4[:, 3] = np.random.default_rng(22).uniform(1.0, 40.0, len(D4)).astype(np.float32)
+    assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
+
+
+def test_tail_pool_deep_stack(fresh_core):
+    """Pooled rays whose stacks reach past the LDS part into the global spill area (a chain-like
+    BLAS) keep their spilled entries: the receiving lane adopts the stack column, LDS and global."""
+    k = np.arange(120, dtype=np.float32)
+    x = (6.0 * 0.93 ** k).astype(np.float32)
+    s_ = (0.02 * 0.93 ** k).astype(np.float32)
+    z0 = np.zeros_like(x)
+    v0, v1, v2 = np.stack([x, -s_, z0], 1), np.stack([x + s_, s_, z0], 1), np.stack([x - s_, s_, s_], 1)
+    sc = scene.config2_scene(n=5000, width=64, height=36)
+    sc.meshes.append(abi.tris_from_vertices(v0, v1, v2, 0))
+    sc.instances.append((1, np.eye(4, dtype=np.float32)))
+    fresh_core.setting("traceVersion", 4)
+    fresh_core.setting("traceBlocksPerCU", 1)
+    fresh_core.setting("tailPool", 64)
+    o = _load_both(fresh_core, sc, 64, 36)
+    O4, D4 = _random_rays(120001, 23)
+    rng = np.random.default_rng(24)
+    j = rng.integers(0, len(x), 60000)
+    d = ((v0[j] + v1[j] + v2[j]) / 3).astype(np.float32) - O4[:60000, :3]
+    D4[:60000, :3] = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    hg, ho = fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4)
+    assert (ho[:60000, 2] == 1).mean() > 0.2
+    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+
+
+@pytest.mark.parametrize("pool", [16, 64])
+def test_tail_pool_frame_parity(fresh_core, pool):
+    """A depth-4 room frame (closest and shadow rays) with the tail pool on matches the oracle."""
+    w, h = 192, 108
+    sc = scene.room_scene(40000, w, h)
+    o = _load_both(fresh_core, sc, w, h)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", 4)
+    fresh_core.setting("tailPool", pool)
+    sc.render_frame(fresh_core)
+    sc.render_frame(o)
+    assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
+    ag, ao = fresh_core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
