@@ -29,10 +29,11 @@ def band_rows(rank: int, nranks: int, height: int, band: int = BAND) -> np.ndarr
 def assemble(tiles, nranks: int, height: int, band: int = BAND, xp=np):
     """Rank 0: scatter the gathered per-rank row blocks (rows, width, 4) into the full frame."""
     width = tiles[0].shape[1]
-    out = xp.zeros((height, width, 4), dtype=tiles[0].dtype) if xp is np else None
+    # the ranks' bands partition the rows, so every row of the frame is written: no zero fill
+    out = xp.empty((height, width, 4), dtype=tiles[0].dtype) if xp is np else None
     if out is None:  # torch
         import torch
-        out = torch.zeros((height, width, 4), dtype=tiles[0].dtype, device=tiles[0].device)
+        out = torch.empty((height, width, 4), dtype=tiles[0].dtype, device=tiles[0].device)
         for r, t in enumerate(tiles):
             idx = torch.as_tensor(band_rows(r, nranks, height, band), device=t.device)
             out.index_copy_(0, idx, t)
