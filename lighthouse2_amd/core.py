@@ -69,6 +69,7 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
         "lh2_core_copy_accumulator_rows": [_P, _P, C.c_int, C.c_int],
         "lh2_core_ray_counts": [_P, _U],
         "lh2_core_pack_tile": [_P, _P],
+        "lh2_core_pack_tile_ordered": [_P, _P, _P],
         "lh2_core_tile_rows": [_P, C.POINTER(C.c_int)],
         "lh2_core_stream": [_P, C.POINTER(_P)],
         "lh2_core_trace_closest": [_P, _F, _F, C.c_int, _U],
@@ -222,12 +223,13 @@ class RenderCore:
         torch ops and collectives on the tile see the finished rows."""
         if order_torch:
             # the previous frame's gather may still read this tile on torch's / RCCL's stream: the core
-            # stream waits for it (GPU-side wait, so that gather overlaps this frame's rendering)
+            # stream waits for it (GPU-side wait, so that gather overlaps this frame's rendering), and
+            # torch's stream for the pack (the pack launch's own stop event: no marker between kernels)
             import torch
-            torch.cuda.ExternalStream(self.stream_ptr()).wait_stream(torch.cuda.current_stream())
-        self._chk(self.lib.lh2_core_pack_tile(self.h, C.c_void_p(device_ptr)))
-        if order_torch:
-            torch.cuda.current_stream().wait_stream(torch.cuda.ExternalStream(self.stream_ptr()))
+            s = torch.cuda.current_stream().cuda_stream
+            self._chk(self.lib.lh2_core_pack_tile_ordered(self.h, C.c_void_p(device_ptr), C.c_void_p(s)))
+        else:
+            self._chk(self.lib.lh2_core_pack_tile(self.h, C.c_void_p(device_ptr)))
 
     def stream_ptr(self) -> int:
         s = C.c_void_p()

@@ -172,6 +172,7 @@ LH2_EXPORT int lh2_core_get_accumulator( lh2_core c, float* out ) { return wrap(
 LH2_EXPORT int lh2_core_get_frame( lh2_core c, float* out ) { return wrap( [&] { R( c )->GetFrame( out ); } ); }
 LH2_EXPORT int lh2_core_copy_accumulator_rows( lh2_core c, void* dst, int y0, int y1 ) { return wrap( [&] { R( c )->CopyAccumulatorRows( dst, y0, y1 ); } ); }
 LH2_EXPORT int lh2_core_pack_tile( lh2_core c, void* dst ) { return wrap( [&] { R( c )->PackTile( dst ); } ); }
+LH2_EXPORT int lh2_core_pack_tile_ordered( lh2_core c, void* dst, void* consumerStream ) { return wrap( [&] { R( c )->PackTile( dst, true, consumerStream ); } ); }
 LH2_EXPORT int lh2_core_tile_rows( lh2_core c, int* rows ) { return wrap( [&] { *rows = R( c )->TileRows(); } ); }
 LH2_EXPORT int lh2_core_stream( lh2_core c, void** stream ) { return wrap( [&] { *stream = (void*)R( c )->stream; } ); }
 LH2_EXPORT int lh2_core_ray_counts( lh2_core c, uint32_t* out17 ) { return wrap( [&] { R( c )->GetRayCounts( out17 ); } ); }

@@ -1841,10 +1841,10 @@ void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, Launch
 	if (p->primeRef) LH2_LAUNCH( k_shade_ref, grid, 256, st, ev, *s, *p );
 	else LH2_LAUNCH( k_shade, grid, 256, st, ev, *s, *p );
 }
-void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, hipStream_t st )
+void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st )
 {
-	if (rows * w <= 0) return;
-	k_pack_rows<<<(rows * w + 255) / 256, 256, 0, st>>>( acc, dst, w, y0, band, bandStride, rows );
+	if (rows * w <= 0) { if (ev.stop) (void)hipEventRecord( ev.stop, st ); return; }
+	LH2_LAUNCH( k_pack_rows, (rows * w + 255) / 256, 256, st, ev, acc, dst, w, y0, band, bandStride, rows );
 }
 void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st )
 {

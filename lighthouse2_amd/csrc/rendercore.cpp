@@ -935,13 +935,29 @@ void RenderCore::CopyAccumulatorRows( void* devDst, int y0, int y1 )
 	CHK_HIP( hipStreamSynchronize( stream ) );
 }
 
-void RenderCore::PackTile( void* devDst )
+void RenderCore::PackTile( void* devDst, bool ordered, void* consumer )
 {
 	const int rows = TileRows();
 	const int band = tileBand > 0 ? tileBand : std::max( 1, rows ), stride = tileBand > 0 ? tileStride : std::max( 1, rows );
 	/* asynchronous: consumers on other streams order themselves after the core stream (lh2_core_stream),
 	   so the host can queue the next frame while this one finishes */
-	lh2_launch_pack_rows( accumulator.ptr, (float4*)devDst, scrwidth, std::max( 0, tileY0 ), band, stride, rows, stream );
+	if (!ordered)
+	{
+		lh2_launch_pack_rows( accumulator.ptr, (float4*)devDst, scrwidth, std::max( 0, tileY0 ), band, stride, rows, {}, stream );
+		return;
+	}
+	/* ordered with a consumer stream (torch's, whose gather reads devDst): the pack waits for the
+	   consumer's earlier work on devDst, and the consumer for the pack, through a marker on the
+	   consumer stream and the pack launch's own stop event (no marker between the core's kernels);
+	   consumer may be the null stream */
+	if (!evConsumer) CHK_HIP( hipEventCreateWithFlags( &evConsumer, hipEventDisableTiming ) );
+	if (!evPacked) CHK_HIP( hipEventCreate( &evPacked ) );
+	CHK_HIP( hipEventRecord( evConsumer, (hipStream_t)consumer ) );
+	/* the consumer's earlier work is usually long done (the previous frame's gather): then no wait
+	   (a wait packet costs the core stream ~9 us even when its event has completed) */
+	if (hipEventQuery( evConsumer ) != hipSuccess) CHK_HIP( hipStreamWaitEvent( stream, evConsumer, 0 ) );
+	lh2_launch_pack_rows( accumulator.ptr, (float4*)devDst, scrwidth, std::max( 0, tileY0 ), band, stride, rows, { nullptr, evPacked }, stream );
+	CHK_HIP( hipStreamWaitEvent( (hipStream_t)consumer, evPacked, 0 ) );
 }
 
 void RenderCore::GetFrame( float* hostOut4 )
@@ -1121,6 +1137,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	}
 	if (evFork) (void)hipEventDestroy( evFork );
 	evFork = nullptr;
+	for (hipEvent_t* e : { &evConsumer, &evPacked }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
 	for (auto& e : evFrame) (void)hipEventDestroy( e );
 	for (auto& e : evStage) (void)hipEventDestroy( e );
 	for (int i = 0; i < 2; i++) { if (stage[i]) (void)hipHostFree( stage[i] ); stage[i] = nullptr, stageBytes[i] = 0; }

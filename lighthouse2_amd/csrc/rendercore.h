@@ -124,7 +124,8 @@ public:
 	void Synchronize();
 	void GetAccumulator( float* hostOut4 );                /* full frame, raw accumulator */
 	void CopyAccumulatorRows( void* devDst, int y0, int y1 ); /* D2D copy of rows [y0,y1) */
-	void PackTile( void* devDst );                         /* owned rows, local order (async) */
+	void PackTile( void* devDst, bool ordered = false, void* consumer = nullptr );   /* owned rows, local order (async); ordered: with the stream consumer (null: the null stream) both ways */
+	hipEvent_t evConsumer = nullptr, evPacked = nullptr;
 	void GetFrame( float* hostOut4 );                      /* finalizeRender output: acc / samplesTaken */
 	int SamplesTaken() const { return samplesTaken; }
 	void GetRayCounts( uint32_t* out17 );
