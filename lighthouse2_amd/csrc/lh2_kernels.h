@@ -64,6 +64,10 @@ struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path st
 	uint32_t R0;
 	float spreadAngle;               /* ViewPyramid::spreadAngle: ray cone width per unit distance (texture LOD) */
 	int primeRef;                    /* RenderCore_PrimeRef shading (k_shade_ref) */
+	/* no lights, no material that can emit (colour > 1, colour maps) or cut out, pathLength > 1: a hit
+	   on a path that cannot extend (ENOUGH_BOUNCES or the last vertex) adds and emits nothing, so
+	   k_shade<true> drops it after reading its hit and flags (misses still sample the sky) */
+	int terminal;
 };
 
 struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (any) out */

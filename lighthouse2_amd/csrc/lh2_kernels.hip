@@ -1318,6 +1318,7 @@ LH2_DEV const float4* HitInstance( const SceneDev& s, const int primIdx, const i
 #ifndef LH2_SHADE_MINWAVES
 #define LH2_SHADE_MINWAVES 3
 #endif
+template <bool TERM>
 __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const SceneDev s, const ShadeParams p )
 {
 	/* the block's segment of the path stream (its XCD's), and the segment's share of the grid */
@@ -1334,7 +1335,11 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const Scen
 		{
 			/* the five input records first, all in flight together (the hit starts the dependent chain) */
 			const uint4 hd = p.hits[jobIndex];
-			const float4 T4 = p.T4[jobIndex], O4 = p.rayO[jobIndex], D4 = p.rayD[jobIndex], Q4 = p.Q4[jobIndex];
+			const float4 T4 = p.T4[jobIndex];
+			/* ShadeParams::terminal: a hit that cannot extend ends here with no contribution (emission
+			   at :127-153 needs colour > 1, NEE at :168-208 a light, :211 stops the extension) */
+			if (TERM && (int)hd.y != NOHIT && ((fbits( T4.w ) & ENOUGH_BOUNCES) || p.pathLength == p.maxPathLength)) goto compact;
+			const float4 O4 = p.rayO[jobIndex], D4 = p.rayD[jobIndex], Q4 = p.Q4[jobIndex];
 			__builtin_amdgcn_sched_barrier( 0 );
 			const float HIT_T = __uint_as_float( hd.x );
 			const int PRIMIDX = (int)hd.y;
@@ -1483,6 +1488,29 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const Scen
 				else atomicOr( &p.counters->shadowOverflow, 1u );
 			}
 		}
+	}
+}
+
+/* ShadeParams::terminal at the last vertex (pathLength == maxPathLength): k_shade<true> would drop
+   every hit, so the pass is the misses' sky samples (pathtracer.h:87-93, the same arithmetic as
+   k_shade's miss branch) and nothing else: a small kernel at full occupancy instead of the 3-wave
+   shade.  An all-zero contribution (no sky) is not added: x + 0 == x for every accumulator value */
+__global__ __launch_bounds__( 256 ) void k_shade_last( const SceneDev s, const ShadeParams p )
+{
+	const uint32_t seg = blockIdx.x % LH2_SEGS;
+	const uint32_t count = p.segCounts[seg * LH2_SEGCOUNT_STRIDE], segBase = seg * p.segStride;
+	const uint32_t gstride = ((gridDim.x - seg + LH2_SEGS - 1) / LH2_SEGS) * 256u;
+	const uint32_t wh = (uint32_t)(p.w * p.h);
+	for (uint32_t i = (blockIdx.x / LH2_SEGS) * 256u + threadIdx.x; i < count; i += gstride)
+	{
+		const uint32_t jobIndex = segBase + i;
+		if ((int)p.hits[jobIndex].y != NOHIT) continue;
+		const float4 T4 = p.T4[jobIndex], D4 = p.rayD[jobIndex], Q4 = p.Q4[jobIndex];
+		const uint32_t pixelIdx = (fbits( T4.w ) >> 8) % wh;
+		v3 contribution = muls( mul3( xyz( T4 ), SampleSkydome( s, xyz( D4 ) ) ), 1.0f / Q4.x );
+		contribution = clampintensity( s.clampValue, contribution );
+		contribution = fixnan( contribution );
+		if (contribution.x != 0 || contribution.y != 0 || contribution.z != 0) acc_add( p.acc, pixelIdx, contribution );
 	}
 }
 
@@ -1835,11 +1863,25 @@ int lh2_trace_blocks_per_cu( void )
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_any<1, 1>, 256, 0 ) != hipSuccess) n2 = 4;
 	return n1 > n2 ? n1 : n2;
 }
+static int lh2_shade_last_grid( void )   /* k_shade_last: every CU full (occupancy x CUs), at least a block per segment */
+{
+	static int g = 0;
+	if (!g)
+	{
+		int n = 0, dev = 0, cus = 0;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_shade_last, 256, 0 ) != hipSuccess || n < 1) n = 4;
+		if (hipGetDevice( &dev ) != hipSuccess || hipDeviceGetAttribute( &cus, hipDeviceAttributeMultiprocessorCount, dev ) != hipSuccess || cus < 1) cus = 256;
+		g = n * cus < LH2_SEGS ? LH2_SEGS : n * cus;
+	}
+	return g;
+}
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st )
 {
 	grid = grid < LH2_SEGS ? LH2_SEGS : grid;   /* every segment needs a block */
 	if (p->primeRef) LH2_LAUNCH( k_shade_ref, grid, 256, st, ev, *s, *p );
-	else LH2_LAUNCH( k_shade, grid, 256, st, ev, *s, *p );
+	else if (p->terminal && p->pathLength == p->maxPathLength) LH2_LAUNCH( k_shade_last, lh2_shade_last_grid(), 256, st, ev, *s, *p );
+	else if (p->terminal) LH2_LAUNCH( k_shade<true>, grid, 256, st, ev, *s, *p );
+	else LH2_LAUNCH( k_shade<false>, grid, 256, st, ev, *s, *p );
 }
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st )
 {

@@ -231,6 +231,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
 	else if (!strcmp( name, "packetWidth" )) packetWidth = value >= 4 ? 4 : 2;   /* packets over the BVH2 / BVH4 */
 	else if (!strcmp( name, "pathGroups" )) pathGroups = std::min( LH2_MAX_GROUPS, std::max( 1, (int)value ) );   /* pipelined path groups per frame */
+	else if (!strcmp( name, "terminalShade" )) terminalShade = value != 0;   /* drop hits that cannot contribute before shading them (ShadeParams::terminal) */
 	else if (!strcmp( name, "tailPool" )) tailPool = std::min( 64, std::max( 0, (int)value ) );   /* hand a dry wave's rays to another wave of its workgroup (0: off) */
 	else if (!strcmp( name, "tailLanes" )) tailLanes = std::min( 64, std::max( 0, (int)value ) );   /* traversal tail hand-off (0: off) */
 	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (default: occupancy limit) */
@@ -286,10 +287,15 @@ void RenderCore::SetMaterials( const lh2_CoreMaterial* mat, int n )   /* renderc
 {
 	std::vector<uint4> recs( (size_t)std::max( n, 1 ) * 8 );
 	memset( recs.data(), 0, recs.size() * sizeof( uint4 ) );
-	diffuseOnly = true;
+	diffuseOnly = true, canEmit = false;
 	for (int i = 0; i < n; i++)
 	{
 		const lh2_CoreMaterial& m = mat[i];
+		/* IsEmissive (colour > 1 after the fp16 round, which keeps x <= 1 at or below 1; NaN counts as
+		   emissive here), colour and detail maps (texels can exceed 1) and alpha cut-outs */
+		if (!(m.color.value.x <= 1.0f && m.color.value.y <= 1.0f && m.color.value.z <= 1.0f) || m.color.textureID != -1 ||
+			m.detailColor.textureID != -1 || (m.flags & 2))
+			canEmit = true;
 		/* a path can only continue past its second vertex through a specular event (ROUGHNESS <= 0.001,
 		   a transmission sample) or an alpha cut-out (ENOUGH_BOUNCES = S_BOUNCED, pathtracer.h:33,211) */
 		if (TOCHAR( m.roughness.value ) == 0 || TOCHAR( m.transmission.value ) != 0 || (m.flags & 2) || m.roughness.textureID != -1)
@@ -740,6 +746,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			sp.acc = accumulator.ptr, sp.counters = c;
 			sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
 			sp.primeRef = primeRef;
+			sp.terminal = !primeRef && !shadows && !canEmit && pathLength > 1 && terminalShade;
 			sp.probePixel = probeX + scrwidth * probeY;
 			sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
 			sp.spreadAngle = view.spreadAngle;

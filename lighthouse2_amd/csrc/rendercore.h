@@ -192,6 +192,7 @@ private:
 	float geometryEpsilon = 0.0f, clampValue = 10.0f;
 	int maxPathLength = 16;
 	bool diffuseOnly = false;            /* SetMaterials: no material can continue a path past its second vertex */
+	bool canEmit = true;                 /* SetMaterials: some material may shade as emissive (colour > 1 or colour maps) or cut out */
 	int primeRef = 0;                    /* RenderCore_PrimeRef validation mode (setting "primeRef") */
 	int probeX = 0, probeY = 0;
 	/* target + frame buffers */
@@ -207,7 +208,8 @@ private:
 	hipEvent_t evFork = nullptr;
 	bool tileChanged = false;
 	bool frameShadows = true;            /* the last frame queued shadow-ray launches (the scene has lights) */            /* the next restart clears the whole accumulator, not only the tile's pixels */
-	int tailPool = 0;                    /* tail pool threshold: a dry wave with at most this many rays hands them to another wave of its workgroup (0: off) */
+	bool terminalShade = true;           /* k_shade<true> for shade passes whose hits cannot contribute (ShadeParams::terminal) */
+	int tailPool = 0;                   /* tail pool threshold: a dry wave with at most this many rays hands them to another wave of its workgroup (0: off) */
 	int tailLanes = 0;                   /* hand a dry wave's rays on when fewer are active (0: off; restarting them costs more than the tail, profiles/r01c_sweep_tail.txt) */
 	FrameStats* hostStats = nullptr;     /* pinned */
 	bool statsPending = false;

@@ -426,3 +426,36 @@ def test_tail_pool_frame_parity(fresh_core, pool):
     assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
     ag, ao = fresh_core.accumulator(), o.accumulator()
     assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+
+
+@pytest.mark.parametrize("kind", ["diffuse", "emissive", "specular"])
+def test_terminal_shade_frame_parity(fresh_core, kind):
+    """Scenes without lights (the bench's config 2): the last shade pass drops hits that cannot
+    contribute (ShadeParams::terminal).  With an emissive quad but no light list the core must keep
+    shading them (its colour > 1 makes them emit).  With every other triangle a mirror, paths go on
+    past their second vertex, so the drop runs in mid-path shade passes (k_shade<true>) as well as in
+    the last one (k_shade_last).  Oracle parity, and the same frame with the drop switched off
+    matches to float-summation order."""
+    w, h = 160, 90
+    sc = scene.config2_scene(n=20000, width=w, height=h, sky=True, light=kind == "emissive")
+    sc.area_lights = []
+    if kind == "specular":
+        sc.materials.append(abi.make_material((0.9, 0.9, 0.9), roughness=0.0))
+        sc.meshes[0].view(np.uint32)[::2, abi.TRI["material"]] = 1
+    o = _load_both(fresh_core, sc, w, h)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", 5)
+    sc.render_frame(fresh_core)
+    sc.render_frame(o)
+    cg, co = fresh_core.ray_counts(), o.ray_counts()
+    assert np.array_equal(cg, co), (cg, co)
+    assert co[1] > 0 and (kind != "specular" or co[3] > 0), co
+    ag, ao = fresh_core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+    assert rel_l2(ag[..., 3], ao[..., 3]) <= 1e-6
+    fresh_core.setting("terminalShade", 0)
+    sc.render_frame(fresh_core)
+    a0 = fresh_core.accumulator()
+    fresh_core.setting("terminalShade", 1)
+    assert rel_l2(ag[..., :3], a0[..., :3]) <= 1e-6
+    assert np.array_equal(ag[..., 3], a0[..., 3])
