@@ -231,6 +231,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
 	else if (!strcmp( name, "packetWidth" )) packetWidth = value >= 4 ? 4 : 2;   /* packets over the BVH2 / BVH4 */
 	else if (!strcmp( name, "pathGroups" )) pathGroups = std::min( LH2_MAX_GROUPS, std::max( 1, (int)value ) );   /* pipelined path groups per frame */
+	else if (!strcmp( name, "singleInstanceStart" )) singleInstanceStart = value != 0;   /* one instance: rays start at its TLAS leaf */
 	else if (!strcmp( name, "terminalShade" )) terminalShade = value != 0;   /* drop hits that cannot contribute before shading them (ShadeParams::terminal) */
 	else if (!strcmp( name, "tailPool" )) tailPool = std::min( 64, std::max( 0, (int)value ) );   /* hand a dry wave's rays to another wave of its workgroup (0: off) */
 	else if (!strcmp( name, "tailLanes" )) tailLanes = std::min( 64, std::max( 0, (int)value ) );   /* traversal tail hand-off (0: off) */
@@ -630,6 +631,12 @@ SceneDev RenderCore::MakeSceneDev() const
 	s.argb32Count = (uint32_t)dArgb32.count, s.nrm32Count = (uint32_t)dNrm32.count;
 	s.tlasRoot = tlasRoot, s.instCount = (int)instances.size();
 	s.nodes4 = dNodes4.ptr, s.tlasRoot4 = blasNode4Count;
+	/* one instance of a non-empty mesh: rays start at its TLAS leaf (MAKE_LEAF( 0, 1 ) = ~0) and skip
+	   the TLAS root's box test, which can only cull (TopLevelBVH::Traverse bvh.cpp:594-649); the
+	   instance transform runs as at the leaf, so the hits are unchanged: one loop iteration less per ray */
+	if (singleInstanceStart && instances.size() == 1 && instances[0].mesh >= 0 && instances[0].mesh < (int)meshes.size() &&
+		meshes[instances[0].mesh]->triCount > 0)
+		s.tlasRoot = s.tlasRoot4 = ~0;
 	s.instDesc = dInstDesc.ptr, s.materials = dMaterials.ptr;
 	s.areaLights = dArea.ptr, s.pointLights = dPoint.ptr, s.spotLights = dSpot.ptr, s.dirLights = dDir.ptr;
 	s.nArea = nArea, s.nPoint = nPoint, s.nSpot = nSpot, s.nDir = nDir;

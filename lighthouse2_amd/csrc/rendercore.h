@@ -208,7 +208,8 @@ private:
 	hipEvent_t evFork = nullptr;
 	bool tileChanged = false;
 	bool frameShadows = true;            /* the last frame queued shadow-ray launches (the scene has lights) */            /* the next restart clears the whole accumulator, not only the tile's pixels */
-	bool terminalShade = true;           /* k_shade<true> for shade passes whose hits cannot contribute (ShadeParams::terminal) */
+	bool singleInstanceStart = true;     /* one instance of a non-empty mesh: rays start at its TLAS leaf (SceneDev::tlasRoot) */
+	bool terminalShade = true;          /* k_shade<true> for shade passes whose hits cannot contribute (ShadeParams::terminal) */
 	int tailPool = 0;                   /* tail pool threshold: a dry wave with at most this many rays hands them to another wave of its workgroup (0: off) */
 	int tailLanes = 0;                   /* hand a dry wave's rays on when fewer are active (0: off; restarting them costs more than the tail, profiles/r01c_sweep_tail.txt) */
 	FrameStats* hostStats = nullptr;     /* pinned */
