@@ -1318,8 +1318,14 @@ LH2_DEV const float4* HitInstance( const SceneDev& s, const int primIdx, const i
 #ifndef LH2_SHADE_MINWAVES
 #define LH2_SHADE_MINWAVES 3
 #endif
-template <bool TERM>
-__global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const SceneDev s, const ShadeParams p )
+#ifndef LH2_SHADE_NL_MINWAVES
+#define LH2_SHADE_NL_MINWAVES 4   /* 128 VGPRs, 9 spilled; 3 waves: 144, none (A/B: profiles/r01g_ab_shade_nolights.jsonl) */
+#endif
+/* NL: a scene without lights.  NEE (pathtracer.h:168-208) then never yields a shadow ray
+   (RandomPointOnLight: lightPdf 0), so its code is compiled out, except the two random numbers it
+   draws past sample 1, which later draws depend on */
+template <bool TERM, bool NL>
+__global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAVES ) void k_shade( const SceneDev s, const ShadeParams p )
 {
 	/* the block's segment of the path stream (its XCD's), and the segment's share of the grid */
 	const uint32_t seg = blockIdx.x % LH2_SEGS;
@@ -1416,7 +1422,8 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade( const Scen
 				const float faceDir = (dot3( D, N ) > 0) ? -1 : 1;
 				if (faceDir == 1) sd.transmittance = s3( 0 );
 				throughput = muls( throughput, 1.0f / bsdfPdf );
-				if (!(data & S_SPECULAR))
+				if (NL && !(data & S_SPECULAR) && sampleIdx >= 2) (void)RandomFloat( seed ), (void)RandomFloat( seed );
+				if (!NL && !(data & S_SPECULAR))
 				{
 					float r0, r1, pickProb = 0, lightPdf = 0;
 					if (sampleIdx < 2) r0 = bnv[0], r1 = bnv[1];
@@ -1880,8 +1887,9 @@ void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, Launch
 	grid = grid < LH2_SEGS ? LH2_SEGS : grid;   /* every segment needs a block */
 	if (p->primeRef) LH2_LAUNCH( k_shade_ref, grid, 256, st, ev, *s, *p );
 	else if (p->terminal && p->pathLength == p->maxPathLength) LH2_LAUNCH( k_shade_last, lh2_shade_last_grid(), 256, st, ev, *s, *p );
-	else if (p->terminal) LH2_LAUNCH( k_shade<true>, grid, 256, st, ev, *s, *p );
-	else LH2_LAUNCH( k_shade<false>, grid, 256, st, ev, *s, *p );
+	else if (p->terminal) LH2_LAUNCH( (k_shade<true, true>), grid, 256, st, ev, *s, *p );
+	else if (s->nArea + s->nPoint + s->nSpot + s->nDir == 0) LH2_LAUNCH( (k_shade<false, true>), grid, 256, st, ev, *s, *p );
+	else LH2_LAUNCH( (k_shade<false, false>), grid, 256, st, ev, *s, *p );
 }
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st )
 {

@@ -485,3 +485,22 @@ def test_single_instance_start_bitexact(fresh_core, version, start):
         sc.render_frame(fresh_core)
         sc.render_frame(o)
         assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
+
+
+def test_no_lights_rng_stream_past_sample_256(fresh_core):
+    """Without lights the shade kernel compiles NEE out (k_shade<*, NL>) but still draws its two random
+    numbers past sample 1: from sample 256 on the BSDF sample uses the same seed's later draws, so
+    a missing draw would change every extension direction there."""
+    w, h, spp = 16, 9, 260
+    sc = scene.config2_scene(n=20000, width=w, height=h, sky=True)
+    sc.materials.append(abi.make_material((0.9, 0.9, 0.9), roughness=0.0))
+    sc.meshes[0].view(np.uint32)[::2, abi.TRI["material"]] = 1
+    o = _load_both(fresh_core, sc, w, h, spp=spp)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", 4)
+    sc.render_frame(fresh_core)
+    sc.render_frame(o)
+    cg, co = fresh_core.ray_counts(), o.ray_counts()
+    assert np.array_equal(cg, co), (cg, co)
+    ag, ao = fresh_core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
