@@ -20,14 +20,26 @@ def pytest_configure(config):
 
 
 def _ensure_built():
-    lib = ROOT / "lighthouse2_amd" / "libRenderCore_MI355X.so"
+    """Build (incrementally) unless the library already carries the checked-out sources' hash; then
+    refuse to test a library built from other sources (lh2_version() "srchash=...")."""
+    from lighthouse2_amd import build_info
     orc = ROOT / "oracle" / "liboracle.so"
-    if not lib.exists() or not orc.exists():
+    want = build_info.source_hash()
+    if build_info.library_hash() != want or not orc.exists():
         import __graft_entry__
         __graft_entry__.build()
+    got = build_info.library_hash()
+    if got != want:
+        raise RuntimeError(f"libRenderCore_MI355X.so srchash={got} but the sources hash to {want}")
+    print(f"lighthouse2_amd: libRenderCore_MI355X.so srchash={got} (matches sources)", file=sys.stderr)
 
 
 _ensure_built()
+
+
+def pytest_report_header(config):
+    from lighthouse2_amd import build_info
+    return f"libRenderCore_MI355X.so srchash={build_info.library_hash()} sources={build_info.source_hash()}"
 
 
 @pytest.fixture(scope="session")
