@@ -161,8 +161,11 @@ class Scene:
         if self.textures:
             core.set_textures(self.textures)
         core.set_materials(self.materials)
-        for i, m in enumerate(self.meshes):
-            core.set_geometry(i, m)
+        if hasattr(core, "set_geometries"):      # the CPU oracle builds its meshes' BVHs in parallel
+            core.set_geometries(self.meshes)
+        else:
+            for i, m in enumerate(self.meshes):
+                core.set_geometry(i, m)
         for i, (mesh, T) in enumerate(self.instances):
             core.set_instance(i, mesh, T)
         core.set_instance(len(self.instances), -1, None)

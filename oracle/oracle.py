@@ -46,7 +46,7 @@ def lib() -> C.CDLL:
         L.orc_create.restype = _P
         sig = {
             "orc_destroy": [_P], "orc_set_bluenoise": [_P, C.POINTER(C.c_uint8)], "orc_set_max_path_length": [_P, C.c_int],
-            "orc_set_geometry": [_P, C.c_int, _P, C.c_int], "orc_set_instance": [_P, C.c_int, C.c_int, _F],
+            "orc_set_geometry": [_P, C.c_int, _P, C.c_int], "orc_set_geometry_many": [_P, C.c_int, C.c_int, _P, _P, C.c_int], "orc_set_instance": [_P, C.c_int, C.c_int, _F],
             "orc_update_toplevel": [_P], "orc_set_materials": [_P, _P, C.c_int],
             "orc_set_lights": [_P, _P, C.c_int, _P, C.c_int, _P, C.c_int, _P, C.c_int],
             "orc_set_sky": [_P, _F, C.c_int, C.c_int], "orc_set_textures": [_P, _P, C.c_int],
@@ -161,6 +161,14 @@ class Oracle:
     def set_geometry(self, idx, tris):
         tris = np.ascontiguousarray(tris, np.float32)
         self.L.orc_set_geometry(self.o, idx, tris.ctypes.data_as(_P), len(tris))
+
+    def set_geometries(self, meshes, first=0):
+        """SetGeometry for every mesh, the per-mesh builds spread over the oracle's threads."""
+        keep = [np.ascontiguousarray(m, np.float32) for m in meshes]
+        ptrs = (C.c_void_p * max(1, len(keep)))(*[k.ctypes.data for k in keep])
+        counts = np.array([len(k) for k in keep] or [0], np.int32)
+        self.L.orc_set_geometry_many(self.o, int(first), len(keep), C.cast(ptrs, _P), counts.ctypes.data_as(_P),
+                                     self.threads)
 
     def set_instance(self, idx, mesh, T=None):
         m = np.ascontiguousarray(np.eye(4, dtype=np.float32) if T is None else T, np.float32)

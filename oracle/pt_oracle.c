@@ -331,6 +331,37 @@ void orc_set_geometry( Oracle* o, int meshIdx, const lh2_CoreTri* tris, int T )
 	if (T > 0) { bart_subdivide( m, 0 ); bart_update_bounds( m ); }
 }
 
+/* test-infrastructure convenience: SetGeometry for meshes [first, first+count) built on nthreads threads
+   (each mesh's build is the single-threaded restatement above; meshes are independent) */
+typedef struct { Oracle* o; int first, count; const lh2_CoreTri* const* tris; const int* counts; int t, nt; } GeomJob;
+static void* geom_worker( void* p )
+{
+	GeomJob* j = (GeomJob*)p;
+	for (int i = j->t; i < j->count; i += j->nt) orc_set_geometry( j->o, j->first + i, j->tris[i], j->counts[i] );
+	return 0;
+}
+void orc_set_geometry_many( Oracle* o, int first, int count, const lh2_CoreTri* const* tris, const int* counts, int nthreads )
+{
+	if (count <= 0) return;
+	if (first + count > o->meshCount)
+	{
+		o->meshes = (Mesh*)realloc( o->meshes, sizeof( Mesh ) * (first + count) );
+		for (int i = o->meshCount; i < first + count; i++) memset( &o->meshes[i], 0, sizeof( Mesh ) );
+		o->meshCount = first + count;
+	}
+	if (nthreads < 1) nthreads = 1;
+	if (nthreads > count) nthreads = count;
+	GeomJob* jobs = (GeomJob*)calloc( nthreads, sizeof( GeomJob ) );
+	pthread_t* th = (pthread_t*)calloc( nthreads, sizeof( pthread_t ) );
+	for (int t = 0; t < nthreads; t++)
+	{
+		jobs[t] = (GeomJob){ o, first, count, tris, counts, t, nthreads };
+		if (nthreads > 1) pthread_create( &th[t], 0, geom_worker, &jobs[t] ); else geom_worker( &jobs[t] );
+	}
+	if (nthreads > 1) for (int t = 0; t < nthreads; t++) pthread_join( th[t], 0 );
+	free( jobs ); free( th );
+}
+
 /* mat4::Inverted, RenderSystem/common_types.h:586-628 (MESA formula) */
 void orc_mat4_inverse( const float* c, float* out )
 {

@@ -35,6 +35,7 @@ void orc_destroy( Oracle* o );
 void orc_set_bluenoise( Oracle* o, const uint8_t* table327680 );
 void orc_set_max_path_length( Oracle* o, int maxPathLength );
 void orc_set_geometry( Oracle* o, int meshIdx, const lh2_CoreTri* tris, int triCount );
+void orc_set_geometry_many( Oracle* o, int first, int count, const lh2_CoreTri* const* tris, const int* counts, int nthreads );
 void orc_set_instance( Oracle* o, int instIdx, int meshIdx, const float* mat16 );
 void orc_update_toplevel( Oracle* o );
 void orc_set_materials( Oracle* o, const lh2_CoreMaterial* mats, int count );

@@ -1,0 +1,119 @@
+"""Summaries of tools/pmc_round.sh (gpurun_out/pmc) committed under profiles/ for bench.py's roofline:
+
+  profiles/<tag>_pmc_trace_sq.json       SQ issue counters of the dominant kernel, per launch (median
+                                         over launches): VALU wave-instructions, VALU lane utilisation,
+                                         effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration), and the
+                                         VALU issue rate against the SIMD-32 peak (a wave64 VALU
+                                         instruction takes 2 cycles of one SIMD: MI355X_MICROARCH.md,
+                                         per-instruction constants; 1024 SIMDs).
+  profiles/<tag>_pmc_config5_traffic.json  HBM bytes per launch of every kernel of config-5 frames
+                                         (2 x FETCH_SIZE per the gfx950 calibration + WRITE_SIZE, KiB ->
+                                         B), each from its own --pmc pass, and the achieved GB/s.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import json
+import pathlib
+import statistics
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+SIMDS = 256 * 4
+CLOCK_GHZ = 2.4
+
+
+def dispatches(path, kernel=None):
+    """{dispatch id: {"kernel", "ns", counter: value}} from a rocprofv3 counter_collection.csv."""
+    out = collections.OrderedDict()
+    for r in csv.DictReader(open(path)):
+        if kernel and kernel not in r["Kernel_Name"]:
+            continue
+        d = out.setdefault(r["Dispatch_Id"], {"kernel": r["Kernel_Name"],
+                                              "ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return out
+
+
+def med(ds, key):
+    return statistics.median(d[key] for d in ds)
+
+
+def trace_sq(src, kernel):
+    ds = list(dispatches(src / "sq1" / "run_counter_collection.csv", kernel).values())
+    ds2 = list(dispatches(src / "sq2" / "run_counter_collection.csv", kernel).values())
+    ns = med(ds, "ns")
+    valu = med(ds, "SQ_INSTS_VALU")
+    clk = med(ds, "GRBM_GUI_ACTIVE") / 8 / ns           # GHz (sum over the 8 XCDs)
+    cycles = ns * clk
+    rate = valu / ns                                   # G wave-instructions / s
+    peak = SIMDS * CLOCK_GHZ / 2
+    counters = {k: med(ds, k) for k in ds[0] if k.startswith(("SQ_", "GRBM_"))}
+    counters.update({k: med(ds2, k) for k in ds2[0] if k.startswith("SQ_")})
+    return {
+        "kernel": f"{kernel} (config-2 bounce rays from the 1080p primary hits, tools/trace_kernel_bench.py --set bounce)",
+        "launches": len(ds), "launch_ms_median": ns / 1e6,
+        "counters_per_launch_median": counters,
+        "effective_clock_ghz": round(clk, 3),
+        "valu_wave_insts_per_launch": valu,
+        "valu_issue_rate_g_per_s": round(rate, 1),
+        "valu_issue_peak_g_per_s": peak,
+        "valu_issue_frac": round(rate / peak, 4),
+        "valu_issue_frac_at_effective_clock": round(valu * 2 / (SIMDS * cycles), 4),
+        "valu_lane_utilisation": round(counters["SQ_THREAD_CYCLES_VALU"] / (64 * counters["SQ_ACTIVE_INST_VALU"]), 4),
+        "valu_busy_frac_quad_cycles": round(counters["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cycles), 4),
+        "wave_cycles_waiting_frac": round(counters["SQ_WAIT_ANY"] / counters["SQ_WAVE_CYCLES"], 4)
+        if "SQ_WAIT_ANY" in counters else None,
+        "note": "VALU issue peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (SIMD-32); "
+                "SQ_ACTIVE_INST_* and SQ_WAVE_CYCLES count quad-cycles (MI355X_MICROARCH.md)",
+    }
+
+
+def config5_traffic(src):
+    f = dispatches(src / "c5_fetch" / "run_counter_collection.csv")
+    w = dispatches(src / "c5_write" / "run_counter_collection.csv")
+    per = collections.defaultdict(lambda: {"fetch": [], "write": [], "ns": []})
+    for d in f.values():
+        per[d["kernel"]]["fetch"].append(2.0 * d["FETCH_SIZE"] * 1024.0)
+        per[d["kernel"]]["ns"].append(d["ns"])
+    for d in w.values():
+        per[d["kernel"]]["write"].append(d["WRITE_SIZE"] * 1024.0)
+        per[d["kernel"]]["ns"].append(d["ns"])
+    rows = []
+    for k, v in per.items():
+        if len(v["fetch"]) < 3 or not v["write"]:
+            continue
+        b = statistics.median(v["fetch"]) + statistics.median(v["write"])
+        ns = statistics.median(v["ns"])
+        rows.append({"kernel": k, "launches": len(v["fetch"]), "bytes_per_launch": b,
+                     "fetch_bytes": statistics.median(v["fetch"]), "write_bytes": statistics.median(v["write"]),
+                     "launch_ms_median": ns / 1e6, "hbm_gb_s": round(b / ns, 1), "hbm_frac": round(b / ns / 8000.0, 4)})
+    rows.sort(key=lambda r: -r["launch_ms_median"] * r["launches"])
+    return {"workload": "config 5: 100 x 100k-triangle instanced meshes, per-frame TLAS, 1920x1080 8 spp "
+                        "(tools/bench_configs.py --configs 5 --frames 3 --warmup 1)",
+            "kernels": rows,
+            "note": "HBM bytes = 2 x FETCH_SIZE (gfx950 calibration) + WRITE_SIZE per launch (medians over "
+                    "launches, separate --pmc passes); FETCH_SIZE also counts Infinity-Cache hits, so this "
+                    "is an upper bound of DRAM traffic"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--src", default=str(ROOT / "gpurun_out" / "pmc"))
+    ap.add_argument("--kernel", default="k_trace_closest<false, 4>")
+    a = ap.parse_args()
+    src = pathlib.Path(a.src)
+    dst = ROOT / "profiles"
+    sq = trace_sq(src, a.kernel)
+    (dst / f"{a.tag}_pmc_trace_sq.json").write_text(json.dumps(sq, indent=1) + "\n")
+    print(json.dumps(sq, indent=1))
+    if (src / "c5_fetch").exists():
+        c5 = config5_traffic(src)
+        (dst / f"{a.tag}_pmc_config5_traffic.json").write_text(json.dumps(c5, indent=1) + "\n")
+        print(json.dumps(c5, indent=1))
+
+
+if __name__ == "__main__":
+    main()
