@@ -3,17 +3,23 @@
 Workload (BASELINE.json configs[1]): 100k random triangles (xorshift32 seed
 0x12345678, v0 ~ U[-5,5]^3, edge 0.5), camera (0,0,-12) -> +z, FOV 40, 16:9, material white 0.8
 roughness 1.  One step = one complete frame of the wavefront path tracer through the reference
-CoreAPI (camera rays, closest-hit BVH2 traversal, shade/extend/NEE, next bounce, shadow rays,
+CoreAPI (camera rays, closest-hit BVH traversal, shade/extend/NEE, next bounce, shadow rays,
 finalize) = primary + secondary extension rays (ENOUGH_BOUNCES = S_BOUNCED ends diffuse paths
 after the second vertex, pathtracer.h:33,211), plus, for N > 1, the accumulator gather to rank 0.
 
-Multi-GPU (weak scaling): with N ranks the frame is 1920 x (1080 N) pixels of the same 16:9 view,
-dealt in 8-row bands round-robin, so each GPU traces a 1080p frame's worth of paths per step.
+Multi-GPU, two measurements per run:
+  value (weak scaling): with N ranks the frame is 1920 x (1080 N) pixels of the same 16:9 view,
+    dealt in 8-row bands round-robin, so each GPU traces a 1080p frame's worth of paths per step;
+  "config4" (strong scaling, BASELINE.json configs[3]): the config-3 scene (1M-triangle room,
+    maxPathLength 4, lights) at 3840 x 2160, 1 spp, the same frame split across the N ranks in
+    8-row bands, gathered to rank 0 over RCCL every frame.
+Both: time = max over ranks of the K-step time between barriers; value = rays of all ranks / time.
 
-value = (primary + secondary rays of all ranks) x K / (max over ranks of the K-step time).
-The roofline object is for the dominant kernel (closest-hit traversal) measured with HIP events
-on the core's stream: algorithmic bytes per ray = 32 (ray) + 20 (hit) + 32 n_node + 36 n_tri with
-n from the committed reference-traversal fixture (tests/golden/config2_visits.json).
+roofline: the dominant kernel (the per-ray BVH4 closest-hit traversal of the frame's bounce rays),
+timed live with the HIP events its launches record, priced by the resource the counters say binds
+it: VALU issue (SQ_INSTS_VALU per launch, rocprofv3 --pmc, profiles/*_pmc_trace_sq.json) against
+the chip's VALU issue peak.  The HBM view is kept beside it: measured bytes per launch (FETCH_SIZE /
+WRITE_SIZE passes, profiles/*_pmc_traffic.json) and the SURVEY §8(d) algorithmic byte model.
 """
 from __future__ import annotations
 
@@ -33,16 +39,43 @@ sys.path.insert(0, str(ROOT))
 import torch  # noqa: E402  (import before the core: one HIP runtime in the process)
 import torch.distributed as dist  # noqa: E402
 
-from lighthouse2_amd import scene  # noqa: E402
+from lighthouse2_amd import build_info, scene  # noqa: E402
 from lighthouse2_amd.core import RenderCore  # noqa: E402
-from lighthouse2_amd.parallel import BAND, band_rows, gather_tiles  # noqa: E402
+from lighthouse2_amd.parallel import BAND, TileGather  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+SIMDS, CLOCK_GHZ = 256 * 4, 2.4
+# the per-ray closest-hit kernel of incoherent rays per traversal loop version (rocprofv3 names)
+TRACE_KERNEL = {4: "k_trace_closest<false, 4>", 5: "k_trace_closest4d"}
 
 
 def log(msg):
     if int(os.environ.get("RANK", "0")) == 0:
         print(msg, file=sys.stderr, flush=True)
+
+
+def newest(pattern, pred=lambda d: True):
+    """(path, dict) of the newest committed profile summary matching pattern and pred."""
+    for f in sorted(glob.glob(str(ROOT / "profiles" / pattern)), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if pred(d):
+            return pathlib.Path(f).name, d
+    return None, None
+
+
+def valu_cycles_per_instruction():
+    """Measured SIMD cycles per wave64 v_fma_f32 at full occupancy (tools/valu_rate, committed under
+    profiles/); 2 (SIMD-32, MI355X_MICROARCH.md per-instruction constants) when absent."""
+    files = sorted(glob.glob(str(ROOT / "profiles" / "*valu_rate*.jsonl")))
+    if files:
+        rows = [json.loads(line) for line in open(files[-1]) if line.strip().startswith("{")]
+        rows = [r for r in rows if r.get("waves_per_simd", 0) >= 4]
+        if rows:
+            return min(r["cycles_per_wave_inst"] for r in rows), pathlib.Path(files[-1]).name
+    return 2.0, None
 
 
 def cpu_baseline(sc, width, height, seconds):
@@ -91,17 +124,125 @@ def cpu_baseline(sc, width, height, seconds):
                       f"{threads} threads, {el:.1f} s"}
 
 
-def latest_pmc_traffic():
-    """HBM bytes per closest-hit launch from the committed rocprofv3 --pmc summary (FETCH_SIZE doubled
-    per the gfx950 calibration in MI355X_MICROARCH.md §HBM, WRITE_SIZE as is), if present."""
-    files = sorted(glob.glob(str(ROOT / "profiles" / "*pmc_traffic*.json")))
-    if not files:
-        return None
-    try:
-        d = json.load(open(files[-1]))
-        return d.get("bytes_per_launch")
-    except Exception:
-        return None
+def timed_frames(core, sc, gather, steps, warmup, world, dev, per_frame=None):
+    """warmup + steps frames (render, pack the owned rows, gather); returns (max-over-ranks seconds,
+    rays of all ranks per frame [primary + bounce 1, deeper, shadow], this rank's counts)."""
+    def step():
+        sc.render_frame(core, converge=1)     # Restart: the same paths every step
+        core.pack_tile(gather.send.data_ptr())    # owned accumulator rows (ordered with torch's stream)
+        return gather.gather()
+
+    for _ in range(warmup):
+        step()
+    counts = core.ray_counts()
+    tot = torch.tensor([int(counts[0]) + int(counts[1]), int(counts[2:16].sum()), int(counts[16])], dtype=torch.int64,
+                       device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return float(el.item()), [int(x) for x in tot.tolist()], counts
+
+
+def config4(args, rank, world, local, dev):
+    """BASELINE configs[3]: 4K 1 spp of the config-3 room, the frame split across the ranks (strong
+    scaling), RCCL gather of the accumulator rows to rank 0 every frame."""
+    W4, H4 = 3840, 2160
+    sc = scene.room_scene(args.room_tris, W4, H4)
+    core = RenderCore(device=local)
+    core.setting("maxPathLength", 4)
+    for kv in args.setting:
+        k, v = kv.split("=")
+        core.setting(k, float(v))
+    sc.load_into(core)
+    core.set_target(W4, H4, 1)
+    core.set_tile_bands(rank, world, BAND)
+    g = TileGather(rank, world, W4, H4, dev)
+    assert core.tile_rows() == g.rows
+    el, tot, _ = timed_frames(core, sc, g, args.config4_steps, args.warmup, world, dev)
+    core.close()
+    return {"workload": f"config4: room {sc.tri_count} tris (config-3 scene, maxPathLength 4, 2 area lights), "
+                        f"{W4}x{H4} 1 spp, frame split across {world} GPU(s) in {BAND}-row bands, RCCL gather of the "
+                        f"accumulator rows to rank 0 per frame",
+            "scaling": "strong", "n_gpus": world, "steps": args.config4_steps,
+            "value": round(tot[0] * args.config4_steps / el / 1e6, 3), "unit": "Mrays/s (primary+secondary)",
+            "ms_per_frame": round(el / args.config4_steps * 1e3, 4),
+            "rays_per_frame": {"primary_plus_bounce1": tot[0], "deeper": tot[1], "shadow": tot[2]}}
+
+
+def roofline_of(core, sc, W, H, dev, kernel_iters):
+    """The dominant kernel (bounce-ray closest hit, per-ray traversal) and the primary-ray launch, timed
+    with their own HIP events; priced by the committed counter summaries of the same kernels."""
+    o4, d4, _ = core.generate_eye_rays(sc.view, 0, 0)
+    perm = scene.tiled_order(W, H)        # the in-frame ray order (8x8 pixel block per wave)
+    o4, d4 = np.ascontiguousarray(o4[perm]), np.ascontiguousarray(d4[perm])
+
+    def launch(o, d, coherent):
+        n = len(o)
+        ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
+        hits = torch.empty((n, 4), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        core.setting("unitCoherent", 1 if coherent else 0)   # launched exactly as the frame launches it
+        core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), 2)
+        ms = core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), kernel_iters)
+        core.setting("unitCoherent", 0)
+        return ms, hits.cpu().numpy().view(np.uint32)
+
+    ms_p, hits_p = launch(o4, d4, True)
+    bo, bd = scene.bounce_rays(sc.meshes[0], o4, d4, hits_p)
+    ms, _ = launch(bo, bd, False)
+    n, n_p = len(bo), len(o4)
+    version = int(core.get_setting("traceVersion"))
+    kname = TRACE_KERNEL.get(version, f"traceVersion {version}")
+    cyc, cyc_src = valu_cycles_per_instruction()
+    peak = SIMDS * CLOCK_GHZ / cyc                     # G wave64 VALU instructions / s
+    sq_src, sq = newest("*_pmc_trace_sq.json", lambda d: d.get("kernel", "").startswith(kname))
+    tr_src, tr = newest("*_pmc_traffic.json", lambda d: d.get("kernel", "").startswith(kname))
+    fix = json.load(open(ROOT / "tests" / "golden" / "config2_bounce_visits.json"))
+    bpr = 32 + 20 + 32 * fix["mean_node_records"] + 36 * fix["mean_tri_tests"]
+    model_gbs = bpr * n / (ms * 1e-3) / 1e9
+    valu = sq["valu_wave_insts_per_launch"] if sq else None
+    achieved = valu / (ms * 1e-3) / 1e9 if valu else None
+    traffic = tr["bytes_per_launch"] if tr else None
+    hbm_gbs = traffic / (ms * 1e-3) / 1e9 if traffic else None
+    roof = {
+        "bound": "valu", "achieved": round(achieved, 1) if achieved else None, "peak": round(peak, 1),
+        "unit": "G wave64 VALU instructions/s", "frac": round(achieved / peak, 4) if achieved else None,
+        "traffic": traffic,
+        "kernel": f"{kname} (per-ray BVH4 traversal, traceVersion {version}, the core's default settings) on the "
+                  f"frame's {n} diffuse bounce rays, in-frame order",
+        "kernel_ms": round(ms, 4), "rays_per_launch": n,
+        "valu_insts_per_launch": valu, "valu_lane_utilisation": sq.get("valu_lane_utilisation") if sq else None,
+        "peak_basis": f"{SIMDS} SIMDs x {CLOCK_GHZ} GHz / {cyc:.2f} cycles per wave64 VALU instruction "
+                      f"({cyc_src or 'MI355X_MICROARCH.md: 2 (SIMD-32)'})",
+        "evidence": {"sq": sq_src, "traffic": tr_src},
+        "hbm": {"measured_GBs": round(hbm_gbs, 1) if hbm_gbs else None,
+                "measured_frac": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs else None,
+                "model_bytes_per_ray": round(bpr, 1), "model_GBs": round(model_gbs, 1),
+                "model_frac": round(model_gbs / HBM_PEAK_GBS, 4),
+                "model": "SURVEY §8(d): 32 ray + 20 hit + 32 x node records + 36 x triangle tests of the reference "
+                         "BVH2 traversal (tests/golden/config2_bounce_visits.json); the BVH and triangles are "
+                         "L2 / Infinity-Cache resident, so DRAM sees the measured bytes, not the model"},
+    }
+    psq_src, psq = newest("*_pmc_packet_sq.json")
+    pvalu = psq["valu_wave_insts_per_launch"] if psq and "valu_wave_insts_per_launch" in psq else None
+    prim = {"bound": "valu", "kernel": ("k_trace_closest_packet (wave-uniform packet traversal)"
+                                        if core.get_setting("usePackets") else kname) + " on the 1080p primary rays",
+            "kernel_ms": round(ms_p, 4), "rays_per_launch": n_p,
+            "achieved": round(pvalu / (ms_p * 1e-3) / 1e9, 1) if pvalu else None, "peak": round(peak, 1),
+            "frac": round(pvalu / (ms_p * 1e-3) / 1e9 / peak, 4) if pvalu else None, "evidence": psq_src}
+    detail = {"trace_Mrays_s_bounce": round(n / (ms * 1e-3) / 1e6, 1),
+              "trace_Mrays_s_primary": round(n_p / (ms_p * 1e-3) / 1e6, 1)}
+    return roof, prim, detail, model_gbs
 
 
 def main():
@@ -112,11 +253,19 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--tris", type=int, default=100_000)
+    ap.add_argument("--room-tris", type=int, default=1_000_000)
+    ap.add_argument("--config4-steps", type=int, default=10)
+    ap.add_argument("--no-config4", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--setting", action="append", default=[], help="name=value core setting before loading (A/B runs)")
     args = ap.parse_args()
+
+    # provenance: the library must be built from the checked-out sources (lh2_version() "srchash=")
+    want, got = build_info.source_hash(), build_info.library_hash()
+    if want != got:
+        raise SystemExit(f"libRenderCore_MI355X.so srchash={got} but the sources hash to {want}: rebuild it")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -139,72 +288,23 @@ def main():
     core.set_target(W, H, 1)
     core.set_tile_bands(rank, world, BAND)
     build_s = time.perf_counter() - t0
-    rows = core.tile_rows()
-    assert rows == len(band_rows(rank, world, H))
-    tile = torch.empty((rows, W, 4), dtype=torch.float32, device=dev)
-
-    def step():
-        sc.render_frame(core, converge=1)     # Restart: the same paths every step
-        core.pack_tile(tile.data_ptr())       # owned accumulator rows (waits for the frame)
-        return gather_tiles(tile, rank, world, H)
-
-    for _ in range(args.warmup):
-        step()
-    counts = core.ray_counts()
+    gather = TileGather(rank, world, W, H, dev)
+    assert core.tile_rows() == gather.rows
+    elapsed, tot, counts = timed_frames(core, sc, gather, args.steps, args.warmup, world, dev)
     st = core.stats()
-    rays_rank = int(counts[0]) + int(counts[1])         # primary + secondary (CoreStats semantics)
-    tot = torch.tensor([rays_rank, int(counts[2:16].sum()), int(counts[16])], dtype=torch.int64, device=dev)
-    if world > 1:
-        dist.all_reduce(tot)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
-    rays_total = int(tot[0].item())
+    rays_total = tot[0]
     value = rays_total * args.steps / elapsed / 1e6
+    ms_step = elapsed / args.steps * 1e3
 
+    out = None
     if rank == 0:
-        # ---- roofline of the dominant kernel: closest hit on the frame's bounce rays (per-ray traversal,
-        # ~half the frame), and beside it the primary-ray launch (packet traversal when auto-selected) ----
-        o4, d4, _ = core.generate_eye_rays(sc.view, 0, 0)
-        perm = scene.tiled_order(W, H)        # the in-frame ray order (8x8 pixel block per wave)
-        o4, d4 = np.ascontiguousarray(o4[perm]), np.ascontiguousarray(d4[perm])
-
-        def launch(o, d, coherent):
-            n = len(o)
-            ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
-            hits = torch.empty((n, 4), dtype=torch.int32, device=dev)
-            torch.cuda.synchronize()
-            core.setting("unitCoherent", 1 if coherent else 0)   # launched exactly as the frame launches it
-            core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), 2)
-            ms = core.trace_closest_device(ro.data_ptr(), rd.data_ptr(), n, hits.data_ptr(), args.kernel_iters)
-            core.setting("unitCoherent", 0)
-            return ms, hits.cpu().numpy().view(np.uint32)
-
-        def bytes_per_ray(name):
-            fix = json.load(open(ROOT / "tests" / "golden" / name))
-            return 32 + 20 + 32 * fix["mean_node_records"] + 36 * fix["mean_tri_tests"]
-
-        ms_p, hits_p = launch(o4, d4, True)
-        bo, bd = scene.bounce_rays(sc.meshes[0], o4, d4, hits_p)
-        ms, _ = launch(bo, bd, False)
-        n, n_p = len(bo), len(o4)
-        bpr, bpr_p = bytes_per_ray("config2_bounce_visits.json"), bytes_per_ray("config2_visits.json")
-        achieved = bpr * n / (ms * 1e-3) / 1e9
-        achieved_p = bpr_p * n_p / (ms_p * 1e-3) / 1e9
-        traffic = latest_pmc_traffic()
+        roof, prim, det, model_gbs = roofline_of(core, sc, W, H, dev, args.kernel_iters)
+        # the per-ray byte model of the kernels timed in a step must fit the step at HBM peak (the packet
+        # kernel fetches each node once per 64 rays, so it is priced by its VALU issue, not this model)
+        step_model_gbs = model_gbs * roof["kernel_ms"] / ms_step
+        assert step_model_gbs <= HBM_PEAK_GBS, ("byte model exceeds HBM peak over the step", step_model_gbs)
+        roof["hbm"]["model_GBs_over_step"] = round(step_model_gbs, 1)
         info = core.scene_info()
-        # RenderCore::UsePackets (auto): BVH + triangle footprint <= packetMaxMB (16 MiB)
-        packets = (info["nodes"] * 64 + info["tris"] * 48) <= 16 * 1048576
         out = {
             "metric": "Mrays/s (primary+secondary) at 1080p 1spp",
             "value": round(value, 3),
@@ -212,7 +312,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -220,39 +320,29 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"config2: {args.tris} random tris (xorshift32 0x12345678), {W}x{H} frame "
                                    f"({args.width}x{args.height} paths per GPU, {BAND}-row bands), 1 spp, "
-                                   f"full wavefront frame (primary + bounce-1 rays)",
+                                   f"full wavefront frame (primary + bounce-1 rays); strong scaling of config 4 "
+                                   f"(4K, frame split across the GPUs) in 'config4'",
                        "frame": [W, H], "spp": 1, "tris": args.tris, "parallelism": f"tiles{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "kernel": "k_trace_closest<false, 4> (per-ray BVH4 traversal, the core's default settings) on "
-                                   "the frame's diffuse bounce rays, in-frame order", "kernel_ms": round(ms, 4),
-                         "bytes_per_ray": round(bpr, 1), "rays_per_launch": n,
-                         "bytes_model": "32 ray + 20 hit + 32 x node records + 36 x triangle tests of the reference "
-                                        "traversal (tests/golden/config2_bounce_visits.json)"},
-            "roofline_primary": {"bound": "hbm", "achieved": round(achieved_p, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": round(achieved_p / HBM_PEAK_GBS, 4),
-                                 "kernel": ("k_trace_closest_packet (wave-uniform packet traversal)" if packets
-                                            else "k_trace_closest<true, 4>") + " on the 1080p primary rays",
-                                 "kernel_ms": round(ms_p, 4), "bytes_per_ray": round(bpr_p, 1), "rays_per_launch": n_p,
-                                 "note": "per-ray byte model; a packet fetches each node once per 64 rays (scalar "
-                                         "loads), so frac > 1 is possible and means the kernel is not HBM-bound"},
+            "roofline": roof,
+            "roofline_primary": prim,
             "detail": {"primary_rays": int(counts[0]), "secondary_rays": int(counts[1]),
-                       "deep_rays": int(counts[2:16].sum()), "shadow_rays": int(counts[16]),
-                       "trace_Mrays_s_bounce": round(n / (ms * 1e-3) / 1e6, 1),
-                       "trace_Mrays_s_primary": round(n_p / (ms_p * 1e-3) / 1e6, 1),
+                       "deep_rays": int(counts[2:16].sum()), "shadow_rays": int(counts[16]), **det,
                        "trace_Mrays_s_frame": round(rays_total / world / ((st.traceTime0 + st.traceTime1) * 1e6), 1)
                        if st.traceTime0 + st.traceTime1 > 0 else None,
                        "traceTime0_ms": round(st.traceTime0 * 1e3, 4), "traceTime1_ms": round(st.traceTime1 * 1e3, 4),
                        "shadeTime_ms": round(st.shadeTime * 1e3, 4), "bvh_nodes": info["nodes"],
                        "bvh_depth": info["max_depth"], "setup_s": round(build_s, 3)},
+            "build": {"srchash": got, "lh2_version": core.lib.lh2_version().decode()},
         }
+    core.close()
+    c4 = None if args.no_config4 else config4(args, rank, world, local, dev)
+    if rank == 0:
+        out["config4"] = c4
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(sc, args.width, args.height, args.cpu_seconds)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    core.close()
     if world > 1:
         dist.destroy_process_group()
 

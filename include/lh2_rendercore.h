@@ -32,7 +32,7 @@
      lh2_core_set_tile, lh2_core_set_tile_bands, lh2_core_sync, lh2_core_get_accumulator, lh2_core_get_frame,
      lh2_core_copy_accumulator_rows, lh2_core_pack_tile, lh2_core_pack_tile_ordered, lh2_core_tile_rows, lh2_core_stream, lh2_core_ray_counts, lh2_core_trace_closest,
      lh2_core_trace_any, lh2_core_trace_closest_device, lh2_core_generate_eye_rays,
-     lh2_core_scene_info, lh2_set_device, lh2_xorshift_floats, lh2_version.
+     lh2_core_scene_info, lh2_core_get_setting, lh2_set_device, lh2_xorshift_floats, lh2_version.
 */
 #ifndef LH2_RENDERCORE_H
 #define LH2_RENDERCORE_H
@@ -57,6 +57,7 @@ int lh2_core_get_stats( lh2_core core, lh2_CoreStats* out );
 int lh2_core_set_probe( lh2_core core, int x, int y );
 int lh2_core_set_target( lh2_core core, uint32_t width, uint32_t height, uint32_t spp );
 int lh2_core_setting( lh2_core core, const char* name, float value );
+int lh2_core_get_setting( lh2_core core, const char* name, float* value );   /* extension: current value (-1: unknown name) */
 int lh2_core_render( lh2_core core, const lh2_ViewPyramid* view, int converge );
 int lh2_core_shutdown( lh2_core core );
 int lh2_core_set_textures( lh2_core core, const lh2_CoreTexDesc* tex, int count );

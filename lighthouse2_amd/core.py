@@ -52,6 +52,7 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
         "lh2_core_set_probe": [_P, C.c_int, C.c_int],
         "lh2_core_set_target": [_P, C.c_uint32, C.c_uint32, C.c_uint32],
         "lh2_core_setting": [_P, C.c_char_p, C.c_float],
+        "lh2_core_get_setting": [_P, C.c_char_p, C.POINTER(C.c_float)],
         "lh2_core_render": [_P, C.POINTER(abi.ViewPyramid), C.c_int],
         "lh2_core_shutdown": [_P],
         "lh2_core_set_textures": [_P, _P, C.c_int],
@@ -132,6 +133,11 @@ class RenderCore:
 
     def setting(self, name: str, value: float) -> None:
         self._chk(self.lib.lh2_core_setting(self.h, name.encode(), float(value)))
+
+    def get_setting(self, name: str) -> float:
+        v = C.c_float(0)
+        self._chk(self.lib.lh2_core_get_setting(self.h, name.encode(), C.byref(v)))
+        return v.value
 
     def set_probe(self, x: int, y: int) -> None:
         self._chk(self.lib.lh2_core_set_probe(self.h, int(x), int(y)))

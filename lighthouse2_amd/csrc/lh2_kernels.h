@@ -129,6 +129,7 @@ int lh2_trace_blocks_per_cu( void );
 int lh2_packet_blocks_per_cu( void );
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
+void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
 void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st );
 }
 

@@ -530,6 +530,7 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 
 #include "lh2_trace2.inc"
 #include "lh2_trace_packet.inc"
+#include "lh2_trace4d.inc"
 
 /* packet traversal of coherent (8x8-tiled primary) rays: wave-uniform, no LDS stack */
 /* 8 waves per SIMD (64 VGPRs, ~32 spilled outside the node loop): the packet loop is bound by the
@@ -1759,6 +1760,18 @@ __global__ void k_pack_rows( const float4* __restrict__ acc, float4* __restrict_
 	dst[i] = acc[gy * w + x];
 }
 
+/* the inverse of k_pack_rows: rows packed by another device's core (rank `rank` of the band partition)
+   back into this core's accumulator (the in-process multi-device gather, csrc/multidevice.cpp) */
+__global__ void k_unpack_rows( const float4* __restrict__ src, float4* __restrict__ acc, const int w, const int y0, const int band,
+	const int bandStride, const int rows )
+{
+	const int i = threadIdx.x + blockIdx.x * blockDim.x;
+	if (i >= rows * w) return;
+	const int lr = i / w, x = i % w;
+	const int gy = y0 + (lr / band) * bandStride + lr % band;
+	acc[gy * w + x] = src[i];
+}
+
 /* ---- host-side launchers (extern "C", no torch / no HIP types beyond the stream) ---------- */
 /* Launches go through hipExtLaunchKernelGGL: its start / stop events are recorded by the kernel's own
    dispatch packet, where a hipEventRecord between two launches costs a barrier packet and ~5 us of
@@ -1804,7 +1817,8 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
 		const bool tail = a->tailOut && a->tailLanes;
 		TraceArgs t = tail_args( *a );
 		const LaunchEvents e1 = { ev.start, tail ? nullptr : ev.stop }, e2 = { nullptr, ev.stop };
-		if (a->version == 4 && s->nodes4)
+		if (a->version == 5 && s->nodes4) LH2_LAUNCH( k_trace_closest4d, grid, 256, st, ev, *s, *a );   /* leaf slot, lh2_trace4d.inc */
+		else if (a->version == 4 && s->nodes4)
 		{
 			if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 4>), grid, 256, st, e1, *s, *a );
 			else LH2_LAUNCH( (k_trace_closest<false, 4>), grid, 256, st, e1, *s, *a );
@@ -1834,6 +1848,11 @@ void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int 
 		else if (fused) LH2_LAUNCH( (k_trace_any_packet<1, 2>), grid, 256, st, ev, *s, *a );
 		else if (v4) LH2_LAUNCH( (k_trace_any_packet<0, 4>), grid, 256, st, ev, *s, *a );
 		else LH2_LAUNCH( (k_trace_any_packet<0, 2>), grid, 256, st, ev, *s, *a );
+	}
+	else if (a->version == 5 && s->nodes4)
+	{
+		if (fused) LH2_LAUNCH( (k_trace_any4d<1>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_any4d<0>), grid, 256, st, ev, *s, *a );
 	}
 	else if (a->version >= 2)
 	{
@@ -1895,6 +1914,11 @@ void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int ba
 {
 	if (rows * w <= 0) { if (ev.stop) (void)hipEventRecord( ev.stop, st ); return; }
 	LH2_LAUNCH( k_pack_rows, (rows * w + 255) / 256, 256, st, ev, acc, dst, w, y0, band, bandStride, rows );
+}
+void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st )
+{
+	if (rows * w <= 0) { if (ev.stop) (void)hipEventRecord( ev.stop, st ); return; }
+	LH2_LAUNCH( k_unpack_rows, (rows * w + 255) / 256, 256, st, ev, src, acc, w, y0, band, bandStride, rows );
 }
 void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st )
 {

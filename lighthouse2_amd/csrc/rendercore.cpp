@@ -140,7 +140,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipMemsetAsync( dTlasDepth.ptr, 0, sizeof( int ), stream ) );
 	dInstDesc.resize( 1 );   /* shading reads record 0 for a miss (HitInstance): it always exists */
 	CHK_HIP( hipMemsetAsync( dInstDesc.ptr, 0, sizeof( lh2_CoreInstanceDesc ), stream ) );
-	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 4, std::max( 1, atoi( tv ) ) );   /* A/B runs */
+	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 5, std::max( 0, atoi( tv ) ) );   /* A/B runs */
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
 }
@@ -178,6 +178,19 @@ bool RenderCore::UsePackets() const
 	if (packetPrimary >= 0) return packetPrimary != 0;
 	const double bytes = ((double)blasNodeCount + tlasCapacity) * 64.0 + (double)blasTriCount * 48.0;
 	return bytes <= (double)packetMaxMB * 1048576.0;
+}
+
+/* traversal loop of the per-ray launches (setting "traceVersion", 0: auto).  Auto: the BVH4 loop with
+   one record fetch per iteration (5, lh2_trace4d.inc) once the BVH4 + triangles outgrow the 256 MB
+   Infinity Cache - its single round trip per iteration pays where node fetches reach DRAM (config 5,
+   1 GB: 13.36 vs 13.70 ms per frame) - else the v4 loop (config 2, 11 MB: 0.874 vs 0.888 ms on the
+   bounce rays; profiles/r02h_ab_slp.txt) */
+int RenderCore::TraceVersion() const
+{
+	if (traceVersion) return (traceVersion >= 4 && !bvh4) ? 2 : traceVersion;
+	if (!bvh4) return 2;
+	const double bytes = ((double)blasNode4Count + tlasCapacity) * 128.0 + (double)blasTriCount * 48.0;
+	return bytes > (double)traceFetchMB * 1048576.0 ? 5 : 4;
 }
 
 void RenderCore::EnsureBuffers()
@@ -241,13 +254,30 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	}
 	else if (!strcmp( name, "packetShadow" )) packetShadow = value != 0;     /* packet traversal of the shadow rays */
 	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice uses the primary-ray launch */
-	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 4, std::max( 1, (int)value ) );   /* traversal loop: 1, 2 (BVH2), 4 (BVH4) */
-	else if (!strcmp( name, "bvh4" )) { bvh4 = value != 0; if (!bvh4 && traceVersion == 4) traceVersion = 2; }   /* before SetGeometry */
+	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 5, std::max( 0, (int)value ) );   /* traversal loop: 1, 2 (BVH2), 4 (BVH4), 5 (BVH4, one fetch per iteration), 0 auto */
+	else if (!strcmp( name, "traceFetchMB" )) traceFetchMB = std::max( 0.0f, value );
+	else if (!strcmp( name, "bvh4" )) { bvh4 = value != 0; if (!bvh4 && traceVersion >= 4) traceVersion = 2; }   /* before SetGeometry */
 	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
 	else if (!strcmp( name, "gpuTlas" )) { gpuTlas = value != 0; instancesDirty = true; }
 	else if (!strcmp( name, "plocRadius" )) gpuBvh.radius = std::min( 32, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "blocksPerCU" )) { blocksPerCU = std::min( 16, std::max( 1, (int)value ) ); if (scrwidth) EnsureBuffers(); }
 	/* other names ("clampDirect", "filter", "TAA", ...) are ignored, as in the reference */
+}
+
+/* the current value of a setting (extension: the reference has no getter); false for unknown names */
+bool RenderCore::GetSetting( const char* name, float& value ) const
+{
+	struct { const char* n; float v; } t[] = {
+		{ "epsilon", geometryEpsilon }, { "clampValue", clampValue }, { "maxPathLength", (float)maxPathLength },
+		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
+		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
+		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
+		{ "pathGroups", (float)pathGroups }, { "singleInstanceStart", (float)singleInstanceStart },
+		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "traceFetchMB", traceFetchMB }, { "bvh4", (float)bvh4 },
+		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "blocksPerCU", (float)blocksPerCU },
+		{ "packetShadow", (float)packetShadow }, { "usePackets", (float)UsePackets() } };
+	for (const auto& e : t) if (!strcmp( name, e.n )) { value = e.v; return true; }
+	return false;
 }
 
 void RenderCore::SetTextures( const lh2_CoreTexDesc* tex, int textureCount )   /* rendercore.cpp:276-292 */
@@ -735,7 +765,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			g.pl = pathLength;
 			Counters* c = g.counters.ptr;
 			TraceArgs ta{};
-			ta.version = traceVersion;
+			ta.version = TraceVersion();
 			ta.rayO = g.rayO[g.in].ptr, ta.rayD = g.rayD[g.in].ptr, ta.segCounts = c->segActive, ta.segStride = g.segStride;
 			ta.cursor = g.cursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
 			ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
@@ -765,7 +795,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				/* RenderCore_PrimeRef traces the shadow rays of every bounce right after it
 				   (rendercore.cpp connect step), fused with finalizeConnections */
 				TraceArgs ts{};
-				ts.version = traceVersion;
+				ts.version = TraceVersion();
 				ts.rayO = g.shO.ptr, ts.rayD = g.shD.ptr, ts.segCounts = c->segShadow, ts.segStride = g.shadowStride;
 				ts.cursor = g.cursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
@@ -801,7 +831,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		if (!primeRef && shadows)
 		{
 			TraceArgs ta{};
-			ta.version = traceVersion;
+			ta.version = TraceVersion();
 			ta.rayO = g.shO.ptr, ta.rayD = g.shD.ptr, ta.segCounts = g.counters.ptr->segShadow, ta.segStride = g.shadowStride;
 			ta.cursor = g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 			ta.mask = g.shMask.ptr, ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = g.gstack.ptr;
@@ -840,6 +870,27 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	framePrimeRef = primeRef;
 	statsPending = true;
 	frameHostMs = std::chrono::duration<double, std::milli>( std::chrono::high_resolution_clock::now() - t0 ).count();
+}
+
+void RenderCore::UnpackTile( const void* devSrc, int rank, int nranks, int band )
+{
+	int rows = 0;
+	for (int y = rank * band; y < scrheight; y += nranks * band) rows += std::min( band, scrheight - y );
+	lh2_launch_unpack_rows( (const float4*)devSrc, accumulator.ptr, scrwidth, rank * band, band, nranks * band, rows, {}, stream );
+}
+
+void RenderCore::FinalizeFrame()
+{
+	if (!samplesTaken) return;
+	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, nullptr, {}, stream );
+	if (glResource)
+	{
+		hipArray_t arr = nullptr;
+		CHK_HIP( hipGraphicsMapResources( 1, &glResource, stream ) );
+		CHK_HIP( hipGraphicsSubResourceGetMappedArray( &arr, glResource, 0, 0 ) );
+		CHK_HIP( hipMemcpy2DToArrayAsync( arr, 0, 0, frame.ptr, sizeof( float4 ) * scrwidth, sizeof( float4 ) * scrwidth, scrheight, hipMemcpyDeviceToDevice, stream ) );
+		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, stream ) );
+	}
 }
 
 int RenderCore::TileRows() const
@@ -990,7 +1041,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	CHK_HIP( hipMemsetAsync( ovf.ptr, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
-	ta.version = traceVersion;
+	ta.version = TraceVersion();
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
 	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
 	ta.packet = unitCoherent && UsePackets() ? PacketMode() : 0;
@@ -1013,7 +1064,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	CHK_HIP( hipMemsetAsync( m.ptr, 0, words * 4, stream ) );
 	const SceneDev sd = MakeSceneDev();
 	TraceArgs ta{};
-	ta.version = traceVersion;
+	ta.version = TraceVersion();
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 	ta.packet = unitCoherent && packetShadow ? PacketMode() : 0;
 	SetTail( ta, grp[0] );
@@ -1049,7 +1100,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 	for (int i = 0; i < iterations; i++)
 	{
 		TraceArgs ta{};
-		ta.version = traceVersion;
+		ta.version = TraceVersion();
 		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = cursors.ptr + (size_t)i * LH2_CURSOR_WORDS;
 		ta.hits = (uint4*)hitsOut, ta.gstack = grp[0].gstack.ptr;
 		/* unitCoherent: trace as the frame traces its (tiled) primary rays */

@@ -104,6 +104,7 @@ public:
 	void SetTarget( uint32_t w, uint32_t h, uint32_t spp );
 	void SetInteropTexture( uint32_t glTextureId );   /* 0: headless (frame stays in the device buffer) */
 	void Setting( const char* name, float value );
+	bool GetSetting( const char* name, float& value ) const;
 	void Render( const lh2_ViewPyramid& view, int converge );
 	void Shutdown();
 	void SetTextures( const lh2_CoreTexDesc* tex, int textureCount );
@@ -127,6 +128,13 @@ public:
 	void PackTile( void* devDst, bool ordered = false, void* consumer = nullptr );   /* owned rows, local order (async); ordered: with the stream consumer (null: the null stream) both ways */
 	hipEvent_t evConsumer = nullptr, evPacked = nullptr;
 	void GetFrame( float* hostOut4 );                      /* finalizeRender output: acc / samplesTaken */
+	/* in-process multi-device gather (multidevice.cpp): rows packed by the core of rank `rank` of a
+	   band partition, already on this device, into this accumulator (async); then the frame output
+	   of the whole accumulator again (finalizeRender + display copy, no statistics) */
+	void UnpackTile( const void* devSrc, int rank, int nranks, int band );
+	void FinalizeFrame();
+	hipStream_t Stream() const { return stream; }
+	int Device() const { return device; }
 	int SamplesTaken() const { return samplesTaken; }
 	void GetRayCounts( uint32_t* out17 );
 	void TraceClosest( const float* orgTmin4, const float* dirTmax4, int n, uint32_t* hits4 );   /* host in/out */
@@ -222,7 +230,9 @@ private:
 	   bvhMaxLeaf 2 / leafBatch 16, config 5 2 % slower */
 	int refillPrimary = 48, refillOther = 48, leafBatch = 0, leafBatchPrimary = 8;
 	int bvhMaxLeaf = 1;
-	int traceVersion = 4;
+	int traceVersion = 0;                /* 0: auto (TraceVersion) */
+	float traceFetchMB = 256.0f;         /* auto: traceVersion 5 above this BVH4 + triangle footprint */
+	int TraceVersion() const;
 	int unitCoherent = 0;
 	int packetPrimary = -1;              /* wave-uniform packet traversal for 8x8-tiled primary rays (-1: by scene size) */
 	float packetMaxMB = 16.0f;

@@ -14,6 +14,9 @@ from lighthouse2_amd.record import CallRecorder
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 LIB = ROOT / "lighthouse2_amd" / "libRenderCore_MI355X.so"
+# the replay host compiled against the REFERENCE's core_api_base.h (oracle/Makefile.ref, built in the
+# container where /root/reference exists; the binary travels to the GPU box)
+REF_HOST = ROOT / "oracle" / "_ref" / "reference_rendersystem"
 
 
 @pytest.fixture(scope="module")
@@ -24,8 +27,10 @@ def driver(tmp_path_factory):
     return exe
 
 
-def _record(path, sc, w, h, frames, spp=1):
+def _record(path, sc, w, h, frames, spp=1, pre=()):
     with CallRecorder(path) as rec:
+        for k, v in pre:
+            rec.setting(k, v)
         rec.set_target(w, h, spp)
         sc.load_into(rec)
         rec.set_probe(w // 2, h // 2)
@@ -67,6 +72,53 @@ def test_vtable_host_frame_matches_oracle(driver, tmp_path):
     counts = o.ray_counts()
     ost = o.stats()
     assert st["frames"] == 2
+    assert st["primaryRayCount"] == counts[0] and st["bounce1RayCount"] == counts[1]
+    assert (st["probedInstid"], st["probedTriid"]) == (ost.probedInstid, ost.probedTriid)
+    rel = np.linalg.norm(acc[..., :3] - ref[..., :3]) / np.linalg.norm(ref[..., :3])
+    assert rel <= 1e-4
+
+
+@pytest.mark.skipif(not REF_HOST.exists(), reason="reference-header replay host not built (no /root/reference)")
+def test_reference_header_host_parses(tmp_path):
+    w, h = 64, 36
+    sc = scene.room_scene(6000, w, h)
+    calls = tmp_path / "calls.bin"
+    _record(calls, sc, w, h, frames=2)
+    out = subprocess.run([str(REF_HOST), str(LIB), str(calls), str(tmp_path / "acc.bin"), "--parse-only"],
+                         check=True, capture_output=True, text=True).stdout
+    assert json.loads(out) == {"calls": 15, "frames": 2, "width": w, "height": h}
+
+
+def _oracle_frames(sc, w, h, frames):
+    from oracle.oracle import Oracle
+    o = Oracle()
+    o.set_target(w, h, 1)
+    sc.load_into(o)
+    o.set_probe(w // 2, h // 2)
+    for f in range(frames):
+        sc.render_frame(o, converge=1 if f == 0 else 0)
+    return o.accumulator(), o.ray_counts(), o.stats()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [1, 2])
+def test_reference_header_host_frame_matches_oracle(tmp_path, devices):
+    """The core driven through the reference's own CoreAPI_Base declaration (core_api_base.h:78-114):
+    CoreStats returned by value, int2 / Convergence by value, the reference GLTexture and mat4 types.
+    With deviceCount 2 (a Setting call through the same vtable, before SetTarget) the core splits the
+    frame over two sub-cores (on a one-GPU box both on device 0) and gathers it."""
+    assert REF_HOST.exists(), "oracle/_ref/reference_rendersystem missing: build it where /root/reference exists"
+    w, h = 128, 72
+    sc = scene.room_scene(20000, w, h)
+    calls = tmp_path / "calls.bin"
+    _record(calls, sc, w, h, frames=2, pre=(("deviceCount", devices),) if devices > 1 else ())
+    res = subprocess.run([str(REF_HOST), str(LIB), str(calls), str(tmp_path / "acc.bin")], capture_output=True,
+                         text=True, timeout=300)
+    assert res.returncode == 0 and res.stdout.strip(), (res.returncode, res.stdout, res.stderr)
+    st = json.loads(res.stdout.strip().splitlines()[-1])
+    acc = np.fromfile(tmp_path / "acc.bin", np.float32).reshape(h, w, 4)
+    ref, counts, ost = _oracle_frames(sc, w, h, 2)
+    assert st["frames"] == 2 and st["SMcount"] >= 1 and "gfx950" in st["deviceName"]
     assert st["primaryRayCount"] == counts[0] and st["bounce1RayCount"] == counts[1]
     assert (st["probedInstid"], st["probedTriid"]) == (ost.probedInstid, ost.probedTriid)
     rel = np.linalg.norm(acc[..., :3] - ref[..., :3]) / np.linalg.norm(ref[..., :3])

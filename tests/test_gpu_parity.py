@@ -295,10 +295,11 @@ def test_packet_shadow_frame_parity(fresh_core):
     assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
 
 
-@pytest.mark.parametrize("version,leaf_batch,max_leaf", [(1, 0, 2), (1, 16, 2), (2, 0, 2), (2, 16, 1), (4, 0, 1), (4, 16, 2), (4, 8, 4)])
+@pytest.mark.parametrize("version,leaf_batch,max_leaf", [(1, 0, 2), (1, 16, 2), (2, 0, 2), (2, 16, 1), (4, 0, 1), (4, 16, 2), (4, 8, 4),
+                                                       (5, 0, 1), (5, 0, 2), (5, 0, 4)])
 def test_traversal_variants_bitexact(fresh_core, version, leaf_batch, max_leaf):
     """Every per-ray traversal loop (trace_stream, lh2_trace2.inc over the BVH2 and over the BVH4
-    collapse), with and without leaf parking, over trees of different leaf sizes, returns the
+    collapse, lh2_trace4d.inc with its leaf slot), with and without leaf parking, over trees of different leaf sizes, returns the
     oracle's hit records and occlusion bits: hits do not depend on the tree or the visiting order."""
     fresh_core.setting("bvhMaxLeaf", max_leaf)
     fresh_core.setting("traceVersion", version)
@@ -315,7 +316,8 @@ def test_traversal_variants_bitexact(fresh_core, version, leaf_batch, max_leaf):
     assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
 
 
-def test_bvh4_deep_stack(fresh_core):
+@pytest.mark.parametrize("version", [4, 5])
+def test_bvh4_deep_stack(fresh_core, version):
     """A deep BLAS (triangles shrinking geometrically along a line: a chain-like SAH tree) next to the
     random cloud: BVH4 nodes push up to three children per level, the LDS part of the traversal
     stack spills into the global part, and hits stay exact."""
@@ -330,7 +332,7 @@ def test_bvh4_deep_stack(fresh_core):
     sc = scene.config2_scene(n=5000, width=64, height=36)
     sc.meshes.append(chain)
     sc.instances.append((1, np.eye(4, dtype=np.float32)))
-    fresh_core.setting("traceVersion", 4)
+    fresh_core.setting("traceVersion", version)
     o = _load_both(fresh_core, sc, 64, 36)
     info = fresh_core.scene_info()
     assert info["max_depth"] >= 14, info
@@ -344,6 +346,8 @@ def test_bvh4_deep_stack(fresh_core):
     hg, ho = fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4)
     assert (ho[:10000, 2] == 1).mean() > 0.2   # instance 1 (the chain) is hit
     assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+    D4[:, 3] = np.random.default_rng(15).uniform(1.0, 20.0, len(D4)).astype(np.float32)
+    assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
 
 
 @pytest.mark.parametrize("groups", [1, 3, 4])
@@ -461,7 +465,7 @@ def test_terminal_shade_frame_parity(fresh_core, kind):
     assert np.array_equal(ag[..., 3], a0[..., 3])
 
 
-@pytest.mark.parametrize("version", [1, 2, 4])
+@pytest.mark.parametrize("version", [1, 2, 4, 5])
 @pytest.mark.parametrize("start", [0, 1])
 def test_single_instance_start_bitexact(fresh_core, version, start):
     """One instance (sheared and scaled): with singleInstanceStart the rays begin at its TLAS leaf
@@ -479,7 +483,7 @@ def test_single_instance_start_bitexact(fresh_core, version, start):
     assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
     D4[:, 3] = np.random.default_rng(4).uniform(1.0, 20.0, len(D4)).astype(np.float32)
     assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
-    if version == 4:
+    if version >= 4:
         fresh_core.setting("epsilon", 1e-4)
         o.setting("epsilon", 1e-4)
         sc.render_frame(fresh_core)
@@ -502,5 +506,22 @@ def test_no_lights_rng_stream_past_sample_256(fresh_core):
     sc.render_frame(o)
     cg, co = fresh_core.ray_counts(), o.ray_counts()
     assert np.array_equal(cg, co), (cg, co)
+    ag, ao = fresh_core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+
+
+@pytest.mark.parametrize("version", [4, 5])
+def test_lit_room_frame_traversal_versions(fresh_core, version):
+    """The whole lit frame (closest hits of every bounce, any-hit shadow rays with the fused connect)
+    through the BVH4 loops: identical ray counts and accumulator."""
+    w, h = 128, 72
+    sc = scene.room_scene(40000, w, h)
+    fresh_core.setting("traceVersion", version)
+    o = _load_both(fresh_core, sc, w, h)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", 4)
+    sc.render_frame(fresh_core)
+    sc.render_frame(o)
+    assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
     ag, ao = fresh_core.accumulator(), o.accumulator()
     assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL

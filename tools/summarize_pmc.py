@@ -3,9 +3,10 @@
   profiles/<tag>_pmc_trace_sq.json       SQ issue counters of the dominant kernel, per launch (median
                                          over launches): VALU wave-instructions, VALU lane utilisation,
                                          effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration), and the
-                                         VALU issue rate against the SIMD-32 peak (a wave64 VALU
-                                         instruction takes 2 cycles of one SIMD: MI355X_MICROARCH.md,
-                                         per-instruction constants; 1024 SIMDs).
+                                         VALU issue rate against the chip's VALU issue peak (1024
+                                         SIMDs x 2.4 GHz / the cycles per wave64 VALU instruction that
+                                         tools/valu_rate measured: 4.1 at 4-8 waves per SIMD).
+  profiles/<tag>_pmc_packet_sq.json      the same for the primary-ray packet launch.
   profiles/<tag>_pmc_config5_traffic.json  HBM bytes per launch of every kernel of config-5 frames
                                          (2 x FETCH_SIZE per the gfx950 calibration + WRITE_SIZE, KiB ->
                                          B), each from its own --pmc pass, and the achieved GB/s.
@@ -24,6 +25,18 @@ SIMDS = 256 * 4
 CLOCK_GHZ = 2.4
 
 
+def cycles_per_valu():
+    """SIMD cycles per wave64 VALU instruction measured by tools/valu_rate (committed jsonl), else 2."""
+    import glob
+    files = sorted(glob.glob(str(ROOT / "profiles" / "*valu_rate*.jsonl")))
+    if files:
+        rows = [json.loads(x) for x in open(files[-1]) if x.strip().startswith("{")]
+        rows = [r for r in rows if r.get("waves_per_simd", 0) >= 4]
+        if rows:
+            return min(r["cycles_per_wave_inst"] for r in rows)
+    return 2.0
+
+
 def dispatches(path, kernel=None):
     """{dispatch id: {"kernel", "ns", counter: value}} from a rocprofv3 counter_collection.csv."""
     out = collections.OrderedDict()
@@ -40,19 +53,21 @@ def med(ds, key):
     return statistics.median(d[key] for d in ds)
 
 
-def trace_sq(src, kernel):
-    ds = list(dispatches(src / "sq1" / "run_counter_collection.csv", kernel).values())
-    ds2 = list(dispatches(src / "sq2" / "run_counter_collection.csv", kernel).values())
+def trace_sq(src, kernel, p1="sq1", p2="sq2", what="config-2 bounce rays from the 1080p primary hits, tools/trace_kernel_bench.py --set bounce"):
+    ds = list(dispatches(src / p1 / "run_counter_collection.csv", kernel).values())
+    ds2 = list(dispatches(src / p2 / "run_counter_collection.csv", kernel).values()) if p2 else []
     ns = med(ds, "ns")
     valu = med(ds, "SQ_INSTS_VALU")
     clk = med(ds, "GRBM_GUI_ACTIVE") / 8 / ns           # GHz (sum over the 8 XCDs)
     cycles = ns * clk
     rate = valu / ns                                   # G wave-instructions / s
-    peak = SIMDS * CLOCK_GHZ / 2
+    cyc = cycles_per_valu()
+    peak = SIMDS * CLOCK_GHZ / cyc
     counters = {k: med(ds, k) for k in ds[0] if k.startswith(("SQ_", "GRBM_"))}
-    counters.update({k: med(ds2, k) for k in ds2[0] if k.startswith("SQ_")})
+    if ds2:
+        counters.update({k: med(ds2, k) for k in ds2[0] if k.startswith("SQ_")})
     return {
-        "kernel": f"{kernel} (config-2 bounce rays from the 1080p primary hits, tools/trace_kernel_bench.py --set bounce)",
+        "kernel": f"{kernel} ({what})",
         "launches": len(ds), "launch_ms_median": ns / 1e6,
         "counters_per_launch_median": counters,
         "effective_clock_ghz": round(clk, 3),
@@ -60,13 +75,15 @@ def trace_sq(src, kernel):
         "valu_issue_rate_g_per_s": round(rate, 1),
         "valu_issue_peak_g_per_s": peak,
         "valu_issue_frac": round(rate / peak, 4),
-        "valu_issue_frac_at_effective_clock": round(valu * 2 / (SIMDS * cycles), 4),
+        "valu_issue_frac_at_effective_clock": round(valu * cyc / (SIMDS * cycles), 4),
+        "cycles_per_valu_instruction": cyc,
         "valu_lane_utilisation": round(counters["SQ_THREAD_CYCLES_VALU"] / (64 * counters["SQ_ACTIVE_INST_VALU"]), 4),
         "valu_busy_frac_quad_cycles": round(counters["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cycles), 4),
         "wave_cycles_waiting_frac": round(counters["SQ_WAIT_ANY"] / counters["SQ_WAVE_CYCLES"], 4)
         if "SQ_WAIT_ANY" in counters else None,
-        "note": "VALU issue peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (SIMD-32); "
-                "SQ_ACTIVE_INST_* and SQ_WAVE_CYCLES count quad-cycles (MI355X_MICROARCH.md)",
+        "note": "VALU issue peak = 1024 SIMDs x 2.4 GHz / cycles per wave64 VALU instruction, measured by "
+                "tools/valu_rate (profiles/*valu_rate*.jsonl: 4.1 at 4-8 waves/SIMD); SQ_ACTIVE_INST_* and "
+                "SQ_WAVE_CYCLES count quad-cycles (MI355X_MICROARCH.md)",
     }
 
 
@@ -109,6 +126,11 @@ def main():
     sq = trace_sq(src, a.kernel)
     (dst / f"{a.tag}_pmc_trace_sq.json").write_text(json.dumps(sq, indent=1) + "\n")
     print(json.dumps(sq, indent=1))
+    if (src / "pk1").exists():
+        pk = trace_sq(src, "k_trace_closest_packet", "pk1", None, "config-2 1080p primary rays in the frame's 8x8-tiled "
+                                                                   "order, tools/trace_kernel_bench.py --set primary")
+        (dst / f"{a.tag}_pmc_packet_sq.json").write_text(json.dumps(pk, indent=1) + "\n")
+        print(json.dumps(pk, indent=1))
     if (src / "c5_fetch").exists():
         c5 = config5_traffic(src)
         (dst / f"{a.tag}_pmc_config5_traffic.json").write_text(json.dumps(c5, indent=1) + "\n")

@@ -61,7 +61,7 @@ def main():
         "fetch_bytes": fetch_b, "write_bytes": write_b,
         "bytes_per_launch": fetch_b + write_b,
         "bytes_per_ray": (fetch_b + write_b) / rays,
-        "algorithmic_bytes_per_ray": bench["roofline"]["bytes_per_ray"],
+        "algorithmic_bytes_per_ray": bench["roofline"]["hbm"]["model_bytes_per_ray"],
         "pmc_launch_ms_median": statistics.median(fd + wd) / 1e6,
         "rocprof_bench_roofline_launch_ms_mean": trace_ms,
         "bench_hip_event_launch_ms": bench["roofline"]["kernel_ms"],
