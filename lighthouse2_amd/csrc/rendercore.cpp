@@ -140,7 +140,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipMemsetAsync( dTlasDepth.ptr, 0, sizeof( int ), stream ) );
 	dInstDesc.resize( 1 );   /* shading reads record 0 for a miss (HitInstance): it always exists */
 	CHK_HIP( hipMemsetAsync( dInstDesc.ptr, 0, sizeof( lh2_CoreInstanceDesc ), stream ) );
-	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 5, std::max( 0, atoi( tv ) ) );   /* A/B runs */
+	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 6, std::max( 0, atoi( tv ) ) );   /* A/B runs */
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
 }
@@ -180,17 +180,18 @@ bool RenderCore::UsePackets() const
 	return bytes <= (double)packetMaxMB * 1048576.0;
 }
 
-/* traversal loop of the per-ray launches (setting "traceVersion", 0: auto).  Auto: the BVH4 loop with
-   one record fetch per iteration (5, lh2_trace4d.inc) once the BVH4 + triangles outgrow the 256 MB
-   Infinity Cache - its single round trip per iteration pays where node fetches reach DRAM (config 5,
-   1 GB: 13.36 vs 13.70 ms per frame) - else the v4 loop (config 2, 11 MB: 0.874 vs 0.888 ms on the
-   bounce rays; profiles/r02h_ab_slp.txt) */
+/* traversal loop of the per-ray launches (setting "traceVersion", 0: auto).  Auto: lh2_trace4d.inc (BVH4,
+   packed-FMA slabs, LDS child references, rcp box reciprocals, the single instance entered at ray
+   set-up); while the BVH4 + triangles fit the 256 MB Infinity Cache each branch fetches its own record
+   (6: config 2 bounce rays 0.86 vs 0.88 ms for the v4 loop, config 3 2.68 vs 2.77 ms per frame), beyond
+   it every lane's record is fetched at once, one round trip per iteration (5: config 5, 1 GB, 13.31 vs
+   13.68 ms; profiles/r02j_ab_versions.txt) */
 int RenderCore::TraceVersion() const
 {
 	if (traceVersion) return (traceVersion >= 4 && !bvh4) ? 2 : traceVersion;
 	if (!bvh4) return 2;
 	const double bytes = ((double)blasNode4Count + tlasCapacity) * 128.0 + (double)blasTriCount * 48.0;
-	return bytes > (double)traceFetchMB * 1048576.0 ? 5 : 4;
+	return bytes > (double)traceFetchMB * 1048576.0 ? 5 : 6;
 }
 
 void RenderCore::EnsureBuffers()
@@ -254,7 +255,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	}
 	else if (!strcmp( name, "packetShadow" )) packetShadow = value != 0;     /* packet traversal of the shadow rays */
 	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice uses the primary-ray launch */
-	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 5, std::max( 0, (int)value ) );   /* traversal loop: 1, 2 (BVH2), 4 (BVH4), 5 (BVH4, one fetch per iteration), 0 auto */
+	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 6, std::max( 0, (int)value ) );   /* traversal loop: 1, 2 (BVH2), 4 (BVH4), 5 / 6 (BVH4, lh2_trace4d.inc: one fetch per iteration / per branch), 0 auto */
 	else if (!strcmp( name, "traceFetchMB" )) traceFetchMB = std::max( 0.0f, value );
 	else if (!strcmp( name, "bvh4" )) { bvh4 = value != 0; if (!bvh4 && traceVersion >= 4) traceVersion = 2; }   /* before SetGeometry */
 	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
