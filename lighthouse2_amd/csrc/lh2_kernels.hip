@@ -1817,8 +1817,9 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
 		const bool tail = a->tailOut && a->tailLanes;
 		TraceArgs t = tail_args( *a );
 		const LaunchEvents e1 = { ev.start, tail ? nullptr : ev.stop }, e2 = { nullptr, ev.stop };
-		if (a->version == 5 && s->nodes4) LH2_LAUNCH( k_trace_closest4d<true>, grid, 256, st, ev, *s, *a );   /* lh2_trace4d.inc */
-		else if (a->version == 6 && s->nodes4) LH2_LAUNCH( k_trace_closest4d<false>, grid, 256, st, ev, *s, *a );
+		if (a->version == 5 && s->nodes4) LH2_LAUNCH( k_trace_closest4d<1>, grid, 256, st, ev, *s, *a );   /* lh2_trace4d.inc */
+		else if (a->version == 6 && s->nodes4) LH2_LAUNCH( k_trace_closest4d<0>, grid, 256, st, ev, *s, *a );
+		else if (a->version == 7 && s->nodes4) LH2_LAUNCH( k_trace_closest4d<2>, grid, 256, st, ev, *s, *a );
 		else if (a->version == 4 && s->nodes4)
 		{
 			if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 4>), grid, 256, st, e1, *s, *a );
@@ -1852,11 +1853,13 @@ void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int 
 	}
 	else if (a->version >= 5 && s->nodes4)
 	{
-		const bool u = a->version == 5;
-		if (fused && u) LH2_LAUNCH( (k_trace_any4d<1, true>), grid, 256, st, ev, *s, *a );
-		else if (fused) LH2_LAUNCH( (k_trace_any4d<1, false>), grid, 256, st, ev, *s, *a );
-		else if (u) LH2_LAUNCH( (k_trace_any4d<0, true>), grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( (k_trace_any4d<0, false>), grid, 256, st, ev, *s, *a );
+		const int m = a->version == 5 ? 1 : a->version == 7 ? 2 : 0;
+		if (fused && m == 1) LH2_LAUNCH( (k_trace_any4d<1, 1>), grid, 256, st, ev, *s, *a );
+		else if (fused && m == 2) LH2_LAUNCH( (k_trace_any4d<1, 2>), grid, 256, st, ev, *s, *a );
+		else if (fused) LH2_LAUNCH( (k_trace_any4d<1, 0>), grid, 256, st, ev, *s, *a );
+		else if (m == 1) LH2_LAUNCH( (k_trace_any4d<0, 1>), grid, 256, st, ev, *s, *a );
+		else if (m == 2) LH2_LAUNCH( (k_trace_any4d<0, 2>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_any4d<0, 0>), grid, 256, st, ev, *s, *a );
 	}
 	else if (a->version >= 2)
 	{

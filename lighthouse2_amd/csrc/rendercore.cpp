@@ -140,7 +140,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipMemsetAsync( dTlasDepth.ptr, 0, sizeof( int ), stream ) );
 	dInstDesc.resize( 1 );   /* shading reads record 0 for a miss (HitInstance): it always exists */
 	CHK_HIP( hipMemsetAsync( dInstDesc.ptr, 0, sizeof( lh2_CoreInstanceDesc ), stream ) );
-	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 6, std::max( 0, atoi( tv ) ) );   /* A/B runs */
+	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 7, std::max( 0, atoi( tv ) ) );   /* A/B runs */
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
 }
@@ -182,16 +182,17 @@ bool RenderCore::UsePackets() const
 
 /* traversal loop of the per-ray launches (setting "traceVersion", 0: auto).  Auto: lh2_trace4d.inc (BVH4,
    packed-FMA slabs, LDS child references, rcp box reciprocals, the single instance entered at ray
-   set-up); while the BVH4 + triangles fit the 256 MB Infinity Cache each branch fetches its own record
-   (6: config 2 bounce rays 0.86 vs 0.88 ms for the v4 loop, config 3 2.68 vs 2.77 ms per frame), beyond
-   it every lane's record is fetched at once, one round trip per iteration (5: config 5, 1 GB, 13.31 vs
-   13.68 ms; profiles/r02j_ab_versions.txt) */
+   set-up).  While the BVH4 + triangles fit the 256 MB Infinity Cache each branch fetches its own record
+   and every reached leaf is tested at once (6: config-2 bounce rays 0.86 ms vs 0.88 for the v4 loop,
+   config 3 2.68 vs 2.77 ms per frame); beyond it leaves are parked in a one-entry slot and tested in
+   batches of leafBatch (default 16) lanes (7: config 5, 1 GB, 12.89 ms per frame vs 13.31 for the one-fetch
+   loop 5 and 13.68 for 6; profiles/r02j_ab_versions.txt, r02l_ab_slot.txt) */
 int RenderCore::TraceVersion() const
 {
 	if (traceVersion) return (traceVersion >= 4 && !bvh4) ? 2 : traceVersion;
 	if (!bvh4) return 2;
 	const double bytes = ((double)blasNode4Count + tlasCapacity) * 128.0 + (double)blasTriCount * 48.0;
-	return bytes > (double)traceFetchMB * 1048576.0 ? 5 : 6;
+	return bytes > (double)traceFetchMB * 1048576.0 ? 7 : 6;
 }
 
 void RenderCore::EnsureBuffers()
@@ -255,7 +256,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	}
 	else if (!strcmp( name, "packetShadow" )) packetShadow = value != 0;     /* packet traversal of the shadow rays */
 	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice uses the primary-ray launch */
-	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 6, std::max( 0, (int)value ) );   /* traversal loop: 1, 2 (BVH2), 4 (BVH4), 5 / 6 (BVH4, lh2_trace4d.inc: one fetch per iteration / per branch), 0 auto */
+	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 7, std::max( 0, (int)value ) );   /* traversal loop: 1, 2 (BVH2), 4 (BVH4), 5 / 6 (BVH4, lh2_trace4d.inc: one fetch per iteration / per branch), 0 auto */
 	else if (!strcmp( name, "traceFetchMB" )) traceFetchMB = std::max( 0.0f, value );
 	else if (!strcmp( name, "bvh4" )) { bvh4 = value != 0; if (!bvh4 && traceVersion >= 4) traceVersion = 2; }   /* before SetGeometry */
 	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */

@@ -296,7 +296,8 @@ def test_packet_shadow_frame_parity(fresh_core):
 
 
 @pytest.mark.parametrize("version,leaf_batch,max_leaf", [(1, 0, 2), (1, 16, 2), (2, 0, 2), (2, 16, 1), (4, 0, 1), (4, 16, 2), (4, 8, 4),
-                                                       (5, 0, 1), (5, 0, 2), (5, 0, 4), (6, 0, 1), (6, 0, 2), (6, 0, 4)])
+                                                       (5, 0, 1), (5, 0, 2), (5, 0, 4), (6, 0, 1), (6, 0, 2), (6, 0, 4),
+                                                       (7, 0, 1), (7, 1, 2), (7, 32, 1), (7, 8, 4)])
 def test_traversal_variants_bitexact(fresh_core, version, leaf_batch, max_leaf):
     """Every per-ray traversal loop (trace_stream, lh2_trace2.inc over the BVH2 and over the BVH4
     collapse, lh2_trace4d.inc with its leaf slot), with and without leaf parking, over trees of different leaf sizes, returns the
@@ -316,7 +317,7 @@ def test_traversal_variants_bitexact(fresh_core, version, leaf_batch, max_leaf):
     assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
 
 
-@pytest.mark.parametrize("version", [4, 5, 6])
+@pytest.mark.parametrize("version", [4, 5, 6, 7])
 def test_bvh4_deep_stack(fresh_core, version):
     """A deep BLAS (triangles shrinking geometrically along a line: a chain-like SAH tree) next to the
     random cloud: BVH4 nodes push up to three children per level, the LDS part of the traversal
@@ -465,7 +466,7 @@ def test_terminal_shade_frame_parity(fresh_core, kind):
     assert np.array_equal(ag[..., 3], a0[..., 3])
 
 
-@pytest.mark.parametrize("version", [1, 2, 4, 5, 6])
+@pytest.mark.parametrize("version", [1, 2, 4, 5, 6, 7])
 @pytest.mark.parametrize("start", [0, 1])
 def test_single_instance_start_bitexact(fresh_core, version, start):
     """One instance (sheared and scaled): with singleInstanceStart the rays begin at its TLAS leaf
@@ -510,7 +511,7 @@ def test_no_lights_rng_stream_past_sample_256(fresh_core):
     assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
 
 
-@pytest.mark.parametrize("version", [4, 5, 6])
+@pytest.mark.parametrize("version", [4, 5, 6, 7])
 def test_lit_room_frame_traversal_versions(fresh_core, version):
     """The whole lit frame (closest hits of every bounce, any-hit shadow rays with the fused connect)
     through the BVH4 loops: identical ray counts and accumulator."""
