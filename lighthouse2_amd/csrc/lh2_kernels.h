@@ -121,7 +121,8 @@ struct FrameStatsDev
 
 extern "C" {
 void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, LaunchEvents ev, hipStream_t st );
-void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, uint32_t* hostActiveLog, LaunchEvents ev, hipStream_t st );
+void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, uint32_t* hostActiveLog, uint32_t* shadowSnap,
+	uint32_t* shadowCursor, LaunchEvents ev, hipStream_t st );
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st );

@@ -1706,9 +1706,18 @@ __global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t segSt
 {
 	init_counters( c, pathCount, segStride, cursors, cursorWords, blockIdx.x * blockDim.x + threadIdx.x );
 }
-__global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength, int resetShadow, uint32_t* hostActiveLog )
+__global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength, int resetShadow, uint32_t* hostActiveLog,
+	uint32_t* shadowSnap, uint32_t* shadowCursor )
 {
 	if (threadIdx.x != 0) return;
+	/* the shadow split: the shadow rays queued so far (segment by segment) are traced by an early launch
+	   with these counts, the final shadow launch starts its work queues behind them */
+	if (shadowSnap)
+		for (int k = 0; k < LH2_SEGS; k++)
+		{
+			const uint32_t n = c->segShadow[k * LH2_SEGCOUNT_STRIDE];
+			shadowSnap[k * LH2_SEGCOUNT_STRIDE] = n, shadowCursor[k * LH2_CURSOR_STRIDE] = n;
+		}
 	/* the extension rays become the next bounce's paths, segment by segment */
 	uint32_t ext = 0, sh = 0;
 	for (int k = 0; k < LH2_SEGS; k++)
@@ -1795,9 +1804,10 @@ void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStri
 {
 	LH2_LAUNCH( k_init_counters, (cursorWords + 255) / 256 + 1, 256, st, ev, c, pathCount, segStride, cursors, cursorWords );
 }
-void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, uint32_t* hostActiveLog, LaunchEvents ev, hipStream_t st )
+void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, uint32_t* hostActiveLog, uint32_t* shadowSnap,
+	uint32_t* shadowCursor, LaunchEvents ev, hipStream_t st )
 {
-	LH2_LAUNCH( k_counters_next, 1, 64, st, ev, c, log, pathLength, resetShadow, hostActiveLog );
+	LH2_LAUNCH( k_counters_next, 1, 64, st, ev, c, log, pathLength, resetShadow, hostActiveLog, shadowSnap, shadowCursor );
 }
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, LaunchEvents ev, hipStream_t st )
 {

@@ -131,6 +131,10 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 		CHK_HIP( hipEventCreateWithFlags( &g.evDone, hipEventDisableTiming ) );
 	}
 	CHK_HIP( hipEventCreateWithFlags( &evFork, hipEventDisableTiming ) );
+	CHK_HIP( hipStreamCreateWithFlags( &sideStream, hipStreamNonBlocking ) );
+	CHK_HIP( hipEventCreate( &evSideStart ) );
+	CHK_HIP( hipEventCreate( &evSideStop ) );
+	shadowSnap.resize( LH2_SEGS * LH2_SEGCOUNT_STRIDE );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
@@ -220,6 +224,7 @@ void RenderCore::EnsureStack( PathGroup& g )
 {
 	const size_t need = (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256;
 	if (g.gstack.count < need) g.gstack.resize( need );
+	if (&g == &grp[0] && sideStack.count < need) sideStack.resize( need );
 }
 
 void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439-457 */
@@ -245,6 +250,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
 	else if (!strcmp( name, "packetWidth" )) packetWidth = value >= 4 ? 4 : 2;   /* packets over the BVH2 / BVH4 */
+	else if (!strcmp( name, "shadowSplit" )) shadowSplit = std::min( LH2_MAX_BOUNCES, std::max( 0, (int)value ) );   /* early shadow launch after this bounce (0: off) */
 	else if (!strcmp( name, "pathGroups" )) pathGroups = std::min( LH2_MAX_GROUPS, std::max( 1, (int)value ) );   /* pipelined path groups per frame */
 	else if (!strcmp( name, "singleInstanceStart" )) singleInstanceStart = value != 0;   /* one instance: rays start at its TLAS leaf */
 	else if (!strcmp( name, "terminalShade" )) terminalShade = value != 0;   /* drop hits that cannot contribute before shading them (ShadeParams::terminal) */
@@ -274,7 +280,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
-		{ "pathGroups", (float)pathGroups }, { "singleInstanceStart", (float)singleInstanceStart },
+		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "traceFetchMB", traceFetchMB }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "blocksPerCU", (float)blocksPerCU },
 		{ "packetShadow", (float)packetShadow }, { "usePackets", (float)UsePackets() } };
@@ -755,6 +761,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	   rays and their launches are not queued */
 	const bool shadows = nArea + nPoint + nSpot + nDir > 0;
 	frameShadows = shadows;
+	const int splitL = (shadows && !primeRef && G == 1 && shadowSplit > 0 && shadowSplit < maxPL) ? shadowSplit : 0;
+	frameSplit = false;
 	/* the bounce loop, the groups' launches interleaved */
 	for (int pathLength = 1; pathLength <= maxPL; pathLength++)
 	{
@@ -808,8 +816,24 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				g.fromShadowB[pathLength] = g.prevStop, g.prevStop = g.evShadowB[pathLength];
 			}
 			/* the kernel writes this bounce's extension-ray count into the pinned activeLog itself */
-			lh2_launch_counters_next( c, g.rayLog.ptr, pathLength, primeRef, g.activeLog, { nullptr, g.evCount[pathLength] }, g.st );
+			const bool split = pathLength == splitL;
+			lh2_launch_counters_next( c, g.rayLog.ptr, pathLength, primeRef, g.activeLog, split ? shadowSnap.ptr : nullptr,
+				split ? g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr, { nullptr, g.evCount[pathLength] }, g.st );
 			g.prevStop = g.evCount[pathLength];
+			if (split)
+			{
+				/* the shadow rays queued so far, on the side stream, beside the later bounces; the final
+				   shadow launch's work queues start behind them (k_counters_next) */
+				CHK_HIP( hipStreamWaitEvent( sideStream, g.evCount[pathLength], 0 ) );
+				TraceArgs ta{};
+				ta.version = TraceVersion();
+				ta.rayO = g.shO.ptr, ta.rayD = g.shD.ptr, ta.segCounts = shadowSnap.ptr, ta.segStride = g.shadowStride;
+				ta.cursor = g.cursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+				ta.mask = g.shMask.ptr, ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = sideStack.ptr;
+				ta.packet = packetShadow ? PacketMode() : 0;
+				lh2_launch_trace_any( &sd, &ta, grid, 1, { evSideStart, evSideStop }, sideStream );
+				frameSplit = true;
+			}
 		}
 		if (!any) break;
 		/* early exit without stalling the GPU: wait for the count of a group's previous bounce while
@@ -842,6 +866,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, g.evShadow }, g.st );
 			g.fromShadow = g.prevStop;
 		}
+		if (gi == 0 && frameSplit) CHK_HIP( hipStreamWaitEvent( stream, evSideStop, 0 ) );   /* join the side stream's shadow launch */
 		if (gi)
 		{
 			CHK_HIP( hipEventRecord( g.evDone, g.st ) );

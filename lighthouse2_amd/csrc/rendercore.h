@@ -212,6 +212,18 @@ private:
 	   config 2 (1 group 1.88 ms, 2 groups 1.97, 4 groups 2.16, profiles/r01c_ab_path_groups.jsonl):
 	   concurrent traversals slow each other down and a shade pass beside a traversal takes 4x longer */
 	int pathGroups = 1;
+	/* shadow split (setting "shadowSplit", 0: off): the shadow rays queued by the first shadowSplit
+	   bounces are traced on a second stream while the later bounces run (their launches hold few rays:
+	   config 3's bounces 3 and 4 trace 0.53 M and 60 k rays in 266 + 208 us); the final shadow launch
+	   traces the rest.  One path group, no PrimeRef.  Off: measured no faster (config 3 2.71 ms off,
+	   2.72 / 2.74 / 2.75 with 1 / 2 / 3), the shade passes beside the side launch slow down by as much
+	   as the shadow pass gains (profiles/r02n_ab_shadow_split.txt) */
+	int shadowSplit = 0;
+	hipStream_t sideStream = nullptr;
+	hipEvent_t evSideStart = nullptr, evSideStop = nullptr;
+	DevBuf<uint32_t> shadowSnap;
+	DevBuf<int> sideStack;               /* the side launch's global traversal stack (it runs beside group 0's) */
+	bool frameSplit = false;
 	int frameGroups = 1;
 	hipEvent_t evFork = nullptr;
 	bool tileChanged = false;

@@ -526,3 +526,22 @@ def test_lit_room_frame_traversal_versions(fresh_core, version):
     assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
     ag, ao = fresh_core.accumulator(), o.accumulator()
     assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+
+
+@pytest.mark.parametrize("split", [0, 1, 2, 3])
+def test_shadow_split_frame_parity(fresh_core, split):
+    """The shadow rays of the first `split` bounces traced on a side stream beside the later bounces,
+    the rest by the final shadow launch (setting shadowSplit): identical ray counts and accumulator."""
+    w, h = 128, 72
+    sc = scene.room_scene(40000, w, h)
+    fresh_core.setting("shadowSplit", split)
+    o = _load_both(fresh_core, sc, w, h)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", 4)
+    for f in range(2):
+        sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
+        sc.render_frame(o, converge=1 if f == 0 else 0)
+        assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
+    ag, ao = fresh_core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+    assert fresh_core.stats().shadowTraceTime > 0
