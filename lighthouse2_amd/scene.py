@@ -97,39 +97,91 @@ def _norm(v: np.ndarray) -> np.ndarray:
     return (v * (np.float32(1) / np.sqrt(np.float32(np.dot(v, v))))).astype(np.float32)
 
 
+_LIBM = None
+
+
+def _tanf(x: np.float32) -> np.float32:
+    """C tanf (the reference's camera.cpp calls it on a float): libm through ctypes, so the screen size
+    rounds exactly as Camera::GetView's does."""
+    global _LIBM
+    import ctypes
+    if _LIBM is None:
+        _LIBM = ctypes.CDLL("libm.so.6")
+        _LIBM.tanf.restype = ctypes.c_float
+        _LIBM.tanf.argtypes = [ctypes.c_float]
+    return np.float32(_LIBM.tanf(float(x)))
+
+
 def camera_view(pos, direction, fov_deg: float = 40.0, aspect: float = 16 / 9, focal: float = 5.0,
                 aperture: float = 0.0, distortion: float = 0.0, pixel_height: int = 1080) -> abi.ViewPyramid:
-    pos = _f3(*pos)
-    z = _norm(_f3(*direction))
+    """Camera::GetView (RenderSystem/camera.cpp:96-117, CalculateMatrix :40-58) in float32, in the
+    reference's evaluation order (helper_math.h host forms: normalize = v * (1 / sqrtf(dot)), length =
+    sqrtf(dot), cross / dot component-wise); pinned bit for bit to the reference compiled from its
+    sources (tests/test_golden.py::test_camera_view_matches_reference).  `direction` is used as given
+    (Camera::direction is kept normalised by the app)."""
+    f32 = np.float32
+
+    def v3(x, y, z):
+        return (f32(x), f32(y), f32(z))
+
+    def add(a, b):
+        return (f32(a[0] + b[0]), f32(a[1] + b[1]), f32(a[2] + b[2]))
+
+    def sub(a, b):
+        return (f32(a[0] - b[0]), f32(a[1] - b[1]), f32(a[2] - b[2]))
+
+    def smul(s, a):                    # float * float3
+        return (f32(s * a[0]), f32(s * a[1]), f32(s * a[2]))
+
+    def vmul(a, s):                    # float3 * float
+        return (f32(a[0] * s), f32(a[1] * s), f32(a[2] * s))
+
+    def dot(a, b):
+        return f32(f32(f32(a[0] * b[0]) + f32(a[1] * b[1])) + f32(a[2] * b[2]))
+
+    def cross(a, b):
+        return (f32(f32(a[1] * b[2]) - f32(a[2] * b[1])), f32(f32(a[2] * b[0]) - f32(a[0] * b[2])),
+                f32(f32(a[0] * b[1]) - f32(a[1] * b[0])))
+
+    def normalize(a):
+        return vmul(a, f32(f32(1) / np.sqrt(dot(a, a))))
+
+    def length(a):
+        return np.sqrt(dot(a, a))
+
+    P = v3(*pos)
+    z = v3(*direction)
     if abs(float(z[1])) > 0.99:
-        y = _f3(1, 0, 0)
+        y = v3(1, 0, 0)
     else:
-        y = _f3(0, 1, 0)
-    x = _norm(np.cross(z, y).astype(np.float32))
-    y = np.cross(x, z).astype(np.float32)
+        y = v3(0, 1, 0)
+    x = normalize(cross(z, y))
+    y = cross(x, z)
     right, up, forward = x, y, z
-    fov = np.float32(fov_deg)
-    pi = np.float32(math.pi)
-    screen = np.float32(math.tan(float(fov) / 2 / (180 / math.pi)))
-    f = np.float32(focal)
-    a = np.float32(aspect)
-    C = pos + f * forward
-    p1 = C - screen * right * f * a + screen * f * up
-    p2 = C + screen * right * f * a + screen * f * up
-    p3 = C - screen * right * f * a - screen * f * up
+    fov, a, fd = f32(fov_deg), f32(aspect), f32(focal)
+    pi = f32(3.14159265358979323846264)
+    screen = _tanf(f32(f32(fov / f32(2)) / f32(f32(180) / pi)))
+    C = add(P, smul(fd, forward))
+    t_r = vmul(vmul(smul(screen, right), fd), a)          # screenSize * right * focalDistance * aspectRatio
+    t_u = smul(f32(screen * fd), up)                        # screenSize * focalDistance * up
+    p1 = add(sub(C, t_r), t_u)
+    p2 = add(add(C, t_r), t_u)
+    p3 = sub(sub(C, t_r), t_u)
     v = abi.ViewPyramid()
-    v.pos = abi.float3(*map(float, pos))
-    v.p1 = abi.float3(*map(float, p1.astype(np.float32)))
-    v.p2 = abi.float3(*map(float, p2.astype(np.float32)))
-    v.p3 = abi.float3(*map(float, p3.astype(np.float32)))
-    v.aperture = float(aperture)
-    v.spreadAngle = float(fov * pi / np.float32(180) / np.float32(pixel_height))
-    v.focalDistance = float(focal)
-    v.distortion = float(distortion)
-    u1 = C - screen * right * a + screen * up
-    u2 = C + screen * right * a + screen * up
-    u3 = C - screen * right * a - screen * up
-    v.imagePlane = float(np.linalg.norm(u1 - u2) * np.linalg.norm(u1 - u3))
+    v.pos = abi.float3(*map(float, P))
+    v.p1 = abi.float3(*map(float, p1))
+    v.p2 = abi.float3(*map(float, p2))
+    v.p3 = abi.float3(*map(float, p3))
+    v.aperture = float(f32(aperture))
+    v.spreadAngle = float(f32(f32(f32(fov * pi) / f32(180)) / f32(pixel_height)))
+    v.focalDistance = float(fd)
+    v.distortion = float(f32(distortion))
+    u_r = vmul(smul(screen, right), a)                      # screenSize * right * aspectRatio
+    u_u = smul(screen, up)
+    u1 = add(sub(C, u_r), u_u)
+    u2 = add(add(C, u_r), u_u)
+    u3 = sub(sub(C, u_r), u_u)
+    v.imagePlane = float(f32(length(sub(u1, u2)) * length(sub(u1, u3))))
     return v
 
 

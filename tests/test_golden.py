@@ -102,3 +102,99 @@ def test_oracle_frame_regression(name, make):
     sc.render_frame(o)
     assert np.array_equal(o.ray_counts(), g[name + "_counts"])
     assert np.array_equal(o.accumulator(), g[name + "_acc"])
+
+
+# ---------------------------------------------------------------------------------------------------
+# host-side conversions pinned to the reference compiled from its sources (oracle/ref_pins.cpp ->
+# oracle/_ref/libref_pins.so, oracle/Makefile.ref): mat4::Inverted, half(float), Camera::GetView
+# ---------------------------------------------------------------------------------------------------
+PINS = pathlib.Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "libref_pins.so"
+
+
+def _pins():
+    import ctypes as C
+    L = C.CDLL(str(PINS))
+    P = C.c_void_p
+    L.pin_mat4_inverted.argtypes = [P, P]
+    L.pin_float_to_half.argtypes = [P, P, C.c_int]
+    L.pin_camera_view.argtypes = [P, P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, P]
+    return L
+
+
+@pytest.mark.skipif(not PINS.exists(), reason="reference pins not built (no /root/reference)")
+def test_mat4_inverse_matches_reference():
+    """The instance inverse of UpdateToplevel (orc_mat4_inverse; the core's RenderCore::UpdateToplevel
+    and device TLAS build use the same formula) equals lighthouse2::mat4::Inverted bit for bit
+    (RenderSystem/common_types.h:586-628)."""
+    import ctypes as C
+    from oracle import oracle as orc_mod
+    L = _pins()
+    rng = np.random.default_rng(21)
+    mats = []
+    for k in range(400):
+        m = np.eye(4, dtype=np.float32)
+        if k % 4 == 0:
+            m[:3, :3] = scene.rotation_y(float(rng.uniform(0, 6.3)))[:3, :3]
+        elif k % 4 == 1:
+            m[:3, :3] = rng.normal(size=(3, 3))                      # general linear (shear, scale)
+        elif k % 4 == 2:
+            m[:3, :3] = np.diag(rng.uniform(0.01, 100, 3))
+        else:
+            m = rng.normal(size=(4, 4))                             # projective
+        m[:3, 3] = rng.uniform(-50, 50, 3)
+        mats.append(np.ascontiguousarray(m, np.float32))
+    mats.append(np.zeros((4, 4), np.float32))                       # singular: identity in both
+    lib = orc_mod.lib()
+    for m in mats:
+        ref = np.zeros(16, np.float32)
+        L.pin_mat4_inverted(m.ctypes.data, ref.ctypes.data)
+        ours = np.zeros(16, np.float32)
+        lib.orc_mat4_inverse(m.ravel().ctypes.data_as(C.POINTER(C.c_float)), ours.ctypes.data_as(C.POINTER(C.c_float)))
+        assert np.array_equal(ours.view(np.uint32), ref.view(np.uint32)), m
+
+
+@pytest.mark.skipif(not PINS.exists(), reason="reference pins not built (no /root/reference)")
+def test_half_conversion_matches_reference():
+    """lh2_f2h (include/lh2_detmath.h; the core's SetMaterials and the oracle) equals half_float::half(float)
+    of half2.1.0/half.hpp (round to nearest, HALF_ROUND_STYLE 1), the conversion RenderCore_OptixPrime_B
+    applies to material colours, on every rounding tie, subnormals, overflow and random values."""
+    from oracle import oracle as orc_mod
+    L = _pins()
+    rng = np.random.default_rng(22)
+    h = np.arange(0, 0x7c00, dtype=np.uint32)                   # every finite positive half
+    f16 = h.astype(np.uint16).view(np.float16).astype(np.float32)
+    up = np.nextafter(f16, np.float32(np.inf))
+    mid = ((f16.astype(np.float64) + np.concatenate([f16[1:], [65536.0]]).astype(np.float64)) / 2).astype(np.float32)
+    x = np.concatenate([f16, up, mid, np.nextafter(mid, np.float32(0)), np.nextafter(mid, np.float32(np.inf)),
+                        rng.normal(scale=1, size=20000), rng.normal(scale=1e-5, size=5000), rng.normal(scale=3e4, size=5000),
+                        np.float32([65504, 65519.99, 65520, 1e10, np.inf])]).astype(np.float32)
+    x = np.concatenate([x, -x])
+    ref = np.zeros(len(x), np.uint16)
+    L.pin_float_to_half(x.ctypes.data, ref.ctypes.data, len(x))
+    ours = orc_mod.detmath(7, x)                                    # lh2_h2f(lh2_f2h(x))
+    want = ref.view(np.float16).astype(np.float32)
+    assert np.array_equal(ours.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.skipif(not PINS.exists(), reason="reference pins not built (no /root/reference)")
+@pytest.mark.parametrize("cam", [
+    ((0, 0, -12), (0, 0, 1), 40, 16 / 9, 5, 0, 0, (1920, 1080)),       # config 2 (bench)
+    ((0, 6, 11), (0, -0.15, -1), 60, 16 / 9, 5, 0, 0, (1920, 1080)),   # config 3 room
+    ((0, 60, -80), (0, -0.6, 1), 50, 16 / 9, 5, 0, 0, (1920, 1080)),   # config 5
+    ((0.3, 0.2, -12), (0.05, -0.02, 1), 50, 96 / 54, 5, 0.05, 0.05, (96, 54)),
+    ((1, 30, 2), (0.01, -1, 0.05), 75, 1.0, 2.5, 0.1, 0.0, (640, 640)),   # looking down: CalculateMatrix's other branch
+])
+def test_camera_view_matches_reference(cam):
+    """scene.camera_view (the ViewPyramid every test scene and the bench render with) equals
+    Camera::GetView (RenderSystem/camera.cpp:96-117) bit for bit."""
+    L = _pins()
+    pos, d, fov, aspect, focal, aperture, distortion, (px, py) = cam
+    dn = np.asarray(d, np.float64)
+    dn = (dn / np.linalg.norm(dn)).astype(np.float32)               # Camera::direction is kept normalised
+    ref = np.zeros(17, np.float32)
+    L.pin_camera_view(np.asarray(pos, np.float32).ctypes.data, dn.ctypes.data, fov, aspect, focal, aperture, distortion,
+                      px, py, ref.ctypes.data)
+    v = scene.camera_view(pos, dn, fov_deg=fov, aspect=aspect, focal=focal, aperture=aperture, distortion=distortion,
+                          pixel_height=py)
+    ours = np.frombuffer(bytes(v), np.float32)
+    assert np.array_equal(ours.view(np.uint32), ref.view(np.uint32)), (ours, ref)
