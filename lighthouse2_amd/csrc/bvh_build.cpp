@@ -48,6 +48,7 @@ struct Builder
 	std::atomic<int> threadsLeft{ 0 };
 	int maxLeaf;
 	float C_TRAV = 1.0f;
+	uint32_t sweepMax = 0;        /* nodes of at most this many primitives: exact SAH sweep over sorted centroids */
 
 	explicit Builder( const std::vector<Aabb>& p ) : prims( p ) {}
 
@@ -99,10 +100,33 @@ struct Builder
 				if (cost < bestCost) bestCost = cost, bestAxis = a, bestBin = b;
 			}
 		}
+		/* exact SAH sweep for small nodes: every split position of the centroid order on each axis */
+		uint32_t sweepMid = 0;
+		if (count <= sweepMax)
+		{
+			std::vector<uint32_t> order( count ), bestOrder;
+			std::vector<float> rightArea( count + 1 );
+			for (int a = 0; a < 3; a++)
+			{
+				std::copy( idx.begin() + first, idx.begin() + first + count, order.begin() );
+				std::sort( order.begin(), order.end(), [&]( uint32_t p, uint32_t q ) { return cent[p * 3 + a] < cent[q * 3 + a] || (cent[p * 3 + a] == cent[q * 3 + a] && p < q); } );
+				Aabb acc = empty_box();
+				for (uint32_t i = count; i-- > 1;) { grow( acc, prims[order[i]] ); rightArea[i] = area( acc ); }
+				acc = empty_box();
+				for (uint32_t i = 1; i < count; i++)
+				{
+					grow( acc, prims[order[i - 1]] );
+					const float cost = C_TRAV + C_ISECT * (area( acc ) * (float)i + rightArea[i] * (float)(count - i)) / std::max( parentArea, 1e-30f );
+					if (cost < bestCost) bestCost = cost, bestAxis = a, sweepMid = i, bestOrder = order;
+				}
+			}
+			if (sweepMid) std::copy( bestOrder.begin(), bestOrder.end(), idx.begin() + first );
+		}
 		const float leafCost = C_ISECT * (float)count;
 		if (count <= (uint32_t)maxLeaf && (bestAxis < 0 || leafCost <= bestCost)) { make_leaf( ni, first, count, box ); return; }
 		uint32_t mid;
-		if (bestAxis >= 0)
+		if (sweepMid) mid = first + sweepMid;
+		else if (bestAxis >= 0)
 		{
 			const float ext = cbox.hi[bestAxis] - cbox.lo[bestAxis];
 			const float scale = (float)BINS * 0.99999f / ext;
@@ -145,7 +169,7 @@ inline int make_leaf_ref( uint32_t first, uint32_t count ) { return (int)~((firs
 
 }  // namespace
 
-void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost )
+void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost, int sweepMax )
 {
 	const uint32_t N = (uint32_t)prims.size();
 	if (maxLeaf < 1) maxLeaf = 1;
@@ -153,6 +177,7 @@ void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOut
 	Builder b( prims );
 	b.maxLeaf = maxLeaf;
 	b.C_TRAV = traversalCost > 0 ? traversalCost : 1.0f;
+	b.sweepMax = (uint32_t)std::max( 0, sweepMax );
 	const float C_TRAV = b.C_TRAV;
 	b.cent.resize( (size_t)N * 3 );
 	b.idx.resize( N );

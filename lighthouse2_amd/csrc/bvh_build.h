@@ -25,8 +25,9 @@ struct BvhOutput
 };
 
 /* prims: per-primitive bounds; maxLeaf: largest leaf; threads: worker threads (0 = hw);
-   traversalCost: SAH cost of a node visit relative to one triangle test */
-void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost = 1.0f );
+   traversalCost: SAH cost of a node visit relative to one triangle test; sweepMax: nodes of at most
+   this many primitives split by an exact SAH sweep over the sorted centroids (0: binned only) */
+void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost = 1.0f, int sweepMax = 0 );
 
 /* BVH2 (16 floats per node, root 0) -> BVH4 (32 floats per node, root 0; layout: lh2_device.h) by
    greedy surface-area collapse; returns the BVH4 depth (interior levels) */

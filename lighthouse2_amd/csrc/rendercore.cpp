@@ -246,6 +246,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
+	else if (!strcmp( name, "bvhSweep" )) bvhSweep = std::max( 0, (int)value );   /* exact SAH sweep for nodes of <= this many triangles */
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
@@ -279,7 +280,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "epsilon", geometryEpsilon }, { "clampValue", clampValue }, { "maxPathLength", (float)maxPathLength },
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
-		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
+		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "traceFetchMB", traceFetchMB }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "blocksPerCU", (float)blocksPerCU },
@@ -429,7 +430,7 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 			}
 		}
 		BvhOutput bvh;
-		BuildBvh2( prims, bvhMaxLeaf, 0, bvh, bvhTraversalCost );
+		BuildBvh2( prims, bvhMaxLeaf, 0, bvh, bvhTraversalCost, bvhSweep );
 		std::vector<float> tris48( (size_t)std::max( triangleCount, 1 ) * 12, 0.0f );
 		for (size_t j = 0; j < bvh.perm.size(); j++)
 		{

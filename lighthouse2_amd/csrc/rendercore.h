@@ -242,6 +242,7 @@ private:
 	   bvhMaxLeaf 2 / leafBatch 16, config 5 2 % slower */
 	int refillPrimary = 48, refillOther = 48, leafBatch = 0, leafBatchPrimary = 8;
 	int bvhMaxLeaf = 1;
+	int bvhSweep = 0;                    /* exact SAH sweep below this node size (setting "bvhSweep") */
 	int traceVersion = 0;                /* 0: auto (TraceVersion) */
 	float traceFetchMB = 256.0f;         /* auto: traceVersion 5 above this BVH4 + triangle footprint */
 	int TraceVersion() const;
