@@ -529,8 +529,8 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 }
 
 #include "lh2_trace2.inc"
-#include "lh2_trace_packet.inc"
 #include "lh2_trace4d.inc"
+#include "lh2_trace_packet.inc"
 
 /* packet traversal of coherent (8x8-tiled primary) rays: wave-uniform, no LDS stack */
 /* 8 waves per SIMD (64 VGPRs, ~32 spilled outside the node loop): the packet loop is bound by the
