@@ -5,7 +5,8 @@ Workload (BASELINE.json configs[1]): 100k random triangles
 roughness 1.  One step = one complete frame of the wavefront path tracer through the reference
 CoreAPI (camera rays, closest-hit BVH traversal, shade/extend/NEE, next bounce, shadow rays,
 finalize) = primary + secondary extension rays (ENOUGH_BOUNCES = S_BOUNCED ends diffuse paths
-after the second vertex, pathtracer.h:33,211), plus, for N > 1, the accumulator gather to rank 0.
+after the second vertex, pathtracer.h:33,211), plus, for N > 1, the pack of the owned rows and their
+gather to rank 0 (one rank keeps the finished frame in the core's frame buffer).
 
 Multi-GPU, two measurements per run:
   value (weak scaling): with N ranks the frame is 1920 x (1080 N) pixels of the same 16:9 view,
@@ -125,10 +126,13 @@ def cpu_baseline(sc, width, height, seconds):
 
 
 def timed_frames(core, sc, gather, steps, warmup, world, dev, per_frame=None):
-    """warmup + steps frames (render, pack the owned rows, gather); returns (max-over-ranks seconds,
-    rays of all ranks per frame [primary + bounce 1, deeper, shadow], this rank's counts)."""
+    """warmup + steps frames (render; N > 1: pack the owned rows, gather); returns (max-over-ranks
+    seconds, rays of all ranks per frame [primary + bounce 1, deeper, shadow], this rank's counts).
+    With one rank the finished frame is the core's own frame buffer: there is nothing to exchange."""
     def step():
         sc.render_frame(core, converge=1)     # Restart: the same paths every step
+        if world == 1:
+            return None
         core.pack_tile(gather.send.data_ptr())    # owned accumulator rows (ordered with torch's stream)
         return gather.gather()
 

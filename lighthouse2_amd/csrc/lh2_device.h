@@ -37,16 +37,18 @@ struct alignas( 16 ) DevInstance
 
 struct Counters   /* core_settings.h:81-91 plus device-side error flags */
 {
-	/* totals kept by k_init_counters / k_counters_next (activePaths: paths of this bounce, read by the
-	   host's early exit); the rays themselves are counted per segment below, and the host sums segShadow
-	   for the statistics (extensionRays, shadowRays stay 0) */
+	/* totals kept by the camera launch and the bounce hand-off (advance_bounce: the last block of a
+	   shade launch, or k_counters_next; activePaths: paths of the next bounce); the rays themselves are
+	   counted per segment below, and the host sums segShadow for the statistics (extensionRays,
+	   shadowRays stay 0) */
 	uint32_t activePaths, extensionRays, shadowRays, totalExtensionRays;
 	uint32_t totalShadowRays; int probedInstid, probedTriid; float probedDist;
-	uint32_t reserved0, shadowOverflow, pad0, pad1;
+	uint32_t reserved0, shadowOverflow, shadeDone, pad1;   /* shadeDone: blocks of the running shade launch that finished */
 	uint32_t pad2[20];
-	/* per-segment counts of the segmented streams (lh2_kernels.h, LH2_SEGS), 128 B apart: paths of
-	   this bounce, extension rays for the next, shadow rays queued */
-	uint32_t segActive[8 * 32], segExt[8 * 32], segShadow[8 * 32];
+	/* per-segment counts of the segmented streams (lh2_kernels.h, LH2_SEGS), 128 B apart.  The path
+	   counts ping-pong: the paths of pathLength L are counted in segPath[(L - 1) & 1], and its shade
+	   launch counts the extension rays (pathLength L + 1) into segPath[L & 1]; shadow rays queued */
+	uint32_t segPath[2][8 * 32], segShadow[8 * 32];
 };
 
 /* ---- small vector helpers with the reference's evaluation order --------------------------- */

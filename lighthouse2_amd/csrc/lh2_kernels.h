@@ -51,9 +51,20 @@ struct SceneDev       /* everything the traversal and shading kernels read, by v
 	uint32_t argb32Count, nrm32Count;
 };
 
+struct BounceAdvance  /* the hand-off to the next bounce (advance_bounce, lh2_kernels.hip) */
+{
+	const uint32_t* segNext;         /* the extension rays' segment counts: the next bounce's paths */
+	uint32_t* segRetire;             /* this bounce's path counts, zeroed for the next shade launch's extensions */
+	uint32_t* rayCountLog;           /* [pathLength] = rays of the next bounce */
+	uint32_t* hostActiveLog;         /* pinned host copy of the same (the host's early exit), or null */
+	uint32_t* shadowSnap; uint32_t* shadowCursor;   /* the shadow split's snapshot, or null */
+};
+
 struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path state */
 {
 	const uint32_t* segCounts; uint32_t segStride;     /* input paths: a segmented stream (see LH2_SEGS) */
+	uint32_t* segOut;                                  /* extension rays: segment counts (Counters::segPath) */
+	int advance; BounceAdvance adv;                    /* nonzero: the launch's last block hands off to the next bounce */
 	uint32_t shadowStride;                             /* shadow-ray segments: capacity of each */
 	const float4* rayO; const float4* rayD; const float4* T4; const float4* Q4; const uint4* hits;
 	float4* rayOut; float4* rayDOut; float4* T4Out; float4* Q4Out;
@@ -121,8 +132,7 @@ struct FrameStatsDev
 
 extern "C" {
 void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, LaunchEvents ev, hipStream_t st );
-void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, uint32_t* hostActiveLog, uint32_t* shadowSnap,
-	uint32_t* shadowCursor, LaunchEvents ev, hipStream_t st );
+void lh2_launch_counters_next( Counters* c, const BounceAdvance* a, int pathLength, int resetShadow, LaunchEvents ev, hipStream_t st );
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st );

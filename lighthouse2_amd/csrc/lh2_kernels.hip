@@ -46,7 +46,7 @@ LH2_DEV uint32_t wave_alloc( bool want, uint32_t* counter )
 	return want ? base + lanes_below( m ) : 0xffffffffu;
 }
 
-static_assert( sizeof( ((Counters*)0)->segActive ) == LH2_SEGS * LH2_SEGCOUNT_STRIDE * 4, "Counters segment layout" );
+static_assert( sizeof( ((Counters*)0)->segShadow ) == LH2_SEGS * LH2_SEGCOUNT_STRIDE * 4, "Counters segment layout" );
 
 /* [lo, hi): segment c of a trace launch's ray stream (lh2_kernels.h, LH2_SEGS).  Wave-uniform, and
    said so (readfirstlane): kept in SGPRs, they cost the traversal loop no VGPRs (which it has none
@@ -141,14 +141,14 @@ LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_
 	{
 		/* the camera writes the paths densely: segment i is [i * segStride, (i + 1) * segStride) */
 		const uint32_t lo = (uint32_t)i * segStride;
-		c->segActive[i * LH2_SEGCOUNT_STRIDE] = pathCount > lo ? min( pathCount - lo, segStride ) : 0u;
-		c->segExt[i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadow[i * LH2_SEGCOUNT_STRIDE] = 0;
+		c->segPath[0][i * LH2_SEGCOUNT_STRIDE] = pathCount > lo ? min( pathCount - lo, segStride ) : 0u;
+		c->segPath[1][i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadow[i * LH2_SEGCOUNT_STRIDE] = 0;
 	}
 	if (i != 0) return;
 	c->activePaths = pathCount, c->extensionRays = 0, c->shadowRays = 0;
 	c->totalExtensionRays = pathCount, c->totalShadowRays = 0;
 	c->probedInstid = -1, c->probedTriid = -1, c->probedDist = 0;
-	c->reserved0 = 0, c->shadowOverflow = 0;
+	c->reserved0 = 0, c->shadowOverflow = 0, c->shadeDone = 0;
 }
 
 __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const uint8_t* __restrict__ bn, float4* __restrict__ rayO,
@@ -1313,6 +1313,7 @@ LH2_DEV const float4* HitInstance( const SceneDev& s, const int primIdx, const i
 }
 
 /* ---- shade kernel: pathtracer.h:54-245 --------------------------------------------------- */
+LH2_DEV void shade_epilogue( const ShadeParams& p );   /* the bounce hand-off, below */
 /* 3 waves per SIMD (<= 168 VGPRs, 4 spilled): the kernel is load-latency bound (a dependent chain of
    hit -> instance -> triangle -> material loads per path), 0.285 -> 0.244 ms per frame on config 2
    over the unbounded 171-VGPR build (2 waves); 4 waves spill ~100 VGPRs */
@@ -1487,7 +1488,7 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 		/* wave-level compaction of extension and shadow rays into this block's segment of the output
 		   streams (one atomicAdd per wave each, on the segment's own counter) */
 		{
-			const uint32_t es = wave_alloc( doExt, &p.counters->segExt[seg * LH2_SEGCOUNT_STRIDE] );
+			const uint32_t es = wave_alloc( doExt, &p.segOut[seg * LH2_SEGCOUNT_STRIDE] );
 			if (doExt) { const uint32_t o = segBase + es; p.rayOut[o] = eO; p.rayDOut[o] = eD; p.T4Out[o] = eT; p.Q4Out[o] = eQ; }
 			const uint32_t ss = wave_alloc( doShadow, &p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE] );
 			if (doShadow)
@@ -1497,6 +1498,7 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 			}
 		}
 	}
+	if (p.advance) shade_epilogue( p );
 }
 
 /* ShadeParams::terminal at the last vertex (pathLength == maxPathLength): k_shade<true> would drop
@@ -1690,7 +1692,7 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const 
 		}
 	compact:
 		{
-			const uint32_t es = wave_alloc( doExt, &p.counters->segExt[seg * LH2_SEGCOUNT_STRIDE] );
+			const uint32_t es = wave_alloc( doExt, &p.segOut[seg * LH2_SEGCOUNT_STRIDE] );
 			if (doExt) { const uint32_t o = segBase + es; p.rayOut[o] = eO; p.rayDOut[o] = eD; p.T4Out[o] = eT; p.Q4Out[o] = eQ; }
 			const uint32_t ss = wave_alloc( doShadow, &p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE] );
 			if (doShadow)
@@ -1706,33 +1708,58 @@ __global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t segSt
 {
 	init_counters( c, pathCount, segStride, cursors, cursorWords, blockIdx.x * blockDim.x + threadIdx.x );
 }
-__global__ void k_counters_next( Counters* c, uint32_t* rayCountLog, int pathLength, int resetShadow, uint32_t* hostActiveLog,
-	uint32_t* shadowSnap, uint32_t* shadowCursor )
+/* the hand-off from bounce L to bounce L + 1 (InitCountersSubsequent, .cuda.cu:76-84): the extension
+   rays counted into segNext become the next bounce's paths (the counts ping-pong, Counters::segPath),
+   the retired counts of bounce L are zeroed for the shade launch of L + 1; the shadow split's snapshot;
+   one thread, after every block of the shade launch of bounce L has finished */
+LH2_DEV void advance_bounce( Counters* c, const BounceAdvance& a, const int pathLength, const int resetShadow )
 {
-	if (threadIdx.x != 0) return;
 	/* the shadow split: the shadow rays queued so far (segment by segment) are traced by an early launch
 	   with these counts, the final shadow launch starts its work queues behind them */
-	if (shadowSnap)
+	if (a.shadowSnap)
 		for (int k = 0; k < LH2_SEGS; k++)
 		{
-			const uint32_t n = c->segShadow[k * LH2_SEGCOUNT_STRIDE];
-			shadowSnap[k * LH2_SEGCOUNT_STRIDE] = n, shadowCursor[k * LH2_CURSOR_STRIDE] = n;
+			const uint32_t n = __hip_atomic_load( &c->segShadow[k * LH2_SEGCOUNT_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+			a.shadowSnap[k * LH2_SEGCOUNT_STRIDE] = n, a.shadowCursor[k * LH2_CURSOR_STRIDE] = n;
 		}
-	/* the extension rays become the next bounce's paths, segment by segment */
 	uint32_t ext = 0, sh = 0;
 	for (int k = 0; k < LH2_SEGS; k++)
 	{
-		const uint32_t e = c->segExt[k * LH2_SEGCOUNT_STRIDE];
-		ext += e, c->segActive[k * LH2_SEGCOUNT_STRIDE] = e, c->segExt[k * LH2_SEGCOUNT_STRIDE] = 0;
+		ext += __hip_atomic_load( &a.segNext[k * LH2_SEGCOUNT_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+		a.segRetire[k * LH2_SEGCOUNT_STRIDE] = 0;
 		sh += c->segShadow[k * LH2_SEGCOUNT_STRIDE];
 		if (resetShadow) c->segShadow[k * LH2_SEGCOUNT_STRIDE] = 0;
 	}
-	rayCountLog[pathLength] = ext;     /* rays traced at pathLength + 1 */
+	a.rayCountLog[pathLength] = ext;     /* rays traced at pathLength + 1 */
 	c->totalExtensionRays += ext;
 	c->activePaths = ext;
-	if (resetShadow) c->totalShadowRays += sh;   /* InitCountersSubsequent (.cuda.cu:76-84) */
+	if (resetShadow) c->totalShadowRays += sh;
 	/* the host's early exit reads this after the launch's stop event (no copy launch) */
-	if (hostActiveLog) __hip_atomic_store( hostActiveLog + pathLength, ext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+	if (a.hostActiveLog) __hip_atomic_store( a.hostActiveLog + pathLength, ext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+}
+
+/* the end of a shade launch that hands off to the next bounce (ShadeParams::advance): its last block
+   to finish runs advance_bounce, so the hand-off needs no launch of its own (one dependent launch,
+   ~10 us, less per bounce) */
+LH2_DEV void shade_epilogue( const ShadeParams& p )
+{
+	/* no fences: an agent-scope fence writes back the XCD's L2 (the launch's ray outputs) in every
+	   block, +75 us per shade launch on config 2.  The counts are device-scope atomics that every wave
+	   waited for (wave_alloc uses their return values) before the block's arrival is issued, so they
+	   are performed when the last block reads them with device-scope loads */
+	__shared__ uint32_t lastBlock;
+	__syncthreads();
+	if (threadIdx.x == 0)
+		lastBlock = __hip_atomic_fetch_add( &p.counters->shadeDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ) == gridDim.x - 1;
+	__syncthreads();
+	if (!lastBlock || threadIdx.x != 0) return;
+	__hip_atomic_store( &p.counters->shadeDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+	advance_bounce( p.counters, p.adv, p.pathLength, 0 );
+}
+
+__global__ void k_counters_next( Counters* c, const BounceAdvance a, int pathLength, int resetShadow )
+{
+	if (threadIdx.x == 0) advance_bounce( c, a, pathLength, resetShadow );
 }
 __global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale, const FrameStatsDev fs )
 {
@@ -1804,10 +1831,9 @@ void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStri
 {
 	LH2_LAUNCH( k_init_counters, (cursorWords + 255) / 256 + 1, 256, st, ev, c, pathCount, segStride, cursors, cursorWords );
 }
-void lh2_launch_counters_next( Counters* c, uint32_t* log, int pathLength, int resetShadow, uint32_t* hostActiveLog, uint32_t* shadowSnap,
-	uint32_t* shadowCursor, LaunchEvents ev, hipStream_t st )
+void lh2_launch_counters_next( Counters* c, const BounceAdvance* a, int pathLength, int resetShadow, LaunchEvents ev, hipStream_t st )
 {
-	LH2_LAUNCH( k_counters_next, 1, 64, st, ev, c, log, pathLength, resetShadow, hostActiveLog, shadowSnap, shadowCursor );
+	LH2_LAUNCH( k_counters_next, 1, 64, st, ev, c, *a, pathLength, resetShadow );
 }
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, LaunchEvents ev, hipStream_t st )
 {

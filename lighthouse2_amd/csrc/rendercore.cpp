@@ -734,6 +734,9 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	/* no specular event and no alpha cut-out in any material: every path ends at its second vertex,
 	   so the bounce after it would be empty; not launching it saves three launches (~25 us) */
 	if (!primeRef && diffuseOnly) maxPL = std::min( maxPL, 2 );
+	/* the frame's start: a marker before the camera launch (~4 us of idle GPU), not the launch's own start
+	   event (hipExtLaunchKernelGGL start events cost ~8 us: tools/launch_gap.hip, profiles/r02q_launch_gap.txt) */
+	CHK_HIP( hipEventRecord( evFrame[0], stream ) );
 	if (G > 1) CHK_HIP( hipEventRecord( evFork, stream ) );   /* the other groups start after the accumulator reset */
 	for (int gi = 0; gi < G; gi++)
 	{
@@ -754,7 +757,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		cg.initC = g.counters.ptr, cg.cursors = g.cursors.ptr, cg.cursorWords = LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS;
 		cg.pathCount = g.count, cg.segStride = g.segStride;
 		cg.clearAcc = restart && G == 1 && !tileChanged ? accumulator.ptr : nullptr;
-		lh2_launch_camera( &cg, dBlueNoise.ptr, g.rayO[0].ptr, g.rayD[0].ptr, g.T4[0].ptr, g.Q4[0].ptr, (int)g.count, { gi ? nullptr : evFrame[0], g.evCamera }, g.st );
+		lh2_launch_camera( &cg, dBlueNoise.ptr, g.rayO[0].ptr, g.rayD[0].ptr, g.T4[0].ptr, g.Q4[0].ptr, (int)g.count, { nullptr, g.evCamera }, g.st );
 		g.prevStop = g.evCamera;
 	}
 	if (restart) tileChanged = false;
@@ -777,7 +780,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			Counters* c = g.counters.ptr;
 			TraceArgs ta{};
 			ta.version = TraceVersion();
-			ta.rayO = g.rayO[g.in].ptr, ta.rayD = g.rayD[g.in].ptr, ta.segCounts = c->segActive, ta.segStride = g.segStride;
+			/* the path counts ping-pong (Counters::segPath): this bounce's paths, and its extension rays */
+			uint32_t* segIn = c->segPath[(pathLength - 1) & 1];
+			uint32_t* segNext = c->segPath[pathLength & 1];
+			ta.rayO = g.rayO[g.in].ptr, ta.rayD = g.rayD[g.in].ptr, ta.segCounts = segIn, ta.segStride = g.segStride;
 			ta.cursor = g.cursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
 			ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
 			ta.packet = pathLength == 1 && tiledRays && UsePackets() ? PacketMode() : 0;
@@ -787,7 +793,14 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : grid, { nullptr, g.evTrace[pathLength] }, g.st );
 			g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
 			ShadeParams sp{};
-			sp.segCounts = c->segActive, sp.segStride = g.segStride, sp.shadowStride = g.shadowStride;
+			sp.segCounts = segIn, sp.segOut = segNext, sp.segStride = g.segStride, sp.shadowStride = g.shadowStride;
+			/* the hand-off to the next bounce: the shade launch's last block (no launch of its own), except
+			   in PrimeRef mode, where the bounce's shadow rays are traced (and their counts reset) first */
+			const bool split = pathLength == splitL;
+			const BounceAdvance adv{ segNext, segIn, g.rayLog.ptr, g.activeLog, split ? shadowSnap.ptr : nullptr,
+				split ? g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr };
+			sp.advance = pathLength < maxPL && !primeRef;
+			sp.adv = adv;
 			sp.rayO = g.rayO[g.in].ptr, sp.rayD = g.rayD[g.in].ptr, sp.T4 = g.T4[g.in].ptr, sp.Q4 = g.Q4[g.in].ptr, sp.hits = g.hits.ptr;
 			sp.rayOut = g.rayO[1 - g.in].ptr, sp.rayDOut = g.rayD[1 - g.in].ptr, sp.T4Out = g.T4[1 - g.in].ptr, sp.Q4Out = g.Q4[1 - g.in].ptr;
 			sp.shO = g.shO.ptr, sp.shD = g.shD.ptr, sp.shP = g.shP.ptr;
@@ -816,16 +829,18 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, g.evShadowB[pathLength] }, g.st );
 				g.fromShadowB[pathLength] = g.prevStop, g.prevStop = g.evShadowB[pathLength];
 			}
-			/* the kernel writes this bounce's extension-ray count into the pinned activeLog itself */
-			const bool split = pathLength == splitL;
-			lh2_launch_counters_next( c, g.rayLog.ptr, pathLength, primeRef, g.activeLog, split ? shadowSnap.ptr : nullptr,
-				split ? g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr, { nullptr, g.evCount[pathLength] }, g.st );
-			g.prevStop = g.evCount[pathLength];
+			/* the hand-off writes this bounce's extension-ray count into the pinned activeLog itself */
+			g.countReady[pathLength] = g.evShade[pathLength];
+			if (primeRef)
+			{
+				lh2_launch_counters_next( c, &adv, pathLength, 1, { nullptr, g.evCount[pathLength] }, g.st );
+				g.prevStop = g.countReady[pathLength] = g.evCount[pathLength];
+			}
 			if (split)
 			{
 				/* the shadow rays queued so far, on the side stream, beside the later bounces; the final
-				   shadow launch's work queues start behind them (k_counters_next) */
-				CHK_HIP( hipStreamWaitEvent( sideStream, g.evCount[pathLength], 0 ) );
+				   shadow launch's work queues start behind them (advance_bounce) */
+				CHK_HIP( hipStreamWaitEvent( sideStream, g.countReady[pathLength], 0 ) );
 				TraceArgs ta{};
 				ta.version = TraceVersion();
 				ta.rayO = g.shO.ptr, ta.rayD = g.shD.ptr, ta.segCounts = shadowSnap.ptr, ta.segStride = g.shadowStride;
@@ -845,7 +860,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			if (g.done) continue;
 			if (pathLength >= 2)
 			{
-				CHK_HIP( hipEventSynchronize( g.evCount[pathLength - 1] ) );
+				CHK_HIP( hipEventSynchronize( g.countReady[pathLength - 1] ) );
 				if (g.activeLog[pathLength - 1] == 0) { g.done = true; continue; }
 			}
 			g.in = 1 - g.in;

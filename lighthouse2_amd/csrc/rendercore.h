@@ -79,6 +79,7 @@ struct PathGroup
 	uint32_t* activeLog = nullptr;       /* pinned: extension rays after each bounce (k_counters_next) */
 	hipEvent_t evTrace[LH2_MAX_BOUNCES + 1] = {}, evShade[LH2_MAX_BOUNCES + 1] = {}, evShadowB[LH2_MAX_BOUNCES + 1] = {};
 	hipEvent_t evCount[LH2_MAX_BOUNCES + 2] = {}, evCamera = nullptr, evShadow = nullptr, evDone = nullptr;
+	hipEvent_t countReady[LH2_MAX_BOUNCES + 2] = {};   /* [L]: the event after which bounce L's hand-off is done (evShade or evCount, not owned) */
 	/* a launch carries only a stop event (a start event costs its dispatch ~5 us of idle GPU); a timed
 	   interval runs from the group's previous launch's stop event, so it includes the launch gap */
 	hipEvent_t fromTrace[LH2_MAX_BOUNCES + 1] = {}, fromShade[LH2_MAX_BOUNCES + 1] = {}, fromShadowB[LH2_MAX_BOUNCES + 1] = {}, fromShadow = nullptr;
