@@ -165,48 +165,242 @@ struct Builder
 	}
 };
 
+/* ---- spatial splits (SBVH; the algorithm of Stich, Friedrich and Dietrich, "Spatial Splits in
+   Bounding Volume Hierarchies", HPG 2009) -----------------------------------------------------
+   A node whose best object split leaves children that overlap (overlap area > alpha x root area) also
+   tries spatial splits: BINS equal slabs of the node box per axis, each reference clipped into every
+   slab it crosses (the triangle polygon cut by the slab planes, intersected with the reference's
+   box), entry / exit counts per slab.  A chosen spatial split sends the references that straddle the
+   plane to both children, each with its clipped box, so the children do not overlap and a ray visits
+   fewer of them.  A triangle then has references in several leaves: each copy is the same triangle
+   record, so every leaf that a ray tests it in yields the same hit (same t, same tie rule), and the
+   union of its references' boxes covers the whole triangle (the clipped boxes are widened by a few
+   ulps on the axes the cut moves, and both sides of a cut include the plane). */
+struct Ref { Aabb box; uint32_t prim; };
+
+struct SpatialBuilder
+{
+	const float* tv = nullptr;    /* 9 floats (v0, v1, v2) per primitive */
+	std::vector<TNode> nodes;
+	std::vector<uint32_t> perm;   /* leaf slots, allocated per leaf (may repeat a primitive) */
+	std::atomic<int> nodeCount{ 0 };
+	std::atomic<uint32_t> permCount{ 0 };
+	std::atomic<int64_t> refBudget{ 0 };   /* references that spatial splits may still add */
+	std::atomic<int> threadsLeft{ 0 };
+	int maxLeaf = 1;
+	float C_TRAV = 1.0f, alpha = 1e-5f, rootArea = 1.0f;
+
+	void make_leaf( int ni, const std::vector<Ref>& refs, const Aabb& box )
+	{
+		const uint32_t first = permCount.fetch_add( (uint32_t)refs.size() );
+		for (size_t i = 0; i < refs.size(); i++) perm[first + i] = refs[i].prim;
+		TNode& n = nodes[ni];
+		n.box = box, n.left = n.right = -1, n.first = first, n.count = (uint32_t)refs.size();
+	}
+	static float widen( const float x ) { return std::fabs( x ) * 4e-7f + 1e-30f; }
+	static bool valid( const Aabb& b ) { return b.lo[0] <= b.hi[0] && b.lo[1] <= b.hi[1] && b.lo[2] <= b.hi[2]; }
+	/* the parts of reference r on either side of the plane x[a] = p */
+	void split_ref( const Ref& r, const int a, const float p, Ref& L, Ref& R ) const
+	{
+		L.prim = R.prim = r.prim, L.box = empty_box(), R.box = empty_box();
+		const float* v = tv + (size_t)r.prim * 9;
+		auto add = []( Aabb& b, const float* x ) { for (int k = 0; k < 3; k++) b.lo[k] = std::min( b.lo[k], x[k] ), b.hi[k] = std::max( b.hi[k], x[k] ); };
+		for (int i = 0; i < 3; i++)
+		{
+			const float* v0 = v + i * 3;
+			const float* v1 = v + ((i + 1) % 3) * 3;
+			if (v0[a] <= p) add( L.box, v0 );
+			if (v0[a] >= p) add( R.box, v0 );
+			if ((v0[a] < p && v1[a] > p) || (v0[a] > p && v1[a] < p))
+			{
+				const float t = (p - v0[a]) / (v1[a] - v0[a]);
+				float x[3], lo[3], hi[3];
+				for (int k = 0; k < 3; k++) x[k] = v0[k] + t * (v1[k] - v0[k]);
+				for (int k = 0; k < 3; k++) lo[k] = x[k] - widen( x[k] ), hi[k] = x[k] + widen( x[k] );
+				lo[a] = hi[a] = p;
+				add( L.box, lo ), add( L.box, hi ), add( R.box, lo ), add( R.box, hi );
+			}
+		}
+		/* both sides include the plane; neither leaves the reference's box */
+		L.box.hi[a] = std::max( L.box.hi[a], p ), R.box.lo[a] = std::min( R.box.lo[a], p );
+		for (int k = 0; k < 3; k++)
+		{
+			L.box.lo[k] = std::max( L.box.lo[k], r.box.lo[k] ), L.box.hi[k] = std::min( L.box.hi[k], r.box.hi[k] );
+			R.box.lo[k] = std::max( R.box.lo[k], r.box.lo[k] ), R.box.hi[k] = std::min( R.box.hi[k], r.box.hi[k] );
+		}
+		L.box.hi[a] = std::min( L.box.hi[a], p ), R.box.lo[a] = std::max( R.box.lo[a], p );
+	}
+
+	void build( int ni, std::vector<Ref>& refs )
+	{
+		const uint32_t count = (uint32_t)refs.size();
+		Aabb box = empty_box(), cbox = empty_box();
+		for (const Ref& r : refs)
+		{
+			grow( box, r.box );
+			for (int k = 0; k < 3; k++)
+			{
+				const float c = 0.5f * r.box.lo[k] + 0.5f * r.box.hi[k];
+				cbox.lo[k] = std::min( cbox.lo[k], c ), cbox.hi[k] = std::max( cbox.hi[k], c );
+			}
+		}
+		if (count <= (uint32_t)std::min( 2, maxLeaf )) { make_leaf( ni, refs, box ); return; }
+		const float parentArea = std::max( area( box ), 1e-30f );
+		/* object split: binned SAH over the reference centroids */
+		float bestCost = std::numeric_limits<float>::max();
+		int bestAxis = -1, bestBin = -1;
+		Aabb bestL = empty_box(), bestR = empty_box();
+		for (int a = 0; a < 3; a++)
+		{
+			const float ext = cbox.hi[a] - cbox.lo[a];
+			if (!(ext > 0)) continue;
+			const float scale = (float)BINS * 0.99999f / ext;
+			Aabb bb[BINS]; uint32_t bc[BINS];
+			for (int b = 0; b < BINS; b++) bb[b] = empty_box(), bc[b] = 0;
+			for (const Ref& r : refs)
+			{
+				int b = (int)(((0.5f * r.box.lo[a] + 0.5f * r.box.hi[a]) - cbox.lo[a]) * scale);
+				b = std::min( std::max( b, 0 ), BINS - 1 );
+				bc[b]++, grow( bb[b], r.box );
+			}
+			Aabb rightBox[BINS]; uint32_t rightCount[BINS];
+			Aabb acc = empty_box(); uint32_t n = 0;
+			for (int b = BINS - 1; b > 0; b--) { grow( acc, bb[b] ); n += bc[b]; rightBox[b] = acc, rightCount[b] = n; }
+			acc = empty_box(); n = 0;
+			for (int b = 0; b < BINS - 1; b++)
+			{
+				grow( acc, bb[b] ); n += bc[b];
+				if (n == 0 || rightCount[b + 1] == 0) continue;
+				const float cost = C_TRAV + C_ISECT * (area( acc ) * n + area( rightBox[b + 1] ) * rightCount[b + 1]) / parentArea;
+				if (cost < bestCost) bestCost = cost, bestAxis = a, bestBin = b, bestL = acc, bestR = rightBox[b + 1];
+			}
+		}
+		/* spatial split, where the object split's children overlap */
+		int spAxis = -1;
+		float spPos = 0, spCost = std::numeric_limits<float>::max();
+		if (bestAxis >= 0 && refBudget.load( std::memory_order_relaxed ) > 0)
+		{
+			Aabb ov;
+			for (int k = 0; k < 3; k++) ov.lo[k] = std::max( bestL.lo[k], bestR.lo[k] ), ov.hi[k] = std::min( bestL.hi[k], bestR.hi[k] );
+			if (valid( ov ) && area( ov ) > alpha * rootArea)
+			{
+				for (int a = 0; a < 3; a++)
+				{
+					const float lo = box.lo[a], ext = box.hi[a] - lo;
+					if (!(ext > 0)) continue;
+					const float w = ext / (float)BINS;
+					Aabb bb[BINS]; uint32_t entry[BINS], exitc[BINS];
+					for (int b = 0; b < BINS; b++) bb[b] = empty_box(), entry[b] = exitc[b] = 0;
+					auto bin_of = [&]( float x ) { int b = (int)((x - lo) / w); return std::min( std::max( b, 0 ), BINS - 1 ); };
+					for (const Ref& r : refs)
+					{
+						const int b0 = bin_of( r.box.lo[a] ), b1 = std::max( b0, bin_of( r.box.hi[a] ) );
+						entry[b0]++, exitc[b1]++;
+						Ref cur = r;
+						for (int b = b0; b < b1; b++)
+						{
+							Ref L, R;
+							split_ref( cur, a, lo + w * (float)(b + 1), L, R );
+							if (valid( L.box )) grow( bb[b], L.box );
+							cur = R;
+							if (!valid( cur.box )) break;
+						}
+						if (valid( cur.box )) grow( bb[b1], cur.box );
+					}
+					Aabb rightBox[BINS]; uint32_t rightCount[BINS];
+					Aabb acc = empty_box(); uint32_t n = 0;
+					for (int b = BINS - 1; b > 0; b--) { grow( acc, bb[b] ); n += exitc[b]; rightBox[b] = acc, rightCount[b] = n; }
+					acc = empty_box(); n = 0;
+					for (int b = 0; b < BINS - 1; b++)
+					{
+						grow( acc, bb[b] ); n += entry[b];
+						if (n == 0 || rightCount[b + 1] == 0) continue;
+						const float cost = C_TRAV + C_ISECT * (area( acc ) * n + area( rightBox[b + 1] ) * rightCount[b + 1]) / parentArea;
+						if (cost < spCost) spCost = cost, spAxis = a, spPos = lo + w * (float)(b + 1);
+					}
+				}
+			}
+		}
+		const float splitCost = std::min( bestCost, spCost );
+		const float leafCost = C_ISECT * (float)count;
+		if (count <= (uint32_t)maxLeaf && (splitCost == std::numeric_limits<float>::max() || leafCost <= splitCost)) { make_leaf( ni, refs, box ); return; }
+		std::vector<Ref> left, right;
+		left.reserve( count ), right.reserve( count );
+		bool spatial = spAxis >= 0 && spCost < bestCost;
+		if (spatial)
+		{
+			/* the straddling references come out of the duplication budget (reserved before the split) */
+			int64_t straddle = 0;
+			for (const Ref& r : refs) straddle += r.box.lo[spAxis] < spPos && r.box.hi[spAxis] > spPos;
+			if (refBudget.fetch_sub( straddle ) < straddle) refBudget.fetch_add( straddle ), spatial = false;
+		}
+		if (spatial)
+		{
+			for (const Ref& r : refs)
+			{
+				if (r.box.hi[spAxis] <= spPos) left.push_back( r );
+				else if (r.box.lo[spAxis] >= spPos) right.push_back( r );
+				else
+				{
+					Ref L, R;
+					split_ref( r, spAxis, spPos, L, R );
+					const bool lv = valid( L.box ), rv = valid( R.box );
+					if (lv) left.push_back( L );
+					if (rv) right.push_back( R );
+					if (!lv && !rv) left.push_back( r );
+				}
+			}
+			/* a split that does not shrink both sides could recurse forever: take the object split */
+			if (left.size() >= count || right.size() >= count) left.clear(), right.clear(), spatial = false;
+		}
+		if (!spatial && bestAxis >= 0)
+		{
+			const float ext = cbox.hi[bestAxis] - cbox.lo[bestAxis];
+			const float scale = (float)BINS * 0.99999f / ext;
+			for (const Ref& r : refs)
+			{
+				int b = (int)(((0.5f * r.box.lo[bestAxis] + 0.5f * r.box.hi[bestAxis]) - cbox.lo[bestAxis]) * scale);
+				b = std::min( std::max( b, 0 ), BINS - 1 );
+				(b <= bestBin ? left : right).push_back( r );
+			}
+		}
+		if (left.empty() || right.empty())
+		{
+			/* every centroid identical (or degenerate): split the list in the middle */
+			left.assign( refs.begin(), refs.begin() + count / 2 );
+			right.assign( refs.begin() + count / 2, refs.end() );
+		}
+		const int c = nodeCount.fetch_add( 2 );
+		TNode& nd = nodes[ni];
+		nd.box = box, nd.left = c, nd.right = c + 1, nd.first = 0, nd.count = 0;
+		std::vector<Ref>().swap( refs );
+		if (count >= PAR_THRESHOLD && threadsLeft.fetch_sub( 1 ) > 0)
+		{
+			std::thread t( [this, c, &left]() { build( c, left ); } );
+			build( c + 1, right );
+			t.join();
+			threadsLeft.fetch_add( 1 );
+		}
+		else
+		{
+			if (count >= PAR_THRESHOLD) threadsLeft.fetch_add( 1 );
+			build( c, left );
+			build( c + 1, right );
+		}
+	}
+};
+
 inline int make_leaf_ref( uint32_t first, uint32_t count ) { return (int)~((first << 4) | (count - 1)); }
 
-}  // namespace
-
-void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost, int sweepMax )
+/* interior nodes in DFS pre-order into the child-pair layout (lh2_device.h); leaves reference their
+   ranges of out.perm */
+static void Flatten( const std::vector<TNode>& tn, const float C_TRAV, BvhOutput& out )
 {
-	const uint32_t N = (uint32_t)prims.size();
-	if (maxLeaf < 1) maxLeaf = 1;
-	if (maxLeaf > 16) maxLeaf = 16;
-	Builder b( prims );
-	b.maxLeaf = maxLeaf;
-	b.C_TRAV = traversalCost > 0 ? traversalCost : 1.0f;
-	b.sweepMax = (uint32_t)std::max( 0, sweepMax );
-	const float C_TRAV = b.C_TRAV;
-	b.cent.resize( (size_t)N * 3 );
-	b.idx.resize( N );
-	for (uint32_t i = 0; i < N; i++)
-	{
-		b.idx[i] = i;
-		for (int k = 0; k < 3; k++) b.cent[i * 3 + k] = 0.5f * prims[i].lo[k] + 0.5f * prims[i].hi[k];
-	}
-	b.nodes.resize( std::max<size_t>( 2 * (size_t)N + 1, 3 ) );
-	b.nodeCount = 1;
-	unsigned hw = std::thread::hardware_concurrency();
-	b.threadsLeft = (threads > 0 ? threads : (int)(hw ? hw : 4)) - 1;
-	out.nodes.clear(); out.perm.clear(); out.maxDepth = 0; out.leafCount = 0; out.sah = 0;
 	const float nanv = std::numeric_limits<float>::quiet_NaN();
-	if (N == 0)
-	{
-		/* root with two empty (NaN) children: never hit */
-		out.nodes.assign( 16, nanv );
-		int refs[4] = { make_leaf_ref( 0, 1 ), make_leaf_ref( 0, 1 ), 0, 0 };
-		memcpy( &out.nodes[12], refs, 16 );
-		return;
-	}
-	b.build( 0, 0, N );
-	out.perm = b.idx;
-	/* flatten interior nodes in DFS pre-order into the child-pair layout */
 	struct Item { int tnode; int gpu; int depth; };
 	std::vector<Item> stack;
 	auto emit = [&]() { out.nodes.resize( out.nodes.size() + 16 ); return (int)(out.nodes.size() / 16) - 1; };
-	const TNode& root = b.nodes[0];
+	const TNode& root = tn[0];
 	const float rootArea = std::max( area( root.box ), 1e-30f );
 	if (root.left < 0)
 	{
@@ -226,10 +420,10 @@ void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOut
 	{
 		const Item it = stack.back();
 		stack.pop_back();
-		const TNode& t = b.nodes[it.tnode];
+		const TNode& t = tn[it.tnode];
 		sah += C_TRAV * area( t.box ) / rootArea;
 		out.maxDepth = std::max( out.maxDepth, it.depth );
-		const TNode* ch[2] = { &b.nodes[t.left], &b.nodes[t.right] };
+		const TNode* ch[2] = { &tn[t.left], &tn[t.right] };
 		int refs[2];
 		for (int c = 0; c < 2; c++)
 		{
@@ -265,6 +459,75 @@ void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOut
 		if (ch[0]->left >= 0) stack.push_back( { t.left, gidx[0], it.depth + 1 } );
 	}
 	out.sah = sah;
+}
+
+static void BuildSbvh( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost,
+	const float* triVerts, float alpha, float budget )
+{
+	const uint32_t N = (uint32_t)prims.size();
+	SpatialBuilder b;
+	b.tv = triVerts, b.maxLeaf = maxLeaf, b.C_TRAV = traversalCost > 0 ? traversalCost : 1.0f, b.alpha = alpha;
+	const int64_t extra = (int64_t)((double)N * std::min( budget, 4.0f ));
+	b.refBudget = extra;
+	const size_t maxRefs = (size_t)N + (size_t)extra;   /* splits reserve their added references first */
+	b.perm.resize( maxRefs );
+	b.nodes.resize( 2 * maxRefs + 1 );
+	b.nodeCount = 1;
+	unsigned hw = std::thread::hardware_concurrency();
+	b.threadsLeft = (threads > 0 ? threads : (int)(hw ? hw : 4)) - 1;
+	std::vector<Ref> refs( N );
+	Aabb root = empty_box();
+	for (uint32_t i = 0; i < N; i++) refs[i].box = prims[i], refs[i].prim = i, grow( root, prims[i] );
+	b.rootArea = std::max( area( root ), 1e-30f );
+	b.build( 0, refs );
+	b.perm.resize( b.permCount.load() );
+	out.nodes.clear(); out.perm = std::move( b.perm ); out.maxDepth = 0; out.leafCount = 0; out.sah = 0;
+	b.nodes.resize( (size_t)b.nodeCount.load() );
+	Flatten( b.nodes, b.C_TRAV, out );
+}
+
+}  // namespace
+
+void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost, int sweepMax,
+	const float* triVerts, float spatialAlpha, float spatialBudget )
+{
+	const uint32_t N = (uint32_t)prims.size();
+	if (maxLeaf < 1) maxLeaf = 1;
+	if (maxLeaf > 16) maxLeaf = 16;
+	if (triVerts && spatialAlpha > 0 && spatialBudget > 0 && N >= 2)
+	{
+		BuildSbvh( prims, maxLeaf, threads, out, traversalCost, triVerts, spatialAlpha, spatialBudget );
+		return;
+	}
+	Builder b( prims );
+	b.maxLeaf = maxLeaf;
+	b.C_TRAV = traversalCost > 0 ? traversalCost : 1.0f;
+	b.sweepMax = (uint32_t)std::max( 0, sweepMax );
+	const float C_TRAV = b.C_TRAV;
+	b.cent.resize( (size_t)N * 3 );
+	b.idx.resize( N );
+	for (uint32_t i = 0; i < N; i++)
+	{
+		b.idx[i] = i;
+		for (int k = 0; k < 3; k++) b.cent[i * 3 + k] = 0.5f * prims[i].lo[k] + 0.5f * prims[i].hi[k];
+	}
+	b.nodes.resize( std::max<size_t>( 2 * (size_t)N + 1, 3 ) );
+	b.nodeCount = 1;
+	unsigned hw = std::thread::hardware_concurrency();
+	b.threadsLeft = (threads > 0 ? threads : (int)(hw ? hw : 4)) - 1;
+	out.nodes.clear(); out.perm.clear(); out.maxDepth = 0; out.leafCount = 0; out.sah = 0;
+	const float nanv = std::numeric_limits<float>::quiet_NaN();
+	if (N == 0)
+	{
+		/* root with two empty (NaN) children: never hit */
+		out.nodes.assign( 16, nanv );
+		int refs[4] = { make_leaf_ref( 0, 1 ), make_leaf_ref( 0, 1 ), 0, 0 };
+		memcpy( &out.nodes[12], refs, 16 );
+		return;
+	}
+	b.build( 0, 0, N );
+	out.perm = b.idx;
+	Flatten( b.nodes, C_TRAV, out );
 }
 
 /* ---- BVH2 -> BVH4 (greedy surface-area collapse) ------------------------------------------

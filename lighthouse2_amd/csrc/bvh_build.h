@@ -8,6 +8,7 @@
    (t, instance, triangle)), only the traversal cost does.
 */
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 #include <vector>
 
@@ -26,8 +27,12 @@ struct BvhOutput
 
 /* prims: per-primitive bounds; maxLeaf: largest leaf; threads: worker threads (0 = hw);
    traversalCost: SAH cost of a node visit relative to one triangle test; sweepMax: nodes of at most
-   this many primitives split by an exact SAH sweep over the sorted centroids (0: binned only) */
-void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost = 1.0f, int sweepMax = 0 );
+   this many primitives split by an exact SAH sweep over the sorted centroids (0: binned only);
+   triVerts (9 floats per primitive: the triangle's vertices), spatialAlpha > 0 and spatialBudget > 0:
+   spatial splits (SBVH) where the object split's children overlap by more than spatialAlpha x the
+   root's surface area, adding at most spatialBudget x N references (out.perm then repeats primitives) */
+void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost = 1.0f, int sweepMax = 0,
+	const float* triVerts = nullptr, float spatialAlpha = 0.0f, float spatialBudget = 0.0f );
 
 /* BVH2 (16 floats per node, root 0) -> BVH4 (32 floats per node, root 0; layout: lh2_device.h) by
    greedy surface-area collapse; returns the BVH4 depth (interior levels) */

@@ -247,6 +247,8 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
 	else if (!strcmp( name, "bvhSweep" )) bvhSweep = std::max( 0, (int)value );   /* exact SAH sweep for nodes of <= this many triangles */
+	else if (!strcmp( name, "bvhSpatial" )) bvhSpatial = std::max( 0.0f, value );   /* SBVH overlap threshold (x root area); 0: off */
+	else if (!strcmp( name, "bvhSpatialBudget" )) bvhSpatialBudget = std::min( 4.0f, std::max( 0.0f, value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
@@ -280,7 +282,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "epsilon", geometryEpsilon }, { "clampValue", clampValue }, { "maxPathLength", (float)maxPathLength },
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
-		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
+		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "traceFetchMB", traceFetchMB }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "blocksPerCU", (float)blocksPerCU },
@@ -407,6 +409,7 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 		gpuBvh.BuildBlas( m.shadeTris.ptr, triangleCount, bvhMaxLeaf, bvhTraversalCost, &nodes, &tris48, r, stream );
 		m.bvhNodes.adopt( nodes, (size_t)r.nodeCount * 4 );
 		m.bvhTris.adopt( tris48, (size_t)triangleCount * 3 );
+		m.leafTris = triangleCount;
 		m.nodeCount = r.nodeCount, m.maxDepth = r.maxDepth;
 		for (int k = 0; k < 3; k++) m.aabbLo[k] = r.lo[k], m.aabbHi[k] = r.hi[k];
 		/* pathological inputs (e.g. long runs of nearly coincident triangles) can make a clustered tree
@@ -429,9 +432,22 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 				m.aabbLo[k] = std::min( m.aabbLo[k], prims[i].lo[k] ), m.aabbHi[k] = std::max( m.aabbHi[k], prims[i].hi[k] );
 			}
 		}
+		/* spatial splits (bvhSpatial > 0) clip triangles: the builder gets their vertices */
+		std::vector<float> verts;
+		if (bvhSpatial > 0)
+		{
+			verts.resize( (size_t)triangleCount * 9 );
+			for (int i = 0; i < triangleCount; i++)
+			{
+				const lh2_CoreTri& t = tris[i];
+				const float v[9] = { t.vertex0.x, t.vertex0.y, t.vertex0.z, t.vertex1.x, t.vertex1.y, t.vertex1.z, t.vertex2.x, t.vertex2.y, t.vertex2.z };
+				memcpy( &verts[(size_t)i * 9], v, sizeof( v ) );
+			}
+		}
 		BvhOutput bvh;
-		BuildBvh2( prims, bvhMaxLeaf, 0, bvh, bvhTraversalCost, bvhSweep );
-		std::vector<float> tris48( (size_t)std::max( triangleCount, 1 ) * 12, 0.0f );
+		BuildBvh2( prims, bvhMaxLeaf, 0, bvh, bvhTraversalCost, bvhSweep, verts.empty() ? nullptr : verts.data(), bvhSpatial, bvhSpatialBudget );
+		/* one triangle record per leaf slot (a spatial split can reference a triangle from several leaves) */
+		std::vector<float> tris48( std::max<size_t>( bvh.perm.size(), 1 ) * 12, 0.0f );
 		for (size_t j = 0; j < bvh.perm.size(); j++)
 		{
 			const uint32_t ti = bvh.perm[j];
@@ -444,6 +460,7 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 		}
 		m.bvhNodes.upload( (const float4*)bvh.nodes.data(), bvh.nodes.size() / 4, stream );
 		m.bvhTris.upload( (const float4*)tris48.data(), tris48.size() / 4, stream );
+		m.leafTris = (int)bvh.perm.size();
 		m.nodeCount = (int)(bvh.nodes.size() / 16), m.maxDepth = bvh.maxDepth;
 		if (bvh4) BuildBlas4( m, bvh.nodes.data() );
 	}
@@ -498,14 +515,14 @@ void RenderCore::SetInstance( int instanceIdx, int meshIdx, const float* M )   /
 void RenderCore::ConcatenateBlas( int ni )
 {
 	meshNodeBase.assign( meshes.size(), 0 ), meshTriBase.assign( meshes.size(), 0 ), meshNode4Base.assign( meshes.size(), 0 );
-	int nodeTotal = 0, triTotal = 0, node4Total = 0;
+	int nodeTotal = 0, triTotal = 0, node4Total = 0, meshTris = 0;
 	maxBlasDepth = 0, maxBlas4Depth = 0;
 	std::vector<float> bounds( std::max<size_t>( meshes.size(), 1 ) * 6, 0.0f );
 	for (size_t mi = 0; mi < meshes.size(); mi++)
 	{
 		const CoreMeshHost& m = *meshes[mi];
 		meshNodeBase[mi] = nodeTotal, meshTriBase[mi] = triTotal, meshNode4Base[mi] = node4Total;
-		nodeTotal += m.nodeCount, triTotal += m.triCount, node4Total += m.node4Count;
+		nodeTotal += m.nodeCount, triTotal += m.leafTris, node4Total += m.node4Count, meshTris += m.triCount;
 		maxBlasDepth = std::max( maxBlasDepth, m.maxDepth ), maxBlas4Depth = std::max( maxBlas4Depth, m.depth4 );
 		for (int k = 0; k < 3; k++) bounds[mi * 6 + k] = m.aabbLo[k], bounds[mi * 6 + 3 + k] = m.aabbHi[k];
 		if (m.triCount == 0) bounds[mi * 6] = 1.0f, bounds[mi * 6 + 3] = 0.0f;   /* empty-mesh marker */
@@ -521,11 +538,11 @@ void RenderCore::ConcatenateBlas( int ni )
 		const CoreMeshHost& m = *meshes[mi];
 		GpuBvhBuilder::Relocate( m.bvhNodes.ptr, m.nodeCount, meshNodeBase[mi], (uint32_t)meshTriBase[mi], dNodes.ptr, stream );
 		if (bvh4) GpuBvhBuilder::Relocate4( m.bvh4Nodes.ptr, m.node4Count, meshNode4Base[mi], (uint32_t)meshTriBase[mi], dNodes4.ptr, stream );
-		if (m.triCount) CHK_HIP( hipMemcpyAsync( dTris.ptr + (size_t)meshTriBase[mi] * 3, m.bvhTris.ptr, sizeof( float4 ) * 3 * (size_t)m.triCount, hipMemcpyDeviceToDevice, stream ) );
+		if (m.leafTris) CHK_HIP( hipMemcpyAsync( dTris.ptr + (size_t)meshTriBase[mi] * 3, m.bvhTris.ptr, sizeof( float4 ) * 3 * (size_t)m.leafTris, hipMemcpyDeviceToDevice, stream ) );
 	}
 	dMeshBounds.upload( bounds.data(), bounds.size(), stream );
 	CHK_HIP( hipStreamSynchronize( stream ) );
-	blasNodeCount = nodeTotal, blasTriCount = triTotal, blasNode4Count = node4Total;
+	blasNodeCount = nodeTotal, blasTriCount = triTotal, blasNode4Count = node4Total, blasMeshTris = meshTris;
 	geometryDirty = false;
 }
 
@@ -1210,7 +1227,7 @@ void RenderCore::SceneInfo( int* nodeCount, int* triCount, int* maxDepth, int* i
 {
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	if (nodeCount) *nodeCount = blasNodeCount;
-	if (triCount) *triCount = blasTriCount;
+	if (triCount) *triCount = blasMeshTris;
 	if (tlasOnDevice)
 	{
 		int d = 0;

@@ -44,6 +44,7 @@ template <class T> struct DevBuf
 struct CoreMeshHost   /* RenderCore always copies what it needs (rendercore.h:57): all of it on the device */
 {
 	int triCount = 0;
+	int leafTris = 0;                    /* triangle records of the BLAS leaves (> triCount with spatial splits) */
 	float aabbLo[3], aabbHi[3];          /* lo.x > hi.x: empty mesh */
 	DevBuf<float4> shadeTris;            /* CoreTri4[] in original order, for shading */
 	DevBuf<float4> bvhNodes, bvhTris;    /* BLAS with mesh-local refs; relocated into the scene arrays by UpdateToplevel */
@@ -171,7 +172,7 @@ private:
 	DevBuf<float4> dNodes4;              /* BVH4: all BLAS (relocated), then the TLAS as two-child nodes */
 	DevBuf<uint8_t> dInst;                 /* DevInstance[] */
 	DevBuf<lh2_CoreInstanceDesc> dInstDesc;
-	int tlasRoot = 0, blasNodeCount = 0, blasTriCount = 0, sceneMaxDepth = 0;
+	int tlasRoot = 0, blasNodeCount = 0, blasTriCount = 0, blasMeshTris = 0, sceneMaxDepth = 0;   /* blasTriCount: leaf triangle records; blasMeshTris: triangles */
 	std::vector<int> meshNodeBase, meshTriBase, meshNode4Base;
 	int tlasCapacity = 0, maxBlasDepth = 0;
 	int blasNode4Count = 0, maxBlas4Depth = 0;
@@ -244,6 +245,8 @@ private:
 	int refillPrimary = 48, refillOther = 48, leafBatch = 0, leafBatchPrimary = 8;
 	int bvhMaxLeaf = 1;
 	int bvhSweep = 0;                    /* exact SAH sweep below this node size (setting "bvhSweep") */
+	float bvhSpatial = 1e-5f;            /* spatial splits (SBVH): overlap threshold x root area; 0 = off */
+	float bvhSpatialBudget = 1.0f;       /* ... adding at most this many references per triangle */
 	int traceVersion = 0;                /* 0: auto (TraceVersion) */
 	float traceFetchMB = 256.0f;         /* auto: traceVersion 5 above this BVH4 + triangle footprint */
 	int TraceVersion() const;

@@ -317,6 +317,31 @@ def test_traversal_variants_bitexact(fresh_core, version, leaf_batch, max_leaf):
     assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
 
 
+@pytest.mark.parametrize("version,max_leaf,alpha", [(6, 1, 1e-5), (6, 4, 1e-5), (7, 1, 1e-5), (4, 2, 1e-5), (1, 2, 1e-5),
+                                                     (6, 1, 1e-7), (6, 1, 0.0)])
+def test_spatial_splits_bitexact(fresh_core, version, max_leaf, alpha):
+    """Spatial splits (bvhSpatial, the default: SBVH references, a triangle in several leaves with
+    clipped boxes; 0 = object splits only) change the tree only: closest hits, occlusion and a
+    packet-traced frame equal the oracle's."""
+    fresh_core.setting("bvhSpatial", alpha)
+    fresh_core.setting("bvhSpatialBudget", 1.0)
+    fresh_core.setting("bvhMaxLeaf", max_leaf)
+    fresh_core.setting("traceVersion", version)
+    sc = scene.config2_scene(n=20000, width=64, height=36)
+    o = _load_both(fresh_core, sc, 64, 36)
+    assert fresh_core.get_setting("bvhSpatial") == np.float32(alpha)
+    O4, D4 = _random_rays(30001, 21, radius=8.0)
+    hg, ho = fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4)
+    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.3
+    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+    D4[:, 3] = np.random.default_rng(22).uniform(0.5, 20.0, len(D4)).astype(np.float32)
+    assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
+    sc.render_frame(fresh_core)
+    sc.render_frame(o)
+    assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
+    assert rel_l2(fresh_core.accumulator()[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
+
+
 @pytest.mark.parametrize("version", [4, 5, 6, 7])
 def test_bvh4_deep_stack(fresh_core, version):
     """A deep BLAS (triangles shrinking geometrically along a line: a chain-like SAH tree) next to the

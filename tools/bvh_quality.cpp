@@ -1,0 +1,167 @@
+/* bvh_quality.cpp - host-side traversal cost of the core's BVH4 (tools only): builds the BLAS the way
+   RenderCore::SetGeometry does (bvh_build.cpp: binned SAH, optionally spatial splits, greedy BVH4
+   collapse), then traces sample rays with a nearest-first BVH4 walk and reports node steps and
+   triangle tests per ray - the work the GPU traversal loop does per ray.
+     rays "camera": a pinhole camera grid; "surface": from random points on random triangles, cosine
+     distributed about the normal (a stand-in for the bounce rays).
+   Build: g++ -O2 -std=c++17 -pthread tools/bvh_quality.cpp lighthouse2_amd/csrc/bvh_build.cpp -o /tmp/bvh_quality
+   Run:   /tmp/bvh_quality tris.bin [alpha budget maxLeaf]   (tris.bin: float32 v0 v1 v2 per triangle)
+          camera: pos (0, 0, -12), looking +z, vertical FOV 40, 16:9 (config 2), or --camera px py pz tx ty tz */
+#include "../lighthouse2_amd/csrc/bvh_build.h"
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+using namespace lh2;
+
+namespace {
+
+struct V3 { float x, y, z; };
+V3 sub( V3 a, V3 b ) { return { a.x - b.x, a.y - b.y, a.z - b.z }; }
+V3 cross( V3 a, V3 b ) { return { a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x }; }
+float dot( V3 a, V3 b ) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+V3 norm( V3 a ) { const float l = std::sqrt( dot( a, a ) ); return { a.x / l, a.y / l, a.z / l }; }
+
+struct Stats { double nodes = 0, tris = 0, hits = 0; int rays = 0; };
+
+struct Scene
+{
+	std::vector<float> tv;          /* 9 per triangle */
+	std::vector<float> n4;          /* BVH4 nodes */
+	std::vector<uint32_t> perm;
+
+	bool intersect( uint32_t t, V3 o, V3 d, float& tb ) const
+	{
+		const float* v = &tv[(size_t)t * 9];
+		const V3 v0 = { v[0], v[1], v[2] }, e1 = sub( { v[3], v[4], v[5] }, v0 ), e2 = sub( { v[6], v[7], v[8] }, v0 );
+		const V3 p = cross( d, e2 );
+		const float det = dot( e1, p );
+		if (std::fabs( det ) < 1e-12f) return false;
+		const float inv = 1.0f / det;
+		const V3 s = sub( o, v0 );
+		const float u = dot( s, p ) * inv;
+		if (u < 0 || u > 1) return false;
+		const V3 q = cross( s, e1 );
+		const float w = dot( d, q ) * inv;
+		if (w < 0 || u + w > 1) return false;
+		const float tt = dot( e2, q ) * inv;
+		if (tt > 1e-4f && tt < tb) { tb = tt; return true; }
+		return false;
+	}
+	void trace( V3 o, V3 d, Stats& st ) const
+	{
+		const V3 id = { 1.0f / d.x, 1.0f / d.y, 1.0f / d.z };
+		float tb = 1e30f;
+		int stack[256], sp = 0, node = 0;
+		bool hit = false;
+		while (true)
+		{
+			if (node >= 0)
+			{
+				st.nodes++;
+				const float* q = &n4[(size_t)node * 32];
+				const int* refs = (const int*)(q + 24);
+				float tn[4]; int order[4], nh = 0;
+				for (int c = 0; c < 4; c++)
+				{
+					const float* b = q + (c >> 1) * 12;
+					const int j = c & 1;
+					const float lx = b[j * 4 + 0], hx = b[j * 4 + 1], ly = b[j * 4 + 2], hy = b[j * 4 + 3], lz = b[8 + j * 2], hz = b[9 + j * 2];
+					if (!(lx == lx)) continue;
+					const float ax = (lx - o.x) * id.x, bx = (hx - o.x) * id.x, ay = (ly - o.y) * id.y, by = (hy - o.y) * id.y;
+					const float az = (lz - o.z) * id.z, bz = (hz - o.z) * id.z;
+					const float n = std::fmax( std::fmax( std::fmin( ax, bx ), std::fmin( ay, by ) ), std::fmax( std::fmin( az, bz ), 0.0f ) );
+					const float f = std::fmin( std::fmin( std::fmax( ax, bx ), std::fmax( ay, by ) ), std::fmax( az, bz ) );
+					if (n <= f * 1.00001f && n <= tb) { tn[nh] = n, order[nh] = refs[c]; nh++; }
+				}
+				for (int i = 1; i < nh; i++)
+					for (int k = i; k > 0 && tn[k] < tn[k - 1]; k--) std::swap( tn[k], tn[k - 1] ), std::swap( order[k], order[k - 1] );
+				for (int i = nh - 1; i >= 1; i--) stack[sp++] = order[i];
+				if (nh) { node = order[0]; continue; }
+			}
+			else
+			{
+				const uint32_t first = (uint32_t)(~node) >> 4;
+				const int cnt = (int)((uint32_t)(~node) & 15u) + 1;
+				for (int k = 0; k < cnt; k++) { st.tris++; hit |= intersect( perm[first + k], o, d, tb ); }
+			}
+			if (sp == 0) break;
+			node = stack[--sp];
+		}
+		st.hits += hit;
+		st.rays++;
+	}
+};
+
+}  // namespace
+
+int main( int argc, char** argv )
+{
+	if (argc < 2) { std::fprintf( stderr, "usage: bvh_quality tris.bin [alpha budget maxLeaf]\n" ); return 1; }
+	const float alpha = argc > 2 ? (float)atof( argv[2] ) : 0.0f, budget = argc > 3 ? (float)atof( argv[3] ) : 0.3f;
+	const int maxLeaf = argc > 4 ? atoi( argv[4] ) : 1;
+	Scene sc;
+	FILE* f = std::fopen( argv[1], "rb" );
+	if (!f) return 1;
+	std::fseek( f, 0, SEEK_END );
+	const long bytes = std::ftell( f );
+	std::fseek( f, 0, SEEK_SET );
+	sc.tv.resize( bytes / 4 );
+	if (std::fread( sc.tv.data(), 4, sc.tv.size(), f ) != sc.tv.size()) return 1;
+	std::fclose( f );
+	const size_t N = sc.tv.size() / 9;
+	std::vector<Aabb> prims( N );
+	for (size_t i = 0; i < N; i++)
+		for (int k = 0; k < 3; k++)
+		{
+			const float* v = &sc.tv[i * 9];
+			prims[i].lo[k] = std::fmin( std::fmin( v[k], v[3 + k] ), v[6 + k] );
+			prims[i].hi[k] = std::fmax( std::fmax( v[k], v[3 + k] ), v[6 + k] );
+		}
+	const auto t0 = std::chrono::steady_clock::now();
+	BvhOutput out;
+	BuildBvh2( prims, maxLeaf, 0, out, 1.0f, 0, alpha > 0 ? sc.tv.data() : nullptr, alpha, budget );
+	const double buildS = std::chrono::duration<double>( std::chrono::steady_clock::now() - t0 ).count();
+	const int depth4 = CollapseBvh4( out.nodes.data(), out.nodes.size() / 16, sc.n4 );
+	sc.perm = out.perm;
+	/* rays */
+	std::mt19937 rng( 1234 );
+	std::uniform_real_distribution<float> U( 0.0f, 1.0f );
+	Stats cam, surf;
+	const V3 cp = { 0, 0, -12 };
+	const float th = std::tan( 40.0f * 3.14159265f / 360.0f ), aspect = 16.0f / 9.0f;
+	for (int y = 0; y < 144; y++)
+		for (int x = 0; x < 256; x++)
+		{
+			const float sx = ((x + 0.5f) / 256.0f * 2 - 1) * th * aspect, sy = ((y + 0.5f) / 144.0f * 2 - 1) * th;
+			sc.trace( cp, norm( { sx, sy, 1.0f } ), cam );
+		}
+	for (int i = 0; i < 40000; i++)
+	{
+		const uint32_t t = (uint32_t)(U( rng ) * N) % N;
+		const float* v = &sc.tv[(size_t)t * 9];
+		float a = U( rng ), b = U( rng );
+		if (a + b > 1) a = 1 - a, b = 1 - b;
+		const V3 v0 = { v[0], v[1], v[2] }, e1 = sub( { v[3], v[4], v[5] }, v0 ), e2 = sub( { v[6], v[7], v[8] }, v0 );
+		V3 n = norm( cross( e1, e2 ) );
+		if (U( rng ) < 0.5f) n = { -n.x, -n.y, -n.z };
+		const V3 o = { v0.x + a * e1.x + b * e2.x + n.x * 1e-4f, v0.y + a * e1.y + b * e2.y + n.y * 1e-4f, v0.z + a * e1.z + b * e2.z + n.z * 1e-4f };
+		const V3 tt = std::fabs( n.x ) > 0.9f ? V3{ 0, 1, 0 } : V3{ 1, 0, 0 };
+		const V3 T = norm( cross( n, tt ) ), B = cross( n, T );
+		const float r1 = U( rng ), r2 = U( rng ), r = std::sqrt( r1 ), ph = 6.2831853f * r2, cz = std::sqrt( 1 - r1 );
+		const V3 d = norm( { T.x * r * std::cos( ph ) + B.x * r * std::sin( ph ) + n.x * cz, T.y * r * std::cos( ph ) + B.y * r * std::sin( ph ) + n.y * cz,
+			T.z * r * std::cos( ph ) + B.z * r * std::sin( ph ) + n.z * cz } );
+		sc.trace( o, d, surf );
+	}
+	std::printf( "{\"tris\": %zu, \"alpha\": %g, \"budget\": %g, \"maxLeaf\": %d, \"refs\": %zu, \"nodes2\": %zu, \"nodes4\": %zu, \"depth2\": %d, "
+		"\"depth4\": %d, \"sah\": %.3f, \"build_s\": %.2f, \"camera\": {\"nodes\": %.2f, \"tris\": %.2f, \"hit\": %.3f}, "
+		"\"surface\": {\"nodes\": %.2f, \"tris\": %.2f, \"hit\": %.3f}}\n",
+		N, alpha, budget, maxLeaf, out.perm.size(), out.nodes.size() / 16, sc.n4.size() / 32, out.maxDepth, depth4, out.sah, buildS,
+		cam.nodes / cam.rays, cam.tris / cam.rays, cam.hits / cam.rays, surf.nodes / surf.rays, surf.tris / surf.rays, surf.hits / surf.rays );
+	return 0;
+}
