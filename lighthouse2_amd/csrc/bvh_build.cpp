@@ -5,6 +5,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <thread>
 
@@ -397,6 +398,29 @@ inline int make_leaf_ref( uint32_t first, uint32_t count ) { return (int)~((firs
 static void Flatten( const std::vector<TNode>& tn, const float C_TRAV, BvhOutput& out )
 {
 	const float nanv = std::numeric_limits<float>::quiet_NaN();
+	/* the leaves' primitives in DFS order (left before right), so that every subtree's leaves occupy
+	   one contiguous range of out.perm (the BVH4 collapse may merge a small subtree into one leaf) */
+	std::vector<uint32_t> dfsPerm;
+	dfsPerm.reserve( out.perm.size() );
+	std::vector<uint32_t> leafFirst( tn.size(), 0 );
+	{
+		std::vector<int> st{ 0 };
+		while (!st.empty())
+		{
+			const int k = st.back();
+			st.pop_back();
+			const TNode& t = tn[k];
+			if (t.left < 0)
+			{
+				leafFirst[k] = (uint32_t)dfsPerm.size();
+				for (uint32_t i = 0; i < t.count; i++) dfsPerm.push_back( out.perm[t.first + i] );
+				continue;
+			}
+			st.push_back( t.right ), st.push_back( t.left );
+		}
+	}
+	out.perm.swap( dfsPerm );
+	auto make_leaf_ref = [&]( uint32_t, uint32_t count, int k ) { return (int)~((leafFirst[k] << 4) | (count - 1)); };
 	struct Item { int tnode; int gpu; int depth; };
 	std::vector<Item> stack;
 	auto emit = [&]() { out.nodes.resize( out.nodes.size() + 16 ); return (int)(out.nodes.size() / 16) - 1; };
@@ -409,7 +433,7 @@ static void Flatten( const std::vector<TNode>& tn, const float C_TRAV, BvhOutput
 		n[0] = root.box.lo[0], n[1] = root.box.hi[0], n[2] = root.box.lo[1], n[3] = root.box.hi[1];
 		n[4] = nanv, n[5] = nanv, n[6] = nanv, n[7] = nanv;
 		n[8] = root.box.lo[2], n[9] = root.box.hi[2], n[10] = nanv, n[11] = nanv;
-		int refs[4] = { make_leaf_ref( root.first, root.count ), make_leaf_ref( 0, 1 ), 0, 0 };
+		int refs[4] = { make_leaf_ref( root.first, root.count, 0 ), (int)~0u, 0, 0 };
 		memcpy( n + 12, refs, 16 );
 		out.maxDepth = 1, out.leafCount = 1, out.sah = C_TRAV + C_ISECT * root.count;
 		return;
@@ -429,7 +453,7 @@ static void Flatten( const std::vector<TNode>& tn, const float C_TRAV, BvhOutput
 		{
 			if (ch[c]->left < 0)
 			{
-				refs[c] = make_leaf_ref( ch[c]->first, ch[c]->count );
+				refs[c] = make_leaf_ref( ch[c]->first, ch[c]->count, c ? t.right : t.left );
 				out.leafCount++;
 				sah += C_ISECT * ch[c]->count * area( ch[c]->box ) / rootArea;
 			}
@@ -598,6 +622,169 @@ int CollapseBvh4( const float* nodes2, size_t nodeCount2, std::vector<float>& no
 		for (int i = 0; i < 4; i++)
 		{
 			/* slots i = 0, 1 in q0..q2, slots 2, 3 in q3..q5: (lo.x, hi.x, lo.y, hi.y) per slot, z pairs */
+			float* b = q + (i >> 1) * 12;
+			const int j = i & 1;
+			const bool used = i < n;
+			b[j * 4 + 0] = used ? list[i].lo[0] : nanv, b[j * 4 + 1] = used ? list[i].hi[0] : nanv;
+			b[j * 4 + 2] = used ? list[i].lo[1] : nanv, b[j * 4 + 3] = used ? list[i].hi[1] : nanv;
+			b[8 + j * 2] = used ? list[i].lo[2] : nanv, b[9 + j * 2] = used ? list[i].hi[2] : nanv;
+		}
+		memcpy( q + 24, refs, 16 );
+	}
+	return depth;
+}
+
+
+/* ---- BVH2 -> BVH4 by dynamic programming over the BVH2 (surface-area cost) ----------------------
+   The collapse of Ylitie, Karras and Laine ("Efficient Incoherent Ray Traversal on GPUs Through
+   Compressed Wide BVHs", HPG 2017, section 4) for four-wide nodes: for every BVH2 subtree and every
+   slot count j <= 4, the cheapest way to hand it to a BVH4 parent as at most j entries - one BVH4
+   node, one leaf (a subtree of at most maxLeafTris triangles, its leaves contiguous in the DFS perm
+   order that Flatten emits), or its two children's entries side by side - under the expected cost
+   area x (cNode per node step, cLeaf + cTri x triangles per leaf visit).  Costs are in units of a
+   node step of the traversal loop. */
+int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>& nodes4, float cLeaf, float cTri, int maxLeafTris )
+{
+	const float nanv = std::numeric_limits<float>::quiet_NaN();
+	nodes4.assign( 32, 0.0f );
+	if (nodeCount2 == 0) { for (int i = 0; i < 24; i++) nodes4[i] = nanv; return 1; }
+	maxLeafTris = std::min( 16, std::max( 1, maxLeafTris ) );
+	const float INF = std::numeric_limits<float>::infinity();
+	struct Ent { float lo[3], hi[3]; int ref; };                 /* a BVH2 child: box + reference */
+	auto child = [&]( size_t k, int c, Ent& e ) {
+		const float* n = nodes2 + k * 16;
+		e.lo[0] = n[c * 4 + 0], e.hi[0] = n[c * 4 + 1], e.lo[1] = n[c * 4 + 2], e.hi[1] = n[c * 4 + 3];
+		e.lo[2] = n[8 + c * 2], e.hi[2] = n[9 + c * 2];
+		int r[2];
+		memcpy( r, n + 12, 8 );
+		e.ref = r[c];
+		return e.lo[0] == e.lo[0];   /* NaN box: no child */
+	};
+	auto harea = []( const Ent& e ) {
+		const float dx = std::max( 0.0f, e.hi[0] - e.lo[0] ), dy = std::max( 0.0f, e.hi[1] - e.lo[1] ), dz = std::max( 0.0f, e.hi[2] - e.lo[2] );
+		return dx * dy + dy * dz + dz * dx;
+	};
+	/* per BVH2 node: its children, triangle count, first perm slot, and d[j] (j = 1..4) with choices */
+	const size_t N2 = nodeCount2;
+	std::vector<Ent> ch( N2 * 2 );
+	std::vector<uint8_t> nch( N2 );
+	std::vector<uint32_t> tris( N2 ), first( N2 );
+	std::vector<float> d( N2 * 5, INF ), asNode( N2, INF );
+	std::vector<int8_t> choice( N2 * 5, 0 );     /* d[j]: 0 = one entry (node or leaf), -1 = as d[j-1], i > 0: i entries to child 0 */
+	std::vector<int8_t> nodeSplit( N2, 0 );      /* asNode: entries to child 0 (0: single child takes all) */
+	std::vector<uint8_t> nodeCnt( N2, 0 );
+	auto ent_tris = [&]( const Ent& e ) { return e.ref < 0 ? (uint32_t)(((uint32_t)(~e.ref) & 15u) + 1) : tris[e.ref]; };
+	auto ent_first = [&]( const Ent& e ) { return e.ref < 0 ? (uint32_t)(~e.ref) >> 4 : first[e.ref]; };
+	auto dist = [&]( const Ent& e, int j ) {
+		if (e.ref < 0) return harea( e ) * (cLeaf + cTri * (float)ent_tris( e ));
+		return d[(size_t)e.ref * 5 + j];
+	};
+	for (size_t kk = N2; kk-- > 0;)
+	{
+		int m = 0;
+		for (int c = 0; c < 2; c++) { Ent e; if (child( kk, c, e )) ch[kk * 2 + m++] = e; }
+		nch[kk] = (uint8_t)m;
+		uint32_t t = 0, f = std::numeric_limits<uint32_t>::max();
+		for (int c = 0; c < m; c++) t += ent_tris( ch[kk * 2 + c] ), f = std::min( f, ent_first( ch[kk * 2 + c] ) );
+		tris[kk] = t, first[kk] = m ? f : 0;
+	}
+	/* the root's box: the union of its children */
+	Ent rootE;
+	for (int k = 0; k < 3; k++) rootE.lo[k] = INF, rootE.hi[k] = -INF;
+	for (int c = 0; c < nch[0]; c++) for (int k = 0; k < 3; k++) rootE.lo[k] = std::min( rootE.lo[k], ch[c].lo[k] ), rootE.hi[k] = std::max( rootE.hi[k], ch[c].hi[k] );
+	rootE.ref = 0;
+	std::vector<float> area2( N2, 0.0f );
+	area2[0] = harea( rootE );
+	for (size_t kk = 0; kk < N2; kk++) for (int c = 0; c < nch[kk]; c++) if (ch[kk * 2 + c].ref >= 0) area2[ch[kk * 2 + c].ref] = harea( ch[kk * 2 + c] );
+	/* split(k, m): the cheapest m entries made of k's children */
+	auto split = [&]( size_t k, int m, int& at ) {
+		float best = INF;
+		at = 0;
+		if (nch[k] == 1) { best = dist( ch[k * 2], m ); at = 0; return best; }
+		if (nch[k] == 0) return 0.0f;
+		for (int i = 1; i < m; i++)
+		{
+			const float c = dist( ch[k * 2], i ) + dist( ch[k * 2 + 1], m - i );
+			if (c < best) best = c, at = i;
+		}
+		return best;
+	};
+	for (size_t kk = N2; kk-- > 0;)
+	{
+		const float A = area2[kk];
+		/* as a BVH4 node: the best 2..4 entries of its children */
+		float bestN = INF;
+		for (int m = 2; m <= 4; m++)
+		{
+			int at;
+			const float c = split( kk, m, at );
+			if (c < bestN) bestN = c, nodeSplit[kk] = (int8_t)at, nodeCnt[kk] = (uint8_t)m;
+		}
+		if (nch[kk] < 2) { int at; bestN = split( kk, 4, at ); nodeSplit[kk] = 0, nodeCnt[kk] = 4; }
+		asNode[kk] = A * 1.0f + bestN;
+		const float asLeaf = tris[kk] <= (uint32_t)maxLeafTris && tris[kk] > 0 ? A * (cLeaf + cTri * (float)tris[kk]) : INF;
+		d[kk * 5 + 1] = std::min( asNode[kk], asLeaf ), choice[kk * 5 + 1] = 0;
+		for (int j = 2; j <= 4; j++)
+		{
+			int at;
+			const float c = split( kk, j, at );
+			if (c < d[kk * 5 + j - 1]) d[kk * 5 + j] = c, choice[kk * 5 + j] = (int8_t)(nch[kk] == 1 ? 100 : at);
+			else d[kk * 5 + j] = d[kk * 5 + j - 1], choice[kk * 5 + j] = -1;
+		}
+	}
+	auto is_leaf_choice = [&]( size_t k ) {
+		const float asLeaf = tris[k] <= (uint32_t)maxLeafTris && tris[k] > 0 ? area2[k] * (cLeaf + cTri * (float)tris[k]) : INF;
+		return asLeaf < asNode[k];
+	};
+	/* expand(e, j): the entries that d chose for e with j slots */
+	std::function<void( const Ent&, int, std::vector<Ent>& )> expand = [&]( const Ent& e, int j, std::vector<Ent>& out ) {
+		if (e.ref < 0) { out.push_back( e ); return; }
+		const size_t k = (size_t)e.ref;
+		while (j > 1 && choice[k * 5 + j] == -1) j--;
+		if (j == 1 || choice[k * 5 + j] == 0)
+		{
+			Ent x = e;
+			if (is_leaf_choice( k )) x.ref = (int)~((first[k] << 4) | (tris[k] - 1));
+			out.push_back( x );
+			return;
+		}
+		if (choice[k * 5 + j] == 100) { expand( ch[k * 2], j, out ); return; }
+		const int i = choice[k * 5 + j];
+		expand( ch[k * 2], i, out );
+		expand( ch[k * 2 + 1], j - i, out );
+	};
+	struct Item { size_t node2; int node4, depth; };
+	std::vector<Item> queue{ { 0, 0, 1 } };
+	int depth = 1;
+	for (size_t qi = 0; qi < queue.size(); qi++)
+	{
+		const Item it = queue[qi];
+		depth = std::max( depth, it.depth );
+		std::vector<Ent> list;
+		const size_t k = it.node2;
+		if (nch[k] == 1) expand( ch[k * 2], nodeCnt[k], list );
+		else if (nch[k] == 2)
+		{
+			const int i = nodeSplit[k];
+			expand( ch[k * 2], i, list );
+			expand( ch[k * 2 + 1], nodeCnt[k] - i, list );
+		}
+		int refs[4] = { 0, 0, 0, 0 };
+		const int n = (int)list.size();
+		for (int i = 0; i < n; i++)
+		{
+			if (list[i].ref >= 0)
+			{
+				const int child4 = (int)(nodes4.size() / 32);
+				nodes4.resize( nodes4.size() + 32, 0.0f );
+				queue.push_back( { (size_t)list[i].ref, child4, it.depth + 1 } );
+				refs[i] = child4;
+			}
+			else refs[i] = list[i].ref;
+		}
+		float* q = &nodes4[(size_t)it.node4 * 32];
+		for (int i = 0; i < 4; i++)
+		{
 			float* b = q + (i >> 1) * 12;
 			const int j = i & 1;
 			const bool used = i < n;

@@ -38,4 +38,8 @@ void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOut
    greedy surface-area collapse; returns the BVH4 depth (interior levels) */
 int CollapseBvh4( const float* nodes2, size_t nodeCount2, std::vector<float>& nodes4 );
 
+/* the same by dynamic programming over surface-area costs (node step 1, leaf visit cLeaf + cTri per
+   triangle); subtrees of at most maxLeafTris triangles may become one leaf (BVH2 leaves in DFS order) */
+int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>& nodes4, float cLeaf, float cTri, int maxLeafTris );
+
 }  // namespace lh2

@@ -1314,11 +1314,12 @@ LH2_DEV const float4* HitInstance( const SceneDev& s, const int primIdx, const i
 
 /* ---- shade kernel: pathtracer.h:54-245 --------------------------------------------------- */
 LH2_DEV void shade_epilogue( const ShadeParams& p );   /* the bounce hand-off, below */
-/* 3 waves per SIMD (<= 168 VGPRs, 4 spilled): the kernel is load-latency bound (a dependent chain of
-   hit -> instance -> triangle -> material loads per path), 0.285 -> 0.244 ms per frame on config 2
-   over the unbounded 171-VGPR build (2 waves); 4 waves spill ~100 VGPRs */
+/* 4 waves per SIMD (<= 128 VGPRs): the kernel is load-latency bound (a dependent chain of hit ->
+   instance -> triangle -> material loads per path).  Round 1: 3 waves over the unbounded 171-VGPR
+   build, 0.285 -> 0.244 ms on config 2; round 2 (no SLP, 145 VGPRs unbounded): 4 waves at 128 VGPRs
+   + 36 B of spills, config-3 shade 0.565 -> 0.548 ms per frame (profiles/r02s_ab_collapse_shade4.txt) */
 #ifndef LH2_SHADE_MINWAVES
-#define LH2_SHADE_MINWAVES 3
+#define LH2_SHADE_MINWAVES 4
 #endif
 #ifndef LH2_SHADE_NL_MINWAVES
 #define LH2_SHADE_NL_MINWAVES 4   /* 128 VGPRs, 9 spilled; 3 waves: 144, none (A/B: profiles/r01g_ab_shade_nolights.jsonl) */

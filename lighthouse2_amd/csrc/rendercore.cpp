@@ -249,6 +249,10 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "bvhSweep" )) bvhSweep = std::max( 0, (int)value );   /* exact SAH sweep for nodes of <= this many triangles */
 	else if (!strcmp( name, "bvhSpatial" )) bvhSpatial = std::max( 0.0f, value );   /* SBVH overlap threshold (x root area); 0: off */
 	else if (!strcmp( name, "bvhSpatialBudget" )) bvhSpatialBudget = std::min( 4.0f, std::max( 0.0f, value ) );
+	else if (!strcmp( name, "bvh4Collapse" )) bvh4Collapse = value != 0;
+	else if (!strcmp( name, "bvh4LeafTris" )) bvh4LeafTris = std::min( 16, std::max( 1, (int)value ) );
+	else if (!strcmp( name, "bvh4LeafCost" )) bvh4LeafCost = std::max( 0.0f, value );
+	else if (!strcmp( name, "bvh4TriCost" )) bvh4TriCost = std::max( 0.0f, value );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
@@ -282,7 +286,8 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "epsilon", geometryEpsilon }, { "clampValue", clampValue }, { "maxPathLength", (float)maxPathLength },
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
-		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
+		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
+		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "traceFetchMB", traceFetchMB }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "blocksPerCU", (float)blocksPerCU },
@@ -496,7 +501,9 @@ void RenderCore::SetTail( TraceArgs& ta, PathGroup& g )
 void RenderCore::BuildBlas4( CoreMeshHost& m, const float* nodes2 )
 {
 	std::vector<float> n4;
-	m.depth4 = CollapseBvh4( nodes2, (size_t)m.nodeCount, n4 );
+	/* bvh4Collapse 1: dynamic-programming collapse (surface-area costs, optional leaf merging); 0: greedy */
+	m.depth4 = bvh4Collapse ? CollapseBvh4Sah( nodes2, (size_t)m.nodeCount, n4, bvh4LeafCost, bvh4TriCost, bvh4LeafTris )
+		: CollapseBvh4( nodes2, (size_t)m.nodeCount, n4 );
 	m.bvh4Nodes.upload( (const float4*)n4.data(), n4.size() / 4, stream );
 	m.node4Count = (int)(n4.size() / 32);
 }

@@ -247,6 +247,9 @@ private:
 	int bvhSweep = 0;                    /* exact SAH sweep below this node size (setting "bvhSweep") */
 	float bvhSpatial = 1e-5f;            /* spatial splits (SBVH): overlap threshold x root area; 0 = off */
 	float bvhSpatialBudget = 1.0f;       /* ... adding at most this many references per triangle */
+	int bvh4Collapse = 1;                /* BVH4 collapse: 0 greedy (CollapseBvh4), 1 dynamic programming (CollapseBvh4Sah) */
+	int bvh4LeafTris = 1;                /* ... merging subtrees of at most this many triangles into one leaf */
+	float bvh4LeafCost = 0.4f, bvh4TriCost = 0.5f;   /* ... its costs of a leaf visit and a triangle test (node step = 1) */
 	int traceVersion = 0;                /* 0: auto (TraceVersion) */
 	float traceFetchMB = 256.0f;         /* auto: traceVersion 5 above this BVH4 + triangle footprint */
 	int TraceVersion() const;

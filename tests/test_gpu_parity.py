@@ -342,6 +342,29 @@ def test_spatial_splits_bitexact(fresh_core, version, max_leaf, alpha):
     assert rel_l2(fresh_core.accumulator()[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
 
 
+@pytest.mark.parametrize("version,leaf_tris", [(6, 1), (6, 2), (6, 4), (7, 4), (4, 3), (5, 2)])
+def test_bvh4_dp_collapse_bitexact(fresh_core, version, leaf_tris):
+    """The dynamic-programming BVH4 collapse (bvh4Collapse 1), merging small subtrees into leaves of up
+    to leaf_tris triangles, over an SBVH tree with instances: hits, occlusion and a frame equal the
+    oracle's."""
+    fresh_core.setting("bvh4Collapse", 1)
+    fresh_core.setting("bvh4LeafTris", leaf_tris)
+    fresh_core.setting("traceVersion", version)
+    sc = scene.instanced_scene(meshes=3, tris_per_mesh=6000, width=64, height=36, grid=2, spacing=10.0)
+    scene.animate_instances(sc, 1)
+    o = _load_both(fresh_core, sc, 64, 36)
+    O4, D4 = _random_rays(30001, 31, radius=30.0)
+    hg, ho = fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4)
+    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.05
+    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+    D4[:, 3] = np.random.default_rng(32).uniform(1.0, 40.0, len(D4)).astype(np.float32)
+    assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
+    sc.render_frame(fresh_core)
+    sc.render_frame(o)
+    assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
+    assert rel_l2(fresh_core.accumulator()[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
+
+
 @pytest.mark.parametrize("version", [4, 5, 6, 7])
 def test_bvh4_deep_stack(fresh_core, version):
     """A deep BLAS (triangles shrinking geometrically along a line: a chain-like SAH tree) next to the

@@ -27,7 +27,7 @@ V3 cross( V3 a, V3 b ) { return { a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, 
 float dot( V3 a, V3 b ) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 V3 norm( V3 a ) { const float l = std::sqrt( dot( a, a ) ); return { a.x / l, a.y / l, a.z / l }; }
 
-struct Stats { double nodes = 0, tris = 0, hits = 0; int rays = 0; };
+struct Stats { double nodes = 0, tris = 0, leaves = 0, hits = 0; int rays = 0; };
 
 struct Scene
 {
@@ -88,6 +88,7 @@ struct Scene
 			{
 				const uint32_t first = (uint32_t)(~node) >> 4;
 				const int cnt = (int)((uint32_t)(~node) & 15u) + 1;
+				st.leaves++;
 				for (int k = 0; k < cnt; k++) { st.tris++; hit |= intersect( perm[first + k], o, d, tb ); }
 			}
 			if (sp == 0) break;
@@ -127,7 +128,10 @@ int main( int argc, char** argv )
 	BvhOutput out;
 	BuildBvh2( prims, maxLeaf, 0, out, 1.0f, 0, alpha > 0 ? sc.tv.data() : nullptr, alpha, budget );
 	const double buildS = std::chrono::duration<double>( std::chrono::steady_clock::now() - t0 ).count();
-	const int depth4 = CollapseBvh4( out.nodes.data(), out.nodes.size() / 16, sc.n4 );
+	const float cLeaf = argc > 5 ? (float)atof( argv[5] ) : -1.0f, cTri = argc > 6 ? (float)atof( argv[6] ) : 0.5f;
+	const int mlt = argc > 7 ? atoi( argv[7] ) : 1;
+	const int depth4 = cLeaf < 0 ? CollapseBvh4( out.nodes.data(), out.nodes.size() / 16, sc.n4 )
+		: CollapseBvh4Sah( out.nodes.data(), out.nodes.size() / 16, sc.n4, cLeaf, cTri, mlt );
 	sc.perm = out.perm;
 	/* rays */
 	std::mt19937 rng( 1234 );
@@ -159,9 +163,10 @@ int main( int argc, char** argv )
 		sc.trace( o, d, surf );
 	}
 	std::printf( "{\"tris\": %zu, \"alpha\": %g, \"budget\": %g, \"maxLeaf\": %d, \"refs\": %zu, \"nodes2\": %zu, \"nodes4\": %zu, \"depth2\": %d, "
-		"\"depth4\": %d, \"sah\": %.3f, \"build_s\": %.2f, \"camera\": {\"nodes\": %.2f, \"tris\": %.2f, \"hit\": %.3f}, "
-		"\"surface\": {\"nodes\": %.2f, \"tris\": %.2f, \"hit\": %.3f}}\n",
+		"\"depth4\": %d, \"sah\": %.3f, \"build_s\": %.2f, \"camera\": {\"nodes\": %.2f, \"leaves\": %.2f, \"tris\": %.2f, \"hit\": %.3f}, "
+		"\"surface\": {\"nodes\": %.2f, \"leaves\": %.2f, \"tris\": %.2f, \"hit\": %.3f}, \"valu_model\": %.0f}\n",
 		N, alpha, budget, maxLeaf, out.perm.size(), out.nodes.size() / 16, sc.n4.size() / 32, out.maxDepth, depth4, out.sah, buildS,
-		cam.nodes / cam.rays, cam.tris / cam.rays, cam.hits / cam.rays, surf.nodes / surf.rays, surf.tris / surf.rays, surf.hits / surf.rays );
+		cam.nodes / cam.rays, cam.leaves / cam.rays, cam.tris / cam.rays, cam.hits / cam.rays, surf.nodes / surf.rays, surf.leaves / surf.rays, surf.tris / surf.rays, surf.hits / surf.rays,
+		(175.0 * surf.nodes + 66.0 * surf.leaves + 86.0 * surf.tris) / surf.rays );
 	return 0;
 }
