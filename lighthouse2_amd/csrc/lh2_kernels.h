@@ -54,7 +54,9 @@ struct SceneDev       /* everything the traversal and shading kernels read, by v
 struct BounceAdvance  /* the hand-off to the next bounce (advance_bounce, lh2_kernels.hip) */
 {
 	const uint32_t* segNext;         /* the extension rays' segment counts: the next bounce's paths */
+	const uint32_t* segNextBack;     /* ... and those at the segments' ends (two-ended segments) */
 	uint32_t* segRetire;             /* this bounce's path counts, zeroed for the next shade launch's extensions */
+	uint32_t* segRetireBack;
 	uint32_t* rayCountLog;           /* [pathLength] = rays of the next bounce */
 	uint32_t* hostActiveLog;         /* pinned host copy of the same (the host's early exit), or null */
 	uint32_t* shadowSnap; uint32_t* shadowCursor;   /* the shadow split's snapshot, or null */
@@ -63,7 +65,12 @@ struct BounceAdvance  /* the hand-off to the next bounce (advance_bounce, lh2_ke
 struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path state */
 {
 	const uint32_t* segCounts; uint32_t segStride;     /* input paths: a segmented stream (see LH2_SEGS) */
-	uint32_t* segOut;                                  /* extension rays: segment counts (Counters::segPath) */
+	const uint32_t* segBack;                           /* ... with records at the segments' ends (null: none) */
+	uint32_t* segOut; uint32_t* segOutBack;            /* extension rays: segment counts (Counters::segPath / segBack) */
+	/* extension rays whose chord through the scene box (chordLo, chordHi) is at most chordCut go to the
+	   end of their segment (segOutBack): the next trace launch takes them last, so the rays left in
+	   flight when its work queues run dry are short ones (longest-first scheduling); 0: all at the start */
+	float chordLo[3], chordHi[3], chordCut;
 	int advance; BounceAdvance adv;                    /* nonzero: the launch's last block hands off to the next bounce */
 	uint32_t shadowStride;                             /* shadow-ray segments: capacity of each */
 	const float4* rayO; const float4* rayD; const float4* T4; const float4* Q4; const uint4* hits;
@@ -87,6 +94,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	/* the rays: a segmented stream (see LH2_SEGS), counts from device memory (segCounts), or, with
 	   segCounts null, countFixed rays stored densely (segments of segStride) */
 	const uint32_t* segCounts; uint32_t segStride; uint32_t countFixed;
+	const uint32_t* segBack;                          /* two-ended segments: rays at the segments' ends (null: none) */
 	uint32_t* cursor;                                 /* LH2_SEGS zeroed work-queue heads, LH2_CURSOR_STRIDE apart */
 	uint4* hits;                                      /* closest: {t, triid, instid, uv16} */
 	uint32_t* mask;                                   /* any, mode 0: occlusion bits */

@@ -51,16 +51,21 @@ static_assert( sizeof( ((Counters*)0)->segShadow ) == LH2_SEGS * LH2_SEGCOUNT_ST
 /* [lo, hi): segment c of a trace launch's ray stream (lh2_kernels.h, LH2_SEGS).  Wave-uniform, and
    said so (readfirstlane): kept in SGPRs, they cost the traversal loop no VGPRs (which it has none
    to spare: with two more live VGPRs the compiler spilled the stack pointers next to the LDS push) */
-LH2_DEV void seg_range( const TraceArgs& a, uint32_t c, uint32_t& lo, uint32_t& hi )
+LH2_DEV void seg_range( const TraceArgs& a, uint32_t c, uint32_t& lo, uint32_t& hi, uint32_t& split, uint32_t& gap )
 {
 	c = __builtin_amdgcn_readfirstlane( c );
-	uint32_t n;
+	uint32_t n, nb = 0;
 	lo = c * a.segStride;
-	if (a.segCounts) n = a.segCounts[c * LH2_SEGCOUNT_STRIDE];
+	if (a.segCounts) n = a.segCounts[c * LH2_SEGCOUNT_STRIDE], nb = a.segBack ? a.segBack[c * LH2_SEGCOUNT_STRIDE] : 0u;
 	else n = a.countFixed > lo ? min( a.countFixed - lo, a.segStride ) : 0u;
 	lo = __builtin_amdgcn_readfirstlane( lo );
-	hi = __builtin_amdgcn_readfirstlane( lo + n );
+	hi = __builtin_amdgcn_readfirstlane( lo + n + nb );
+	/* two-ended segment: queue positions [lo, split) are records lo.., the rest sit at the segment's end */
+	split = __builtin_amdgcn_readfirstlane( lo + n );
+	gap = __builtin_amdgcn_readfirstlane( nb ? a.segStride - n - nb : 0u );
 }
+/* the record of queue position j of a two-ended segment */
+LH2_DEV uint32_t seg_index( const uint32_t j, const uint32_t split, const uint32_t gap ) { return j < split ? j : j + gap; }
 
 /* no rays in any segment: the launch returns at once (a bounce after the last one, or no shadow rays) */
 LH2_DEV bool stream_empty( const TraceArgs& a )
@@ -68,7 +73,7 @@ LH2_DEV bool stream_empty( const TraceArgs& a )
 	if (!a.segCounts) return a.countFixed == 0;
 	uint32_t any = 0;
 #pragma unroll
-	for (int k = 0; k < LH2_SEGS; k++) any |= a.segCounts[k * LH2_SEGCOUNT_STRIDE];
+	for (int k = 0; k < LH2_SEGS; k++) any |= a.segCounts[k * LH2_SEGCOUNT_STRIDE] | (a.segBack ? a.segBack[k * LH2_SEGCOUNT_STRIDE] : 0u);
 	return any == 0;
 }
 
@@ -143,6 +148,7 @@ LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_
 		const uint32_t lo = (uint32_t)i * segStride;
 		c->segPath[0][i * LH2_SEGCOUNT_STRIDE] = pathCount > lo ? min( pathCount - lo, segStride ) : 0u;
 		c->segPath[1][i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadow[i * LH2_SEGCOUNT_STRIDE] = 0;
+		c->segBack[0][i * LH2_SEGCOUNT_STRIDE] = 0, c->segBack[1][i * LH2_SEGCOUNT_STRIDE] = 0;
 	}
 	if (i != 0) return;
 	c->activePaths = pathCount, c->extensionRays = 0, c->shadowRays = 0;
@@ -423,8 +429,8 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 	bool active = false, exhausted = false;
 	/* this wave's segment of the ray stream: blocks go round-robin over the 8 XCDs, so blockIdx % 8
 	   gives each XCD its own segment and cursor; a dry segment moves the wave on to the next one */
-	uint32_t chunk = blockIdx.x % LH2_CHUNKS, tried = 0, lo, hi;
-	seg_range( a, chunk, lo, hi );
+	uint32_t chunk = blockIdx.x % LH2_CHUNKS, tried = 0, lo, hi, split, gap;
+	seg_range( a, chunk, lo, hi, split, gap );
 	TraceState q;
 	q.idx = 0, q.tmin = 0, q.sp = 0, q.blasSp = -1, q.cur = 0, q.curInst = -1, q.leaf = 0;
 	while (true)
@@ -437,9 +443,10 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 			{
 				/* uniform address (readfirstlane): the compiler then merges the idle lanes' adds into
 				   one atomic per wave, handing out consecutive indices in lane order */
-				q.idx = lo + atomicAdd( a.cursor + __builtin_amdgcn_readfirstlane( chunk ) * LH2_CURSOR_STRIDE, 1u );
-				if (q.idx < hi)
+				const uint32_t j = lo + atomicAdd( a.cursor + __builtin_amdgcn_readfirstlane( chunk ) * LH2_CURSOR_STRIDE, 1u );
+				if (j < hi)
 				{
+					q.idx = seg_index( j, split, gap );
 					const float4 o4 = a.rayO[q.idx], d4 = a.rayD[q.idx];
 					setup_ray( q.r, mk3( o4.x, o4.y, o4.z ), mk3( d4.x, d4.y, d4.z ) );
 					q.tmin = o4.w;
@@ -453,7 +460,7 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 			{
 				if (++tried == LH2_CHUNKS) exhausted = true;
 				chunk = (chunk + 1) % LH2_CHUNKS;
-				seg_range( a, chunk, lo, hi );
+				seg_range( a, chunk, lo, hi, split, gap );
 			}
 		}
 		if (__ballot( active ) == 0)
@@ -1312,6 +1319,27 @@ LH2_DEV const float4* HitInstance( const SceneDev& s, const int primIdx, const i
 	return (const float4*)id->triangles + (size_t)primIdx * 11;
 }
 
+/* a shade launch's input segment: its records (front + back), the front records, and the gap between
+   the two ends (two-ended segments, ShadeParams::chordCut) */
+LH2_DEV void shade_segment( const ShadeParams& p, const uint32_t seg, uint32_t& count, uint32_t& front, uint32_t& gap )
+{
+	front = p.segCounts[seg * LH2_SEGCOUNT_STRIDE];
+	const uint32_t back = p.segBack ? p.segBack[seg * LH2_SEGCOUNT_STRIDE] : 0u;
+	count = front + back;
+	gap = back ? p.segStride - count : 0u;
+}
+/* the record of position i of such a segment (relative to its start) */
+LH2_DEV uint32_t seg_pos( const uint32_t i, const uint32_t front, const uint32_t gap ) { return i < front ? i : i + gap; }
+/* the distance along the ray from its origin to where it leaves the scene box (a lower bound of what
+   it can traverse; ordering only, so a fast reciprocal is fine) */
+LH2_DEV float scene_chord( const ShadeParams& p, const float4 o, const float4 d )
+{
+	const float ix = __builtin_amdgcn_rcpf( d.x ), iy = __builtin_amdgcn_rcpf( d.y ), iz = __builtin_amdgcn_rcpf( d.z );
+	const float tx = fmaxf( (p.chordLo[0] - o.x) * ix, (p.chordHi[0] - o.x) * ix );
+	const float ty = fmaxf( (p.chordLo[1] - o.y) * iy, (p.chordHi[1] - o.y) * iy );
+	const float tz = fmaxf( (p.chordLo[2] - o.z) * iz, (p.chordHi[2] - o.z) * iz );
+	return fminf( fminf( tx, ty ), tz );
+}
 /* ---- shade kernel: pathtracer.h:54-245 --------------------------------------------------- */
 LH2_DEV void shade_epilogue( const ShadeParams& p );   /* the bounce hand-off, below */
 /* 4 waves per SIMD (<= 128 VGPRs): the kernel is load-latency bound (a dependent chain of hit ->
@@ -1332,12 +1360,14 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 {
 	/* the block's segment of the path stream (its XCD's), and the segment's share of the grid */
 	const uint32_t seg = blockIdx.x % LH2_SEGS;
-	const uint32_t count = p.segCounts[seg * LH2_SEGCOUNT_STRIDE], segBase = seg * p.segStride;
+	uint32_t count, front, gap;
+	shade_segment( p, seg, count, front, gap );
+	const uint32_t segBase = seg * p.segStride;
 	const uint32_t gstride = ((gridDim.x - seg + LH2_SEGS - 1) / LH2_SEGS) * 256u;
 	const int w = p.w, h = p.h;
 	for (uint32_t base = (blockIdx.x / LH2_SEGS) * 256u; base < count; base += gstride)
 	{
-		const uint32_t jobIndex = segBase + base + threadIdx.x;
+		const uint32_t jobIndex = segBase + seg_pos( base + threadIdx.x, front, gap );
 		bool doExt = false, doShadow = false;
 		float4 eO, eD, eT, eQ, sO, sD, sP;
 		if (base + threadIdx.x < count)
@@ -1489,8 +1519,15 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 		/* wave-level compaction of extension and shadow rays into this block's segment of the output
 		   streams (one atomicAdd per wave each, on the segment's own counter) */
 		{
-			const uint32_t es = wave_alloc( doExt, &p.segOut[seg * LH2_SEGCOUNT_STRIDE] );
-			if (doExt) { const uint32_t o = segBase + es; p.rayOut[o] = eO; p.rayDOut[o] = eD; p.T4Out[o] = eT; p.Q4Out[o] = eQ; }
+			/* two-ended segment: a ray with a short chord through the scene goes to the end (traced last) */
+			const bool late = doExt && p.chordCut > 0 && scene_chord( p, eO, eD ) <= p.chordCut;
+			const uint32_t es = wave_alloc( doExt && !late, &p.segOut[seg * LH2_SEGCOUNT_STRIDE] );
+			const uint32_t eb = wave_alloc( late, &p.segOutBack[seg * LH2_SEGCOUNT_STRIDE] );
+			if (doExt)
+			{
+				const uint32_t o = segBase + (late ? p.segStride - 1u - eb : es);
+				p.rayOut[o] = eO; p.rayDOut[o] = eD; p.T4Out[o] = eT; p.Q4Out[o] = eQ;
+			}
 			const uint32_t ss = wave_alloc( doShadow, &p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE] );
 			if (doShadow)
 			{
@@ -1509,12 +1546,14 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 __global__ __launch_bounds__( 256 ) void k_shade_last( const SceneDev s, const ShadeParams p )
 {
 	const uint32_t seg = blockIdx.x % LH2_SEGS;
-	const uint32_t count = p.segCounts[seg * LH2_SEGCOUNT_STRIDE], segBase = seg * p.segStride;
+	uint32_t count, front, gap;
+	shade_segment( p, seg, count, front, gap );
+	const uint32_t segBase = seg * p.segStride;
 	const uint32_t gstride = ((gridDim.x - seg + LH2_SEGS - 1) / LH2_SEGS) * 256u;
 	const uint32_t wh = (uint32_t)(p.w * p.h);
 	for (uint32_t i = (blockIdx.x / LH2_SEGS) * 256u + threadIdx.x; i < count; i += gstride)
 	{
-		const uint32_t jobIndex = segBase + i;
+		const uint32_t jobIndex = segBase + seg_pos( i, front, gap );
 		if ((int)p.hits[jobIndex].y != NOHIT) continue;
 		const float4 T4 = p.T4[jobIndex], D4 = p.rayD[jobIndex], Q4 = p.Q4[jobIndex];
 		const uint32_t pixelIdx = (fbits( T4.w ) >> 8) % wh;
@@ -1606,12 +1645,14 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const 
 {
 	/* the block's segment of the path stream (its XCD's), and the segment's share of the grid */
 	const uint32_t seg = blockIdx.x % LH2_SEGS;
-	const uint32_t count = p.segCounts[seg * LH2_SEGCOUNT_STRIDE], segBase = seg * p.segStride;
+	uint32_t count, front, gap;
+	shade_segment( p, seg, count, front, gap );
+	const uint32_t segBase = seg * p.segStride;
 	const uint32_t gstride = ((gridDim.x - seg + LH2_SEGS - 1) / LH2_SEGS) * 256u;
 	const int w = p.w, h = p.h;
 	for (uint32_t base = (blockIdx.x / LH2_SEGS) * 256u; base < count; base += gstride)
 	{
-		const uint32_t jobIndex = segBase + base + threadIdx.x;
+		const uint32_t jobIndex = segBase + seg_pos( base + threadIdx.x, front, gap );
 		bool doExt = false, doShadow = false;
 		float4 eO, eD, eT, eQ, sO, sD, sP;
 		if (base + threadIdx.x < count)
@@ -1693,8 +1734,15 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const 
 		}
 	compact:
 		{
-			const uint32_t es = wave_alloc( doExt, &p.segOut[seg * LH2_SEGCOUNT_STRIDE] );
-			if (doExt) { const uint32_t o = segBase + es; p.rayOut[o] = eO; p.rayDOut[o] = eD; p.T4Out[o] = eT; p.Q4Out[o] = eQ; }
+			/* two-ended segment: a ray with a short chord through the scene goes to the end (traced last) */
+			const bool late = doExt && p.chordCut > 0 && scene_chord( p, eO, eD ) <= p.chordCut;
+			const uint32_t es = wave_alloc( doExt && !late, &p.segOut[seg * LH2_SEGCOUNT_STRIDE] );
+			const uint32_t eb = wave_alloc( late, &p.segOutBack[seg * LH2_SEGCOUNT_STRIDE] );
+			if (doExt)
+			{
+				const uint32_t o = segBase + (late ? p.segStride - 1u - eb : es);
+				p.rayOut[o] = eO; p.rayDOut[o] = eD; p.T4Out[o] = eT; p.Q4Out[o] = eQ;
+			}
 			const uint32_t ss = wave_alloc( doShadow, &p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE] );
 			if (doShadow)
 			{
@@ -1727,7 +1775,8 @@ LH2_DEV void advance_bounce( Counters* c, const BounceAdvance& a, const int path
 	for (int k = 0; k < LH2_SEGS; k++)
 	{
 		ext += __hip_atomic_load( &a.segNext[k * LH2_SEGCOUNT_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-		a.segRetire[k * LH2_SEGCOUNT_STRIDE] = 0;
+		ext += __hip_atomic_load( &a.segNextBack[k * LH2_SEGCOUNT_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+		a.segRetire[k * LH2_SEGCOUNT_STRIDE] = 0, a.segRetireBack[k * LH2_SEGCOUNT_STRIDE] = 0;
 		sh += c->segShadow[k * LH2_SEGCOUNT_STRIDE];
 		if (resetShadow) c->segShadow[k * LH2_SEGCOUNT_STRIDE] = 0;
 	}

@@ -250,6 +250,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "bvhSpatial" )) bvhSpatial = std::max( 0.0f, value );   /* SBVH overlap threshold (x root area); 0: off */
 	else if (!strcmp( name, "bvhSpatialBudget" )) bvhSpatialBudget = std::min( 4.0f, std::max( 0.0f, value ) );
 	else if (!strcmp( name, "bvh4Collapse" )) bvh4Collapse = value != 0;
+	else if (!strcmp( name, "chordSplit" )) chordSplit = std::max( 0.0f, value );   /* two-ended path segments (longest first); 0: off */
 	else if (!strcmp( name, "bvh4LeafTris" )) bvh4LeafTris = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvh4LeafCost" )) bvh4LeafCost = std::max( 0.0f, value );
 	else if (!strcmp( name, "bvh4TriCost" )) bvh4TriCost = std::max( 0.0f, value );
@@ -287,7 +288,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
+		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "traceFetchMB", traceFetchMB }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "blocksPerCU", (float)blocksPerCU },
@@ -595,6 +596,24 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		memcpy( Ts + (size_t)i * 16, in.T, 64 );
 		meshIds[i] = in.mesh;
 	}
+	/* the scene's world box (instance transforms of the mesh boxes): the shade launches order extension
+	   rays by their chord through it (ShadeParams::chordCut) */
+	for (int k = 0; k < 3; k++) sceneLo[k] = 1e30f, sceneHi[k] = -1e30f;
+	for (int i = 0; i < ni; i++)
+	{
+		const CoreInstanceHost& in = instances[i];
+		const CoreMeshHost& m = *meshes[in.mesh];
+		if (m.triCount == 0) continue;
+		for (int c = 0; c < 8; c++)
+		{
+			const float x = c & 1 ? m.aabbHi[0] : m.aabbLo[0], y = c & 2 ? m.aabbHi[1] : m.aabbLo[1], z = c & 4 ? m.aabbHi[2] : m.aabbLo[2];
+			for (int k = 0; k < 3; k++)
+			{
+				const float w = in.T[k * 4 + 0] * x + in.T[k * 4 + 1] * y + in.T[k * 4 + 2] * z + in.T[k * 4 + 3];
+				sceneLo[k] = std::min( sceneLo[k], w ), sceneHi[k] = std::max( sceneHi[k], w );
+			}
+		}
+	}
 	dInst.resize( nRec * sizeof( DevInstance ) ), dInstDesc.resize( nRec ), dInstT.resize( nRec * 16 ), dInstMesh.resize( nRec );
 	dSceneError.resize( 1 ), dTlasDepth.resize( 1 );
 	CHK_HIP( hipMemcpyAsync( dInst.ptr, di, nRec * sizeof( DevInstance ), hipMemcpyHostToDevice, stream ) );
@@ -807,7 +826,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			/* the path counts ping-pong (Counters::segPath): this bounce's paths, and its extension rays */
 			uint32_t* segIn = c->segPath[(pathLength - 1) & 1];
 			uint32_t* segNext = c->segPath[pathLength & 1];
+			uint32_t* segInBack = c->segBack[(pathLength - 1) & 1];
+			uint32_t* segNextBack = c->segBack[pathLength & 1];
 			ta.rayO = g.rayO[g.in].ptr, ta.rayD = g.rayD[g.in].ptr, ta.segCounts = segIn, ta.segStride = g.segStride;
+			ta.segBack = segInBack;
 			ta.cursor = g.cursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
 			ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
 			ta.packet = pathLength == 1 && tiledRays && UsePackets() ? PacketMode() : 0;
@@ -818,10 +840,18 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
 			ShadeParams sp{};
 			sp.segCounts = segIn, sp.segOut = segNext, sp.segStride = g.segStride, sp.shadowStride = g.shadowStride;
+			sp.segBack = segInBack, sp.segOutBack = segNextBack;
+			/* two-ended path segments: rays with a chord through the scene box below chordSplit x its
+			   largest extent go last (setting "chordSplit"; 0: off) */
+			{
+				const float ext = std::max( std::max( sceneHi[0] - sceneLo[0], sceneHi[1] - sceneLo[1] ), sceneHi[2] - sceneLo[2] );
+				for (int k = 0; k < 3; k++) sp.chordLo[k] = sceneLo[k], sp.chordHi[k] = sceneHi[k];
+				sp.chordCut = ext > 0 ? chordSplit * ext : 0.0f;
+			}
 			/* the hand-off to the next bounce: the shade launch's last block (no launch of its own), except
 			   in PrimeRef mode, where the bounce's shadow rays are traced (and their counts reset) first */
 			const bool split = pathLength == splitL;
-			const BounceAdvance adv{ segNext, segIn, g.rayLog.ptr, g.activeLog, split ? shadowSnap.ptr : nullptr,
+			const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, g.rayLog.ptr, g.activeLog, split ? shadowSnap.ptr : nullptr,
 				split ? g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr };
 			sp.advance = pathLength < maxPL && !primeRef;
 			sp.adv = adv;

@@ -250,6 +250,8 @@ private:
 	int bvh4Collapse = 1;                /* BVH4 collapse: 0 greedy (CollapseBvh4), 1 dynamic programming (CollapseBvh4Sah) */
 	int bvh4LeafTris = 1;                /* ... merging subtrees of at most this many triangles into one leaf */
 	float bvh4LeafCost = 0.4f, bvh4TriCost = 0.5f;   /* ... its costs of a leaf visit and a triangle test (node step = 1) */
+	float chordSplit = 0.35f;            /* extension rays with a chord through the scene box below this x its extent are traced last */
+	float sceneLo[3] = { 0, 0, 0 }, sceneHi[3] = { 0, 0, 0 };   /* world box of the instanced meshes (UpdateToplevel) */
 	int traceVersion = 0;                /* 0: auto (TraceVersion) */
 	float traceFetchMB = 256.0f;         /* auto: traceVersion 5 above this BVH4 + triangle footprint */
 	int TraceVersion() const;

@@ -9,6 +9,7 @@
           camera: pos (0, 0, -12), looking +z, vertical FOV 40, 16:9 (config 2), or --camera px py pz tx ty tz */
 #include "../lighthouse2_amd/csrc/bvh_build.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -27,7 +28,7 @@ V3 cross( V3 a, V3 b ) { return { a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, 
 float dot( V3 a, V3 b ) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 V3 norm( V3 a ) { const float l = std::sqrt( dot( a, a ) ); return { a.x / l, a.y / l, a.z / l }; }
 
-struct Stats { double nodes = 0, tris = 0, leaves = 0, hits = 0; int rays = 0; };
+struct Stats { double nodes = 0, tris = 0, leaves = 0, hits = 0; int rays = 0; std::vector<int> per; std::vector<float> chord; };
 
 struct Scene
 {
@@ -57,13 +58,13 @@ struct Scene
 	{
 		const V3 id = { 1.0f / d.x, 1.0f / d.y, 1.0f / d.z };
 		float tb = 1e30f;
-		int stack[256], sp = 0, node = 0;
+		int stack[256], sp = 0, node = 0, steps = 0;
 		bool hit = false;
 		while (true)
 		{
 			if (node >= 0)
 			{
-				st.nodes++;
+				st.nodes++, steps++;
 				const float* q = &n4[(size_t)node * 32];
 				const int* refs = (const int*)(q + 24);
 				float tn[4]; int order[4], nh = 0;
@@ -88,7 +89,7 @@ struct Scene
 			{
 				const uint32_t first = (uint32_t)(~node) >> 4;
 				const int cnt = (int)((uint32_t)(~node) & 15u) + 1;
-				st.leaves++;
+				st.leaves++, steps++;
 				for (int k = 0; k < cnt; k++) { st.tris++; hit |= intersect( perm[first + k], o, d, tb ); }
 			}
 			if (sp == 0) break;
@@ -96,6 +97,7 @@ struct Scene
 		}
 		st.hits += hit;
 		st.rays++;
+		st.per.push_back( steps );
 	}
 };
 
@@ -126,7 +128,8 @@ int main( int argc, char** argv )
 		}
 	const auto t0 = std::chrono::steady_clock::now();
 	BvhOutput out;
-	BuildBvh2( prims, maxLeaf, 0, out, 1.0f, 0, alpha > 0 ? sc.tv.data() : nullptr, alpha, budget );
+	const float ctrav = getenv( "CTRAV" ) ? (float)atof( getenv( "CTRAV" ) ) : 1.0f;
+	BuildBvh2( prims, maxLeaf, 0, out, ctrav, 0, alpha > 0 ? sc.tv.data() : nullptr, alpha, budget );
 	const double buildS = std::chrono::duration<double>( std::chrono::steady_clock::now() - t0 ).count();
 	const float cLeaf = argc > 5 ? (float)atof( argv[5] ) : -1.0f, cTri = argc > 6 ? (float)atof( argv[6] ) : 0.5f;
 	const int mlt = argc > 7 ? atoi( argv[7] ) : 1;
@@ -161,6 +164,11 @@ int main( int argc, char** argv )
 		const V3 d = norm( { T.x * r * std::cos( ph ) + B.x * r * std::sin( ph ) + n.x * cz, T.y * r * std::cos( ph ) + B.y * r * std::sin( ph ) + n.y * cz,
 			T.z * r * std::cos( ph ) + B.z * r * std::sin( ph ) + n.z * cz } );
 		sc.trace( o, d, surf );
+		/* the ray's chord through the scene box (a predictor of its traversal cost) */
+		float t1 = 1e30f;
+		const float lo[3] = { -5.3f, -5.3f, -5.3f }, hi[3] = { 5.3f, 5.3f, 5.3f }, oo[3] = { o.x, o.y, o.z }, dd[3] = { d.x, d.y, d.z };
+		for (int k = 0; k < 3; k++) t1 = std::fmin( t1, std::fmax( (lo[k] - oo[k]) / dd[k], (hi[k] - oo[k]) / dd[k] ) );
+		surf.chord.push_back( t1 );
 	}
 	std::printf( "{\"tris\": %zu, \"alpha\": %g, \"budget\": %g, \"maxLeaf\": %d, \"refs\": %zu, \"nodes2\": %zu, \"nodes4\": %zu, \"depth2\": %d, "
 		"\"depth4\": %d, \"sah\": %.3f, \"build_s\": %.2f, \"camera\": {\"nodes\": %.2f, \"leaves\": %.2f, \"tris\": %.2f, \"hit\": %.3f}, "
@@ -168,5 +176,22 @@ int main( int argc, char** argv )
 		N, alpha, budget, maxLeaf, out.perm.size(), out.nodes.size() / 16, sc.n4.size() / 32, out.maxDepth, depth4, out.sah, buildS,
 		cam.nodes / cam.rays, cam.leaves / cam.rays, cam.tris / cam.rays, cam.hits / cam.rays, surf.nodes / surf.rays, surf.leaves / surf.rays, surf.tris / surf.rays, surf.hits / surf.rays,
 		(175.0 * surf.nodes + 66.0 * surf.leaves + 86.0 * surf.tris) / surf.rays );
+	if (getenv( "DIST" ))
+	{
+		std::vector<std::pair<float, int>> cs;
+		for (size_t i = 0; i < surf.per.size(); i++) cs.push_back( { surf.chord[i], surf.per[i] } );
+		std::sort( cs.begin(), cs.end() );
+		for (int dcl = 0; dcl < 10; dcl++)
+		{
+			std::vector<int> v;
+			for (size_t i = cs.size() * dcl / 10; i < cs.size() * (dcl + 1) / 10; i++) v.push_back( cs[i].second );
+			std::sort( v.begin(), v.end() );
+			double m = 0; for (int x : v) m += x;
+			std::printf( "chord decile %d (%.2f..): mean %.1f p90 %d p99 %d max %d\n", dcl, cs[cs.size() * dcl / 10].first, m / v.size(), v[v.size() * 9 / 10], v[v.size() * 99 / 100], v.back() );
+		}
+		std::sort( surf.per.begin(), surf.per.end() );
+		const size_t n = surf.per.size();
+		std::printf( "surface iterations per ray: p50 %d p90 %d p99 %d p99.9 %d max %d\n", surf.per[n / 2], surf.per[n * 9 / 10], surf.per[n * 99 / 100], surf.per[n * 999 / 1000], surf.per.back() );
+	}
 	return 0;
 }

@@ -25,6 +25,13 @@ from lighthouse2_amd.core import RenderCore  # noqa: E402
 bounce_rays = scene.bounce_rays   # shared with bench.py and tools/make_fixtures.py
 
 
+def scene_tris_box(sc):
+    """The box of every triangle vertex of the scene's first mesh (config 2: the whole scene)."""
+    t = np.asarray(sc.meshes[0])
+    v = np.concatenate([t[:, 32:35], t[:, 36:39], t[:, 40:43]], 0)
+    return v.min(0), v.max(0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
@@ -40,6 +47,8 @@ def main():
     ap.add_argument("--pre-setting", action="append", default=[], help="name=value set before loading (BVH build)")
     ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
     ap.add_argument("--sweep", action="store_true", help="refill x leafBatch grid")
+    ap.add_argument("--chord", type=float, action="append", default=[],
+                    help="also time the bounce rays with the shortest-chord fraction F of each segment moved to its end")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     sc = scene.config2_scene(n=args.tris)
@@ -59,6 +68,28 @@ def main():
     if args.set in ("both", "bounce", "bounce_sorted"):
         hits = core.trace_closest(O4, D4)
         sets["bounce"] = bounce_rays(sc.meshes[0], O4[perm], D4[perm], hits[perm])   # compacted, in-frame order
+        for f in args.chord:
+            # the chord of each ray through the scene box; per segment (the launch's eighths), the
+            # shortest-chord fraction f goes last, both parts in their in-frame order
+            bo, bd = sets["bounce"]
+            v = scene_tris_box(sc)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                t1 = np.minimum.reduce([np.maximum((v[0][k] - bo[:, k]) / bd[:, k], (v[1][k] - bo[:, k]) / bd[:, k]) for k in range(3)])
+            n = len(bo)
+            seg = (n + 7) // 8
+            order = []
+            for c in range(8):
+                idx = np.arange(c * seg, min(n, (c + 1) * seg))
+                if len(idx) == 0:
+                    continue
+                cut = np.quantile(t1[idx], f)
+                order.append(idx[t1[idx] > cut])
+                order.append(idx[t1[idx] <= cut])
+            if f >= 1.0:
+                # f >= 1: every segment fully sorted by descending chord
+                order = [np.arange(c * seg, min(n, (c + 1) * seg))[np.argsort(-t1[c * seg:min(n, (c + 1) * seg)], kind="stable")] for c in range(8)]
+            order = np.concatenate(order)
+            sets[f"bounce_chord{f}"] = (np.ascontiguousarray(bo[order]), np.ascontiguousarray(bd[order]))
         if args.set in ("both", "bounce_sorted"):
             # sorted by (direction octant, Morton code of the origin): coherent groups of 64 rays
             bo, bd = sets["bounce"]
@@ -90,7 +121,8 @@ def main():
         return
     res = {}
     for name, (o, d) in sets.items():
-        if args.set not in ("both", name) and not (args.set == "bounce_sorted" and name == "bounce_sorted"):
+        if args.set not in ("both", name) and not (args.set == "bounce_sorted" and name == "bounce_sorted") \
+                and not name.startswith("bounce_chord"):
             continue
         n = len(o)
         rf = args.refill_primary if name == "primary" else args.refill
