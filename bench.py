@@ -203,6 +203,9 @@ def roofline_of(core, sc, W, H, dev, kernel_iters):
 
     ms_p, hits_p = launch(o4, d4, True)
     bo, bd = scene.bounce_rays(sc.meshes[0], o4, d4, hits_p)
+    # the frame's shade writes them into two-ended segments (chordSplit): its trace takes them in this order
+    order = scene.chord_order(bo, bd, *scene.mesh_box(sc.meshes[0]), core.get_setting("chordSplit"))
+    bo, bd = np.ascontiguousarray(bo[order]), np.ascontiguousarray(bd[order])
     ms, _ = launch(bo, bd, False)
     n, n_p = len(bo), len(o4)
     version = int(core.get_setting("traceVersion"))
@@ -223,7 +226,7 @@ def roofline_of(core, sc, W, H, dev, kernel_iters):
         "unit": "G wave64 VALU instructions/s", "frac": round(achieved / peak, 4) if achieved else None,
         "traffic": traffic,
         "kernel": f"{kname} (per-ray BVH4 traversal, traceVersion {version}, the core's default settings) on the "
-                  f"frame's {n} diffuse bounce rays, in-frame order",
+                  f"frame's {n} diffuse bounce rays, in the frame's order (two-ended segments, chordSplit)",
         "kernel_ms": round(ms, 4), "rays_per_launch": n,
         "valu_insts_per_launch": valu, "valu_lane_utilisation": sq.get("valu_lane_utilisation") if sq else None,
         "peak_basis": f"{SIMDS} SIMDs x {CLOCK_GHZ} GHz / {cyc:.2f} cycles per wave64 VALU instruction "

@@ -702,6 +702,34 @@ def textured_scene(width: int = 1920, height: int = 1080, tess: int = 24, instan
     return sc
 
 
+def chord_order(O, D, lo, hi, cut, segs=8):
+    """The order in which a frame's trace launch takes rays that a shade launch wrote into two-ended
+    segments (RenderCore setting chordSplit, ShadeParams::chordCut): per segment (the launch's
+    eighths), the rays whose chord through the scene box [lo, hi] exceeds cut x its largest extent,
+    in order, then the others in reverse (they are written from the segment's end).  Returns the
+    permutation."""
+    lo, hi = np.asarray(lo, np.float64), np.asarray(hi, np.float64)
+    c = cut * float((hi - lo).max())
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t = np.minimum.reduce([np.maximum((lo[k] - O[:, k]) / D[:, k], (hi[k] - O[:, k]) / D[:, k]) for k in range(3)])
+    n = len(O)
+    seg = (n + segs - 1) // segs
+    out = []
+    for k in range(segs):
+        idx = np.arange(k * seg, min(n, (k + 1) * seg))
+        late = t[idx] <= c if cut > 0 else np.zeros(len(idx), bool)
+        out += [idx[~late], idx[late][::-1]]
+    return np.concatenate(out)
+
+
+def mesh_box(tris):
+    """The box of a mesh's vertices (CoreTri records)."""
+    t = np.asarray(tris)
+    v = np.concatenate([t[:, abi.TRI["vertex0"]:abi.TRI["vertex0"] + 3], t[:, abi.TRI["vertex1"]:abi.TRI["vertex1"] + 3],
+                        t[:, abi.TRI["vertex2"]:abi.TRI["vertex2"] + 3]], 0)
+    return v.min(0), v.max(0)
+
+
 def bounce_rays(tris, O4, D4, hits, seed=1):
     """Diffuse 'bounce' rays from primary hits, as the first shade pass emits them (bench.py's roofline
     launch, tools/trace_kernel_bench.py, the bounce-visits fixture): cosine-weighted around the face

@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--pre-setting", action="append", default=[], help="name=value set before loading (BVH build)")
     ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
     ap.add_argument("--sweep", action="store_true", help="refill x leafBatch grid")
+    ap.add_argument("--no-chord-order", action="store_true", help="bounce rays in plain in-frame order")
     ap.add_argument("--chord", type=float, action="append", default=[],
                     help="also time the bounce rays with the shortest-chord fraction F of each segment moved to its end")
     args = ap.parse_args()
@@ -67,11 +68,17 @@ def main():
     sets = {"primary": (np.ascontiguousarray(O4[perm]), np.ascontiguousarray(D4[perm]))}
     if args.set in ("both", "bounce", "bounce_sorted"):
         hits = core.trace_closest(O4, D4)
-        sets["bounce"] = bounce_rays(sc.meshes[0], O4[perm], D4[perm], hits[perm])   # compacted, in-frame order
+        bo, bd = bounce_rays(sc.meshes[0], O4[perm], D4[perm], hits[perm])   # compacted, in-frame order
+        plain = (bo, bd)
+        # as the frame's trace takes them: two-ended segments (chordSplit; --no-chord-order: plain in-frame)
+        if not args.no_chord_order:
+            order = scene.chord_order(bo, bd, *scene.mesh_box(sc.meshes[0]), core.get_setting("chordSplit"))
+            bo, bd = np.ascontiguousarray(bo[order]), np.ascontiguousarray(bd[order])
+        sets["bounce"] = (bo, bd)
         for f in args.chord:
             # the chord of each ray through the scene box; per segment (the launch's eighths), the
             # shortest-chord fraction f goes last, both parts in their in-frame order
-            bo, bd = sets["bounce"]
+            bo, bd = plain
             v = scene_tris_box(sc)
             with np.errstate(divide="ignore", invalid="ignore"):
                 t1 = np.minimum.reduce([np.maximum((v[0][k] - bo[:, k]) / bd[:, k], (v[1][k] - bo[:, k]) / bd[:, k]) for k in range(3)])
