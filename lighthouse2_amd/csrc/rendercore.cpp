@@ -1188,7 +1188,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 #endif
 #ifdef LH2_TRACE_TIMES
 	DevBuf<unsigned long long> ttimes;
-	ttimes.resize( (size_t)TraceGrid() * 4 * 4 );
+	ttimes.resize( (size_t)std::max( TraceGrid(), PacketGrid() ) * 4 * 4 );
 #endif
 	/* each launch timed by its own dispatch-recorded start / stop events: msOut is the mean kernel
 	   duration, launch gaps excluded (as rocprofv3 --kernel-trace reports it) */

@@ -54,7 +54,7 @@ struct Scene
 		if (tt > 1e-4f && tt < tb) { tb = tt; return true; }
 		return false;
 	}
-	void trace( V3 o, V3 d, Stats& st ) const
+	void trace( V3 o, V3 d, Stats& st, std::vector<int>* visited = nullptr ) const
 	{
 		const V3 id = { 1.0f / d.x, 1.0f / d.y, 1.0f / d.z };
 		float tb = 1e30f;
@@ -65,6 +65,7 @@ struct Scene
 			if (node >= 0)
 			{
 				st.nodes++, steps++;
+				if (visited) visited->push_back( node );
 				const float* q = &n4[(size_t)node * 32];
 				const int* refs = (const int*)(q + 24);
 				float tn[4]; int order[4], nh = 0;
@@ -176,6 +177,45 @@ int main( int argc, char** argv )
 		N, alpha, budget, maxLeaf, out.perm.size(), out.nodes.size() / 16, sc.n4.size() / 32, out.maxDepth, depth4, out.sah, buildS,
 		cam.nodes / cam.rays, cam.leaves / cam.rays, cam.tris / cam.rays, cam.hits / cam.rays, surf.nodes / surf.rays, surf.leaves / surf.rays, surf.tris / surf.rays, surf.hits / surf.rays,
 		(175.0 * surf.nodes + 66.0 * surf.leaves + 86.0 * surf.tris) / surf.rays );
+	if (getenv( "TILES" ))
+	{
+		/* the config-2 frame's 8x8 primary-ray tiles: per tile, the union of the nodes its rays visit
+		   (what a packet traverses) and the longest ray */
+		const int W = 1920, H = 1080;
+		std::vector<std::pair<int, int>> cost;   /* (union, max steps) */
+		Stats tmp;
+		for (int ty = 0; ty < H / 8; ty++)
+			for (int tx = 0; tx < W / 8; tx++)
+			{
+				std::vector<int> vis;
+				int mx = 0;
+				for (int y = ty * 8; y < ty * 8 + 8; y++)
+					for (int x = tx * 8; x < tx * 8 + 8; x++)
+					{
+						const float sx = ((x + 0.5f) / W * 2 - 1) * th * aspect, sy = ((y + 0.5f) / H * 2 - 1) * th;
+						const size_t before = vis.size();
+						sc.trace( cp, norm( { sx, sy, 1.0f } ), tmp, &vis );
+						mx = std::max( mx, (int)(vis.size() - before) );
+					}
+				std::sort( vis.begin(), vis.end() );
+				const int uni = (int)(std::unique( vis.begin(), vis.end() ) - vis.begin());
+				cost.push_back( { uni, mx } );
+			}
+		if (const char* out = getenv( "TILES_OUT" ))
+			if (FILE* fo = std::fopen( out, "wb" ))
+			{
+				for (auto& c : cost) { const int32_t v = c.first; std::fwrite( &v, 4, 1, fo ); }
+				std::fclose( fo );
+			}
+		std::vector<int> u, m;
+		for (auto& c : cost) u.push_back( c.first ), m.push_back( c.second );
+		std::sort( u.begin(), u.end() ), std::sort( m.begin(), m.end() );
+		const size_t n = u.size();
+		double su = 0; for (int x : u) su += x;
+		std::printf( "tiles %zu: union nodes p50 %d p90 %d p99 %d max %d (sum %.0f, top 1%% share %.3f); longest ray p50 %d p99 %d max %d\n", n,
+			u[n / 2], u[n * 9 / 10], u[n * 99 / 100], u.back(), su, [&]() { double t = 0; for (size_t i = n * 99 / 100; i < n; i++) t += u[i]; return t / su; }(),
+			m[n / 2], m[n * 99 / 100], m.back() );
+	}
 	if (getenv( "DIST" ))
 	{
 		std::vector<std::pair<float, int>> cs;

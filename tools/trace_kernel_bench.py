@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
     ap.add_argument("--sweep", action="store_true", help="refill x leafBatch grid")
     ap.add_argument("--no-chord-order", action="store_true", help="bounce rays in plain in-frame order")
+    ap.add_argument("--tile-cost", default=None, help="int32 per-tile cost file: also time the packets in LPT order")
+    ap.add_argument("--tile-chord", type=float, action="append", default=[],
+                    help="also time the primary packets reordered by their centre ray's chord (fraction F last)")
     ap.add_argument("--chord", type=float, action="append", default=[],
                     help="also time the bounce rays with the shortest-chord fraction F of each segment moved to its end")
     args = ap.parse_args()
@@ -66,6 +69,39 @@ def main():
     O4, D4, _ = core.generate_eye_rays(sc.view, 0, 0)
     perm = scene.tiled_order(1920, 1080)    # in-frame order of the primary rays (k_camera, tiledRays)
     sets = {"primary": (np.ascontiguousarray(O4[perm]), np.ascontiguousarray(D4[perm]))}
+    if args.tile_cost:
+        # primary packets per segment in descending order of a per-tile cost file (int32 per 8x8 tile,
+        # tile order = slot order; tools/bvh_quality.cpp TILES_OUT): longest-processing-time first
+        cost = np.fromfile(args.tile_cost, dtype=np.int32)
+        po, pd = sets["primary"]
+        ntile = len(po) // 64
+        assert len(cost) == ntile
+        seg = (ntile + 7) // 8
+        tiles = np.concatenate([np.arange(c * seg, min(ntile, (c + 1) * seg))[np.argsort(-cost[c * seg:min(ntile, (c + 1) * seg)], kind="stable")]
+                                for c in range(8)])
+        rays = (tiles[:, None] * 64 + np.arange(64)[None, :]).reshape(-1)
+        sets["primary_cost"] = (np.ascontiguousarray(po[rays]), np.ascontiguousarray(pd[rays]))
+    for f in args.tile_chord:
+        # the primary packets (64-ray tiles) reordered per segment by the chord of their centre ray through
+        # the scene box: the shortest fraction f last (f >= 1: every segment sorted by descending chord)
+        po, pd = sets["primary"]
+        lo_, hi_ = scene_tris_box(sc)
+        ctr = np.arange(32, len(po), 64)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            t1 = np.minimum.reduce([np.maximum((lo_[k] - po[ctr, k]) / pd[ctr, k], (hi_[k] - po[ctr, k]) / pd[ctr, k]) for k in range(3)])
+        ntile = len(ctr)
+        seg = (ntile + 7) // 8
+        order = []
+        for c in range(8):
+            ti = np.arange(c * seg, min(ntile, (c + 1) * seg))
+            if f >= 1.0:
+                order.append(ti[np.argsort(-t1[ti], kind="stable")])
+            else:
+                cut = np.quantile(t1[ti], f)
+                order += [ti[t1[ti] > cut], ti[t1[ti] <= cut]]
+        tiles = np.concatenate(order)
+        rays = (tiles[:, None] * 64 + np.arange(64)[None, :]).reshape(-1)
+        sets[f"primary_chord{f}"] = (np.ascontiguousarray(po[rays]), np.ascontiguousarray(pd[rays]))
     if args.set in ("both", "bounce", "bounce_sorted"):
         hits = core.trace_closest(O4, D4)
         bo, bd = bounce_rays(sc.meshes[0], O4[perm], D4[perm], hits[perm])   # compacted, in-frame order
@@ -129,17 +165,18 @@ def main():
     res = {}
     for name, (o, d) in sets.items():
         if args.set not in ("both", name) and not (args.set == "bounce_sorted" and name == "bounce_sorted") \
-                and not name.startswith("bounce_chord"):
+                and not name.startswith("bounce_chord") and not name.startswith("primary_"):
             continue
         n = len(o)
-        rf = args.refill_primary if name == "primary" else args.refill
-        lb = args.leaf_batch_primary if name == "primary" else args.leaf_batch
+        prim = name.startswith("primary")
+        rf = args.refill_primary if prim else args.refill
+        lb = args.leaf_batch_primary if prim else args.leaf_batch
         if rf is not None:
-            core.setting("refillPrimary" if name == "primary" else "refill", rf)
+            core.setting("refillPrimary" if prim else "refill", rf)
         if lb is not None:
-            core.setting("leafBatchPrimary" if name == "primary" else "leafBatch", lb)
+            core.setting("leafBatchPrimary" if prim else "leafBatch", lb)
         if not args.no_frame_launch:
-            core.setting("unitCoherent", 1 if name == "primary" else 0)
+            core.setting("unitCoherent", 1 if prim else 0)
         ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
         h = torch.empty((n, 4), dtype=torch.int32, device=dev)
         torch.cuda.synchronize()
