@@ -621,13 +621,10 @@ int CollapseBvh4( const float* nodes2, size_t nodeCount2, std::vector<float>& no
 		float* q = &nodes4[(size_t)it.node4 * 32];
 		for (int i = 0; i < 4; i++)
 		{
-			/* slots i = 0, 1 in q0..q2, slots 2, 3 in q3..q5: (lo.x, hi.x, lo.y, hi.y) per slot, z pairs */
-			float* b = q + (i >> 1) * 12;
-			const int j = i & 1;
+			/* the six planes of four (lh2_device.h): lo.x, hi.x, lo.y, hi.y, lo.z, hi.z of children 0..3 */
 			const bool used = i < n;
-			b[j * 4 + 0] = used ? list[i].lo[0] : nanv, b[j * 4 + 1] = used ? list[i].hi[0] : nanv;
-			b[j * 4 + 2] = used ? list[i].lo[1] : nanv, b[j * 4 + 3] = used ? list[i].hi[1] : nanv;
-			b[8 + j * 2] = used ? list[i].lo[2] : nanv, b[9 + j * 2] = used ? list[i].hi[2] : nanv;
+			for (int k = 0; k < 3; k++)
+				q[(2 * k) * 4 + i] = used ? list[i].lo[k] : nanv, q[(2 * k + 1) * 4 + i] = used ? list[i].hi[k] : nanv;
 		}
 		memcpy( q + 24, refs, 16 );
 	}
@@ -785,12 +782,10 @@ int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>&
 		float* q = &nodes4[(size_t)it.node4 * 32];
 		for (int i = 0; i < 4; i++)
 		{
-			float* b = q + (i >> 1) * 12;
-			const int j = i & 1;
+			/* the six planes of four (lh2_device.h): lo.x, hi.x, lo.y, hi.y, lo.z, hi.z of children 0..3 */
 			const bool used = i < n;
-			b[j * 4 + 0] = used ? list[i].lo[0] : nanv, b[j * 4 + 1] = used ? list[i].hi[0] : nanv;
-			b[j * 4 + 2] = used ? list[i].lo[1] : nanv, b[j * 4 + 3] = used ? list[i].hi[1] : nanv;
-			b[8 + j * 2] = used ? list[i].lo[2] : nanv, b[9 + j * 2] = used ? list[i].hi[2] : nanv;
+			for (int k = 0; k < 3; k++)
+				q[(2 * k) * 4 + i] = used ? list[i].lo[k] : nanv, q[(2 * k + 1) * 4 + i] = used ? list[i].hi[k] : nanv;
 		}
 		memcpy( q + 24, refs, 16 );
 	}

@@ -539,8 +539,11 @@ __global__ __launch_bounds__( 256 ) void k_tlas_to_bvh4( const float4* __restric
 	const float4* s = nodes2 + (size_t)(base2 + i) * 4;
 	float4* d = nodes4 + (size_t)(base4 + i) * 8;
 	const float nanv = __builtin_nanf( "" );
-	d[0] = s[0], d[1] = s[1], d[2] = s[2];
-	d[3] = d[4] = d[5] = make_float4( nanv, nanv, nanv, nanv );
+	/* BVH2 child pair (c0 lo.x hi.x lo.y hi.y | c1 ... | c0 lo.z hi.z c1 lo.z hi.z) -> the BVH4 planes */
+	const float4 a = s[0], b = s[1], z = s[2];
+	d[0] = make_float4( a.x, b.x, nanv, nanv ), d[1] = make_float4( a.y, b.y, nanv, nanv );
+	d[2] = make_float4( a.z, b.z, nanv, nanv ), d[3] = make_float4( a.w, b.w, nanv, nanv );
+	d[4] = make_float4( z.x, z.z, nanv, nanv ), d[5] = make_float4( z.y, z.w, nanv, nanv );
 	const float4 r = s[3];
 	int ref[2] = { __float_as_int( r.x ), __float_as_int( r.y ) };
 	for (int c = 0; c < 2; c++) if (ref[c] >= 0) ref[c] = ref[c] - base2 + base4;

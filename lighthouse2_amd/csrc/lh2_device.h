@@ -19,9 +19,10 @@
      n1 = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
      n2 = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
      n3 = (c0ref, c1ref, -, -)  ref >= 0: interior node index; ref < 0: leaf, ~ref = first<<4 | (count-1)
-   BVH4 node (128 B, one cache line; the per-ray traversal, traceVersion 4): four children, two
-   child-pair blocks of the BVH2 layout and the four references; unused slots have NaN boxes.
-     q0..q2 = children 0, 1 as n0..n2 above;  q3..q5 = children 2, 3 likewise
+   BVH4 node (128 B, one cache line): four children as six planes of four (child 0..3 in .x...w), so a
+   ray loads its near and far plane of each axis by its direction's signs (two loads per axis, no
+   min / max to order them), then the four references; unused slots have NaN boxes.
+     q0 = lo.x, q1 = hi.x, q2 = lo.y, q3 = hi.y, q4 = lo.z, q5 = hi.z   (children 0..3)
      q6 = (ref0, ref1, ref2, ref3), q7 = 0
    Triangle (48 B, leaf order): (v0.xyz, original index), (e1 = v1-v0, 0), (e2 = v2-v0, 0)
    Instance (64 B): inverse transform rows 0..2, (bvhRoot, triBase, mesh, bvh4Root)          */

@@ -535,6 +535,7 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 	}
 }
 
+#include "lh2_box4.inc"
 #include "lh2_trace2.inc"
 #include "lh2_trace4d.inc"
 #include "lh2_trace_packet.inc"

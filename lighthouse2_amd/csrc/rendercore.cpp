@@ -539,6 +539,9 @@ void RenderCore::ConcatenateBlas( int ni )
 	CHK_HIP( hipStreamSynchronize( stream ) );   /* frames in flight may still read the old arrays */
 	dNodes.free(), dTris.free(), dNodes4.free();
 	dNodes.resize( ((size_t)nodeTotal + tlasCapacity) * 4 );
+	/* the BVH4 loops address nodes with 32-bit buffer offsets (lh2_trace4d.inc): the array stays below 2 GiB */
+	if (bvh4 && ((size_t)node4Total + tlasCapacity) * 128 > 0x7fffffffull)
+		FatalError( "BVH4 of %zu nodes exceeds the 2 GiB the traversal addresses", (size_t)node4Total + tlasCapacity );
 	if (bvh4) dNodes4.resize( ((size_t)node4Total + tlasCapacity) * 8 );
 	dTris.resize( (size_t)std::max( triTotal, 1 ) * 3 );
 	for (size_t mi = 0; mi < meshes.size(); mi++)

@@ -71,9 +71,8 @@ struct Scene
 				float tn[4]; int order[4], nh = 0;
 				for (int c = 0; c < 4; c++)
 				{
-					const float* b = q + (c >> 1) * 12;
-					const int j = c & 1;
-					const float lx = b[j * 4 + 0], hx = b[j * 4 + 1], ly = b[j * 4 + 2], hy = b[j * 4 + 3], lz = b[8 + j * 2], hz = b[9 + j * 2];
+					/* planes of four: lo.x, hi.x, lo.y, hi.y, lo.z, hi.z (lh2_device.h) */
+					const float lx = q[c], hx = q[4 + c], ly = q[8 + c], hy = q[12 + c], lz = q[16 + c], hz = q[20 + c];
 					if (!(lx == lx)) continue;
 					const float ax = (lx - o.x) * id.x, bx = (hx - o.x) * id.x, ay = (ly - o.y) * id.y, by = (hy - o.y) * id.y;
 					const float az = (lz - o.z) * id.z, bz = (hz - o.z) * id.z;
