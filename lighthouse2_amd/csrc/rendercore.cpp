@@ -195,8 +195,9 @@ int RenderCore::TraceVersion() const
 {
 	if (traceVersion) return (traceVersion >= 4 && !bvh4) ? 2 : traceVersion;
 	if (!bvh4) return 2;
-	const double bytes = ((double)blasNode4Count + tlasCapacity) * 128.0 + (double)blasTriCount * 48.0;
-	return bytes > (double)traceFetchMB * 1048576.0 ? 7 : 6;
+	/* the leaf-slot loop with small leaf batches: config-2 bounce rays 0.64 -> 0.60 ms, config 5 (DRAM-resident)
+	   13.25 -> 13.1 ms, config 3 unchanged (profiles/r02y_ab_v7.txt); traceFetchMB no longer decides */
+	return 7;
 }
 
 void RenderCore::EnsureBuffers()

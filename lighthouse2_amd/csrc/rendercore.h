@@ -242,7 +242,7 @@ private:
 	   the sweeps on the config-2 frame (profiles/r01c_sweep_bvh4.jsonl, r01c_ab_bvh4_settings.jsonl:
 	   1.89 ms vs 1.94 for BVH2 with 2-triangle leaves); config 3 (room) runs 4 % faster with
 	   bvhMaxLeaf 2 / leafBatch 16, config 5 2 % slower */
-	int refillPrimary = 48, refillOther = 48, leafBatch = 0, leafBatchPrimary = 8;
+	int refillPrimary = 48, refillOther = 48, leafBatch = 6, leafBatchPrimary = 8;   /* leafBatch: traceVersion 7 leaf batches (r02y) */
 	int bvhMaxLeaf = 1;
 	int bvhSweep = 0;                    /* exact SAH sweep below this node size (setting "bvhSweep") */
 	float bvhSpatial = 1e-5f;            /* spatial splits (SBVH): overlap threshold x root area; 0 = off */
