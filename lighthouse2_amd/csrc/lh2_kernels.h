@@ -24,7 +24,15 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	   (clearAcc non-null: each pixel's first sample zeroes it; the memset of rendercore.cpp:465) */
 	Counters* initC; uint32_t* cursors; int cursorWords; uint32_t pathCount, segStride;
 	float4* clearAcc;
+	/* two-ended primary segments (camAlloc non-null; whole 8x8 tiles, segStride a multiple of 64): a tile
+	   whose centre ray's length inside the scene box (chordLo, chordHi) is at most chordCut is written at
+	   the end of its segment, so the primary trace takes the long (costly) tiles first.  camAlloc: this
+	   frame's per-segment front counts (LH2_SEGS x LH2_SEGCOUNT_STRIDE words) then back counts, zeroed by
+	   the previous frame's camera launch, which zeroes camZero (the other frame's block) for the next */
+	uint32_t* camAlloc; uint32_t* camZero;
+	float chordLo[3], chordHi[3], chordCut;
 };
+#define LH2_CAM_ALLOC_WORDS (2 * 8 * 32)   /* front + back counts of the LH2_SEGS segments */
 
 struct SceneDev       /* everything the traversal and shading kernels read, by value (kernarg) */
 {

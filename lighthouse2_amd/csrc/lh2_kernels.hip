@@ -139,14 +139,16 @@ LH2_DEV v3 RandomPointOnLens( const float r0, float r1, const v3 pos, const floa
 }
 
 /* InitCountersForExtend (.cuda.cu:64-74) plus the frame's work-queue heads; thread i of the launch */
-LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_t segStride, uint32_t* cursors, const int cursorWords, const int i )
+LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_t segStride, uint32_t* cursors, const int cursorWords, const int i,
+	const bool twoEnded = false )
 {
 	if (i < cursorWords) cursors[i] = 0;
 	if (i < LH2_SEGS)
 	{
-		/* the camera writes the paths densely: segment i is [i * segStride, (i + 1) * segStride) */
+		/* the camera writes the paths densely: segment i is [i * segStride, (i + 1) * segStride) (two-ended
+		   primary segments: counted in CameraParams::camAlloc instead) */
 		const uint32_t lo = (uint32_t)i * segStride;
-		c->segPath[0][i * LH2_SEGCOUNT_STRIDE] = pathCount > lo ? min( pathCount - lo, segStride ) : 0u;
+		c->segPath[0][i * LH2_SEGCOUNT_STRIDE] = twoEnded ? 0u : pathCount > lo ? min( pathCount - lo, segStride ) : 0u;
 		c->segPath[1][i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadow[i * LH2_SEGCOUNT_STRIDE] = 0;
 		c->segBack[0][i * LH2_SEGCOUNT_STRIDE] = 0, c->segBack[1][i * LH2_SEGCOUNT_STRIDE] = 0;
 	}
@@ -157,11 +159,24 @@ LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_
 	c->reserved0 = 0, c->shadowOverflow = 0, c->shadeDone = 0;
 }
 
+/* the length of a ray's segment inside the box [lo, hi] (negative: it misses the box); ordering only, so
+   a fast reciprocal is fine.  RenderCore::PrimaryChordCut computes the same on the host */
+LH2_DEV float box_chord( const float lo[3], const float hi[3], const v3 o, const v3 d )
+{
+	const float ix = __builtin_amdgcn_rcpf( d.x ), iy = __builtin_amdgcn_rcpf( d.y ), iz = __builtin_amdgcn_rcpf( d.z );
+	const float ax = (lo[0] - o.x) * ix, bx = (hi[0] - o.x) * ix, ay = (lo[1] - o.y) * iy, by = (hi[1] - o.y) * iy;
+	const float az = (lo[2] - o.z) * iz, bz = (hi[2] - o.z) * iz;
+	const float tn = fmaxf( fmaxf( fminf( ax, bx ), fminf( ay, by ) ), fmaxf( fminf( az, bz ), 0.0f ) );
+	const float tf = fminf( fminf( fmaxf( ax, bx ), fmaxf( ay, by ) ), fmaxf( az, bz ) );
+	return tf - tn;
+}
+
 __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const uint8_t* __restrict__ bn, float4* __restrict__ rayO,
 	float4* __restrict__ rayD, float4* __restrict__ T4, float4* __restrict__ Q4, const int jobCount )
 {
 	const int local = threadIdx.x + blockIdx.x * blockDim.x;
-	if (p.initC) init_counters( p.initC, p.pathCount, p.segStride, p.cursors, p.cursorWords, local );
+	if (p.initC) init_counters( p.initC, p.pathCount, p.segStride, p.cursors, p.cursorWords, local, p.camAlloc != nullptr );
+	if (p.camZero && local < LH2_CAM_ALLOC_WORDS) p.camZero[local] = 0;
 	if (local >= jobCount) return;
 	const int slot = p.slotBase + local;
 	/* slot -> (sample, tile row, x) -> global jobIndex = x + (y + s * h) * w, as camera.h:48-53 */
@@ -219,11 +234,23 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 	}
 	const v3 posOnLens = RandomPointOnLens( r2, r3, mk3( p.pos.x, p.pos.y, p.pos.z ), p.aperture, right, up );
 	const v3 rayDir = normalize3( sub3( posOnPixel, posOnLens ) );
-	/* stored at the launch's own index (a path group's buffers hold its slots only) */
-	rayO[local] = make_float4( posOnLens.x, posOnLens.y, posOnLens.z, p.geometryEpsilon );
-	rayD[local] = make_float4( rayDir.x, rayDir.y, rayDir.z, 1e34f );
-	T4[local] = make_float4( 1, 1, 1, bitsf( ((x + (y + (sampleIndex - (uint32_t)p.pass) * h) * w) << 8) + 1 /* S_SPECULAR */ ) );
-	Q4[local] = make_float4( 1, 0, 0, 0 );
+	/* stored at the launch's own index (a path group's buffers hold its slots only), or, with two-ended
+	   primary segments, the tile goes to the front or the end of its segment by its centre ray's chord */
+	uint32_t out = (uint32_t)local;
+	if (p.camAlloc)
+	{
+		const float len = box_chord( p.chordLo, p.chordHi, posOnLens, rayDir );
+		const bool late = __int_as_float( __builtin_amdgcn_readlane( __float_as_int( len ), 36 ) ) <= p.chordCut;   /* pixel (4, 4) */
+		const uint32_t seg = (uint32_t)local / p.segStride;
+		uint32_t pos = 0;
+		if (lane_id() == 0) pos = atomicAdd( p.camAlloc + (late ? LH2_SEGS * LH2_SEGCOUNT_STRIDE : 0) + seg * LH2_SEGCOUNT_STRIDE, 64u );
+		pos = __builtin_amdgcn_readfirstlane( pos );
+		out = seg * p.segStride + (late ? p.segStride - 64u - pos : pos) + lane_id();
+	}
+	rayO[out] = make_float4( posOnLens.x, posOnLens.y, posOnLens.z, p.geometryEpsilon );
+	rayD[out] = make_float4( rayDir.x, rayDir.y, rayDir.z, 1e34f );
+	T4[out] = make_float4( 1, 1, 1, bitsf( ((x + (y + (sampleIndex - (uint32_t)p.pass) * h) * w) << 8) + 1 /* S_SPECULAR */ ) );
+	Q4[out] = make_float4( 1, 0, 0, 0 );
 	if (p.clearAcc && sampleIndex == (uint32_t)p.pass) p.clearAcc[x + y * w] = make_float4( 0, 0, 0, 0 );
 }
 

@@ -119,6 +119,8 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 		g.counters.resize( 1 );
 		g.cursors.resize( (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
 		g.rayLog.resize( LH2_MAX_BOUNCES + 8 );
+		g.camAlloc.resize( 2 * LH2_CAM_ALLOC_WORDS );
+		CHK_HIP( hipMemsetAsync( g.camAlloc.ptr, 0, sizeof( uint32_t ) * 2 * LH2_CAM_ALLOC_WORDS, stream ) );
 		CHK_HIP( hipMemsetAsync( g.rayLog.ptr, 0, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), stream ) );
 		/* indexed by pathLength; written by k_counters_next (system scope) */
 		CHK_HIP( hipHostMalloc( (void**)&g.activeLog, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), hipHostMallocCoherent ) );
@@ -252,6 +254,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "bvhSpatialBudget" )) bvhSpatialBudget = std::min( 4.0f, std::max( 0.0f, value ) );
 	else if (!strcmp( name, "bvh4Collapse" )) bvh4Collapse = value != 0;
 	else if (!strcmp( name, "chordSplit" )) chordSplit = std::max( 0.0f, value );   /* two-ended path segments (longest first); 0: off */
+	else if (!strcmp( name, "chordSplitPrimary" )) chordSplitPrimary = std::min( 1.0f, std::max( 0.0f, value ) );   /* two-ended primary segments; 0: off */
 	else if (!strcmp( name, "bvh4LeafTris" )) bvh4LeafTris = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvh4LeafCost" )) bvh4LeafCost = std::max( 0.0f, value );
 	else if (!strcmp( name, "bvh4TriCost" )) bvh4TriCost = std::max( 0.0f, value );
@@ -289,7 +292,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
+		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "traceFetchMB", traceFetchMB }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "blocksPerCU", (float)blocksPerCU },
@@ -776,6 +779,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	cp.band = tileBand > 0 ? tileBand : std::max( 1, tileRows ), cp.bandStride = tileBand > 0 ? tileStride : std::max( 1, tileRows );
 	cp.tiled = tiledRays;
 	cp.primeRef = primeRef;
+	const bool twoEndedPrimary = chordSplitPrimary > 0 && tiledRays && !primeRef && scrwidth % 8 == 0 && tileRows % 8 == 0;
+	const float primaryCut = twoEndedPrimary ? PrimaryChordCut( view ) : 0.0f;
 	const int grid = TraceGrid();
 	int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
 	/* no specular event and no alpha cut-out in any material: every path ends at its second vertex,
@@ -804,6 +809,16 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		cg.initC = g.counters.ptr, cg.cursors = g.cursors.ptr, cg.cursorWords = LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS;
 		cg.pathCount = g.count, cg.segStride = g.segStride;
 		cg.clearAcc = restart && G == 1 && !tileChanged ? accumulator.ptr : nullptr;
+		/* two-ended primary segments: whole 8x8 tiles in whole segments only */
+		g.twoEnded = twoEndedPrimary && g.segStride % 64 == 0 && g.count % 64 == 0;
+		if (g.twoEnded)
+		{
+			cg.camAlloc = g.camAlloc.ptr + (g.camFrame & 1) * LH2_CAM_ALLOC_WORDS;
+			cg.camZero = g.camAlloc.ptr + ((g.camFrame + 1) & 1) * LH2_CAM_ALLOC_WORDS;
+			g.camFrame++;
+			for (int k = 0; k < 3; k++) cg.chordLo[k] = sceneLo[k], cg.chordHi[k] = sceneHi[k];
+			cg.chordCut = primaryCut;
+		}
 		lh2_launch_camera( &cg, dBlueNoise.ptr, g.rayO[0].ptr, g.rayD[0].ptr, g.T4[0].ptr, g.Q4[0].ptr, (int)g.count, { nullptr, g.evCamera }, g.st );
 		g.prevStop = g.evCamera;
 	}
@@ -831,6 +846,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			uint32_t* segIn = c->segPath[(pathLength - 1) & 1];
 			uint32_t* segNext = c->segPath[pathLength & 1];
 			uint32_t* segInBack = c->segBack[(pathLength - 1) & 1];
+			if (pathLength == 1 && g.twoEnded)
+			{
+				/* the camera's two-ended segments (zeroed when retired at the hand-off, as segPath[0] is) */
+				segIn = g.camAlloc.ptr + ((g.camFrame - 1) & 1) * LH2_CAM_ALLOC_WORDS;
+				segInBack = segIn + LH2_SEGS * LH2_SEGCOUNT_STRIDE;
+			}
 			uint32_t* segNextBack = c->segBack[pathLength & 1];
 			ta.rayO = g.rayO[g.in].ptr, ta.rayD = g.rayD[g.in].ptr, ta.segCounts = segIn, ta.segStride = g.segStride;
 			ta.segBack = segInBack;
@@ -971,6 +992,39 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	framePrimeRef = primeRef;
 	statsPending = true;
 	frameHostMs = std::chrono::duration<double, std::milli>( std::chrono::high_resolution_clock::now() - t0 ).count();
+}
+
+/* the chordSplitPrimary quantile of the frame's 8x8 tile centre rays' lengths inside the scene box (pinhole
+   rays through the tile centres, at most ~4096 of them; box_chord in lh2_kernels.hip is the device side),
+   recomputed when the view or the box changes */
+float RenderCore::PrimaryChordCut( const lh2_ViewPyramid& view )
+{
+	const float box[7] = { sceneLo[0], sceneLo[1], sceneLo[2], sceneHi[0], sceneHi[1], sceneHi[2], chordSplitPrimary };
+	if (cutValid && !memcmp( &view, &cutView, sizeof( view ) ) && !memcmp( box, cutBox, sizeof( box ) )) return cutValue;
+	const int tw = scrwidth / 8, th = std::max( 1, scrheight / 8 );
+	const int step = std::max( 1, (int)std::ceil( std::sqrt( (double)tw * th / 4096.0 ) ) );
+	std::vector<float> len;
+	for (int ty = 0; ty < th; ty += step)
+		for (int tx = 0; tx < tw; tx += step)
+		{
+			const float fx = (tx * 8 + 4.5f) / scrwidth, fy = (ty * 8 + 4.5f) / scrheight;
+			float d[3], o[3] = { view.pos.x, view.pos.y, view.pos.z };
+			const float p1[3] = { view.p1.x, view.p1.y, view.p1.z }, p2[3] = { view.p2.x, view.p2.y, view.p2.z }, p3[3] = { view.p3.x, view.p3.y, view.p3.z };
+			for (int k = 0; k < 3; k++) d[k] = p1[k] + fx * (p2[k] - p1[k]) + fy * (p3[k] - p1[k]) - o[k];
+			float tn = 0, tf = 1e30f;
+			for (int k = 0; k < 3; k++)
+			{
+				const float inv = 1.0f / d[k], a = (sceneLo[k] - o[k]) * inv, b = (sceneHi[k] - o[k]) * inv;
+				if (a == a && b == b) tn = std::max( tn, std::min( a, b ) ), tf = std::min( tf, std::max( a, b ) );
+			}
+			const float n = std::sqrt( d[0] * d[0] + d[1] * d[1] + d[2] * d[2] );
+			len.push_back( (tf - tn) * n );   /* d is not normalised: scale t to distance */
+		}
+	const size_t q = std::min( len.size() - 1, (size_t)(chordSplitPrimary * (len.size() - 1)) );
+	std::nth_element( len.begin(), len.begin() + q, len.end() );
+	cutValue = len[q], cutView = view, cutValid = true;
+	memcpy( cutBox, box, sizeof( box ) );
+	return cutValue;
 }
 
 void RenderCore::UnpackTile( const void* devSrc, int rank, int nranks, int band )

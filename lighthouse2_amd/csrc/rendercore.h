@@ -75,6 +75,8 @@ struct PathGroup
 	DevBuf<Counters> counters;
 	DevBuf<uint32_t> cursors;            /* LH2_CURSOR_SLOTS x LH2_CURSOR_WORDS work-queue heads */
 	DevBuf<uint32_t> rayLog;
+	DevBuf<uint32_t> camAlloc;           /* two-ended primary segments: 2 frames x LH2_CAM_ALLOC_WORDS (CameraParams::camAlloc) */
+	uint32_t camFrame = 0;
 	DevBuf<uint4> tailRec;               /* tail hand-off records, one per trace thread (TraceArgs::tailOut) */
 	DevBuf<float2> tailUV;
 	uint32_t* activeLog = nullptr;       /* pinned: extension rays after each bounce (k_counters_next) */
@@ -88,6 +90,7 @@ struct PathGroup
 	uint32_t base = 0, count = 0, segStride = 0, shadowStride = 0;
 	int in = 0, pl = 0;
 	bool done = false;
+	bool twoEnded = false;               /* this frame's primary rays are in two-ended segments (CameraParams::camAlloc) */
 	hipEvent_t prevStop = nullptr;
 };
 
@@ -252,6 +255,16 @@ private:
 	float bvh4LeafCost = 0.4f, bvh4TriCost = 0.5f;   /* ... its costs of a leaf visit and a triangle test (node step = 1) */
 	float chordSplit = 0.35f;            /* extension rays with a chord through the scene box below this x its extent are traced last */
 	float sceneLo[3] = { 0, 0, 0 }, sceneHi[3] = { 0, 0, 0 };   /* world box of the instanced meshes (UpdateToplevel) */
+	/* two-ended primary segments (CameraParams::camAlloc): the 8x8 tiles whose centre ray's length inside
+	   the scene box is at most the chordSplitPrimary quantile (over the frame's tile centres) are traced
+	   last; 0: off.  Measured slower (profiles/r02za_ab_primary_chord.txt): the per-wave allocation atomics
+	   of the camera launch contend on 16 words (4K camera 0.11 -> 0.78 ms) and the in-box chord did not
+	   shorten the config-2 packet launch (0.376 -> 0.384 ms): off */
+	float chordSplitPrimary = 0.0f;
+	float PrimaryChordCut( const lh2_ViewPyramid& view );
+	lh2_ViewPyramid cutView{};
+	float cutBox[7] = {}, cutValue = 0;
+	bool cutValid = false;
 	int traceVersion = 0;                /* 0: auto (TraceVersion) */
 	float traceFetchMB = 256.0f;         /* auto: traceVersion 5 above this BVH4 + triangle footprint */
 	int TraceVersion() const;

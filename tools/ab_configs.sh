@@ -6,6 +6,6 @@ ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
 export LH2_BLUENOISE="$ROOT/lighthouse2_amd/data/bluenoise.bin"
 for spec in "$@"; do
   v="${spec%%:*}"; st=""; [ "$spec" != "$v" ] && for kv in $(echo "${spec#*:}" | tr ',' ' '); do st="$st --setting $kv"; done
-  LH2_CORE_LIB="$ROOT/gpuvar/$v/libRenderCore_MI355X.so" timeout -k 10 300 python3 "$ROOT/tools/bench_configs.py" --configs ${CONFIGS:-3,5} --frames 6 $st > /tmp/abc.jsonl || exit 1
+  LH2_CORE_LIB="$ROOT/${VARDIR:-gpuvar}/$v/libRenderCore_MI355X.so" timeout -k 10 300 python3 "$ROOT/tools/bench_configs.py" --configs ${CONFIGS:-3,5} --frames 6 $st > /tmp/abc.jsonl || exit 1
   while read -r l; do echo "{\"spec\": \"$spec\", \"res\": $l}" >> "$ROOT/gpurun_out/ab_configs.jsonl"; done < /tmp/abc.jsonl
 done

@@ -30,22 +30,32 @@ from lighthouse2_amd.core import RenderCore  # noqa: E402
 
 
 def measure(core, sc, frames, warmup, per_frame=None, converge_each=True):
+    """frames timed like bench.py's step loop: one synchronize before and after the K frames (the host
+    queues frame i+1 while the GPU renders frame i); the per-frame-synchronised time (the host's launch
+    latency exposed every frame) is reported beside it"""
     def frame(i):
         if per_frame:
             per_frame(i)
         sc.render_frame(core, converge=1 if converge_each else (1 if i == 0 else 0))
-        core.sync()
     for i in range(warmup):
         frame(i)
+    core.sync()
     counts = core.ray_counts()
     t0 = time.perf_counter()
     for i in range(frames):
         frame(warmup + i)
+    core.sync()
     el = (time.perf_counter() - t0) / frames
     st = core.stats()
+    t0 = time.perf_counter()
+    for i in range(frames):
+        frame(warmup + frames + i)
+        core.sync()
+    el_sync = (time.perf_counter() - t0) / frames
     return {"ms_per_frame": round(el * 1e3, 3),
             "Mrays_s": round((int(counts[0]) + int(counts[1])) / el / 1e6, 1),
             "all_extension_Mrays_s": round(int(counts[:16].sum()) / el / 1e6, 1),
+            "ms_per_frame_synced": round(el_sync * 1e3, 3),
             "primary_rays": int(counts[0]), "bounce1_rays": int(counts[1]),
             "deep_rays": int(counts[2:16].sum()), "shadow_rays": int(counts[16]),
             "traceTime0_ms": round(st.traceTime0 * 1e3, 3), "traceTime1_ms": round(st.traceTime1 * 1e3, 3),
