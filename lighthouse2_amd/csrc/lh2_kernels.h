@@ -68,6 +68,7 @@ struct BounceAdvance  /* the hand-off to the next bounce (advance_bounce, lh2_ke
 	uint32_t* rayCountLog;           /* [pathLength] = rays of the next bounce */
 	uint32_t* hostActiveLog;         /* pinned host copy of the same (the host's early exit), or null */
 	uint32_t* shadowSnap; uint32_t* shadowCursor;   /* the shadow split's snapshot, or null */
+	int zeroLog;                     /* nonzero: also zero rayCountLog past pathLength (the path tail counts into it) */
 };
 
 struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path state */
@@ -125,6 +126,11 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	   hands them, with their traversal state and stack, to another wave of its workgroup through
 	   LDS and exits (0: off) */
 	uint32_t pool;
+	uint32_t shadeBatch;                              /* path tail (k_trace_path4d): shade once >= shadeBatch lanes finished a query */
+	/* terminal trace (k_trace_term4d): the last bounce of a scene whose hits there add nothing (ShadeParams::
+	   terminal); a ray that misses adds its sky sample to acc[pixel] as k_shade_last does (pathT4 / pathQ4:
+	   the path state, wh: pixels per frame) and no hit record is written */
+	const float4* pathT4; const float4* pathQ4; uint32_t wh;
 };
 /* traversal-loop statistics (diagnostic builds with -DLH2_TRACE_STATS; tools/trace_stats.py):
    wave-iterations, active-lane sum, leaf-phase iterations / lanes, walk iterations / lanes,
@@ -155,6 +161,9 @@ void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int 
 int lh2_trace_blocks_per_cu( void );
 int lh2_packet_blocks_per_cu( void );
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
+void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
+void lh2_launch_trace_term( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st );
+int lh2_path_blocks_per_cu( void );
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
 void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
 void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st );

@@ -564,6 +564,15 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 
 #include "lh2_box4.inc"
 #include "lh2_trace2.inc"
+/* the path-tail mode of lh2_trace4d.inc shades with k_shade's code (defined with the shading code below) */
+struct ShadeOut { bool ext, shadow; float4 eO, eD, eT, eQ, sO, sD, sP; };
+template <bool NL>
+LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd, const float4 T4, const float4 O4, const float4 D4, const float4 Q4,
+	const int pathLength, const uint32_t R0, ShadeOut& o );
+/* ... and the terminal trace the miss branch of k_shade_last */
+LH2_DEV v3 SampleSkydome( const SceneDev& s, const v3 D );
+LH2_DEV v3 clampintensity( const float clampValue, v3 c );
+LH2_DEV v3 fixnan( v3 a );
 #include "lh2_trace4d.inc"
 #include "lh2_trace_packet.inc"
 
@@ -1368,6 +1377,150 @@ LH2_DEV float scene_chord( const ShadeParams& p, const float4 o, const float4 d 
 	const float tz = fmaxf( (p.chordLo[2] - o.z) * iz, (p.chordHi[2] - o.z) * iz );
 	return fminf( fminf( tx, ty ), tz );
 }
+/* one path vertex of shadeKernel (pathtracer.h:54-245): the hit record, ray and path state of a path at
+   pathLength in; its extension ray (o.ext) and shadow ray (o.shadow) out.  Shared by k_shade (one launch
+   per bounce) and the path-tail kernel (k_trace_path4d: trace and shade in one loop per lane) */
+template <bool NL>
+LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd, const float4 T4, const float4 O4, const float4 D4, const float4 Q4,
+	const int pathLength, const uint32_t R0, ShadeOut& o )
+{
+	const int w = p.w, h = p.h;
+	const float HIT_T = __uint_as_float( hd.x );
+	const int PRIMIDX = (int)hd.y;
+	const int INSTANCEIDX = PRIMIDX == -1 ? 0 : (int)hd.z;
+	const float HIT_U = (float)(hd.w & 65535) * (1.0f / 65535.0f);
+	const float HIT_V = (float)(hd.w >> 16) * (1.0f / 65535.0f);
+	uint32_t data = fbits( T4.w );
+	const float bsdfPdf = Q4.x;
+	const v3 D = xyz( D4 ), RAY_O = xyz( O4 );
+	v3 throughput = xyz( T4 );
+	const uint32_t pathIdx = data >> 8;
+	const uint32_t pixelIdx = pathIdx % (uint32_t)(w * h);
+	const uint32_t sampleIdx = pathIdx / (uint32_t)(w * h) + (uint32_t)p.pass;
+	/* this vertex's blue-noise samples (dimensions 4..7 + 4 pathLength: r0, r1 for the light, r3, r4
+	   for the BSDF) and the hit's instance record are fetched together, and the sample bytes with
+	   the triangle: the dependent chain is inputs -> (ranking bytes, instance) -> (samples,
+	   triangle) -> material, instead of the table lookups following the material */
+	const BlueNoise4 bnq = blueNoiseFetch4( s.blueNoise, (int)(pixelIdx % (uint32_t)w), (int)(pixelIdx / (uint32_t)w), (int)sampleIdx, 4 + 4 * pathLength );
+	v3 instA, instB, instC;
+	const float4* tri = HitInstance( s, PRIMIDX, INSTANCEIDX, instA, instB, instC );
+	__builtin_amdgcn_sched_barrier( 0 );
+	float bnv[4];
+	blueNoiseFinish4( s.blueNoise, bnq, bnv );
+	if (pathLength == 1) unsafeAtomicAdd( &p.acc[pixelIdx].w, PRIMIDX == NOHIT ? 10000.0f : HIT_T );
+	if (PRIMIDX == NOHIT)
+	{
+		v3 contribution = muls( mul3( throughput, SampleSkydome( s, D ) ), 1.0f / bsdfPdf );
+		contribution = clampintensity( s.clampValue, contribution );
+		contribution = fixnan( contribution );
+		acc_add( p.acc, pixelIdx, contribution );
+		return;
+	}
+	if ((int)pixelIdx == p.probePixel && pathLength == 1 && sampleIdx == 0)
+		p.counters->probedInstid = INSTANCEIDX, p.counters->probedTriid = PRIMIDX, p.counters->probedDist = HIT_T;
+	{
+		ShadingData sd;
+		v3 N, iN, fN, T;
+		const v3 I = add3( RAY_O, smul( HIT_T, D ) );
+		GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, instA, instB, instC, sd, N, iN, fN, T );
+		if (sd.flags & 1)
+		{
+			if (pathLength < p.maxPathLength)
+			{
+				throughput = fixnan( throughput );
+				o.ext = true;
+				o.eO = make_float4( I.x, I.y, I.z, EPSILON ), o.eD = make_float4( D.x, D.y, D.z, 1e34f );
+				o.eT = make_float4( throughput.x, throughput.y, throughput.z, bitsf( data ) ), o.eQ = make_float4( bsdfPdf, 0, 0, 0 );
+			}
+			return;
+		}
+		if (sd.color.x > 1.0f || sd.color.y > 1.0f || sd.color.z > 1.0f)
+		{
+			const float DdotNL = -dot3( D, N );
+			v3 contribution = s3( 0 );
+			if (DdotNL > 0)
+			{
+				if (pathLength == 1 || (data & S_SPECULAR) > 0) contribution = sd.color;
+				else
+				{
+					const v3 lastN = UnpackNormal( fbits( Q4.y ) );
+					const float4 tdata0 = tri[0], tdata5 = tri[5];
+					const float lightPdf = (HIT_T * HIT_T) / (-dot3( D, N ) * tdata5.w);     /* CalculateLightPDF, tri.area */
+					const float pickProb = LightPickProb( s, __float_as_int( tdata0.w ), RAY_O, lastN, I );
+					if ((bsdfPdf + lightPdf * pickProb) > 0) contribution = muls( mul3( throughput, sd.color ), 1.0f / (bsdfPdf + lightPdf * pickProb) );
+				}
+				contribution = clampintensity( s.clampValue, contribution );
+				contribution = fixnan( contribution );
+				acc_add( p.acc, pixelIdx, contribution );
+			}
+			return;
+		}
+		if (ROUGHNESS <= 0.001f || TRANSMISSION > 0.999f) data |= S_SPECULAR; else data &= ~S_SPECULAR;
+		uint32_t seed = WangHash( pathIdx * 17 + R0 );
+		const float faceDir = (dot3( D, N ) > 0) ? -1 : 1;
+		if (faceDir == 1) sd.transmittance = s3( 0 );
+		throughput = muls( throughput, 1.0f / bsdfPdf );
+		if (NL && !(data & S_SPECULAR) && sampleIdx >= 2) (void)RandomFloat( seed ), (void)RandomFloat( seed );
+		if (!NL && !(data & S_SPECULAR))
+		{
+			float r0, r1, pickProb = 0, lightPdf = 0;
+			if (sampleIdx < 2) r0 = bnv[0], r1 = bnv[1];
+			else
+			{
+				r0 = RandomFloat( seed );
+				r1 = RandomFloat( seed );
+			}
+			v3 lightColor = s3( 0 );
+			v3 L = sub3( RandomPointOnLight( s, r0, r1, I, muls( fN, faceDir ), pickProb, lightPdf, lightColor ), I );
+			const float dist = length3( L );
+			L = muls( L, 1.0f / dist );
+			const float NdotL = dot3( L, muls( fN, faceDir ) );
+			if (NdotL > 0 && lightPdf > 0)
+			{
+				float bsdfPdf2;
+				const v3 sampledBSDF = EvaluateBSDF( sd, fN, T, muls( D, -1.0f ), L, bsdfPdf2 );
+				if (bsdfPdf2 > 0)
+				{
+					v3 contribution = muls( mul3( mul3( throughput, sampledBSDF ), lightColor ), NdotL / (pickProb * lightPdf + bsdfPdf2) );
+					contribution = fixnan( contribution );
+					contribution = clampintensity( s.clampValue, contribution );
+					const v3 so = SafeOrigin( I, L, muls( N, faceDir ), s.geometryEpsilon );
+					o.shadow = true;
+					o.sO = make_float4( so.x, so.y, so.z, 0 );
+					o.sD = make_float4( L.x, L.y, L.z, dist - 2 * s.geometryEpsilon );
+					o.sP = make_float4( contribution.x, contribution.y, contribution.z, __uint_as_float( pixelIdx ) );
+				}
+			}
+		}
+		if (data & ENOUGH_BOUNCES || pathLength == p.maxPathLength) return;
+		{
+			v3 R = s3( 0 );
+			float newBsdfPdf = 0, r3, r4;
+			if (sampleIdx < 256) r3 = bnv[2], r4 = bnv[3];
+			else
+			{
+				r3 = RandomFloat( seed );
+				r4 = RandomFloat( seed );
+			}
+			bool specular = false;
+			const v3 bsdf = SampleBSDF( sd, fN, N, T, muls( D, -1.0f ), HIT_T, r3, r4, R, newBsdfPdf, specular );
+			if (newBsdfPdf < EPSILON || newBsdfPdf != newBsdfPdf) return;
+			if (specular) data |= S_SPECULAR;
+			const float pr = ((data & S_SPECULAR) || ((data & S_BOUNCED) == 0)) ? 1 : SurvivalProbability( bsdf );
+			if (pr < RandomFloat( seed )) return;
+			throughput = muls( throughput, 1 / pr );
+			const uint32_t packedNormal = PackNormal( muls( fN, faceDir ) );
+			if (!(data & S_SPECULAR)) data |= data & S_BOUNCED ? S_BOUNCEDTWICE : S_BOUNCED; else data |= S_VIASPECULAR;
+			const v3 eo = SafeOrigin( I, R, muls( N, faceDir ), s.geometryEpsilon );
+			throughput = fixnan( throughput );
+			const v3 nt = muls( mul3( throughput, bsdf ), fabsf( dot3( muls( fN, faceDir ), R ) ) );
+			o.ext = true;
+			o.eO = make_float4( eo.x, eo.y, eo.z, 0 ), o.eD = make_float4( R.x, R.y, R.z, 1e34f );
+			o.eT = make_float4( nt.x, nt.y, nt.z, bitsf( data ) ), o.eQ = make_float4( newBsdfPdf, bitsf( packedNormal ), 0, 0 );
+		}
+	}
+}
+
 /* ---- shade kernel: pathtracer.h:54-245 --------------------------------------------------- */
 LH2_DEV void shade_epilogue( const ShadeParams& p );   /* the bounce hand-off, below */
 /* 4 waves per SIMD (<= 128 VGPRs): the kernel is load-latency bound (a dependent chain of hit ->
@@ -1408,140 +1561,11 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 			if (TERM && (int)hd.y != NOHIT && ((fbits( T4.w ) & ENOUGH_BOUNCES) || p.pathLength == p.maxPathLength)) goto compact;
 			const float4 O4 = p.rayO[jobIndex], D4 = p.rayD[jobIndex], Q4 = p.Q4[jobIndex];
 			__builtin_amdgcn_sched_barrier( 0 );
-			const float HIT_T = __uint_as_float( hd.x );
-			const int PRIMIDX = (int)hd.y;
-			const int INSTANCEIDX = PRIMIDX == -1 ? 0 : (int)hd.z;
-			const float HIT_U = (float)(hd.w & 65535) * (1.0f / 65535.0f);
-			const float HIT_V = (float)(hd.w >> 16) * (1.0f / 65535.0f);
-			uint32_t data = fbits( T4.w );
-			const float bsdfPdf = Q4.x;
-			const v3 D = xyz( D4 ), RAY_O = xyz( O4 );
-			v3 throughput = xyz( T4 );
-			const uint32_t pathIdx = data >> 8;
-			const uint32_t pixelIdx = pathIdx % (uint32_t)(w * h);
-			const uint32_t sampleIdx = pathIdx / (uint32_t)(w * h) + (uint32_t)p.pass;
-			/* this vertex's blue-noise samples (dimensions 4..7 + 4 pathLength: r0, r1 for the light, r3, r4
-			   for the BSDF) and the hit's instance record are fetched together, and the sample bytes with
-			   the triangle: the dependent chain is inputs -> (ranking bytes, instance) -> (samples,
-			   triangle) -> material, instead of the table lookups following the material */
-			const BlueNoise4 bnq = blueNoiseFetch4( s.blueNoise, (int)(pixelIdx % (uint32_t)w), (int)(pixelIdx / (uint32_t)w), (int)sampleIdx, 4 + 4 * p.pathLength );
-			v3 instA, instB, instC;
-			const float4* tri = HitInstance( s, PRIMIDX, INSTANCEIDX, instA, instB, instC );
-			__builtin_amdgcn_sched_barrier( 0 );
-			float bnv[4];
-			blueNoiseFinish4( s.blueNoise, bnq, bnv );
-			if (p.pathLength == 1) unsafeAtomicAdd( &p.acc[pixelIdx].w, PRIMIDX == NOHIT ? 10000.0f : HIT_T );
-			if (PRIMIDX == NOHIT)
-			{
-				v3 contribution = muls( mul3( throughput, SampleSkydome( s, D ) ), 1.0f / bsdfPdf );
-				contribution = clampintensity( s.clampValue, contribution );
-				contribution = fixnan( contribution );
-				acc_add( p.acc, pixelIdx, contribution );
-				goto compact;
-			}
-			if ((int)pixelIdx == p.probePixel && p.pathLength == 1 && sampleIdx == 0)
-				p.counters->probedInstid = INSTANCEIDX, p.counters->probedTriid = PRIMIDX, p.counters->probedDist = HIT_T;
-			{
-				ShadingData sd;
-				v3 N, iN, fN, T;
-				const v3 I = add3( RAY_O, smul( HIT_T, D ) );
-				GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, instA, instB, instC, sd, N, iN, fN, T );
-				if (sd.flags & 1)
-				{
-					if (p.pathLength < p.maxPathLength)
-					{
-						throughput = fixnan( throughput );
-						doExt = true;
-						eO = make_float4( I.x, I.y, I.z, EPSILON ), eD = make_float4( D.x, D.y, D.z, 1e34f );
-						eT = make_float4( throughput.x, throughput.y, throughput.z, bitsf( data ) ), eQ = make_float4( bsdfPdf, 0, 0, 0 );
-					}
-					goto compact;
-				}
-				if (sd.color.x > 1.0f || sd.color.y > 1.0f || sd.color.z > 1.0f)
-				{
-					const float DdotNL = -dot3( D, N );
-					v3 contribution = s3( 0 );
-					if (DdotNL > 0)
-					{
-						if (p.pathLength == 1 || (data & S_SPECULAR) > 0) contribution = sd.color;
-						else
-						{
-							const v3 lastN = UnpackNormal( fbits( Q4.y ) );
-							const float4 tdata0 = tri[0], tdata5 = tri[5];
-							const float lightPdf = (HIT_T * HIT_T) / (-dot3( D, N ) * tdata5.w);     /* CalculateLightPDF, tri.area */
-							const float pickProb = LightPickProb( s, __float_as_int( tdata0.w ), RAY_O, lastN, I );
-							if ((bsdfPdf + lightPdf * pickProb) > 0) contribution = muls( mul3( throughput, sd.color ), 1.0f / (bsdfPdf + lightPdf * pickProb) );
-						}
-						contribution = clampintensity( s.clampValue, contribution );
-						contribution = fixnan( contribution );
-						acc_add( p.acc, pixelIdx, contribution );
-					}
-					goto compact;
-				}
-				if (ROUGHNESS <= 0.001f || TRANSMISSION > 0.999f) data |= S_SPECULAR; else data &= ~S_SPECULAR;
-				uint32_t seed = WangHash( pathIdx * 17 + p.R0 );
-				const float faceDir = (dot3( D, N ) > 0) ? -1 : 1;
-				if (faceDir == 1) sd.transmittance = s3( 0 );
-				throughput = muls( throughput, 1.0f / bsdfPdf );
-				if (NL && !(data & S_SPECULAR) && sampleIdx >= 2) (void)RandomFloat( seed ), (void)RandomFloat( seed );
-				if (!NL && !(data & S_SPECULAR))
-				{
-					float r0, r1, pickProb = 0, lightPdf = 0;
-					if (sampleIdx < 2) r0 = bnv[0], r1 = bnv[1];
-					else
-					{
-						r0 = RandomFloat( seed );
-						r1 = RandomFloat( seed );
-					}
-					v3 lightColor = s3( 0 );
-					v3 L = sub3( RandomPointOnLight( s, r0, r1, I, muls( fN, faceDir ), pickProb, lightPdf, lightColor ), I );
-					const float dist = length3( L );
-					L = muls( L, 1.0f / dist );
-					const float NdotL = dot3( L, muls( fN, faceDir ) );
-					if (NdotL > 0 && lightPdf > 0)
-					{
-						float bsdfPdf2;
-						const v3 sampledBSDF = EvaluateBSDF( sd, fN, T, muls( D, -1.0f ), L, bsdfPdf2 );
-						if (bsdfPdf2 > 0)
-						{
-							v3 contribution = muls( mul3( mul3( throughput, sampledBSDF ), lightColor ), NdotL / (pickProb * lightPdf + bsdfPdf2) );
-							contribution = fixnan( contribution );
-							contribution = clampintensity( s.clampValue, contribution );
-							const v3 so = SafeOrigin( I, L, muls( N, faceDir ), s.geometryEpsilon );
-							doShadow = true;
-							sO = make_float4( so.x, so.y, so.z, 0 );
-							sD = make_float4( L.x, L.y, L.z, dist - 2 * s.geometryEpsilon );
-							sP = make_float4( contribution.x, contribution.y, contribution.z, __uint_as_float( pixelIdx ) );
-						}
-					}
-				}
-				if (data & ENOUGH_BOUNCES || p.pathLength == p.maxPathLength) goto compact;
-				{
-					v3 R = s3( 0 );
-					float newBsdfPdf = 0, r3, r4;
-					if (sampleIdx < 256) r3 = bnv[2], r4 = bnv[3];
-					else
-					{
-						r3 = RandomFloat( seed );
-						r4 = RandomFloat( seed );
-					}
-					bool specular = false;
-					const v3 bsdf = SampleBSDF( sd, fN, N, T, muls( D, -1.0f ), HIT_T, r3, r4, R, newBsdfPdf, specular );
-					if (newBsdfPdf < EPSILON || newBsdfPdf != newBsdfPdf) goto compact;
-					if (specular) data |= S_SPECULAR;
-					const float pr = ((data & S_SPECULAR) || ((data & S_BOUNCED) == 0)) ? 1 : SurvivalProbability( bsdf );
-					if (pr < RandomFloat( seed )) goto compact;
-					throughput = muls( throughput, 1 / pr );
-					const uint32_t packedNormal = PackNormal( muls( fN, faceDir ) );
-					if (!(data & S_SPECULAR)) data |= data & S_BOUNCED ? S_BOUNCEDTWICE : S_BOUNCED; else data |= S_VIASPECULAR;
-					const v3 eo = SafeOrigin( I, R, muls( N, faceDir ), s.geometryEpsilon );
-					throughput = fixnan( throughput );
-					const v3 nt = muls( mul3( throughput, bsdf ), fabsf( dot3( muls( fN, faceDir ), R ) ) );
-					doExt = true;
-					eO = make_float4( eo.x, eo.y, eo.z, 0 ), eD = make_float4( R.x, R.y, R.z, 1e34f );
-					eT = make_float4( nt.x, nt.y, nt.z, bitsf( data ) ), eQ = make_float4( newBsdfPdf, bitsf( packedNormal ), 0, 0 );
-				}
-			}
+			ShadeOut so;
+			so.ext = so.shadow = false;
+			shade_path<NL>( s, p, hd, T4, O4, D4, Q4, p.pathLength, p.R0, so );
+			doExt = so.ext, doShadow = so.shadow;
+			eO = so.eO, eD = so.eD, eT = so.eT, eQ = so.eQ, sO = so.sO, sD = so.sD, sP = so.sP;
 		}
 	compact:
 		/* wave-level compaction of extension and shadow rays into this block's segment of the output
@@ -1590,6 +1614,22 @@ __global__ __launch_bounds__( 256 ) void k_shade_last( const SceneDev s, const S
 		contribution = fixnan( contribution );
 		if (contribution.x != 0 || contribution.y != 0 || contribution.z != 0) acc_add( p.acc, pixelIdx, contribution );
 	}
+}
+
+/* the path tail: bounces shp.pathLength .. maxPathLength in one launch (lh2_trace4d.inc, KIND 3): each
+   lane traces its path's ray, shades the hit with k_shade's code in batches of shadeBatch lanes and walks
+   on with the extension ray in place, so a path's later bounces do not wait for every other path's
+   (the few rays of the deep bounces run latency-bound: config 3's bounces 3 and 4 took 292 + 200 us for
+   ~0.6 M rays as launches of their own).  The shade code's registers set the occupancy */
+#ifndef LH2_PATH_MINWAVES
+#define LH2_PATH_MINWAVES 3   /* 4: 128 VGPRs + 176 B of spills (lit); config 3 tail 0.655 ms at 4, 0.558 ms at 3 */
+#endif
+template <bool NL>
+__global__ __launch_bounds__( 256, LH2_PATH_MINWAVES ) void k_trace_path4d( const SceneDev s, const TraceArgs a, const ShadeParams p )
+{
+	__shared__ int lstack[STACK_LDS * 256];
+	__shared__ int lrefs[4 * 256];
+	trace_stream4d<3, 2, NL>( s, a, lstack + threadIdx.x, lrefs + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &p );
 }
 
 /* counters: .cuda.cu:64-84 */
@@ -1809,6 +1849,7 @@ LH2_DEV void advance_bounce( Counters* c, const BounceAdvance& a, const int path
 		if (resetShadow) c->segShadow[k * LH2_SEGCOUNT_STRIDE] = 0;
 	}
 	a.rayCountLog[pathLength] = ext;     /* rays traced at pathLength + 1 */
+	if (a.zeroLog) for (int k = pathLength + 1; k <= LH2_MAX_BOUNCES; k++) a.rayCountLog[k] = 0;
 	c->totalExtensionRays += ext;
 	c->activePaths = ext;
 	if (resetShadow) c->totalShadowRays += sh;
@@ -2021,6 +2062,22 @@ static int lh2_shade_last_grid( void )   /* k_shade_last: every CU full (occupan
 		g = n * cus < LH2_SEGS ? LH2_SEGS : n * cus;
 	}
 	return g;
+}
+void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st )
+{
+	if (!s->nodes4) return;   /* the host selects the path tail only over a BVH4 */
+	if (s->nArea + s->nPoint + s->nSpot + s->nDir == 0) LH2_LAUNCH( (k_trace_path4d<true>), grid, 256, st, ev, *s, *a, *p );
+	else LH2_LAUNCH( (k_trace_path4d<false>), grid, 256, st, ev, *s, *a, *p );
+}
+void lh2_launch_trace_term( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st )
+{
+	if (s->nodes4) LH2_LAUNCH( k_trace_term4d, grid, 256, st, ev, *s, *a );
+}
+int lh2_path_blocks_per_cu( void )
+{
+	int n = 0;
+	(void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_path4d<false>, 256, 0 );
+	return n;
 }
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st )
 {

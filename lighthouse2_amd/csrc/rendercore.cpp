@@ -107,6 +107,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	dBlueNoise.upload( bn.data(), bn.size(), stream );
 	blocksPerCU = maxBlocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
 	packetBlocksPerCU = std::max( 1, std::min( 8, lh2_packet_blocks_per_cu() ) );
+	pathBlocksPerCU = std::max( 1, std::min( 8, lh2_path_blocks_per_cu() ) );
 	for (int gi = 0; gi < LH2_MAX_GROUPS; gi++)
 	{
 		PathGroup& g = grp[gi];
@@ -254,6 +255,9 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "bvhSpatialBudget" )) bvhSpatialBudget = std::min( 4.0f, std::max( 0.0f, value ) );
 	else if (!strcmp( name, "bvh4Collapse" )) bvh4Collapse = value != 0;
 	else if (!strcmp( name, "chordSplit" )) chordSplit = std::max( 0.0f, value );   /* two-ended path segments (longest first); 0: off */
+	else if (!strcmp( name, "terminalTrace" )) terminalTrace = value != 0;   /* the last terminal bounce's sky samples in its trace launch */
+	else if (!strcmp( name, "pathTail" )) pathTail = std::max( 0, (int)value );   /* bounces from this one in one trace-and-shade launch; 0: off */
+	else if (!strcmp( name, "pathTailBatch" )) pathTailBatch = std::min( 64, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "chordSplitPrimary" )) chordSplitPrimary = std::min( 1.0f, std::max( 0.0f, value ) );   /* two-ended primary segments; 0: off */
 	else if (!strcmp( name, "bvh4LeafTris" )) bvh4LeafTris = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvh4LeafCost" )) bvh4LeafCost = std::max( 0.0f, value );
@@ -292,7 +296,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
+		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "pathTail", (float)pathTail }, { "terminalTrace", (float)terminalTrace }, { "pathTailBatch", (float)pathTailBatch }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "traceFetchMB", traceFetchMB }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "blocksPerCU", (float)blocksPerCU },
@@ -801,7 +805,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		   rays in segments of shadowStride */
 		g.segStride = (g.count + LH2_SEGS - 1) / LH2_SEGS;
 		g.shadowStride = (uint32_t)(g.shO.count / LH2_SEGS);
-		g.in = 0, g.pl = 0, g.done = false;
+		g.in = 0, g.pl = 0, g.done = false, g.tailL = 0;
 		if (gi) CHK_HIP( hipStreamWaitEvent( g.st, evFork, 0 ) );
 		/* the camera launch also resets the group's counters and work-queue heads (k_init_counters) */
 		CameraParams cg = cp;
@@ -829,6 +833,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	frameShadows = shadows;
 	const int splitL = (shadows && !primeRef && G == 1 && shadowSplit > 0 && shadowSplit < maxPL) ? shadowSplit : 0;
 	frameSplit = false;
+	/* the path tail (setting "pathTail"): bounces pathTail .. maxPL in one launch of k_trace_path4d */
+	const int tailL = (!primeRef && G == 1 && !splitL && pathTail >= 2 && pathTail <= maxPL && TraceVersion() == 7 && dNodes4.ptr) ? pathTail : 0;
 	/* the bounce loop, the groups' launches interleaved */
 	for (int pathLength = 1; pathLength <= maxPL; pathLength++)
 	{
@@ -861,6 +867,40 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
 			ta.hits = g.hits.ptr, ta.gstack = g.gstack.ptr;
 			SetTail( ta, g );
+			if (pathLength == tailL)
+			{
+				/* the path tail: trace and shade every remaining bounce in one launch; each path's records
+				   are updated in place, its shadow rays queued for the shadow launch, and rayLog counted */
+				ShadeParams sp{};
+				sp.shadowStride = g.shadowStride;
+				sp.rayO = g.rayO[g.in].ptr, sp.rayD = g.rayD[g.in].ptr, sp.T4 = g.T4[g.in].ptr, sp.Q4 = g.Q4[g.in].ptr;
+				sp.rayOut = g.rayO[g.in].ptr, sp.rayDOut = g.rayD[g.in].ptr, sp.T4Out = g.T4[g.in].ptr, sp.Q4Out = g.Q4[g.in].ptr;
+				sp.shO = g.shO.ptr, sp.shD = g.shD.ptr, sp.shP = g.shP.ptr;
+				sp.acc = accumulator.ptr, sp.counters = c;
+				sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
+				sp.probePixel = probeX + scrwidth * probeY;
+				sp.spreadAngle = view.spreadAngle;
+				sp.adv.rayCountLog = g.rayLog.ptr;
+				ta.shadeBatch = (uint32_t)pathTailBatch;
+				lh2_launch_trace_path( &sd, &ta, &sp, PathGrid(), { nullptr, g.evTrace[pathLength] }, g.st );
+				g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
+				g.tailL = pathLength;   /* no shade interval of its own (Synchronize) */
+				g.done = true;
+				continue;
+			}
+			/* the last bounce of a terminal frame (no lights, nothing that emits or cuts out: its hits add
+			   nothing, ShadeParams::terminal): the trace launch adds the misses' sky samples itself, so there
+			   is no hit record to write and no k_shade_last launch (setting "terminalTrace") */
+			if (pathLength == maxPL && pathLength > 1 && !primeRef && !shadows && !canEmit && terminalShade && terminalTrace &&
+				!ta.packet && TraceVersion() == 7 && dNodes4.ptr)
+			{
+				ta.pathT4 = g.T4[g.in].ptr, ta.pathQ4 = g.Q4[g.in].ptr, ta.acc = accumulator.ptr, ta.wh = (uint32_t)(scrwidth * scrheight);
+				lh2_launch_trace_term( &sd, &ta, grid, { nullptr, g.evTrace[pathLength] }, g.st );
+				g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
+				g.tailL = pathLength;   /* no shade interval of its own (Synchronize) */
+				g.done = true;
+				continue;
+			}
 			lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : grid, { nullptr, g.evTrace[pathLength] }, g.st );
 			g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
 			ShadeParams sp{};
@@ -877,7 +917,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			   in PrimeRef mode, where the bounce's shadow rays are traced (and their counts reset) first */
 			const bool split = pathLength == splitL;
 			const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, g.rayLog.ptr, g.activeLog, split ? shadowSnap.ptr : nullptr,
-				split ? g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr };
+				split ? g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr, pathLength + 1 == tailL };
 			sp.advance = pathLength < maxPL && !primeRef;
 			sp.adv = adv;
 			sp.rayO = g.rayO[g.in].ptr, sp.rayD = g.rayD[g.in].ptr, sp.T4 = g.T4[g.in].ptr, sp.Q4 = g.Q4[g.in].ptr, sp.hits = g.hits.ptr;
@@ -988,7 +1028,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, stream ) );
 	}
 	framePathLengths = 0;
-	for (int gi = 0; gi < G; gi++) hostStats->rayCount[gi][0] = grp[gi].count, framePathLengths = std::max( framePathLengths, grp[gi].pl );
+	for (int gi = 0; gi < G; gi++) hostStats->rayCount[gi][0] = grp[gi].count, framePathLengths = std::max( framePathLengths, grp[gi].tailL ? maxPL : grp[gi].pl );
 	framePrimeRef = primeRef;
 	statsPending = true;
 	frameHostMs = std::chrono::duration<double, std::milli>( std::chrono::high_resolution_clock::now() - t0 ).count();
@@ -1091,7 +1131,12 @@ void RenderCore::Synchronize()
 		coreStats.bounce1RayCount = framePathLengths >= 2 ? rc[1] : 0;
 		coreStats.traceTime1 = framePathLengths >= 2 ? trace( 2 ) : 0;
 		coreStats.deepRayCount = 0, coreStats.traceTimeX = 0;
-		for (int L = 3; L <= framePathLengths; L++) coreStats.deepRayCount = rc[L - 1], coreStats.traceTimeX = trace( L );
+		/* (a path tail's bounces past its first have no launch of their own: their time is in its launch) */
+		for (int L = 3; L <= framePathLengths; L++)
+		{
+			coreStats.deepRayCount = rc[L - 1];
+			if (std::any_of( grp, grp + frameGroups, [L]( const PathGroup& g ) { return L <= g.pl; } )) coreStats.traceTimeX = trace( L );
+		}
 		float shadow = 0, shade = 0;
 		for (int gi = 0; gi < frameGroups; gi++)
 		{
@@ -1100,7 +1145,7 @@ void RenderCore::Synchronize()
 			if (!frameShadows) sh = 0;
 			else if (!framePrimeRef) sh = ms( g.fromShadow, g.evShadow );
 			else for (int L = 1; L < g.pl; L++) sh += ms( g.fromShadowB[L], g.evShadowB[L] );
-			for (int L = 1; L <= g.pl; L++) sd += ms( g.fromShade[L], g.evShade[L] );
+			for (int L = 1; L <= g.pl; L++) if (L != g.tailL) sd += ms( g.fromShade[L], g.evShade[L] );
 			shadow = std::max( shadow, sh ), shade = std::max( shade, sd );
 		}
 		coreStats.shadowTraceTime = shadow;

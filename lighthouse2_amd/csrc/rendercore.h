@@ -90,7 +90,8 @@ struct PathGroup
 	uint32_t base = 0, count = 0, segStride = 0, shadowStride = 0;
 	int in = 0, pl = 0;
 	bool done = false;
-	bool twoEnded = false;               /* this frame's primary rays are in two-ended segments (CameraParams::camAlloc) */
+	bool twoEnded = false;
+	int tailL = 0;                       /* this frame's path-tail launch (pathLength), 0: none */               /* this frame's primary rays are in two-ended segments (CameraParams::camAlloc) */
 	hipEvent_t prevStop = nullptr;
 };
 
@@ -164,8 +165,9 @@ private:
 	SceneDev MakeSceneDev() const;
 	int TraceGrid() const { return smCount * blocksPerCU; }
 	int PacketGrid() const { return smCount * packetBlocksPerCU; }   /* packet kernels: their own occupancy */
+	int PathGrid() const { return smCount * std::min( blocksPerCU, pathBlocksPerCU ); }   /* path tail: its occupancy, within the stack's */
 
-	int device = 0, smCount = 256, blocksPerCU = 5, maxBlocksPerCU = 5, packetBlocksPerCU = 5;
+	int device = 0, smCount = 256, blocksPerCU = 5, maxBlocksPerCU = 5, packetBlocksPerCU = 5, pathBlocksPerCU = 4;
 	bool initialized = false;
 	/* scene */
 	std::vector<CoreMeshHost*> meshes;
@@ -261,6 +263,15 @@ private:
 	   of the camera launch contend on 16 words (4K camera 0.11 -> 0.78 ms) and the in-box chord did not
 	   shorten the config-2 packet launch (0.376 -> 0.384 ms): off */
 	float chordSplitPrimary = 0.0f;
+	/* the path tail (k_trace_path4d): bounces pathTail .. maxPathLength traced and shaded in one launch,
+	   a wave shading its finished queries once pathTailBatch lanes hold one (or none walks); 0: a launch
+	   pair per bounce.  Config 3 (profiles/r02zb_ab_path_tail.txt): 2.542 -> 2.389 ms per frame at 3 / 56
+	   (batches of 16: 2.525, 32: 2.455, 48: 2.43, 64: 2.396; pathTail 2: 2.706, 4: 2.494) */
+	int pathTail = 3, pathTailBatch = 56;
+	/* k_trace_term4d for the last bounce of a terminal frame (no k_shade_last, no hit records).  Measured
+	   slower on config 2 (1.2065 / 1.2053 ms off, 1.2097 / 1.2118 on: the miss lanes' path-state loads and
+	   sky sample stall their waves inside the traversal loop, +20 us, more than the 16 us launch saved): off */
+	int terminalTrace = 0;
 	float PrimaryChordCut( const lh2_ViewPyramid& view );
 	lh2_ViewPyramid cutView{};
 	float cutBox[7] = {}, cutValue = 0;

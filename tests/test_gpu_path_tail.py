@@ -1,0 +1,133 @@
+"""GPU parity of the path tail (setting pathTail, k_trace_path4d): the bounces from pathTail on are
+traced and shaded in one launch, each lane shading its finished closest-hit queries with k_shade's code
+and walking on with the extension ray.  Against the CPU oracle (pathtracer.h:54-245, one launch pair
+per bounce in the reference): identical per-bounce ray counts (rayCount log, counted by the launch's
+per-length atomics), accumulator rel-L2 <= 1e-4, and the same frame with the tail off to float
+summation order."""
+import numpy as np
+import pytest
+
+from lighthouse2_amd import abi, scene
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+REL_L2_TOL = 1e-4
+
+
+def rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _load_both(core, sc, w, h, spp=1):
+    sc.load_into(core)
+    core.set_target(w, h, spp)
+    o = Oracle()
+    sc.load_into(o)
+    o.set_target(w, h, spp)
+    return o
+
+
+def _scene(kind, w, h):
+    if kind == "room":                    # lit: NEE shadow rays from every vertex, glass and mirrors
+        return scene.room_scene(40000, w, h)
+    if kind == "specular":                # no lights: k_trace_path4d<true>, long specular chains
+        sc = scene.config2_scene(n=20000, width=w, height=h, sky=True)
+        sc.area_lights = []
+        sc.materials.append(abi.make_material((0.9, 0.9, 0.9), roughness=0.0))
+        sc.meshes[0].view(np.uint32)[::2, abi.TRI["material"]] = 1
+        return sc
+    sc = scene.instanced_scene(meshes=4, tris_per_mesh=4000, width=w, height=h, grid=2, spacing=10.0)
+    scene.animate_instances(sc, 1)        # several instances: rays re-enter their instance after a shade batch
+    sc.sky = scene.gradient_sky(64, 32)
+    return sc
+
+
+@pytest.mark.parametrize("kind,depth", [("room", 4), ("room", 6), ("specular", 5), ("instanced", 4)])
+@pytest.mark.parametrize("tail", [2, 3])
+def test_path_tail_frame_parity(fresh_core, kind, depth, tail):
+    w, h = 128, 72
+    sc = _scene(kind, w, h)
+    o = _load_both(fresh_core, sc, w, h)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", depth)
+    fresh_core.setting("pathTail", tail)
+    for f in range(2):
+        sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
+        sc.render_frame(o, converge=1 if f == 0 else 0)
+        cg, co = fresh_core.ray_counts(), o.ray_counts()
+        assert np.array_equal(cg, co), (f, cg[:8], co[:8])
+    assert co[1] > 0 and (kind == "instanced" or co[tail - 1] > 0), co[:8]
+    ag, ao = fresh_core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+    assert rel_l2(ag[..., 3], ao[..., 3]) <= 1e-6
+    st = fresh_core.stats()
+    assert st.totalExtensionRays == int(co[:16].sum())
+    # the same two frames with a launch pair per bounce
+    fresh_core.setting("pathTail", 0)
+    for f in range(2):
+        sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
+    a0 = fresh_core.accumulator()
+    assert rel_l2(ag[..., :3], a0[..., :3]) <= 1e-6
+
+
+@pytest.mark.parametrize("batch", [1, 7, 64])
+def test_path_tail_shade_batches(fresh_core, batch):
+    """Every shade batch size (1: shade as soon as a query finishes; 64: only when no lane walks)."""
+    w, h = 96, 54
+    sc = _scene("room", w, h)
+    o = _load_both(fresh_core, sc, w, h)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", 5)
+    fresh_core.setting("pathTail", 2)
+    fresh_core.setting("pathTailBatch", batch)
+    sc.render_frame(fresh_core)
+    sc.render_frame(o)
+    assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
+    assert rel_l2(fresh_core.accumulator()[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
+
+
+def test_path_tail_spp_and_pass_past_256(fresh_core):
+    """Several samples per pixel (path index -> sample) and passes past the blue-noise range (random
+    numbers from the per-path seed, R0 of the lane's own path length)."""
+    w, h = 32, 18
+    sc = _scene("room", w, h)
+    o = _load_both(fresh_core, sc, w, h, spp=4)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", 4)
+    fresh_core.setting("pathTail", 3)
+    for f in range(66):      # 66 x 4 = 264 samples: the last frames run past sample 256
+        sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
+        sc.render_frame(o, converge=1 if f == 0 else 0)
+        if f in (0, 65):
+            assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
+    assert rel_l2(fresh_core.accumulator()[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
+
+
+@pytest.mark.parametrize("kind,depth", [("diffuse", 2), ("diffuse", 4), ("specular", 5)])
+def test_terminal_trace_frame_parity(fresh_core, kind, depth):
+    """A terminal frame's last bounce (no lights, nothing emits or cuts out: ShadeParams::terminal) in
+    one launch of k_trace_term4d (setting terminalTrace): its misses add their sky samples, its hits add
+    nothing, and no k_shade_last runs.  Oracle parity, and the same frame through k_shade_last to float
+    summation order; the bench's config 2 frame takes this path."""
+    w, h = 160, 90
+    sc = scene.config2_scene(n=20000, width=w, height=h, sky=True)
+    if kind == "specular":
+        sc.materials.append(abi.make_material((0.9, 0.9, 0.9), roughness=0.0))
+        sc.meshes[0].view(np.uint32)[::2, abi.TRI["material"]] = 1
+    o = _load_both(fresh_core, sc, w, h)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", depth)
+    fresh_core.setting("terminalTrace", 1)
+    sc.render_frame(fresh_core)
+    sc.render_frame(o)
+    cg, co = fresh_core.ray_counts(), o.ray_counts()
+    assert np.array_equal(cg, co), (cg[:8], co[:8])
+    ag, ao = fresh_core.accumulator(), o.accumulator()
+    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+    assert rel_l2(ag[..., 3], ao[..., 3]) <= 1e-6
+    fresh_core.setting("terminalTrace", 0)
+    sc.render_frame(fresh_core)
+    a0 = fresh_core.accumulator()
+    assert rel_l2(ag[..., :3], a0[..., :3]) <= 1e-6
+    assert np.array_equal(ag[..., 3], a0[..., 3])
