@@ -30,6 +30,7 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	   frame's per-segment front counts (LH2_SEGS x LH2_SEGCOUNT_STRIDE words) then back counts, zeroed by
 	   the previous frame's camera launch, which zeroes camZero (the other frame's block) for the next */
 	uint32_t* camAlloc; uint32_t* camZero;
+	uint32_t* hvZero; uint32_t hvZeroWords;   /* heavy-first packets: the block this frame records into (TraceArgs::hvWrite) */
 	float chordLo[3], chordHi[3], chordCut;
 };
 #define LH2_CAM_ALLOC_WORDS (2 * 8 * 32)   /* front + back counts of the LH2_SEGS segments */
@@ -131,7 +132,18 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	   terminal); a ray that misses adds its sky sample to acc[pixel] as k_shade_last does (pathT4 / pathQ4:
 	   the path state, wh: pixels per frame) and no hit record is written */
 	const float4* pathT4; const float4* pathQ4; uint32_t wh;
+	/* heavy-first packets (packet kernel, hvWrite non-null): the previous frame's packets that took more
+	   than hvFactor x its mean node steps (hvRead: per-segment counts, step sums, a bit per packet and the
+	   lists of packet bits) are taken first, the rest in order; this frame's are recorded into hvWrite.
+	   A packet bit is segment x hvCap + its batch in the segment; hvTiles: packets of the launch */
+	const uint32_t* hvRead; uint32_t* hvWrite; uint32_t hvCap, hvMaskWords, hvTiles; float hvFactor;
 };
+/* layout of a heavy-packet block: counts, step sums (LH2_SEGS x LH2_SEGCOUNT_STRIDE words each), the bit
+   mask (hvMaskWords), then LH2_SEGS lists of hvCap packet bits; the camera launch zeroes the first
+   LH2_HV_MASK + hvMaskWords words of the block the frame writes */
+#define LH2_HV_CNT 0
+#define LH2_HV_SUM (8 * 32)
+#define LH2_HV_MASK (2 * 8 * 32)
 /* traversal-loop statistics (diagnostic builds with -DLH2_TRACE_STATS; tools/trace_stats.py):
    wave-iterations, active-lane sum, leaf-phase iterations / lanes, walk iterations / lanes,
    triangle-test lane sum, triangle-loop iterations, refill events / lanes, iterations / active-lane

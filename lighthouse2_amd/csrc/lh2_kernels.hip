@@ -177,6 +177,7 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 	const int local = threadIdx.x + blockIdx.x * blockDim.x;
 	if (p.initC) init_counters( p.initC, p.pathCount, p.segStride, p.cursors, p.cursorWords, local, p.camAlloc != nullptr );
 	if (p.camZero && local < LH2_CAM_ALLOC_WORDS) p.camZero[local] = 0;
+	if (p.hvZero && (uint32_t)local < p.hvZeroWords) p.hvZero[local] = 0;
 	if (local >= jobCount) return;
 	const int slot = p.slotBase + local;
 	/* slot -> (sample, tile row, x) -> global jobIndex = x + (y + s * h) * w, as camera.h:48-53 */

@@ -255,6 +255,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "bvhSpatialBudget" )) bvhSpatialBudget = std::min( 4.0f, std::max( 0.0f, value ) );
 	else if (!strcmp( name, "bvh4Collapse" )) bvh4Collapse = value != 0;
 	else if (!strcmp( name, "chordSplit" )) chordSplit = std::max( 0.0f, value );   /* two-ended path segments (longest first); 0: off */
+	else if (!strcmp( name, "packetHeavy" )) packetHeavy = std::max( 0.0f, value );   /* heavy-first primary packets; 0: off */
 	else if (!strcmp( name, "terminalTrace" )) terminalTrace = value != 0;   /* the last terminal bounce's sky samples in its trace launch */
 	else if (!strcmp( name, "pathTail" )) pathTail = std::max( 0, (int)value );   /* bounces from this one in one trace-and-shade launch; 0: off */
 	else if (!strcmp( name, "pathTailBatch" )) pathTailBatch = std::min( 64, std::max( 1, (int)value ) );
@@ -296,7 +297,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "pathTail", (float)pathTail }, { "terminalTrace", (float)terminalTrace }, { "pathTailBatch", (float)pathTailBatch }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
+		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "pathTail", (float)pathTail }, { "terminalTrace", (float)terminalTrace }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "traceFetchMB", traceFetchMB }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "blocksPerCU", (float)blocksPerCU },
@@ -815,6 +816,21 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		cg.clearAcc = restart && G == 1 && !tileChanged ? accumulator.ptr : nullptr;
 		/* two-ended primary segments: whole 8x8 tiles in whole segments only */
 		g.twoEnded = twoEndedPrimary && g.segStride % 64 == 0 && g.count % 64 == 0;
+		/* heavy-first primary packets: this frame reads the block the previous one recorded, and records
+		   into the other one, which the camera launch zeroes (a new layout zeroes both) */
+		const bool heavy = packetHeavy > 0 && tiledRays && UsePackets() && !primeRef;
+		if (heavy)
+		{
+			const uint32_t cap = (g.segStride + 63) / 64, maskWords = (LH2_SEGS * cap + 31) / 32;
+			if (cap != g.hvCap)
+			{
+				g.hvCap = cap, g.hvMaskWords = maskWords, g.hvBlock = LH2_HV_MASK + maskWords + LH2_SEGS * cap, g.hvParity = 0;
+				g.hv.resize( 2 * (size_t)g.hvBlock );
+				CHK_HIP( hipMemsetAsync( g.hv.ptr, 0, sizeof( uint32_t ) * 2 * g.hvBlock, g.st ) );
+			}
+			cg.hvZero = g.hv.ptr + (size_t)(1 - g.hvParity) * g.hvBlock, cg.hvZeroWords = LH2_HV_MASK + g.hvMaskWords;
+		}
+		g.hvOn = heavy;
 		if (g.twoEnded)
 		{
 			cg.camAlloc = g.camAlloc.ptr + (g.camFrame & 1) * LH2_CAM_ALLOC_WORDS;
@@ -865,6 +881,18 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
 			ta.packet = pathLength == 1 && tiledRays && UsePackets() ? PacketMode() : 0;
 			ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
+			if (pathLength == 1 && ta.packet && g.hvOn)
+			{
+				ta.hvRead = g.hv.ptr + (size_t)g.hvParity * g.hvBlock, ta.hvWrite = g.hv.ptr + (size_t)(1 - g.hvParity) * g.hvBlock;
+				ta.hvCap = g.hvCap, ta.hvMaskWords = g.hvMaskWords, ta.hvFactor = packetHeavy;
+				ta.hvTiles = 0;
+				for (int k = 0; k < LH2_SEGS; k++)
+				{
+					const uint32_t lo = (uint32_t)k * g.segStride, n = g.count > lo ? std::min( g.count - lo, g.segStride ) : 0u;
+					ta.hvTiles += (n + 63) / 64;
+				}
+				g.hvParity = 1 - g.hvParity;
+			}
 			ta.hits = g.hits.ptr, ta.gstack = g.gstack.ptr;
 			SetTail( ta, g );
 			if (pathLength == tailL)

@@ -77,6 +77,8 @@ struct PathGroup
 	DevBuf<uint32_t> rayLog;
 	DevBuf<uint32_t> camAlloc;           /* two-ended primary segments: 2 frames x LH2_CAM_ALLOC_WORDS (CameraParams::camAlloc) */
 	uint32_t camFrame = 0;
+	DevBuf<uint32_t> hv;                 /* heavy-first packets: two blocks (TraceArgs::hvRead / hvWrite), the frame parity picks */
+	uint32_t hvCap = 0, hvMaskWords = 0, hvBlock = 0, hvParity = 0;
 	DevBuf<uint4> tailRec;               /* tail hand-off records, one per trace thread (TraceArgs::tailOut) */
 	DevBuf<float2> tailUV;
 	uint32_t* activeLog = nullptr;       /* pinned: extension rays after each bounce (k_counters_next) */
@@ -91,7 +93,8 @@ struct PathGroup
 	int in = 0, pl = 0;
 	bool done = false;
 	bool twoEnded = false;
-	int tailL = 0;                       /* this frame's path-tail launch (pathLength), 0: none */               /* this frame's primary rays are in two-ended segments (CameraParams::camAlloc) */
+	int tailL = 0;                       /* this frame's path-tail launch (pathLength), 0: none */
+	bool hvOn = false;                   /* this frame's primary packets run heavy-first (TraceArgs::hvRead) */               /* this frame's primary rays are in two-ended segments (CameraParams::camAlloc) */
 	hipEvent_t prevStop = nullptr;
 };
 
@@ -272,6 +275,9 @@ private:
 	   slower on config 2 (1.2065 / 1.2053 ms off, 1.2097 / 1.2118 on: the miss lanes' path-state loads and
 	   sky sample stall their waves inside the traversal loop, +20 us, more than the 16 us launch saved): off */
 	int terminalTrace = 0;
+	/* heavy-first primary packets (TraceArgs::hvRead): the packets of the previous frame that took more than
+	   packetHeavy x its mean node steps are taken first; 0: off */
+	float packetHeavy = 2.0f;
 	float PrimaryChordCut( const lh2_ViewPyramid& view );
 	lh2_ViewPyramid cutView{};
 	float cutBox[7] = {}, cutValue = 0;

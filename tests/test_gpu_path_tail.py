@@ -131,3 +131,32 @@ def test_terminal_trace_frame_parity(fresh_core, kind, depth):
     a0 = fresh_core.accumulator()
     assert rel_l2(ag[..., :3], a0[..., :3]) <= 1e-6
     assert np.array_equal(ag[..., 3], a0[..., 3])
+
+
+@pytest.mark.parametrize("factor", [0.5, 2.0])
+def test_heavy_first_packets_frames(fresh_core, factor):
+    """Heavy-first primary packets (setting packetHeavy): from the second frame on, the packets that took
+    more than factor x the previous frame's mean node steps are taken first and skipped in the in-order
+    pass.  Every packet is traced exactly once: frame after frame the ray counts and the accumulator
+    match the oracle; a new target size (a new packet layout) starts over."""
+    w, h = 160, 96
+    sc = scene.config2_scene(n=20000, width=w, height=h, sky=True)
+    o = _load_both(fresh_core, sc, w, h)
+    fresh_core.setting("packetHeavy", factor)
+    assert fresh_core.get_setting("usePackets") == 1
+    for f in range(4):
+        sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
+        sc.render_frame(o, converge=1 if f == 0 else 0)
+        assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), f
+    assert rel_l2(fresh_core.accumulator()[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
+    w2, h2 = 96, 64
+    sc2 = scene.config2_scene(n=20000, width=w2, height=h2, sky=True)
+    fresh_core.set_target(w2, h2, 1)
+    o2 = Oracle()
+    sc2.load_into(o2)
+    o2.set_target(w2, h2, 1)
+    for f in range(3):
+        sc2.render_frame(fresh_core, converge=1 if f == 0 else 0)
+        sc2.render_frame(o2, converge=1 if f == 0 else 0)
+        assert np.array_equal(fresh_core.ray_counts(), o2.ray_counts()), f
+    assert rel_l2(fresh_core.accumulator()[..., :3], o2.accumulator()[..., :3]) <= REL_L2_TOL
