@@ -287,7 +287,11 @@ private:
 	int TraceVersion() const;
 	int unitCoherent = 0;
 	int packetPrimary = -1;              /* wave-uniform packet traversal for 8x8-tiled primary rays (-1: by scene size) */
-	float packetMaxMB = 16.0f;
+	/* auto: packets while the BVH + triangles fit the 256 MB Infinity Cache (a packet's node and triangle
+	   records come through the scalar cache, one at a time: beyond the cache each is a DRAM round trip).
+	   Config 3 (134 MB): primary 0.29 -> 0.24 ms with packets; config 5 (1.4 GB): 5.3 -> 7.8 ms
+	   (profiles/r02zc_ab_packets_configs.txt); round 1's limit was 16 MB */
+	float packetMaxMB = 256.0f;
 	/* packets over the BVH2 (2) or the BVH4 (4): BVH2 0.48 ms, BVH4 0.56 ms on the config-2 primary
 	   rays (r01c): fewer, wider steps do not pay when one node fetch already serves 64 rays */
 	int packetWidth = 2;
