@@ -82,6 +82,7 @@ struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path st
 	   flight when its work queues run dry are short ones (longest-first scheduling); 0: all at the start */
 	float chordLo[3], chordHi[3], chordCut;
 	int advance; BounceAdvance adv;                    /* nonzero: the launch's last block hands off to the next bounce */
+	float shadowCut;                                   /* shadow rays at most this long go to the end of their segment (0: none) */
 	uint32_t shadowStride;                             /* shadow-ray segments: capacity of each */
 	const float4* rayO; const float4* rayD; const float4* T4; const float4* Q4; const uint4* hits;
 	float4* rayOut; float4* rayDOut; float4* T4Out; float4* Q4Out;

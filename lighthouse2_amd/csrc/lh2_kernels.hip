@@ -149,7 +149,7 @@ LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_
 		   primary segments: counted in CameraParams::camAlloc instead) */
 		const uint32_t lo = (uint32_t)i * segStride;
 		c->segPath[0][i * LH2_SEGCOUNT_STRIDE] = twoEnded ? 0u : pathCount > lo ? min( pathCount - lo, segStride ) : 0u;
-		c->segPath[1][i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadow[i * LH2_SEGCOUNT_STRIDE] = 0;
+		c->segPath[1][i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadow[i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadowBack[i * LH2_SEGCOUNT_STRIDE] = 0;
 		c->segBack[0][i * LH2_SEGCOUNT_STRIDE] = 0, c->segBack[1][i * LH2_SEGCOUNT_STRIDE] = 0;
 	}
 	if (i != 0) return;
@@ -1581,10 +1581,15 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 				const uint32_t o = segBase + (late ? p.segStride - 1u - eb : es);
 				p.rayOut[o] = eO; p.rayDOut[o] = eD; p.T4Out[o] = eT; p.Q4Out[o] = eQ;
 			}
-			const uint32_t ss = wave_alloc( doShadow, &p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE] );
+			/* shadow rays: the short ones (ShadeParams::shadowCut) from the segment's end, so the shadow launch
+			   takes the long ones first (the host checks that the two ends did not meet) */
+			const bool sLate = doShadow && sD.w <= p.shadowCut;
+			const uint32_t ss = wave_alloc( doShadow && !sLate, &p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE] );
+			const uint32_t sb = wave_alloc( sLate, &p.counters->segShadowBack[seg * LH2_SEGCOUNT_STRIDE] );
 			if (doShadow)
 			{
-				if (ss < p.shadowStride) { const uint32_t o = seg * p.shadowStride + ss; p.shO[o] = sO; p.shD[o] = sD; p.shP[o] = sP; }
+				const uint32_t q = sLate ? sb : ss;
+				if (q < p.shadowStride) { const uint32_t o = seg * p.shadowStride + (sLate ? p.shadowStride - 1u - sb : ss); p.shO[o] = sO; p.shD[o] = sD; p.shP[o] = sP; }
 				else atomicOr( &p.counters->shadowOverflow, 1u );
 			}
 		}
@@ -1846,8 +1851,8 @@ LH2_DEV void advance_bounce( Counters* c, const BounceAdvance& a, const int path
 		ext += __hip_atomic_load( &a.segNext[k * LH2_SEGCOUNT_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
 		ext += __hip_atomic_load( &a.segNextBack[k * LH2_SEGCOUNT_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
 		a.segRetire[k * LH2_SEGCOUNT_STRIDE] = 0, a.segRetireBack[k * LH2_SEGCOUNT_STRIDE] = 0;
-		sh += c->segShadow[k * LH2_SEGCOUNT_STRIDE];
-		if (resetShadow) c->segShadow[k * LH2_SEGCOUNT_STRIDE] = 0;
+		sh += c->segShadow[k * LH2_SEGCOUNT_STRIDE] + c->segShadowBack[k * LH2_SEGCOUNT_STRIDE];
+		if (resetShadow) c->segShadow[k * LH2_SEGCOUNT_STRIDE] = 0, c->segShadowBack[k * LH2_SEGCOUNT_STRIDE] = 0;
 	}
 	a.rayCountLog[pathLength] = ext;     /* rays traced at pathLength + 1 */
 	if (a.zeroLog) for (int k = pathLength + 1; k <= LH2_MAX_BOUNCES; k++) a.rayCountLog[k] = 0;

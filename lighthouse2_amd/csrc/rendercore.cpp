@@ -255,6 +255,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "bvhSpatialBudget" )) bvhSpatialBudget = std::min( 4.0f, std::max( 0.0f, value ) );
 	else if (!strcmp( name, "bvh4Collapse" )) bvh4Collapse = value != 0;
 	else if (!strcmp( name, "chordSplit" )) chordSplit = std::max( 0.0f, value );   /* two-ended path segments (longest first); 0: off */
+	else if (!strcmp( name, "chordSplitShadow" )) chordSplitShadow = std::max( 0.0f, value );   /* two-ended shadow segments; 0: off */
 	else if (!strcmp( name, "packetHeavy" )) packetHeavy = std::max( 0.0f, value );   /* heavy-first primary packets; 0: off */
 	else if (!strcmp( name, "terminalTrace" )) terminalTrace = value != 0;   /* the last terminal bounce's sky samples in its trace launch */
 	else if (!strcmp( name, "pathTail" )) pathTail = std::max( 0, (int)value );   /* bounces from this one in one trace-and-shade launch; 0: off */
@@ -297,7 +298,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "pathTail", (float)pathTail }, { "terminalTrace", (float)terminalTrace }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
+		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "pathTail", (float)pathTail }, { "terminalTrace", (float)terminalTrace }, { "packetHeavy", packetHeavy }, { "chordSplitShadow", chordSplitShadow }, { "pathTailBatch", (float)pathTailBatch }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "traceFetchMB", traceFetchMB }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "blocksPerCU", (float)blocksPerCU },
@@ -849,6 +850,11 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	frameShadows = shadows;
 	const int splitL = (shadows && !primeRef && G == 1 && shadowSplit > 0 && shadowSplit < maxPL) ? shadowSplit : 0;
 	frameSplit = false;
+	/* two-ended shadow segments (setting "chordSplitShadow"): shadow rays shorter than it x the scene's
+	   extent are traced last; not with the shadow split or PrimeRef's per-bounce shadow launches */
+	float shadowCut = -3.0e38f;   /* off: no shadow ray is that short */
+	if (!splitL && !primeRef && chordSplitShadow > 0)
+		shadowCut = chordSplitShadow * std::max( std::max( sceneHi[0] - sceneLo[0], sceneHi[1] - sceneLo[1] ), sceneHi[2] - sceneLo[2] );
 	/* the path tail (setting "pathTail"): bounces pathTail .. maxPL in one launch of k_trace_path4d */
 	const int tailL = (!primeRef && G == 1 && !splitL && pathTail >= 2 && pathTail <= maxPL && TraceVersion() == 7 && dNodes4.ptr) ? pathTail : 0;
 	/* the bounce loop, the groups' launches interleaved */
@@ -910,6 +916,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				sp.spreadAngle = view.spreadAngle;
 				sp.adv.rayCountLog = g.rayLog.ptr;
 				ta.shadeBatch = (uint32_t)pathTailBatch;
+				sp.shadowCut = shadowCut;
 				lh2_launch_trace_path( &sd, &ta, &sp, PathGrid(), { nullptr, g.evTrace[pathLength] }, g.st );
 				g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
 				g.tailL = pathLength;   /* no shade interval of its own (Synchronize) */
@@ -947,6 +954,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, g.rayLog.ptr, g.activeLog, split ? shadowSnap.ptr : nullptr,
 				split ? g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr, pathLength + 1 == tailL };
 			sp.advance = pathLength < maxPL && !primeRef;
+			sp.shadowCut = shadowCut;
 			sp.adv = adv;
 			sp.rayO = g.rayO[g.in].ptr, sp.rayD = g.rayD[g.in].ptr, sp.T4 = g.T4[g.in].ptr, sp.Q4 = g.Q4[g.in].ptr, sp.hits = g.hits.ptr;
 			sp.rayOut = g.rayO[1 - g.in].ptr, sp.rayDOut = g.rayD[1 - g.in].ptr, sp.T4Out = g.T4[1 - g.in].ptr, sp.Q4Out = g.Q4[1 - g.in].ptr;
@@ -1022,6 +1030,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			TraceArgs ta{};
 			ta.version = TraceVersion();
 			ta.rayO = g.shO.ptr, ta.rayD = g.shD.ptr, ta.segCounts = g.counters.ptr->segShadow, ta.segStride = g.shadowStride;
+			ta.segBack = g.counters.ptr->segShadowBack;
 			ta.cursor = g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 			ta.mask = g.shMask.ptr, ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = g.gstack.ptr;
 			ta.packet = packetShadow ? PacketMode() : 0;
@@ -1132,7 +1141,7 @@ int RenderCore::TileRows() const
 static uint32_t QueuedShadowRays( const Counters& c )
 {
 	uint32_t n = 0;
-	for (int k = 0; k < LH2_SEGS; k++) n += c.segShadow[k * LH2_SEGCOUNT_STRIDE];
+	for (int k = 0; k < LH2_SEGS; k++) n += c.segShadow[k * LH2_SEGCOUNT_STRIDE] + c.segShadowBack[k * LH2_SEGCOUNT_STRIDE];
 	return n;
 }
 
@@ -1142,7 +1151,13 @@ void RenderCore::Synchronize()
 	if (statsPending)
 	{
 		statsPending = false;
-		for (int gi = 0; gi < frameGroups; gi++) if (hostStats->counters[gi].shadowOverflow) FatalError( "shadow ray buffer overflow" );
+		for (int gi = 0; gi < frameGroups; gi++)
+		{
+			const Counters& cn = hostStats->counters[gi];
+			bool full = cn.shadowOverflow != 0;   /* a segment's two ends met: same failure */
+			for (int k = 0; k < LH2_SEGS; k++) full = full || cn.segShadow[k * LH2_SEGCOUNT_STRIDE] + cn.segShadowBack[k * LH2_SEGCOUNT_STRIDE] > grp[gi].shadowStride;
+			if (full) FatalError( "shadow ray buffer overflow" );
+		}
 		if (hostStats->sceneError) FatalError( "BVH depth exceeds the traversal stack (%d levels): frame skipped", LH2_STACK_TOTAL );
 		uint32_t rc[LH2_MAX_BOUNCES + 1] = {};   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
 		for (int gi = 0; gi < frameGroups; gi++) for (int L = 0; L <= LH2_MAX_BOUNCES; L++) rc[L] += hostStats->rayCount[gi][L];

@@ -278,6 +278,9 @@ private:
 	/* heavy-first primary packets (TraceArgs::hvRead): the packets of the previous frame that took more than
 	   packetHeavy x its mean node steps are taken first; 0: off */
 	float packetHeavy = 2.0f;
+	/* two-ended shadow segments: shadow rays shorter than chordSplitShadow x the scene's largest extent are
+	   written from their segment's end, so the shadow launch takes the long ones first; 0: off */
+	float chordSplitShadow = 0.0f;   /* measured no faster on config 3 (0.61 ms either way, profiles/r02zd_ab_shadow_chord.txt): off */
 	float PrimaryChordCut( const lh2_ViewPyramid& view );
 	lh2_ViewPyramid cutView{};
 	float cutBox[7] = {}, cutValue = 0;

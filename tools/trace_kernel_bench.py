@@ -145,6 +145,13 @@ def main():
             octant = ((bd[:, 0] < 0).astype(np.int64) << 2) | ((bd[:, 1] < 0).astype(np.int64) << 1) | (bd[:, 2] < 0)
             order = np.argsort((octant << 30) | m, kind="stable")
             sets["bounce_sorted"] = (np.ascontiguousarray(bo[order]), np.ascontiguousarray(bd[order]))
+            # direction octant only (stable: in-frame order within an octant): globally, and per segment
+            order = np.argsort(octant, kind="stable")
+            sets["bounce_oct"] = (np.ascontiguousarray(bo[order]), np.ascontiguousarray(bd[order]))
+            n = len(bo)
+            seg = (n + 7) // 8
+            order = np.concatenate([c * seg + np.argsort(octant[c * seg:min(n, (c + 1) * seg)], kind="stable") for c in range(8)])
+            sets["bounce_octseg"] = (np.ascontiguousarray(bo[order]), np.ascontiguousarray(bd[order]))
             if args.set == "bounce_sorted":
                 del sets["bounce"]
     if args.sweep:
