@@ -247,6 +247,10 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* traversal: test parked BLAS leaves once this many lanes of a wave hold one (0 = every step) */
 	else if (!strcmp( name, "leafBatch" )) leafBatch = std::min( 64, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "leafBatchPrimary" )) leafBatchPrimary = std::min( 64, std::max( 0, (int)value ) );
+	/* the shadow launches' own loop (5, 6, 7 over the BVH4; 0: traceVersion), leaf batch (-1: leafBatch) and refill (0: refill) */
+	else if (!strcmp( name, "shadowVersion" )) shadowVersion = (int)value >= 5 && (int)value <= 7 ? (int)value : 0;
+	else if (!strcmp( name, "leafBatchShadow" )) leafBatchShadow = std::min( 64, std::max( -1, (int)value ) );
+	else if (!strcmp( name, "refillShadow" )) refillShadow = std::min( 64, std::max( 0, (int)value ) );
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
@@ -297,6 +301,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "epsilon", geometryEpsilon }, { "clampValue", clampValue }, { "maxPathLength", (float)maxPathLength },
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
+		{ "shadowVersion", (float)ShadowVersion() }, { "leafBatchShadow", (float)ShadowLeafBatch() }, { "refillShadow", (float)ShadowRefill() },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "pathTail", (float)pathTail }, { "terminalTrace", (float)terminalTrace }, { "packetHeavy", packetHeavy }, { "chordSplitShadow", chordSplitShadow }, { "pathTailBatch", (float)pathTailBatch }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
@@ -974,10 +979,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				/* RenderCore_PrimeRef traces the shadow rays of every bounce right after it
 				   (rendercore.cpp connect step), fused with finalizeConnections */
 				TraceArgs ts{};
-				ts.version = TraceVersion();
+				ts.version = ShadowVersion();
 				ts.rayO = g.shO.ptr, ts.rayD = g.shD.ptr, ts.segCounts = c->segShadow, ts.segStride = g.shadowStride;
 				ts.cursor = g.cursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
-				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
+				ts.refill = ShadowRefill(), ts.leafBatch = ShadowLeafBatch();
 				ts.mask = g.shMask.ptr, ts.potentials = g.shP.ptr, ts.acc = accumulator.ptr, ts.gstack = g.gstack.ptr;
 				ts.packet = packetShadow ? PacketMode() : 0;
 				SetTail( ts, g );
@@ -997,9 +1002,9 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				   shadow launch's work queues start behind them (advance_bounce) */
 				CHK_HIP( hipStreamWaitEvent( sideStream, g.countReady[pathLength], 0 ) );
 				TraceArgs ta{};
-				ta.version = TraceVersion();
+				ta.version = ShadowVersion();
 				ta.rayO = g.shO.ptr, ta.rayD = g.shD.ptr, ta.segCounts = shadowSnap.ptr, ta.segStride = g.shadowStride;
-				ta.cursor = g.cursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+				ta.cursor = g.cursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS, ta.refill = ShadowRefill(), ta.leafBatch = ShadowLeafBatch();
 				ta.mask = g.shMask.ptr, ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = sideStack.ptr;
 				ta.packet = packetShadow ? PacketMode() : 0;
 				lh2_launch_trace_any( &sd, &ta, grid, 1, { evSideStart, evSideStop }, sideStream );
@@ -1028,10 +1033,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		if (!primeRef && shadows)
 		{
 			TraceArgs ta{};
-			ta.version = TraceVersion();
+			ta.version = ShadowVersion();
 			ta.rayO = g.shO.ptr, ta.rayD = g.shD.ptr, ta.segCounts = g.counters.ptr->segShadow, ta.segStride = g.shadowStride;
 			ta.segBack = g.counters.ptr->segShadowBack;
-			ta.cursor = g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+			ta.cursor = g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = ShadowRefill(), ta.leafBatch = ShadowLeafBatch();
 			ta.mask = g.shMask.ptr, ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = g.gstack.ptr;
 			ta.packet = packetShadow ? PacketMode() : 0;
 			SetTail( ta, g );

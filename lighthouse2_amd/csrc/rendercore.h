@@ -251,6 +251,11 @@ private:
 	   1.89 ms vs 1.94 for BVH2 with 2-triangle leaves); config 3 (room) runs 4 % faster with
 	   bvhMaxLeaf 2 / leafBatch 16, config 5 2 % slower */
 	int refillPrimary = 48, refillOther = 48, leafBatch = 6, leafBatchPrimary = 8;   /* leafBatch: traceVersion 7 leaf batches (r02y) */
+	/* the shadow (any-hit) launches: traversal loop, leaf batch and refill of their own (0 / -1 / 0: as the closest-hit launches) */
+	int shadowVersion = 0, leafBatchShadow = -1, refillShadow = 0;
+	int ShadowVersion() const { return shadowVersion && bvh4 ? shadowVersion : TraceVersion(); }
+	uint32_t ShadowLeafBatch() const { return (uint32_t)(leafBatchShadow >= 0 ? leafBatchShadow : leafBatch); }
+	uint32_t ShadowRefill() const { return (uint32_t)(refillShadow ? refillShadow : refillOther); }
 	int bvhMaxLeaf = 1;
 	int bvhSweep = 0;                    /* exact SAH sweep below this node size (setting "bvhSweep") */
 	float bvhSpatial = 1e-5f;            /* spatial splits (SBVH): overlap threshold x root area; 0 = off */
