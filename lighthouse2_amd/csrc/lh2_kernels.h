@@ -138,6 +138,13 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	   lists of packet bits) are taken first, the rest in order; this frame's are recorded into hvWrite.
 	   A packet bit is segment x hvCap + its batch in the segment; hvTiles: packets of the launch */
 	const uint32_t* hvRead; uint32_t* hvWrite; uint32_t hvCap, hvMaskWords, hvTiles; float hvFactor;
+	/* shadow backfill (closest-hit launches, traceVersion 5-7, bfO non-null): once this launch's own queues
+	   are dry and while any of its waves still walks a closest-hit ray, idle lanes take shadow rays queued
+	   by earlier bounces - the stream bfO / bfD, front counts bfCounts (stable during the launch),
+	   bfStride per segment - from the final shadow launch's work-queue heads bfCursor, claimed with a
+	   bounded compare-and-swap so the final launch continues exactly behind them; an unoccluded one adds
+	   its potential (potentials, acc) as that launch would */
+	const float4* bfO; const float4* bfD; const uint32_t* bfCounts; uint32_t bfStride; uint32_t* bfCursor;
 };
 /* layout of a heavy-packet block: counts, step sums (LH2_SEGS x LH2_SEGCOUNT_STRIDE words each), the bit
    mask (hvMaskWords), then LH2_SEGS lists of hvCap packet bits; the camera launch zeroes the first
@@ -179,7 +186,10 @@ void lh2_launch_trace_term( const SceneDev* s, const TraceArgs* a, int grid, Lau
 int lh2_path_blocks_per_cu( void );
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
 void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
-void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st );
+/* the rows of a band partition (k_pack_rows' mapping); rows 0: every pixel */
+struct RowMap { int w, y0, band, bandStride, rows; };
+void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st,
+	const RowMap* rm = nullptr );
 }
 
 /* Segmented ray streams.  A stream of paths or rays lives in LH2_SEGS segments of one buffer:

@@ -1886,7 +1886,10 @@ __global__ void k_counters_next( Counters* c, const BounceAdvance a, int pathLen
 {
 	if (threadIdx.x == 0) advance_bounce( c, a, pathLength, resetShadow );
 }
-__global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale, const FrameStatsDev fs )
+/* rm.rows > 0: only the rows a tile owns (a rank's bands, the k_pack_rows mapping): the other rows are
+   other ranks' and are finalized where the frame is gathered */
+__global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale, const FrameStatsDev fs,
+	const RowMap rm )
 {
 	const int i = threadIdx.x + blockIdx.x * blockDim.x;
 	if (blockIdx.x == 0 && fs.groups > 0)
@@ -1905,8 +1908,14 @@ __global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__
 		if (threadIdx.x == 0) __hip_atomic_store( fs.hostSceneError, *fs.sceneError, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
 	}
 	if (i >= n) return;
-	const float4 a = acc[i];
-	out[i] = make_float4( a.x * scale, a.y * scale, a.z * scale, a.w * scale );
+	int p = i;
+	if (rm.rows > 0)
+	{
+		const int lr = i / rm.w, x = i % rm.w;
+		p = (rm.y0 + (lr / rm.band) * rm.bandStride + lr % rm.band) * rm.w + x;
+	}
+	const float4 a = acc[p];
+	out[p] = make_float4( a.x * scale, a.y * scale, a.z * scale, a.w * scale );
 }
 
 /* copy the rows this tile owns (local row order) out of the full-frame accumulator, for the
@@ -1980,6 +1989,7 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
 		const LaunchEvents e1 = { ev.start, tail ? nullptr : ev.stop }, e2 = { nullptr, ev.stop };
 		if (a->version == 5 && s->nodes4) LH2_LAUNCH( k_trace_closest4d<1>, grid, 256, st, ev, *s, *a );   /* lh2_trace4d.inc */
 		else if (a->version == 6 && s->nodes4) LH2_LAUNCH( k_trace_closest4d<0>, grid, 256, st, ev, *s, *a );
+		else if (a->version == 7 && s->nodes4 && a->bfO) LH2_LAUNCH( k_trace_closest4d_bf<2>, grid, 256, st, ev, *s, *a );
 		else if (a->version == 7 && s->nodes4) LH2_LAUNCH( k_trace_closest4d<2>, grid, 256, st, ev, *s, *a );
 		else if (a->version == 4 && s->nodes4)
 		{
@@ -2104,9 +2114,11 @@ void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int 
 	if (rows * w <= 0) { if (ev.stop) (void)hipEventRecord( ev.stop, st ); return; }
 	LH2_LAUNCH( k_unpack_rows, (rows * w + 255) / 256, 256, st, ev, src, acc, w, y0, band, bandStride, rows );
 }
-void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st )
+void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st, const RowMap* rm )
 {
 	const FrameStatsDev none{};
-	LH2_LAUNCH( k_finalize, n > 0 ? (n + 255) / 256 : 1, 256, st, ev, acc, out, n, scale, fs ? *fs : none );
+	const RowMap all{};
+	if (rm && rm->rows > 0) n = rm->rows * rm->w;
+	LH2_LAUNCH( k_finalize, n > 0 ? (n + 255) / 256 : 1, 256, st, ev, acc, out, n, scale, fs ? *fs : none, rm ? *rm : all );
 }
 }

@@ -251,6 +251,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "shadowVersion" )) shadowVersion = (int)value >= 5 && (int)value <= 7 ? (int)value : 0;
 	else if (!strcmp( name, "leafBatchShadow" )) leafBatchShadow = std::min( 64, std::max( -1, (int)value ) );
 	else if (!strcmp( name, "refillShadow" )) refillShadow = std::min( 64, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "shadowBackfill" )) shadowBackfill = value != 0;   /* shadow rays in the closest-hit launches' tails */
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
@@ -301,7 +302,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "epsilon", geometryEpsilon }, { "clampValue", clampValue }, { "maxPathLength", (float)maxPathLength },
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
-		{ "shadowVersion", (float)ShadowVersion() }, { "leafBatchShadow", (float)ShadowLeafBatch() }, { "refillShadow", (float)ShadowRefill() },
+		{ "shadowVersion", (float)ShadowVersion() }, { "leafBatchShadow", (float)ShadowLeafBatch() }, { "refillShadow", (float)ShadowRefill() }, { "shadowBackfill", (float)shadowBackfill },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "pathTail", (float)pathTail }, { "terminalTrace", (float)terminalTrace }, { "packetHeavy", packetHeavy }, { "chordSplitShadow", chordSplitShadow }, { "pathTailBatch", (float)pathTailBatch }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
@@ -941,6 +942,16 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				g.done = true;
 				continue;
 			}
+			/* shadow backfill: the shadow rays of the bounces before this one (their counts no longer change
+			   during this launch) are the final shadow launch's work; this launch's idle lanes take them in its
+			   tail, from that launch's work-queue heads (one-ended shadow segments only) */
+			if (shadowBackfill && shadows && !primeRef && !splitL && !ta.packet && pathLength >= 2 && TraceVersion() == 7 &&
+				dNodes4.ptr && !(shadowCut > 0.0f))
+			{
+				ta.bfO = g.shO.ptr, ta.bfD = g.shD.ptr, ta.bfCounts = c->segShadow, ta.bfStride = g.shadowStride;
+				ta.bfCursor = g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS;
+				ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr;
+			}
 			lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : grid, { nullptr, g.evTrace[pathLength] }, g.st );
 			g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
 			ShadeParams sp{};
@@ -1060,7 +1071,11 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		fs.hostCounters[gi] = &hostStats->counters[gi], fs.hostRayCount[gi] = hostStats->rayCount[gi] + 1;
 	}
 	fs.sceneError = dSceneError.ptr, fs.hostSceneError = &hostStats->sceneError;
-	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, &fs, { nullptr, evFrame[1] }, stream );
+	/* a tile finalizes its own rows only (a rank of the band partition: the gathered frame is finalized
+	   where it is assembled, MultiDevice / FinalizeFrame) */
+	RowMap rm{};
+	if (tileRows < scrheight) rm = { scrwidth, cp.y0, cp.band, cp.bandStride, tileRows };
+	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, &fs, { nullptr, evFrame[1] }, stream, &rm );
 	if (glResource)
 	{
 		hipArray_t arr = nullptr;

@@ -181,6 +181,7 @@ def test_band_partition_matches_full_frame(core):
     core.set_tile(0, -1)
     sc.render_frame(core)
     full = core.accumulator()
+    full_frame = core.frame()
     tiles = []
     for r in range(world):
         core.set_target(w, h, 1)
@@ -188,6 +189,9 @@ def test_band_partition_matches_full_frame(core):
         sc.render_frame(core)
         rows = core.tile_rows()
         assert rows == len(parallel.band_rows(r, world, h))
+        # the rank finalizes its own rows (k_finalize's row map): they equal the untiled frame's
+        own = np.asarray(parallel.band_rows(r, world, h))
+        assert rel_l2(core.frame()[own][..., :3], full_frame[own][..., :3]) <= 1e-6
         t = torch.empty((rows, w, 4), dtype=torch.float32, device="cuda")
         core.pack_tile(t.data_ptr())
         tiles.append(t.cpu().numpy())
