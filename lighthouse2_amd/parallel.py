@@ -13,7 +13,7 @@ of sky and geometry.  The only collective is the gather of the finished accumula
 tile the core packs its rows into, rank 0's receive block and frame, and the row map that turns
 the received blocks into the frame with one index_select.  A frame then costs the pack, one
 collective and (rank 0) one gather kernel, with no allocation and no host-to-device index upload.
-The in-process multi-device mode of the core itself (setting "deviceCount", csrc/multicore.cpp) is
+The in-process multi-device mode of the core itself (setting "deviceCount", csrc/multidevice.cpp) is
 the same partition with xGMI peer copies instead of a collective.
 """
 from __future__ import annotations
