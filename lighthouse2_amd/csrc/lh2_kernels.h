@@ -17,6 +17,7 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	   y0 + (lr / band) * bandStride + lr % band  (contiguous tile: band = rows) */
 	int y0, band, bandStride, tileRows;
 	int tiled;   /* store rays in 8x8 pixel blocks per wave (coherent traversal); 0 = row-major */
+	int spp;     /* > 1 (tiled, one launch for every slot): the samples of an 8x8 block in consecutive waves */
 	int slotBase;  /* this launch writes slots [slotBase, slotBase + jobCount) of the tile, at 0.. (path groups) */
 	int primeRef;  /* RenderCore_PrimeRef camera: uniform random numbers, no distortion (camera.h:57-60) */
 	/* folded into the camera launch (no launches of their own): the frame's counter / work-queue

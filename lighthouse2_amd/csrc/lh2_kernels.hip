@@ -179,10 +179,21 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 	if (p.camZero && local < LH2_CAM_ALLOC_WORDS) p.camZero[local] = 0;
 	if (p.hvZero && (uint32_t)local < p.hvZeroWords) p.hvZero[local] = 0;
 	if (local >= jobCount) return;
-	const int slot = p.slotBase + local;
+	int slot = p.slotBase + local;
 	/* slot -> (sample, tile row, x) -> global jobIndex = x + (y + s * h) * w, as camera.h:48-53 */
 	const uint32_t w = (uint32_t)p.w, h = (uint32_t)p.h;
 	const uint32_t tilePix = (uint32_t)p.tileRows * w;
+	if (p.spp > 1 && p.tiled && (w & 7u) == 0)
+	{
+		/* storage order only: the spp samples of an 8x8 pixel block go to consecutive waves (sample-major
+		   order puts them a whole frame of rays apart), so they walk the tree while its nodes are still in
+		   the XCD's L2; the remainder rows (tileRows % 8) follow, sample by sample */
+		const uint32_t spp = (uint32_t)p.spp, nFull = ((uint32_t)p.tileRows / 8u) * (w / 8u), full = nFull * 64u * spp;
+		uint32_t sm, r;
+		if ((uint32_t)slot < full) { const uint32_t wv = (uint32_t)slot >> 6; sm = wv % spp, r = (wv / spp) * 64u + ((uint32_t)slot & 63u); }
+		else { const uint32_t q = (uint32_t)slot - full, rem = tilePix - nFull * 64u; sm = q / rem, r = nFull * 64u + q % rem; }
+		slot = (int)(sm * tilePix + r);
+	}
 	const uint32_t s = (uint32_t)slot / tilePix, r = (uint32_t)slot % tilePix;
 	uint32_t lr = r / w, x = r % w;
 	if (p.tiled && (w & 7u) == 0)

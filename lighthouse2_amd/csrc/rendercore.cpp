@@ -251,6 +251,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "shadowVersion" )) shadowVersion = (int)value >= 5 && (int)value <= 7 ? (int)value : 0;
 	else if (!strcmp( name, "leafBatchShadow" )) leafBatchShadow = std::min( 64, std::max( -1, (int)value ) );
 	else if (!strcmp( name, "refillShadow" )) refillShadow = std::min( 64, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "sampleInterleave" )) sampleInterleave = value != 0;   /* the samples of an 8x8 block in consecutive waves */
 	else if (!strcmp( name, "shadowBackfill" )) shadowBackfill = value != 0;   /* shadow rays in the closest-hit launches' tails */
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
@@ -302,7 +303,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "epsilon", geometryEpsilon }, { "clampValue", clampValue }, { "maxPathLength", (float)maxPathLength },
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
-		{ "shadowVersion", (float)ShadowVersion() }, { "leafBatchShadow", (float)ShadowLeafBatch() }, { "refillShadow", (float)ShadowRefill() }, { "shadowBackfill", (float)shadowBackfill },
+		{ "shadowVersion", (float)ShadowVersion() }, { "leafBatchShadow", (float)ShadowLeafBatch() }, { "refillShadow", (float)ShadowRefill() }, { "shadowBackfill", (float)shadowBackfill }, { "sampleInterleave", (float)sampleInterleave },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "pathTail", (float)pathTail }, { "terminalTrace", (float)terminalTrace }, { "packetHeavy", packetHeavy }, { "chordSplitShadow", chordSplitShadow }, { "pathTailBatch", (float)pathTailBatch }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
@@ -790,6 +791,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	cp.y0 = std::max( 0, tileY0 ), cp.tileRows = tileRows;
 	cp.band = tileBand > 0 ? tileBand : std::max( 1, tileRows ), cp.bandStride = tileBand > 0 ? tileStride : std::max( 1, tileRows );
 	cp.tiled = tiledRays;
+	cp.spp = G == 1 && sampleInterleave ? scrspp : 0;
 	cp.primeRef = primeRef;
 	const bool twoEndedPrimary = chordSplitPrimary > 0 && tiledRays && !primeRef && scrwidth % 8 == 0 && tileRows % 8 == 0;
 	const float primaryCut = twoEndedPrimary ? PrimaryChordCut( view ) : 0.0f;

@@ -253,6 +253,7 @@ private:
 	int refillPrimary = 48, refillOther = 48, leafBatch = 6, leafBatchPrimary = 8;   /* leafBatch: traceVersion 7 leaf batches (r02y) */
 	/* the shadow (any-hit) launches: traversal loop, leaf batch and refill of their own (0 / -1 / 0: as the closest-hit launches) */
 	int shadowVersion = 0, leafBatchShadow = -1, refillShadow = 0;
+	int sampleInterleave = 0;            /* spp > 1: the samples of an 8x8 pixel block in consecutive waves (k_camera storage order); config 5 no faster: off (profiles/r02zl_ab_sample_interleave.txt) */
 	int shadowBackfill = 0;              /* closest-hit launches take queued shadow rays in their tail (TraceArgs::bfO); measured slower: off (profiles/r02zg_ab_shadow_backfill.txt) */
 	int ShadowVersion() const { return shadowVersion && bvh4 ? shadowVersion : TraceVersion(); }
 	uint32_t ShadowLeafBatch() const { return (uint32_t)(leafBatchShadow >= 0 ? leafBatchShadow : leafBatch); }
