@@ -213,6 +213,15 @@ void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, co
 #define LH2_MAX_BOUNCES 64                                   /* RenderCore_PrimeRef MAXPATHLENGTH (core_settings.h:25) */
 #define LH2_CURSOR_SLOTS (2 * LH2_MAX_BOUNCES + 4)           /* launches per frame: [L] bounce L, [64 + L] shadow after bounce L, [130] shadow */
 #define LH2_SHADOW_SLOT (2 * LH2_MAX_BOUNCES + 2)
+/* the BVH4 loops' LDS stack (lh2_trace4d.inc): LH2_STACK_TCULL 1 keeps each entry's entry distance (16 bits) beside
+   it, in 12 LDS entries instead of 16 (the same LDS per block), and closest-hit walks pop the entries beyond their
+   closest hit without a node step; the global part is sized for the smaller one.  Parity-exact, measured no faster
+   (config-2 bounce 0.579 vs 0.576 ms, profiles/r02zm_ab_stack_tcull.txt): off */
+#ifndef LH2_STACK_TCULL
+#define LH2_STACK_TCULL 0
+#endif
+#define LH2_STACK4_LDS (LH2_STACK_TCULL ? 12 : LH2_STACK_LDS)
+#define LH2_STACK4_LDS_INTS (LH2_STACK4_LDS * 256 + (LH2_STACK_TCULL ? LH2_STACK4_LDS * 128 : 0))
 #ifndef LH2_STACK_LDS
 #define LH2_STACK_LDS 16
 #endif

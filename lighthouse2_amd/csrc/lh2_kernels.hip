@@ -1644,7 +1644,7 @@ __global__ __launch_bounds__( 256 ) void k_shade_last( const SceneDev s, const S
 template <bool NL>
 __global__ __launch_bounds__( 256, LH2_PATH_MINWAVES ) void k_trace_path4d( const SceneDev s, const TraceArgs a, const ShadeParams p )
 {
-	__shared__ int lstack[STACK_LDS * 256];
+	__shared__ int lstack[LH2_STACK4_LDS_INTS];
 	__shared__ int lrefs[4 * 256];
 	trace_stream4d<3, 2, NL>( s, a, lstack + threadIdx.x, lrefs + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &p );
 }

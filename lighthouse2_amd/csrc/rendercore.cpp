@@ -226,7 +226,7 @@ void RenderCore::EnsureGroup( PathGroup& g, uint32_t paths )
 
 void RenderCore::EnsureStack( PathGroup& g )
 {
-	const size_t need = (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256;
+	const size_t need = (size_t)(LH2_STACK_TOTAL - std::min( LH2_STACK_LDS, LH2_STACK4_LDS )) * TraceGrid() * 256;
 	if (g.gstack.count < need) g.gstack.resize( need );
 	if (&g == &grp[0] && sideStack.count < need) sideStack.resize( need );
 }
