@@ -2071,6 +2071,14 @@ int lh2_packet_blocks_per_cu( void )
 	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_closest_packet<2>, 256, 0 ) != hipSuccess) n = 4;
 	return n;
 }
+/* the any-hit BVH4 kernels' own occupancy (16-entry LDS stack, <= 64 VGPRs: 8 blocks per CU where the closest-hit
+   loops hold 7) */
+int lh2_any4d_blocks_per_cu( void )
+{
+	int n = 0;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_any4d<1, 2>, 256, 0 ) != hipSuccess || n < 1) n = 4;
+	return n;
+}
 int lh2_trace_blocks_per_cu( void )
 {
 	int n1 = 0, n2 = 0;

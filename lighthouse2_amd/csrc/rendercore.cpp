@@ -108,6 +108,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	blocksPerCU = maxBlocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
 	packetBlocksPerCU = std::max( 1, std::min( 8, lh2_packet_blocks_per_cu() ) );
 	pathBlocksPerCU = std::max( 1, std::min( 8, lh2_path_blocks_per_cu() ) );
+	anyBlocksPerCU = std::max( 1, std::min( 8, lh2_any4d_blocks_per_cu() ) );
 	for (int gi = 0; gi < LH2_MAX_GROUPS; gi++)
 	{
 		PathGroup& g = grp[gi];
@@ -226,7 +227,7 @@ void RenderCore::EnsureGroup( PathGroup& g, uint32_t paths )
 
 void RenderCore::EnsureStack( PathGroup& g )
 {
-	const size_t need = (size_t)(LH2_STACK_TOTAL - std::min( LH2_STACK_LDS, LH2_STACK4_LDS )) * TraceGrid() * 256;
+	const size_t need = (size_t)(LH2_STACK_TOTAL - std::min( LH2_STACK_LDS, LH2_STACK4_LDS )) * std::max( TraceGrid(), ShadowGrid() ) * 256;
 	if (g.gstack.count < need) g.gstack.resize( need );
 	if (&g == &grp[0] && sideStack.count < need) sideStack.resize( need );
 }
@@ -252,6 +253,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "leafBatchShadow" )) leafBatchShadow = std::min( 64, std::max( -1, (int)value ) );
 	else if (!strcmp( name, "refillShadow" )) refillShadow = std::min( 64, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "sampleInterleave" )) sampleInterleave = value != 0;   /* the samples of an 8x8 block in consecutive waves */
+	else if (!strcmp( name, "shadowGridOwn" )) { shadowGridOwn = value != 0; if (scrwidth) EnsureBuffers(); }   /* final shadow launch at the any-hit kernels' occupancy */
 	else if (!strcmp( name, "shadowBackfill" )) shadowBackfill = value != 0;   /* shadow rays in the closest-hit launches' tails */
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
@@ -303,7 +305,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "epsilon", geometryEpsilon }, { "clampValue", clampValue }, { "maxPathLength", (float)maxPathLength },
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
-		{ "shadowVersion", (float)ShadowVersion() }, { "leafBatchShadow", (float)ShadowLeafBatch() }, { "refillShadow", (float)ShadowRefill() }, { "shadowBackfill", (float)shadowBackfill }, { "sampleInterleave", (float)sampleInterleave },
+		{ "shadowVersion", (float)ShadowVersion() }, { "leafBatchShadow", (float)ShadowLeafBatch() }, { "refillShadow", (float)ShadowRefill() }, { "shadowBackfill", (float)shadowBackfill }, { "sampleInterleave", (float)sampleInterleave }, { "shadowGridOwn", (float)shadowGridOwn },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "pathTail", (float)pathTail }, { "terminalTrace", (float)terminalTrace }, { "packetHeavy", packetHeavy }, { "chordSplitShadow", chordSplitShadow }, { "pathTailBatch", (float)pathTailBatch }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
 		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
@@ -1053,7 +1055,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ta.mask = g.shMask.ptr, ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = g.gstack.ptr;
 			ta.packet = packetShadow ? PacketMode() : 0;
 			SetTail( ta, g );
-			lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, g.evShadow }, g.st );
+			lh2_launch_trace_any( &sd, &ta, ta.version >= 5 && !ta.packet ? ShadowGrid() : grid, 1, { nullptr, g.evShadow }, g.st );
 			g.fromShadow = g.prevStop;
 		}
 		if (gi == 0 && frameSplit) CHK_HIP( hipStreamWaitEvent( stream, evSideStop, 0 ) );   /* join the side stream's shadow launch */

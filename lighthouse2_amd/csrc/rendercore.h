@@ -169,6 +169,10 @@ private:
 	int TraceGrid() const { return smCount * blocksPerCU; }
 	int PacketGrid() const { return smCount * packetBlocksPerCU; }   /* packet kernels: their own occupancy */
 	int PathGrid() const { return smCount * std::min( blocksPerCU, pathBlocksPerCU ); }   /* path tail: its occupancy, within the stack's */
+	/* the final shadow launch (any-hit BVH4 loops): their own occupancy unless traceBlocksPerCU lowered the grid
+	   (setting "shadowGridOwn" 0: the closest-hit grid) */
+	int ShadowGrid() const { return smCount * (shadowGridOwn && blocksPerCU == maxBlocksPerCU ? std::max( blocksPerCU, anyBlocksPerCU ) : blocksPerCU); }
+	int anyBlocksPerCU = 0, shadowGridOwn = 0;   /* own grid measured no faster (profiles/r02zq_ab_shadow_grid.txt) */
 
 	int device = 0, smCount = 256, blocksPerCU = 5, maxBlocksPerCU = 5, packetBlocksPerCU = 5, pathBlocksPerCU = 4;
 	bool initialized = false;
