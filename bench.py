@@ -183,6 +183,121 @@ def config4(args, rank, world, local, dev):
             "rays_per_frame": {"primary_plus_bounce1": tot[0], "deeper": tot[1], "shadow": tot[2]}}
 
 
+def single_gpu_frames(core, sc, steps, warmup, per_frame=None):
+    """frames timed like the step loop (K frames between two synchronisations, the host queueing frame
+    i + 1 while the GPU renders frame i); Restart frames, or per_frame(i) first (config 5's instance
+    updates).  Returns (seconds per frame, ray counts of the last frame)."""
+    def frame(i):
+        if per_frame:
+            per_frame(i)
+        sc.render_frame(core, converge=1)
+    for i in range(warmup):
+        frame(i)
+    core.sync()
+    counts = core.ray_counts()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        frame(warmup + i)
+    core.sync()
+    return (time.perf_counter() - t0) / steps, counts
+
+
+def frame_record(workload, el, counts, st, setup_s):
+    return {"workload": workload, "ms_per_frame": round(el * 1e3, 4),
+            "value": round((int(counts[0]) + int(counts[1])) / el / 1e6, 3), "unit": "Mrays/s (primary+secondary)",
+            "all_extension_Mrays_s": round(int(counts[:16].sum()) / el / 1e6, 1),
+            "rays_per_frame": {"primary": int(counts[0]), "bounce1": int(counts[1]), "deeper": int(counts[2:16].sum()),
+                               "shadow": int(counts[16])},
+            "coreStats_ms": {"trace0": round(st.traceTime0 * 1e3, 4), "trace1": round(st.traceTime1 * 1e3, 4),
+                             "traceX": round(st.traceTimeX * 1e3, 4), "shadow": round(st.shadowTraceTime * 1e3, 4),
+                             "shade": round(st.shadeTime * 1e3, 4)},
+            "setup_s": round(setup_s, 2)}
+
+
+def config3(args, local):
+    """BASELINE configs[2]: full wavefront path trace, maxPathLength 4, the 1M-triangle procedural room
+    (specular chains, glass, two area lights: NEE + shadow rays), 1080p 1 spp, one GPU."""
+    t0 = time.perf_counter()
+    sc = scene.room_scene(args.room_tris, 1920, 1080)
+    core = RenderCore(device=local)
+    core.setting("maxPathLength", 4)
+    sc.load_into(core)
+    core.set_target(1920, 1080, 1)
+    setup = time.perf_counter() - t0
+    el, counts = single_gpu_frames(core, sc, args.config_steps, args.warmup)
+    r = frame_record(f"config3: room {sc.tri_count} tris, 1920x1080 1 spp, maxPathLength 4, 2 area lights",
+                     el, counts, core.stats(), setup)
+    core.close()
+    return r
+
+
+def config5(args, local):
+    """BASELINE configs[4]: 100 distinct 100k-triangle meshes (10M triangles), one instance each, new
+    seeded rotations of every instance each frame (SetInstance x 100 + UpdateToplevel inside the timed
+    frame), 1080p 8 spp (16,588,800 paths), one GPU."""
+    t0 = time.perf_counter()
+    sc = scene.instanced_scene(meshes=100, tris_per_mesh=100_000, width=1920, height=1080)
+    core = RenderCore(device=local)
+    sc.load_into(core)
+    core.set_target(1920, 1080, 8)
+    setup = time.perf_counter() - t0
+
+    def per_frame(i):
+        scene.animate_instances(sc, i)
+        for k, (mesh, T) in enumerate(sc.instances):
+            core.set_instance(k, mesh, T)
+        core.update_toplevel()
+
+    el, counts = single_gpu_frames(core, sc, args.config_steps, args.warmup, per_frame)
+    r = frame_record("config5: 100 meshes x 100k tris, per-frame instance rotations + TLAS rebuild, 1920x1080 8 spp",
+                     el, counts, core.stats(), setup)
+    core.close()
+    return r
+
+
+def config4_incore(args, ndev):
+    """Config 4 through the path an unchanged application uses: ONE process, one core (CreateCore /
+    RenderSystem, core_api_base.cpp:97-132) with setting "deviceCount" = the GPUs of the run, which
+    partitions the 4K frame over the devices itself and gathers the accumulator rows to device 0 by
+    xGMI peer copies (csrc/multidevice.cpp).  Each frame is driven as RenderSystem::Render drives it:
+    six Setting calls, then Render (rendersystem.cpp:228-238).  At one GPU it is the plain core."""
+    W4, H4 = 3840, 2160
+    t0 = time.perf_counter()
+    sc = scene.room_scene(args.room_tris, W4, H4)
+    core = RenderCore(device=0)
+    if ndev > 1:
+        core.setting("deviceCount", ndev)
+    core.setting("maxPathLength", 4)
+    sc.load_into(core)
+    core.set_target(W4, H4, 1)
+    setup = time.perf_counter() - t0
+
+    def frame():
+        for name, v in (("epsilon", 1e-4), ("clampValue", 10.0), ("clampDirect", 1.0), ("clampIndirect", 1.0),
+                        ("filter", 0.0), ("TAA", 0.0)):
+            core.setting(name, v)
+        core.render(sc.view, 1)
+
+    for _ in range(args.warmup):
+        frame()
+    core.sync()
+    counts = core.ray_counts()
+    t0 = time.perf_counter()
+    for _ in range(args.config4_steps):
+        frame()
+    core.sync()
+    el = (time.perf_counter() - t0) / args.config4_steps
+    core.close()
+    return {"workload": f"config4 in-core: room {sc.tri_count} tris, {W4}x{H4} 1 spp, maxPathLength 4, one process, "
+                        f"deviceCount {ndev} (band partition + xGMI peer-copy gather inside the core), RenderSystem's "
+                        f"six Setting calls + Render per frame",
+            "scaling": "strong", "n_gpus": ndev, "steps": args.config4_steps,
+            "value": round((int(counts[0]) + int(counts[1])) / el / 1e6, 3), "unit": "Mrays/s (primary+secondary)",
+            "ms_per_frame": round(el * 1e3, 4), "setup_s": round(setup, 2),
+            "rays_per_frame": {"primary_plus_bounce1": int(counts[0]) + int(counts[1]),
+                               "deeper": int(counts[2:16].sum()), "shadow": int(counts[16])}}
+
+
 def roofline_of(core, sc, W, H, dev, kernel_iters):
     """The dominant kernel (bounce-ray closest hit, per-ray traversal) and the primary-ray launch, timed
     with their own HIP events; priced by the committed counter summaries of the same kernels."""
@@ -263,6 +378,9 @@ def main():
     ap.add_argument("--room-tris", type=int, default=1_000_000)
     ap.add_argument("--config4-steps", type=int, default=10)
     ap.add_argument("--no-config4", action="store_true")
+    ap.add_argument("--config-steps", type=int, default=10, help="frames timed for configs 3 and 5")
+    ap.add_argument("--no-configs", action="store_true", help="skip configs 3, 5 and config4_incore")
+    ap.add_argument("--no-config5", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -343,8 +461,25 @@ def main():
         }
     core.close()
     c4 = None if args.no_config4 else config4(args, rank, world, local, dev)
+    c4in = c3 = c5 = None
+    if not args.no_configs:
+        # the in-core multi-device run uses the node's first `world` GPUs from rank 0 alone: the other ranks
+        # wait at a host-side (gloo) barrier, so no collective kernel occupies their GPUs meanwhile
+        host = dist.new_group(backend="gloo") if world > 1 else None
+        if world > 1:
+            dist.barrier(group=host)
+        if rank == 0:
+            c4in = config4_incore(args, world)
+            if world == 1:
+                c3 = config3(args, local)
+                c5 = None if args.no_config5 else config5(args, local)
+        if world > 1:
+            dist.barrier(group=host)
     if rank == 0:
         out["config4"] = c4
+        out["config4_incore"] = c4in
+        out["config3"] = c3
+        out["config5"] = c5
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(sc, args.width, args.height, args.cpu_seconds)
         else:

@@ -30,7 +30,7 @@
      lh2_core_update_toplevel            CoreAPI_Base::UpdateToplevel   core_api_base.h:113
    Extensions (no reference counterpart; used by the tile partition, the bench and the tests):
      lh2_core_set_tile, lh2_core_set_tile_bands, lh2_core_sync, lh2_core_get_accumulator, lh2_core_get_frame,
-     lh2_core_copy_accumulator_rows, lh2_core_pack_tile, lh2_core_pack_tile_ordered, lh2_core_tile_rows, lh2_core_stream, lh2_core_ray_counts, lh2_core_trace_closest,
+     lh2_core_copy_accumulator_rows, lh2_core_copy_frame_async, lh2_core_pack_tile, lh2_core_pack_tile_ordered, lh2_core_tile_rows, lh2_core_stream, lh2_core_ray_counts, lh2_core_trace_closest,
      lh2_core_trace_any, lh2_core_trace_closest_device, lh2_core_generate_eye_rays,
      lh2_core_scene_info, lh2_core_get_setting, lh2_set_device, lh2_xorshift_floats, lh2_version.
 */
@@ -76,6 +76,9 @@ int lh2_core_sync( lh2_core core );
 int lh2_core_get_accumulator( lh2_core core, float* out4 );
 int lh2_core_get_frame( lh2_core core, float* out4 );
 int lh2_core_copy_accumulator_rows( lh2_core core, void* deviceDst, int y0, int y1 );
+/* the last finalized frame (w x h float4) -> deviceDst, async on the core stream: the headless display copy
+   (interoptexture.cpp:51-71 copies it into the app's GL texture every frame) */
+int lh2_core_copy_frame_async( lh2_core core, void* deviceDst );
 int lh2_core_pack_tile( lh2_core core, void* deviceDst );   /* owned accumulator rows -> deviceDst (rows x width float4), async on the core stream */
 /* the same, ordered both ways with consumerStream (a hipStream_t that reads deviceDst, e.g. the one
    the gather runs on; null: the null stream): the pack waits for the consumer's earlier work, the

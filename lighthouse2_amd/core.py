@@ -70,6 +70,7 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
         "lh2_core_copy_accumulator_rows": [_P, _P, C.c_int, C.c_int],
         "lh2_core_ray_counts": [_P, _U],
         "lh2_core_pack_tile": [_P, _P],
+        "lh2_core_copy_frame_async": [_P, _P],
         "lh2_core_pack_tile_ordered": [_P, _P, _P],
         "lh2_core_tile_rows": [_P, C.POINTER(C.c_int)],
         "lh2_core_stream": [_P, C.POINTER(_P)],
@@ -236,6 +237,11 @@ class RenderCore:
             self._chk(self.lib.lh2_core_pack_tile_ordered(self.h, C.c_void_p(device_ptr), C.c_void_p(s)))
         else:
             self._chk(self.lib.lh2_core_pack_tile(self.h, C.c_void_p(device_ptr)))
+
+    def copy_frame_async(self, device_ptr: int) -> None:
+        """The last finalized frame into device memory, asynchronously on the core stream (the headless
+        counterpart of the display copy: no host synchronisation)."""
+        self._chk(self.lib.lh2_core_copy_frame_async(self.h, C.c_void_p(device_ptr)))
 
     def stream_ptr(self) -> int:
         s = C.c_void_p()

@@ -186,6 +186,7 @@ void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, Launch
 void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_term( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st );
 int lh2_path_blocks_per_cu( void );
+void lh2_launch_spin( unsigned long long ticks, hipStream_t st );
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
 void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
 /* the rows of a band partition (k_pack_rows' mapping); rows 0: every pixel */

@@ -1953,6 +1953,14 @@ __global__ void k_unpack_rows( const float4* __restrict__ src, float4* __restric
 	acc[gy * w + x] = src[i];
 }
 
+/* a single wave that idles its stream for `ticks` of the 100 MHz real-time counter (tests of the
+   multi-device gather's ordering: MultiDevice setting "gatherStallUs") */
+__global__ void k_spin( const unsigned long long ticks )
+{
+	const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+	while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep( 8 );
+}
+
 /* ---- host-side launchers (extern "C", no torch / no HIP types beyond the stream) ---------- */
 /* Launches go through hipExtLaunchKernelGGL: its start / stop events are recorded by the kernel's own
    dispatch packet, where a hipEventRecord between two launches costs a barrier packet and ~5 us of
@@ -2133,6 +2141,7 @@ void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int 
 	if (rows * w <= 0) { if (ev.stop) (void)hipEventRecord( ev.stop, st ); return; }
 	LH2_LAUNCH( k_unpack_rows, (rows * w + 255) / 256, 256, st, ev, src, acc, w, y0, band, bandStride, rows );
 }
+void lh2_launch_spin( unsigned long long ticks, hipStream_t st ) { hipLaunchKernelGGL( k_spin, dim3( 1 ), dim3( 64 ), 0, st, ticks ); }
 void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st, const RowMap* rm )
 {
 	const FrameStatsDev none{};

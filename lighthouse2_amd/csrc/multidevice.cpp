@@ -42,13 +42,16 @@ MultiDevice::MultiDevice( RenderCore* primary, int count )
 			(void)hipGetLastError();
 		}
 	}
-	send.assign( count, nullptr ), recv.assign( count, nullptr ), rowsOf.assign( count, 0 ), packed.assign( count, nullptr );
+	for (int p = 0; p < 2; p++) send[p].assign( count, nullptr ), copied[p].assign( count, nullptr ), copyPending[p].assign( count, 0 );
+	recv.assign( count, nullptr ), rowsOf.assign( count, 0 ), packed.assign( count, nullptr );
 	errors.assign( count, std::string() );
 	for (int i = 0; i < count; i++)
 	{
 		MD_CHK( hipSetDevice( devices[i] ) );
 		MD_CHK( hipEventCreateWithFlags( &packed[i], hipEventDisableTiming ) );
 	}
+	MD_CHK( hipSetDevice( d0 ) );
+	for (int p = 0; p < 2; p++) for (int i = 0; i < count; i++) MD_CHK( hipEventCreateWithFlags( &copied[p][i], hipEventDisableTiming ) );
 	MD_CHK( hipSetDevice( d0 ) );
 	for (int i = 0; i < count; i++) threads.emplace_back( &MultiDevice::Worker, this, i );
 }
@@ -65,9 +68,11 @@ MultiDevice::~MultiDevice()
 	{
 		(void)hipSetDevice( devices[i] );
 		(void)hipDeviceSynchronize();
-		if (send[i]) (void)hipFree( send[i] );
-		if (recv[i]) { (void)hipSetDevice( devices[0] ); (void)hipFree( recv[i] ); }
+		for (int p = 0; p < 2; p++) if (send[p][i]) (void)hipFree( send[p][i] );
 		if (packed[i]) (void)hipEventDestroy( packed[i] );
+		(void)hipSetDevice( devices[0] );
+		if (recv[i]) (void)hipFree( recv[i] );
+		for (int p = 0; p < 2; p++) if (copied[p][i]) (void)hipEventDestroy( copied[p][i] );
 		if (i > 0) { (void)hipSetDevice( devices[i] ); cores[i]->Shutdown(); delete cores[i]; }
 	}
 	(void)hipSetDevice( devices[0] );
@@ -115,7 +120,27 @@ void MultiDevice::ForEach( const std::function<void( int )>& f )
 
 /* ---- broadcast calls ---------------------------------------------------------------------- */
 void MultiDevice::SetProbePos( int x, int y ) { for (auto* c : cores) c->SetProbePos( x, y ); }
-void MultiDevice::Setting( const char* name, float value ) { ForEach( [&]( int i ) { cores[i]->Setting( name, value ); } ); }
+void MultiDevice::Setting( const char* name, float value )
+{
+	if (OwnSetting( name, value )) return;
+	for (const auto& kv : applied) if (kv.first == name && kv.second == value) return;   /* unchanged: no round trip */
+	ForEach( [&]( int i ) { cores[i]->Setting( name, value ); } );
+	bool found = false;
+	for (auto& kv : applied) if (kv.first == name) kv.second = value, found = true;
+	if (!found) applied.emplace_back( name, value );
+}
+void MultiDevice::ReplaySettings( const std::vector<std::pair<std::string, float>>& kv )
+{
+	std::vector<std::pair<std::string, float>> bc;
+	for (const auto& e : kv) if (!OwnSetting( e.first.c_str(), e.second )) bc.push_back( e );
+	ForEach( [&]( int i ) { if (i > 0) for (const auto& e : bc) cores[i]->Setting( e.first.c_str(), e.second ); } );
+	applied = bc;
+}
+bool MultiDevice::OwnSetting( const char* name, float value )
+{
+	if (!strcmp( name, "gatherStallUs" )) { gatherStallUs = std::max( 0.0f, value ); return true; }
+	return false;
+}
 void MultiDevice::SetTextures( const lh2_CoreTexDesc* tex, int n ) { ForEach( [&]( int i ) { cores[i]->SetTextures( tex, n ); } ); }
 void MultiDevice::SetMaterials( const lh2_CoreMaterial* mat, int n ) { ForEach( [&]( int i ) { cores[i]->SetMaterials( mat, n ); } ); }
 void MultiDevice::SetLights( const lh2_CoreLightTri* a, int na, const lh2_CorePointLight* p, int np, const lh2_CoreSpotLight* s, int ns,
@@ -141,6 +166,7 @@ void MultiDevice::SetTarget( uint32_t w, uint32_t h, uint32_t spp, uint32_t glTe
 		cores[i]->SetTileBands( i, n, band );
 	} );
 	cores[0]->SetInteropTexture( glTexture );   /* the display copy happens on device 0 after the gather */
+	cores[0]->displayAtFinalize = true;         /* ... in FinalizeFrame only, not in its own Render */
 	width = w, height = h;
 	EnsureExchange();
 }
@@ -157,11 +183,16 @@ void MultiDevice::EnsureExchange()
 	}
 	const size_t bytes = maxRows * width * sizeof( float4 );
 	if (bytes <= exchangeBytes) return;
+	Synchronize();   /* frames in flight may still read the old buffers */
 	for (int i = 1; i < n; i++)
 	{
 		MD_CHK( hipSetDevice( devices[i] ) );
-		if (send[i]) MD_CHK( hipFree( send[i] ) );
-		MD_CHK( hipMalloc( &send[i], bytes ) );
+		for (int p = 0; p < 2; p++)
+		{
+			if (send[p][i]) MD_CHK( hipFree( send[p][i] ) );
+			MD_CHK( hipMalloc( &send[p][i], bytes ) );
+			copyPending[p][i] = 0;
+		}
 		MD_CHK( hipSetDevice( devices[0] ) );
 		if (recv[i]) MD_CHK( hipFree( recv[i] ) );
 		MD_CHK( hipMalloc( &recv[i], bytes ) );
@@ -172,24 +203,30 @@ void MultiDevice::EnsureExchange()
 
 void MultiDevice::Render( const lh2_ViewPyramid& view, int converge )
 {
-	const int n = Count();
-	/* every device renders its bands; ranks > 0 pack them for the gather (async on their streams) */
+	const int n = Count(), p = parity;
+	parity ^= 1;
+	/* every device renders its bands; ranks > 0 pack them for the gather (async on their streams), into
+	   this frame parity's send buffer once device 0 has copied the frame two back out of it */
 	ForEach( [&]( int i ) {
 		cores[i]->Render( view, converge );
 		if (i > 0)
 		{
-			cores[i]->PackTile( send[i] );
+			if (copyPending[p][i]) MD_CHK( hipStreamWaitEvent( cores[i]->Stream(), copied[p][i], 0 ) );
+			cores[i]->PackTile( send[p][i] );
 			MD_CHK( hipEventRecord( packed[i], cores[i]->Stream() ) );
 		}
 	} );
 	/* the gather on device 0's stream: peer copy (xGMI DMA) of each rank's rows, then unpack */
 	RenderCore* c0 = cores[0];
+	if (gatherStallUs > 0) lh2_launch_spin( (uint64_t)(gatherStallUs * 100.0f), c0->Stream() );   /* 100 MHz ticks */
 	for (int i = 1; i < n; i++)
 	{
 		MD_CHK( hipStreamWaitEvent( c0->Stream(), packed[i], 0 ) );
 		const size_t bytes = rowsOf[i] * width * sizeof( float4 );
-		if (devices[i] == devices[0]) MD_CHK( hipMemcpyAsync( recv[i], send[i], bytes, hipMemcpyDeviceToDevice, c0->Stream() ) );
-		else MD_CHK( hipMemcpyPeerAsync( recv[i], devices[0], send[i], devices[i], bytes, c0->Stream() ) );
+		if (devices[i] == devices[0]) MD_CHK( hipMemcpyAsync( recv[i], send[p][i], bytes, hipMemcpyDeviceToDevice, c0->Stream() ) );
+		else MD_CHK( hipMemcpyPeerAsync( recv[i], devices[0], send[p][i], devices[i], bytes, c0->Stream() ) );
+		MD_CHK( hipEventRecord( copied[p][i], c0->Stream() ) );
+		copyPending[p][i] = 1;
 		c0->UnpackTile( recv[i], i, n, band );
 	}
 	c0->FinalizeFrame();

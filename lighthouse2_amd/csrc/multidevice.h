@@ -51,8 +51,12 @@ public:
 	/* extensions: the frame's totals over the sub-cores; device 0 holds the gathered accumulator */
 	void GetRayCounts( uint32_t* out17 );
 	void Synchronize();
+	/* the settings the primary already has, onto the sub-cores created with this object */
+	void ReplaySettings( const std::vector<std::pair<std::string, float>>& kv );
 
 	static constexpr int band = 8;   /* rows per band, dealt round-robin over the sub-cores */
+	/* settings the multi-device core keeps itself (not broadcast); false: not one of them */
+	bool OwnSetting( const char* name, float value );
 
 private:
 	/* run f(i) for every sub-core i, each on its own worker thread with its device current */
@@ -62,10 +66,19 @@ private:
 
 	std::vector<RenderCore*> cores;           /* cores[0]: the primary */
 	std::vector<int> devices;
-	/* exchange buffers: send[i] on device i (rank i's packed rows), recv[i] on device 0 */
-	std::vector<void*> send, recv;
+	/* exchange buffers, double-buffered by frame parity: send[p][i] on device i (rank i's packed rows of a
+	   frame of parity p), recv[i] on device 0.  copied[p][i] (device 0's stream, after its copy out of
+	   send[p][i]) orders the pack of frame f + 2 into the same buffer after the copy of frame f: the host
+	   queues frames ahead of the GPU, and a rank may finish frame f + 1 before device 0 gathers frame f */
+	std::vector<void*> send[2], recv;
 	std::vector<size_t> rowsOf;
-	std::vector<hipEvent_t> packed;
+	std::vector<hipEvent_t> packed, copied[2];
+	std::vector<char> copyPending[2];
+	int parity = 0;
+	/* broadcast settings as last applied: a repeated value (RenderSystem sends six per frame,
+	   rendersystem.cpp:231-236) costs no round trip over the worker threads */
+	std::vector<std::pair<std::string, float>> applied;
+	float gatherStallUs = 0;   /* debug: device 0 idles this long before each gather (tests of the ordering) */
 	size_t exchangeBytes = 0;
 	uint32_t width = 0, height = 0;
 	/* worker pool */

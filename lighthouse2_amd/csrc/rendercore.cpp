@@ -1080,7 +1080,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	RowMap rm{};
 	if (tileRows < scrheight) rm = { scrwidth, cp.y0, cp.band, cp.bandStride, tileRows };
 	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, &fs, { nullptr, evFrame[1] }, stream, &rm );
-	if (glResource)
+	if (glResource && !displayAtFinalize)
 	{
 		hipArray_t arr = nullptr;
 		CHK_HIP( hipGraphicsMapResources( 1, &glResource, stream ) );
@@ -1147,6 +1147,11 @@ void RenderCore::FinalizeFrame()
 		CHK_HIP( hipMemcpy2DToArrayAsync( arr, 0, 0, frame.ptr, sizeof( float4 ) * scrwidth, sizeof( float4 ) * scrwidth, scrheight, hipMemcpyDeviceToDevice, stream ) );
 		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, stream ) );
 	}
+}
+
+void RenderCore::CopyFrameAsync( void* devDst )
+{
+	CHK_HIP( hipMemcpyAsync( devDst, frame.ptr, sizeof( float4 ) * (size_t)scrwidth * scrheight, hipMemcpyDeviceToDevice, stream ) );
 }
 
 int RenderCore::TileRows() const

@@ -142,6 +142,8 @@ public:
 	   of the whole accumulator again (finalizeRender + display copy, no statistics) */
 	void UnpackTile( const void* devSrc, int rank, int nranks, int band );
 	void FinalizeFrame();
+	bool displayAtFinalize = false;   /* rank 0 of MultiDevice: the display copy follows the gather (FinalizeFrame) */
+	void CopyFrameAsync( void* devDst );   /* the last finalized frame, D2D on the core stream */
 	hipStream_t Stream() const { return stream; }
 	int Device() const { return device; }
 	int SamplesTaken() const { return samplesTaken; }

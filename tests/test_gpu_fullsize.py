@@ -174,3 +174,58 @@ def test_config5_fullsize_instanced_8spp():
     finally:
         core.close()
         o.close()
+
+
+@pytest.mark.timeout(900)
+def test_config4_fullsize_partitioned_frame():
+    """Config 4 at its size: the config-3 room (1M triangles, maxPathLength 4, lights) at 3840x2160,
+    1 spp = 8,294,400 paths, the frame split over 8 sub-cores in 8-row bands (setting "deviceCount" 8:
+    the partition, the per-rank 4K accumulators and frame buffers, the 2N shadow buffers, the row-map
+    finalize and the gather of multidevice.cpp; on a one-GPU box the 8 sub-cores share device 0).
+    Against the single-device core: identical per-bounce ray counts, accumulator within 1e-6.  Against
+    the oracle: rank 0's bands (set_tile_bands(0, 8, 8), the pixels of pathtracer.h:79-80 it owns)
+    within 1e-4.  Reference sizing: RenderCore_OptixPrime_B/rendercore.cpp:149-209."""
+    from lighthouse2_amd.core import RenderCore
+    W, H, N, BAND = 3840, 2160, 8, 8
+    sc = scene.room_scene(1_000_000, W, H)
+    st = (("maxPathLength", 4),)
+
+    def render(devices):
+        c = RenderCore(device=0)
+        try:
+            if devices > 1:
+                c.setting("deviceCount", devices)
+            for k, v in st:
+                c.setting(k, v)
+            sc.load_into(c)
+            c.set_target(W, H, 1)
+            sc.render_frame(c)
+            return c.accumulator(), c.ray_counts(), c.stats()
+        finally:
+            c.close()
+
+    a8, c8, s8 = render(N)
+    a1, c1, s1 = render(1)
+    assert c1[0] == W * H and c1[16] > 8_000_000
+    assert np.array_equal(c8, c1), (c8, c1)
+    r = rel_l2(a8[..., :3], a1[..., :3])
+    print(f"config4 4K: rays {c1[:4].tolist()} shadow {int(c1[16])}; 8 sub-cores vs 1: rel-L2 {r:.2e}")
+    assert r <= 1e-6
+    assert np.array_equal(a8[..., 3], a1[..., 3])
+    assert (s8.primaryRayCount, s8.bounce1RayCount, s8.totalShadowRays) == (s1.primaryRayCount, s1.bounce1RayCount, s1.totalShadowRays)
+    o = Oracle()
+    try:
+        sc.load_into(o)
+        for k, v in st:
+            o.setting(k, v)
+        o.set_target(W, H, 1)
+        o.set_tile_bands(0, N, BAND)
+        sc.render_frame(o)
+        ao = o.accumulator()
+    finally:
+        o.close()
+    rows = np.concatenate([np.arange(y, min(y + BAND, H)) for y in range(0, H, N * BAND)])
+    r0 = rel_l2(a8[rows, :, :3], ao[rows, :, :3])
+    print(f"config4 4K rank 0 bands ({len(rows)} rows) vs oracle: rel-L2 {r0:.2e}")
+    assert r0 <= REL_L2_TOL
+    assert rel_l2(a8[rows, :, 3], ao[rows, :, 3]) <= 1e-6

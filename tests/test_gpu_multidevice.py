@@ -89,3 +89,82 @@ def test_partition_extensions_refused_with_several_devices():
             c.set_tile_bands(0, 2, 8)
     finally:
         c.close()
+
+
+def test_gather_ordering_under_a_lagging_device0():
+    """The gather of frame f must read frame f's rows even when the host has queued frame f + 1 and
+    the ranks > 0 have rendered and packed it before device 0 copies frame f (multidevice.cpp: the send
+    buffers are double-buffered by frame parity, and a pack waits for device 0's copy out of its buffer
+    two frames back).  Device 0 idles 30 ms before every gather (setting "gatherStallUs"); four
+    converging frames are queued back to back with no host synchronisation, each finalized frame copied
+    on the core stream into its own device buffer (the headless display copy); every one of them must
+    equal the single-device core's frame."""
+    import torch
+    w, h, frames = 160, 96, 4
+    sc = scene.room_scene(30000, w, h)
+    st = (("maxPathLength", 4),)
+    ref = []
+    c = RenderCore(device=0)
+    try:
+        for k, v in st:
+            c.setting(k, v)
+        sc.load_into(c)
+        c.set_target(w, h, 1)
+        for f in range(frames):
+            sc.render_frame(c, converge=1 if f == 0 else 0)
+            ref.append(c.frame())
+    finally:
+        c.close()
+    c = RenderCore(device=0)
+    try:
+        c.setting("deviceCount", 3)
+        c.setting("gatherStallUs", 30000)
+        for k, v in st:
+            c.setting(k, v)
+        sc.load_into(c)
+        c.set_target(w, h, 1)
+        bufs = [torch.zeros((h, w, 4), dtype=torch.float32, device="cuda") for _ in range(frames)]
+        torch.cuda.synchronize()
+        for f in range(frames):
+            sc.render_frame(c, converge=1 if f == 0 else 0)
+            c.copy_frame_async(bufs[f].data_ptr())
+        c.sync()
+        got = [b.cpu().numpy() for b in bufs]
+    finally:
+        c.close()
+    for f in range(frames):
+        r = rel_l2(got[f][..., :3], ref[f][..., :3])
+        print(f"frame {f}: rel-L2 vs one device {r:.2e}")
+        assert r <= 1e-6, (f, r)
+
+
+def test_repeated_settings_each_frame():
+    """RenderSystem::Render sends six settings before every Render (rendersystem.cpp:231-236): with
+    several devices, repeated values are applied once, and a changed value still reaches every sub-core."""
+    w, h = 64, 40
+    sc = scene.config2_scene(n=3000, width=w, height=h, sky=True)
+    c = RenderCore(device=0)
+    try:
+        c.setting("deviceCount", 2)
+        sc.load_into(c)
+        c.set_target(w, h, 1)
+        for f in range(3):
+            for name, v in (("epsilon", 1e-4), ("clampValue", 10.0), ("clampDirect", 1.0), ("clampIndirect", 1.0),
+                            ("filter", 0.0), ("TAA", 0.0)):
+                c.setting(name, v)
+            sc.render_frame(c, converge=1 if f == 0 else 0)
+        a3 = c.accumulator()
+        sc.render_frame(c, converge=1, clamp=0.05)   # changed: every sub-core clamps harder
+        a_low = c.accumulator()
+    finally:
+        c.close()
+    ref = RenderCore(device=0)
+    try:
+        sc.load_into(ref)
+        ref.set_target(w, h, 1)
+        sc.render_frame(ref, converge=1, clamp=0.05)
+        b_low = ref.accumulator()
+    finally:
+        ref.close()
+    assert np.isfinite(a3).all() and a3[..., :3].max() > a_low[..., :3].max()
+    assert rel_l2(a_low[..., :3], b_low[..., :3]) <= 1e-6
