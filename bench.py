@@ -47,7 +47,7 @@ from lighthouse2_amd.parallel import BAND, TileGather  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SIMDS, CLOCK_GHZ = 256 * 4, 2.4
 # the per-ray closest-hit kernel of incoherent rays per traversal loop version (rocprofv3 names)
-TRACE_KERNEL = {4: "k_trace_closest<false, 4>", 5: "k_trace_closest4d<1>", 6: "k_trace_closest4d<0>", 7: "k_trace_closest4d<2>"}
+TRACE_KERNEL = {1: "k_trace_closest<", 7: "k_trace_closest4d"}
 
 
 def log(msg):

@@ -1,7 +1,7 @@
 """Build provenance: the source hash libRenderCore_MI355X.so carries in lh2_version() ("srchash=<16 hex>").
 
 The Makefile (csrc/Makefile, HASH_SRCS / SRC_HASH) hashes the concatenated csrc/ and include/ sources in
-make's $(sort) order; `source_hash()` recomputes the same digest from the checked-out files, and
+make's $(sort) order, then the build flags; `source_hash()` recomputes the same digest from the checked-out files, and
 `library_hash()` reads the one compiled into a library file without loading it (so a stale library can
 be detected, and rebuilt, before any process maps it).
 """
@@ -26,10 +26,12 @@ def _hash_sources() -> list[pathlib.Path]:
     return [(CSRC / n) for n in sorted(set(names), key=lambda s: s.encode())]
 
 
-def source_hash() -> str:
+def source_hash(extra: str = "", slp: str = "-fno-slp-vectorize", arch: str = "gfx950") -> str:
+    """The hash of the sources and of the default build flags (csrc/Makefile EXTRA, SLP, ARCH)."""
     h = hashlib.sha256()
     for p in _hash_sources():
         h.update(p.read_bytes())
+    h.update(f"flags:{extra}|{slp}|{arch}\n".encode())
     return h.hexdigest()[:16]
 
 

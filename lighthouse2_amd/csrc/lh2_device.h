@@ -49,10 +49,10 @@ struct Counters   /* core_settings.h:81-91 plus device-side error flags */
 	/* per-segment counts of the segmented streams (lh2_kernels.h, LH2_SEGS), 128 B apart.  The path
 	   counts ping-pong: the paths of pathLength L are counted in segPath / segBack[(L - 1) & 1], and
 	   its shade launch counts the extension rays (pathLength L + 1) into [L & 1].  A path segment is
-	   two-ended: segPath[k] records from its start, segBack[k] from its end (ShadeParams::chordCut:
-	   the rays with a short chord through the scene go to the end, so they are traced last); shadow
-	   rays queued; shadow segments are two-ended too (ShadeParams::shadowCut: short shadow rays at the end) */
-	uint32_t segPath[2][8 * 32], segBack[2][8 * 32], segShadow[8 * 32], segShadowBack[8 * 32];
+	   two-ended: segPath[k] records from its start, segBack[k] from its end (ShadeParams::chordCut: the
+	   rays with a short chord through the scene go to the end, so they are traced last); shadow rays are
+	   queued per segment */
+	uint32_t segPath[2][8 * 32], segBack[2][8 * 32], segShadow[8 * 32];
 };
 
 /* ---- small vector helpers with the reference's evaluation order --------------------------- */

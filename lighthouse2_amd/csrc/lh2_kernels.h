@@ -17,24 +17,14 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	   y0 + (lr / band) * bandStride + lr % band  (contiguous tile: band = rows) */
 	int y0, band, bandStride, tileRows;
 	int tiled;   /* store rays in 8x8 pixel blocks per wave (coherent traversal); 0 = row-major */
-	int spp;     /* > 1 (tiled, one launch for every slot): the samples of an 8x8 block in consecutive waves */
-	int slotBase;  /* this launch writes slots [slotBase, slotBase + jobCount) of the tile, at 0.. (path groups) */
 	int primeRef;  /* RenderCore_PrimeRef camera: uniform random numbers, no distortion (camera.h:57-60) */
 	/* folded into the camera launch (no launches of their own): the frame's counter / work-queue
 	   reset (initC non-null: what k_init_counters does), and the accumulator reset of a restart
 	   (clearAcc non-null: each pixel's first sample zeroes it; the memset of rendercore.cpp:465) */
 	Counters* initC; uint32_t* cursors; int cursorWords; uint32_t pathCount, segStride;
 	float4* clearAcc;
-	/* two-ended primary segments (camAlloc non-null; whole 8x8 tiles, segStride a multiple of 64): a tile
-	   whose centre ray's length inside the scene box (chordLo, chordHi) is at most chordCut is written at
-	   the end of its segment, so the primary trace takes the long (costly) tiles first.  camAlloc: this
-	   frame's per-segment front counts (LH2_SEGS x LH2_SEGCOUNT_STRIDE words) then back counts, zeroed by
-	   the previous frame's camera launch, which zeroes camZero (the other frame's block) for the next */
-	uint32_t* camAlloc; uint32_t* camZero;
 	uint32_t* hvZero; uint32_t hvZeroWords;   /* heavy-first packets: the block this frame records into (TraceArgs::hvWrite) */
-	float chordLo[3], chordHi[3], chordCut;
 };
-#define LH2_CAM_ALLOC_WORDS (2 * 8 * 32)   /* front + back counts of the LH2_SEGS segments */
 
 struct SceneDev       /* everything the traversal and shading kernels read, by value (kernarg) */
 {
@@ -69,7 +59,6 @@ struct BounceAdvance  /* the hand-off to the next bounce (advance_bounce, lh2_ke
 	uint32_t* segRetireBack;
 	uint32_t* rayCountLog;           /* [pathLength] = rays of the next bounce */
 	uint32_t* hostActiveLog;         /* pinned host copy of the same (the host's early exit), or null */
-	uint32_t* shadowSnap; uint32_t* shadowCursor;   /* the shadow split's snapshot, or null */
 	int zeroLog;                     /* nonzero: also zero rayCountLog past pathLength (the path tail counts into it) */
 };
 
@@ -83,7 +72,6 @@ struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path st
 	   flight when its work queues run dry are short ones (longest-first scheduling); 0: all at the start */
 	float chordLo[3], chordHi[3], chordCut;
 	int advance; BounceAdvance adv;                    /* nonzero: the launch's last block hands off to the next bounce */
-	float shadowCut;                                   /* shadow rays at most this long go to the end of their segment (0: none) */
 	uint32_t shadowStride;                             /* shadow-ray segments: capacity of each */
 	const float4* rayO; const float4* rayD; const float4* T4; const float4* Q4; const uint4* hits;
 	float4* rayOut; float4* rayDOut; float4* T4Out; float4* Q4Out;
@@ -114,38 +102,15 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	int* gstack;                                      /* stack entries past LH2_STACK_LDS */
 	uint32_t refill;                                  /* refill idle lanes once >= refill are idle (1..64) */
 	uint32_t leafBatch;                               /* run triangle tests once >= leafBatch lanes parked a leaf */
-	int version;                                      /* traversal loop: 1 (trace_stream), 2 (lh2_trace2.inc), 4 (BVH4, lh2_trace4.inc) */
-	int packet;                                       /* wave-uniform packet traversal (coherent rays): 1 over the BVH2, 4 over the BVH4 */
-	unsigned long long* stats;                        /* LH2_TRACE_STATS builds: LH2_TSTAT_N per-launch counters */
-	/* tail hand-off (lh2_trace2.inc): once the queue is exhausted, a wave with fewer than tailLanes
-	   active rays appends them to tailOut / tailOutUV {idx, bits(tbest), tri, inst} {u, v} - segment
-	   blockIdx % LH2_SEGS, counters tailCounts (LH2_SEGCOUNT_STRIDE apart), tailStride records per
-	   segment - and exits; a second launch of the same kernel (tail_args) continues them densely
-	   from those records (tailIn) with the closest hit found so far as tmax, which gives the ray the
-	   same closest hit (the hit does not depend on the visiting order) */
-	uint4* tailOut; float2* tailOutUV; uint32_t* tailCounts; uint32_t tailStride, tailLanes;
-	const uint4* tailIn; const float2* tailInUV;
-	/* tail pool (lh2_trace2.inc): once the queue is exhausted, a wave holding at most `pool` rays
-	   hands them, with their traversal state and stack, to another wave of its workgroup through
-	   LDS and exits (0: off) */
-	uint32_t pool;
+	int version;                                      /* traversal loop: 7 (BVH4, lh2_trace4d.inc) or 1 (BVH2, trace_stream) */
+	int packet;                                       /* nonzero: wave-uniform packet traversal (coherent rays, lh2_trace_packet.inc) */
+	unsigned long long* stats;                        /* LH2_TRACE_STATS / LH2_TRACE_TIMES builds: per-launch counters */
 	uint32_t shadeBatch;                              /* path tail (k_trace_path4d): shade once >= shadeBatch lanes finished a query */
-	/* terminal trace (k_trace_term4d): the last bounce of a scene whose hits there add nothing (ShadeParams::
-	   terminal); a ray that misses adds its sky sample to acc[pixel] as k_shade_last does (pathT4 / pathQ4:
-	   the path state, wh: pixels per frame) and no hit record is written */
-	const float4* pathT4; const float4* pathQ4; uint32_t wh;
 	/* heavy-first packets (packet kernel, hvWrite non-null): the previous frame's packets that took more
 	   than hvFactor x its mean node steps (hvRead: per-segment counts, step sums, a bit per packet and the
 	   lists of packet bits) are taken first, the rest in order; this frame's are recorded into hvWrite.
 	   A packet bit is segment x hvCap + its batch in the segment; hvTiles: packets of the launch */
 	const uint32_t* hvRead; uint32_t* hvWrite; uint32_t hvCap, hvMaskWords, hvTiles; float hvFactor;
-	/* shadow backfill (closest-hit launches, traceVersion 5-7, bfO non-null): once this launch's own queues
-	   are dry and while any of its waves still walks a closest-hit ray, idle lanes take shadow rays queued
-	   by earlier bounces - the stream bfO / bfD, front counts bfCounts (stable during the launch),
-	   bfStride per segment - from the final shadow launch's work-queue heads bfCursor, claimed with a
-	   bounded compare-and-swap so the final launch continues exactly behind them; an unoccluded one adds
-	   its potential (potentials, acc) as that launch would */
-	const float4* bfO; const float4* bfD; const uint32_t* bfCounts; uint32_t bfStride; uint32_t* bfCursor;
 };
 /* layout of a heavy-packet block: counts, step sums (LH2_SEGS x LH2_SEGCOUNT_STRIDE words each), the bit
    mask (hvMaskWords), then LH2_SEGS lists of hvCap packet bits; the camera launch zeroes the first
@@ -164,12 +129,10 @@ struct LaunchEvents { hipEvent_t start, stop; };
 
 /* where k_finalize delivers the frame's statistics: the device counters / ray-count log / scene error,
    and the host's pinned FrameStats fields (hostCounters null: nothing is delivered) */
-#define LH2_FS_GROUPS 4
 struct FrameStatsDev
 {
-	int groups;
-	const Counters* counters[LH2_FS_GROUPS]; const uint32_t* rayLog[LH2_FS_GROUPS];
-	Counters* hostCounters[LH2_FS_GROUPS]; uint32_t* hostRayCount[LH2_FS_GROUPS];
+	const Counters* counters; const uint32_t* rayLog;
+	Counters* hostCounters; uint32_t* hostRayCount;
 	const int* sceneError; int* hostSceneError;
 };
 
@@ -180,11 +143,9 @@ void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, 
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st );
 int lh2_trace_blocks_per_cu( void );
-int lh2_any4d_blocks_per_cu( void );
 int lh2_packet_blocks_per_cu( void );
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
-void lh2_launch_trace_term( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st );
 int lh2_path_blocks_per_cu( void );
 void lh2_launch_spin( unsigned long long ticks, hipStream_t st );
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
@@ -208,22 +169,13 @@ void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, co
 #define LH2_SEGS LH2_CHUNKS
 #define LH2_SEGCOUNT_STRIDE 32
 #define LH2_CURSOR_STRIDE 32
-/* per trace launch: the segment heads, the heads of its tail launch, the tail segment counts */
-#define LH2_CURSOR_WORDS (3 * LH2_CHUNKS * LH2_CURSOR_STRIDE)
-#define LH2_TAIL_CURSOR (LH2_CHUNKS * LH2_CURSOR_STRIDE)
-#define LH2_TAIL_COUNT (2 * LH2_CHUNKS * LH2_CURSOR_STRIDE)
+/* per trace launch: the segment heads, then the heavy-first packets' list heads (lh2_trace_packet.inc) */
+#define LH2_CURSOR_WORDS (2 * LH2_CHUNKS * LH2_CURSOR_STRIDE)
+#define LH2_HEAVY_CURSOR (LH2_CHUNKS * LH2_CURSOR_STRIDE)
 #define LH2_MAX_BOUNCES 64                                   /* RenderCore_PrimeRef MAXPATHLENGTH (core_settings.h:25) */
 #define LH2_CURSOR_SLOTS (2 * LH2_MAX_BOUNCES + 4)           /* launches per frame: [L] bounce L, [64 + L] shadow after bounce L, [130] shadow */
 #define LH2_SHADOW_SLOT (2 * LH2_MAX_BOUNCES + 2)
-/* the BVH4 loops' LDS stack (lh2_trace4d.inc): LH2_STACK_TCULL 1 keeps each entry's entry distance (16 bits) beside
-   it, in 12 LDS entries instead of 16 (the same LDS per block), and closest-hit walks pop the entries beyond their
-   closest hit without a node step; the global part is sized for the smaller one.  Parity-exact, measured no faster
-   (config-2 bounce 0.579 vs 0.576 ms, profiles/r02zm_ab_stack_tcull.txt): off */
-#ifndef LH2_STACK_TCULL
-#define LH2_STACK_TCULL 0
-#endif
-#define LH2_STACK4_LDS (LH2_STACK_TCULL ? 12 : LH2_STACK_LDS)
-#define LH2_STACK4_LDS_INTS (LH2_STACK4_LDS * 256 + (LH2_STACK_TCULL ? LH2_STACK4_LDS * 128 : 0))
+/* traversal stacks: LH2_STACK_LDS entries per lane in LDS (16 x 256 x 4 B = 16 KiB per block), the rest in global memory */
 #ifndef LH2_STACK_LDS
 #define LH2_STACK_LDS 16
 #endif

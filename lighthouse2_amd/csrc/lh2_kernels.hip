@@ -139,17 +139,15 @@ LH2_DEV v3 RandomPointOnLens( const float r0, float r1, const v3 pos, const floa
 }
 
 /* InitCountersForExtend (.cuda.cu:64-74) plus the frame's work-queue heads; thread i of the launch */
-LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_t segStride, uint32_t* cursors, const int cursorWords, const int i,
-	const bool twoEnded = false )
+LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_t segStride, uint32_t* cursors, const int cursorWords, const int i )
 {
 	if (i < cursorWords) cursors[i] = 0;
 	if (i < LH2_SEGS)
 	{
-		/* the camera writes the paths densely: segment i is [i * segStride, (i + 1) * segStride) (two-ended
-		   primary segments: counted in CameraParams::camAlloc instead) */
+		/* the camera writes the paths densely: segment i is [i * segStride, (i + 1) * segStride) */
 		const uint32_t lo = (uint32_t)i * segStride;
-		c->segPath[0][i * LH2_SEGCOUNT_STRIDE] = twoEnded ? 0u : pathCount > lo ? min( pathCount - lo, segStride ) : 0u;
-		c->segPath[1][i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadow[i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadowBack[i * LH2_SEGCOUNT_STRIDE] = 0;
+		c->segPath[0][i * LH2_SEGCOUNT_STRIDE] = pathCount > lo ? min( pathCount - lo, segStride ) : 0u;
+		c->segPath[1][i * LH2_SEGCOUNT_STRIDE] = 0, c->segShadow[i * LH2_SEGCOUNT_STRIDE] = 0;
 		c->segBack[0][i * LH2_SEGCOUNT_STRIDE] = 0, c->segBack[1][i * LH2_SEGCOUNT_STRIDE] = 0;
 	}
 	if (i != 0) return;
@@ -159,41 +157,17 @@ LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_
 	c->reserved0 = 0, c->shadowOverflow = 0, c->shadeDone = 0;
 }
 
-/* the length of a ray's segment inside the box [lo, hi] (negative: it misses the box); ordering only, so
-   a fast reciprocal is fine.  RenderCore::PrimaryChordCut computes the same on the host */
-LH2_DEV float box_chord( const float lo[3], const float hi[3], const v3 o, const v3 d )
-{
-	const float ix = __builtin_amdgcn_rcpf( d.x ), iy = __builtin_amdgcn_rcpf( d.y ), iz = __builtin_amdgcn_rcpf( d.z );
-	const float ax = (lo[0] - o.x) * ix, bx = (hi[0] - o.x) * ix, ay = (lo[1] - o.y) * iy, by = (hi[1] - o.y) * iy;
-	const float az = (lo[2] - o.z) * iz, bz = (hi[2] - o.z) * iz;
-	const float tn = fmaxf( fmaxf( fminf( ax, bx ), fminf( ay, by ) ), fmaxf( fminf( az, bz ), 0.0f ) );
-	const float tf = fminf( fminf( fmaxf( ax, bx ), fmaxf( ay, by ) ), fmaxf( az, bz ) );
-	return tf - tn;
-}
-
 __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const uint8_t* __restrict__ bn, float4* __restrict__ rayO,
 	float4* __restrict__ rayD, float4* __restrict__ T4, float4* __restrict__ Q4, const int jobCount )
 {
 	const int local = threadIdx.x + blockIdx.x * blockDim.x;
-	if (p.initC) init_counters( p.initC, p.pathCount, p.segStride, p.cursors, p.cursorWords, local, p.camAlloc != nullptr );
-	if (p.camZero && local < LH2_CAM_ALLOC_WORDS) p.camZero[local] = 0;
+	if (p.initC) init_counters( p.initC, p.pathCount, p.segStride, p.cursors, p.cursorWords, local );
 	if (p.hvZero && (uint32_t)local < p.hvZeroWords) p.hvZero[local] = 0;
 	if (local >= jobCount) return;
-	int slot = p.slotBase + local;
+	const int slot = local;
 	/* slot -> (sample, tile row, x) -> global jobIndex = x + (y + s * h) * w, as camera.h:48-53 */
 	const uint32_t w = (uint32_t)p.w, h = (uint32_t)p.h;
 	const uint32_t tilePix = (uint32_t)p.tileRows * w;
-	if (p.spp > 1 && p.tiled && (w & 7u) == 0)
-	{
-		/* storage order only: the spp samples of an 8x8 pixel block go to consecutive waves (sample-major
-		   order puts them a whole frame of rays apart), so they walk the tree while its nodes are still in
-		   the XCD's L2; the remainder rows (tileRows % 8) follow, sample by sample */
-		const uint32_t spp = (uint32_t)p.spp, nFull = ((uint32_t)p.tileRows / 8u) * (w / 8u), full = nFull * 64u * spp;
-		uint32_t sm, r;
-		if ((uint32_t)slot < full) { const uint32_t wv = (uint32_t)slot >> 6; sm = wv % spp, r = (wv / spp) * 64u + ((uint32_t)slot & 63u); }
-		else { const uint32_t q = (uint32_t)slot - full, rem = tilePix - nFull * 64u; sm = q / rem, r = nFull * 64u + q % rem; }
-		slot = (int)(sm * tilePix + r);
-	}
 	const uint32_t s = (uint32_t)slot / tilePix, r = (uint32_t)slot % tilePix;
 	uint32_t lr = r / w, x = r % w;
 	if (p.tiled && (w & 7u) == 0)
@@ -246,19 +220,7 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 	}
 	const v3 posOnLens = RandomPointOnLens( r2, r3, mk3( p.pos.x, p.pos.y, p.pos.z ), p.aperture, right, up );
 	const v3 rayDir = normalize3( sub3( posOnPixel, posOnLens ) );
-	/* stored at the launch's own index (a path group's buffers hold its slots only), or, with two-ended
-	   primary segments, the tile goes to the front or the end of its segment by its centre ray's chord */
-	uint32_t out = (uint32_t)local;
-	if (p.camAlloc)
-	{
-		const float len = box_chord( p.chordLo, p.chordHi, posOnLens, rayDir );
-		const bool late = __int_as_float( __builtin_amdgcn_readlane( __float_as_int( len ), 36 ) ) <= p.chordCut;   /* pixel (4, 4) */
-		const uint32_t seg = (uint32_t)local / p.segStride;
-		uint32_t pos = 0;
-		if (lane_id() == 0) pos = atomicAdd( p.camAlloc + (late ? LH2_SEGS * LH2_SEGCOUNT_STRIDE : 0) + seg * LH2_SEGCOUNT_STRIDE, 64u );
-		pos = __builtin_amdgcn_readfirstlane( pos );
-		out = seg * p.segStride + (late ? p.segStride - 64u - pos : pos) + lane_id();
-	}
+	const uint32_t out = (uint32_t)local;
 	rayO[out] = make_float4( posOnLens.x, posOnLens.y, posOnLens.z, p.geometryEpsilon );
 	rayD[out] = make_float4( rayDir.x, rayDir.y, rayDir.z, 1e34f );
 	T4[out] = make_float4( 1, 1, 1, bitsf( ((x + (y + (sampleIndex - (uint32_t)p.pass) * h) * w) << 8) + 1 /* S_SPECULAR */ ) );
@@ -269,18 +231,9 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 /* =====================================================================================
    traversal: two-level BVH2, ordered, t-culled, LDS short stack + global spill
    ===================================================================================== */
-#ifndef LH2_TRACE_MINWAVES
-#define LH2_TRACE_MINWAVES 7   /* min waves per SIMD the traversal kernels are compiled for (VGPR cap 72; A/B: tools/build_variants.sh) */
-#endif
+#define LH2_TRACE_MINWAVES 7   /* min waves per SIMD the traversal kernels are compiled for (VGPR cap 72) */
 #define STACK_LDS LH2_STACK_LDS   /* entries per lane kept in LDS: 16 x 256 x 4 B = 16 KB / block */
 #define STACK_TOTAL LH2_STACK_TOTAL /* + global spill; the host checks the tree depth against it */
-
-/* tail pool of one workgroup (lh2_trace2.inc): rays handed between its waves once the work queue is
-   exhausted.  Field f of slot i at w[f * LH2_POOL_CAP + i] (a wave writes a field's 64 words
-   contiguously); lock / count / alive change only under the lock */
-#define LH2_POOL_CAP 64
-#define LH2_POOL_FIELDS 19
-struct TailPool { int lock, count, alive, pad; uint32_t w[LH2_POOL_FIELDS * LH2_POOL_CAP]; };
 
 LH2_DEV float safe_inv( float d ) { return (d > -1e-30f && d < 1e-30f) ? (d < 0 ? -1e30f : 1e30f) : 1.0f / d; }
 
@@ -575,16 +528,11 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 }
 
 #include "lh2_box4.inc"
-#include "lh2_trace2.inc"
 /* the path-tail mode of lh2_trace4d.inc shades with k_shade's code (defined with the shading code below) */
 struct ShadeOut { bool ext, shadow; float4 eO, eD, eT, eQ, sO, sD, sP; };
 template <bool NL>
 LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd, const float4 T4, const float4 O4, const float4 D4, const float4 Q4,
 	const int pathLength, const uint32_t R0, ShadeOut& o );
-/* ... and the terminal trace the miss branch of k_shade_last */
-LH2_DEV v3 SampleSkydome( const SceneDev& s, const v3 D );
-LH2_DEV v3 clampintensity( const float clampValue, v3 c );
-LH2_DEV v3 fixnan( v3 a );
 #include "lh2_trace4d.inc"
 #include "lh2_trace_packet.inc"
 
@@ -592,34 +540,21 @@ LH2_DEV v3 fixnan( v3 a );
 /* 8 waves per SIMD (64 VGPRs, ~32 spilled outside the node loop): the packet loop is bound by the
    latency of its dependent node fetches, and 8 waves hide more of it than the unbounded 94-VGPR
    build's 5: 0.481 -> 0.437 ms on the config-2 primary rays (A/B 5/6/7/8 waves, r01c) */
-#ifndef LH2_PACKET_MINWAVES
 #define LH2_PACKET_MINWAVES 8
-#endif
-template <int W>
-__global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet<0, W>( s, a ); }
-template <int MODE, int W>
-__global__ __launch_bounds__( 256 ) void k_trace_any_packet( const SceneDev s, const TraceArgs a ) { trace_packet<MODE == 0 ? 1 : 2, W>( s, a ); }
+__global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet( s, a ); }
 
-template <bool PARK, int V>
+/* the reference BVH2 loop (traceVersion 1; the BVH4 is not built with setting "bvh4" 0) */
+template <bool PARK>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_closest( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	__shared__ TailPool pool;
-	tail_pool_init( pool );
-	if (V == 4) trace_stream2<0, PARK, 4>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &pool );
-	else if (V == 2) trace_stream2<0, PARK>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &pool );
-	else trace_stream<0, PARK>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	trace_stream<0, PARK>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 }
-
-template <int MODE, int V>
+template <int MODE>
 __global__ __launch_bounds__( 256, LH2_TRACE_MINWAVES ) void k_trace_any( const SceneDev s, const TraceArgs a )
 {
 	__shared__ int lstack[STACK_LDS * 256];
-	__shared__ TailPool pool;
-	tail_pool_init( pool );
-	if (V == 4) trace_stream2<MODE == 0 ? 1 : 2, true, 4>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &pool );
-	else if (V == 2) trace_stream2<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &pool );
-	else trace_stream<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
+	trace_stream<MODE == 0 ? 1 : 2, true>( s, a, lstack + threadIdx.x, a.gstack + blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u );
 }
 
 /* =====================================================================================
@@ -1592,15 +1527,11 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 				const uint32_t o = segBase + (late ? p.segStride - 1u - eb : es);
 				p.rayOut[o] = eO; p.rayDOut[o] = eD; p.T4Out[o] = eT; p.Q4Out[o] = eQ;
 			}
-			/* shadow rays: the short ones (ShadeParams::shadowCut) from the segment's end, so the shadow launch
-			   takes the long ones first (the host checks that the two ends did not meet) */
-			const bool sLate = doShadow && sD.w <= p.shadowCut;
-			const uint32_t ss = wave_alloc( doShadow && !sLate, &p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE] );
-			const uint32_t sb = wave_alloc( sLate, &p.counters->segShadowBack[seg * LH2_SEGCOUNT_STRIDE] );
+			/* shadow rays into the block's segment of the shadow stream */
+			const uint32_t ss = wave_alloc( doShadow, &p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE] );
 			if (doShadow)
 			{
-				const uint32_t q = sLate ? sb : ss;
-				if (q < p.shadowStride) { const uint32_t o = seg * p.shadowStride + (sLate ? p.shadowStride - 1u - sb : ss); p.shO[o] = sO; p.shD[o] = sD; p.shP[o] = sP; }
+				if (ss < p.shadowStride) { const uint32_t o = seg * p.shadowStride + ss; p.shO[o] = sO; p.shD[o] = sD; p.shP[o] = sP; }
 				else atomicOr( &p.counters->shadowOverflow, 1u );
 			}
 		}
@@ -1644,9 +1575,9 @@ __global__ __launch_bounds__( 256 ) void k_shade_last( const SceneDev s, const S
 template <bool NL>
 __global__ __launch_bounds__( 256, LH2_PATH_MINWAVES ) void k_trace_path4d( const SceneDev s, const TraceArgs a, const ShadeParams p )
 {
-	__shared__ int lstack[LH2_STACK4_LDS_INTS];
+	__shared__ int lstack[LH2_STACK_LDS * 256];
 	__shared__ int lrefs[4 * 256];
-	trace_stream4d<3, 2, NL>( s, a, lstack + threadIdx.x, lrefs + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &p );
+	trace_stream4d<3, NL>( s, a, lstack + threadIdx.x, lrefs + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &p );
 }
 
 /* counters: .cuda.cu:64-84 */
@@ -1848,22 +1779,14 @@ __global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t segSt
    one thread, after every block of the shade launch of bounce L has finished */
 LH2_DEV void advance_bounce( Counters* c, const BounceAdvance& a, const int pathLength, const int resetShadow )
 {
-	/* the shadow split: the shadow rays queued so far (segment by segment) are traced by an early launch
-	   with these counts, the final shadow launch starts its work queues behind them */
-	if (a.shadowSnap)
-		for (int k = 0; k < LH2_SEGS; k++)
-		{
-			const uint32_t n = __hip_atomic_load( &c->segShadow[k * LH2_SEGCOUNT_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-			a.shadowSnap[k * LH2_SEGCOUNT_STRIDE] = n, a.shadowCursor[k * LH2_CURSOR_STRIDE] = n;
-		}
 	uint32_t ext = 0, sh = 0;
 	for (int k = 0; k < LH2_SEGS; k++)
 	{
 		ext += __hip_atomic_load( &a.segNext[k * LH2_SEGCOUNT_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
 		ext += __hip_atomic_load( &a.segNextBack[k * LH2_SEGCOUNT_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
 		a.segRetire[k * LH2_SEGCOUNT_STRIDE] = 0, a.segRetireBack[k * LH2_SEGCOUNT_STRIDE] = 0;
-		sh += c->segShadow[k * LH2_SEGCOUNT_STRIDE] + c->segShadowBack[k * LH2_SEGCOUNT_STRIDE];
-		if (resetShadow) c->segShadow[k * LH2_SEGCOUNT_STRIDE] = 0, c->segShadowBack[k * LH2_SEGCOUNT_STRIDE] = 0;
+		sh += c->segShadow[k * LH2_SEGCOUNT_STRIDE];
+		if (resetShadow) c->segShadow[k * LH2_SEGCOUNT_STRIDE] = 0;
 	}
 	a.rayCountLog[pathLength] = ext;     /* rays traced at pathLength + 1 */
 	if (a.zeroLog) for (int k = pathLength + 1; k <= LH2_MAX_BOUNCES; k++) a.rayCountLog[k] = 0;
@@ -1903,19 +1826,16 @@ __global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__
 	const RowMap rm )
 {
 	const int i = threadIdx.x + blockIdx.x * blockDim.x;
-	if (blockIdx.x == 0 && fs.groups > 0)
+	if (blockIdx.x == 0 && fs.hostCounters)
 	{
-		/* block 0 also hands every path group's counters and ray-count log and the scene error to the
-		   host's pinned FrameStats (system-scope stores: no device-to-host copy launches at the end) */
-		for (int g = 0; g < fs.groups; g++)
-		{
-			const uint32_t* src = (const uint32_t*)fs.counters[g];
-			uint32_t* dst = (uint32_t*)fs.hostCounters[g];
-			for (int k = threadIdx.x; k < (int)(sizeof( Counters ) / 4); k += blockDim.x)
-				__hip_atomic_store( dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
-			for (int k = threadIdx.x; k < LH2_MAX_BOUNCES; k += blockDim.x)
-				__hip_atomic_store( fs.hostRayCount[g] + k, fs.rayLog[g][k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
-		}
+		/* block 0 also hands the frame's counters, ray-count log and scene error to the host's pinned
+		   FrameStats (system-scope stores: no device-to-host copy launches at the end) */
+		const uint32_t* src = (const uint32_t*)fs.counters;
+		uint32_t* dst = (uint32_t*)fs.hostCounters;
+		for (int k = threadIdx.x; k < (int)(sizeof( Counters ) / 4); k += blockDim.x)
+			__hip_atomic_store( dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+		for (int k = threadIdx.x; k < LH2_MAX_BOUNCES; k += blockDim.x)
+			__hip_atomic_store( fs.hostRayCount + k, fs.rayLog[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
 		if (threadIdx.x == 0) __hip_atomic_store( fs.hostSceneError, *fs.sceneError, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
 	}
 	if (i >= n) return;
@@ -1965,17 +1885,6 @@ __global__ void k_spin( const unsigned long long ticks )
 /* Launches go through hipExtLaunchKernelGGL: its start / stop events are recorded by the kernel's own
    dispatch packet, where a hipEventRecord between two launches costs a barrier packet and ~5 us of
    idle GPU per event (rocprofv3 kernel trace of the config-2 frame); null events: a plain launch. */
-/* the tail launch of a trace launch: same rays, hits and outputs; rays from the hand-off records */
-static TraceArgs tail_args( const TraceArgs& a )
-{
-	TraceArgs t = a;
-	t.tailIn = a.tailOut, t.tailInUV = a.tailOutUV;
-	t.tailOut = nullptr, t.tailOutUV = nullptr, t.tailLanes = 0;
-	t.segCounts = a.tailCounts, t.segStride = a.tailStride, t.countFixed = 0;
-	t.cursor = a.cursor + LH2_TAIL_CURSOR;
-	return t;
-}
-
 #define LH2_LAUNCH( kernel, grid, block, st, ev, ... ) \
 	hipExtLaunchKernelGGL( kernel, dim3( grid ), dim3( block ), 0, st, (ev).start, (ev).stop, 0, __VA_ARGS__ )
 
@@ -1995,104 +1904,35 @@ void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, 
 }
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st )
 {
-	/* incoherent rays: parked leaves (leafBatch > 0); traversal loop version 1 or 2 (lh2_trace2.inc);
-	   coherent primary rays: packet traversal (lh2_trace_packet.inc) */
-	if (a->packet == 4 && s->nodes4) LH2_LAUNCH( k_trace_closest_packet<4>, grid, 256, st, ev, *s, *a );
-	else if (a->packet) LH2_LAUNCH( k_trace_closest_packet<2>, grid, 256, st, ev, *s, *a );
-	else if (a->version >= 2)
-	{
-		/* with a tail hand-off: the main launch, then the tail launch over the handed-off rays;
-		   the start event goes with the first, the stop event with the second */
-		const bool tail = a->tailOut && a->tailLanes;
-		TraceArgs t = tail_args( *a );
-		const LaunchEvents e1 = { ev.start, tail ? nullptr : ev.stop }, e2 = { nullptr, ev.stop };
-		if (a->version == 5 && s->nodes4) LH2_LAUNCH( k_trace_closest4d<1>, grid, 256, st, ev, *s, *a );   /* lh2_trace4d.inc */
-		else if (a->version == 6 && s->nodes4) LH2_LAUNCH( k_trace_closest4d<0>, grid, 256, st, ev, *s, *a );
-		else if (a->version == 7 && s->nodes4 && a->bfO) LH2_LAUNCH( k_trace_closest4d_bf<2>, grid, 256, st, ev, *s, *a );
-		else if (a->version == 7 && s->nodes4) LH2_LAUNCH( k_trace_closest4d<2>, grid, 256, st, ev, *s, *a );
-		else if (a->version == 4 && s->nodes4)
-		{
-			if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 4>), grid, 256, st, e1, *s, *a );
-			else LH2_LAUNCH( (k_trace_closest<false, 4>), grid, 256, st, e1, *s, *a );
-			if (tail && a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 4>), grid, 256, st, e2, *s, t );
-			else if (tail) LH2_LAUNCH( (k_trace_closest<false, 4>), grid, 256, st, e2, *s, t );
-		}
-		else
-		{
-			if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 2>), grid, 256, st, e1, *s, *a );
-			else LH2_LAUNCH( (k_trace_closest<false, 2>), grid, 256, st, e1, *s, *a );
-			if (tail && a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 2>), grid, 256, st, e2, *s, t );
-			else if (tail) LH2_LAUNCH( (k_trace_closest<false, 2>), grid, 256, st, e2, *s, t );
-		}
-	}
-	else
-	{
-		if (a->leafBatch) LH2_LAUNCH( (k_trace_closest<true, 1>), grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( (k_trace_closest<false, 1>), grid, 256, st, ev, *s, *a );
-	}
+	/* coherent primary rays: packets over the BVH2 (lh2_trace_packet.inc); incoherent rays: the BVH4 loop
+	   (lh2_trace4d.inc), or the reference BVH2 loop (traceVersion 1, or no BVH4) */
+	if (a->packet) LH2_LAUNCH( k_trace_closest_packet, grid, 256, st, ev, *s, *a );
+	else if (a->version == 7 && s->nodes4) LH2_LAUNCH( k_trace_closest4d, grid, 256, st, ev, *s, *a );
+	else if (a->leafBatch) LH2_LAUNCH( k_trace_closest<true>, grid, 256, st, ev, *s, *a );
+	else LH2_LAUNCH( k_trace_closest<false>, grid, 256, st, ev, *s, *a );
 }
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st )
 {
-	if (a->packet)
+	if (a->version == 7 && s->nodes4)
 	{
-		const bool v4 = a->packet == 4 && s->nodes4;
-		if (fused && v4) LH2_LAUNCH( (k_trace_any_packet<1, 4>), grid, 256, st, ev, *s, *a );
-		else if (fused) LH2_LAUNCH( (k_trace_any_packet<1, 2>), grid, 256, st, ev, *s, *a );
-		else if (v4) LH2_LAUNCH( (k_trace_any_packet<0, 4>), grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( (k_trace_any_packet<0, 2>), grid, 256, st, ev, *s, *a );
+		if (fused) LH2_LAUNCH( k_trace_any4d<1>, grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( k_trace_any4d<0>, grid, 256, st, ev, *s, *a );
 	}
-	else if (a->version >= 5 && s->nodes4)
-	{
-		const int m = a->version == 5 ? 1 : a->version == 7 ? 2 : 0;
-		if (fused && m == 1) LH2_LAUNCH( (k_trace_any4d<1, 1>), grid, 256, st, ev, *s, *a );
-		else if (fused && m == 2) LH2_LAUNCH( (k_trace_any4d<1, 2>), grid, 256, st, ev, *s, *a );
-		else if (fused) LH2_LAUNCH( (k_trace_any4d<1, 0>), grid, 256, st, ev, *s, *a );
-		else if (m == 1) LH2_LAUNCH( (k_trace_any4d<0, 1>), grid, 256, st, ev, *s, *a );
-		else if (m == 2) LH2_LAUNCH( (k_trace_any4d<0, 2>), grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( (k_trace_any4d<0, 0>), grid, 256, st, ev, *s, *a );
-	}
-	else if (a->version >= 2)
-	{
-		const bool tail = a->tailOut && a->tailLanes;
-		TraceArgs t = tail_args( *a );
-		const LaunchEvents e1 = { ev.start, tail ? nullptr : ev.stop }, e2 = { nullptr, ev.stop };
-		const bool v4 = a->version == 4 && s->nodes4;
-		for (int pass = 0; pass < (tail ? 2 : 1); pass++)
-		{
-			const TraceArgs& x = pass ? t : *a;
-			const LaunchEvents& e = pass ? e2 : e1;
-			if (v4 && fused) LH2_LAUNCH( (k_trace_any<1, 4>), grid, 256, st, e, *s, x );
-			else if (v4) LH2_LAUNCH( (k_trace_any<0, 4>), grid, 256, st, e, *s, x );
-			else if (fused) LH2_LAUNCH( (k_trace_any<1, 2>), grid, 256, st, e, *s, x );
-			else LH2_LAUNCH( (k_trace_any<0, 2>), grid, 256, st, e, *s, x );
-		}
-	}
-	else
-	{
-		if (fused) LH2_LAUNCH( (k_trace_any<1, 1>), grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( (k_trace_any<0, 1>), grid, 256, st, ev, *s, *a );
-	}
+	else if (fused) LH2_LAUNCH( k_trace_any<1>, grid, 256, st, ev, *s, *a );
+	else LH2_LAUNCH( k_trace_any<0>, grid, 256, st, ev, *s, *a );
 }
 int lh2_packet_blocks_per_cu( void )
 {
 	int n = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_closest_packet<2>, 256, 0 ) != hipSuccess) n = 4;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_closest_packet, 256, 0 ) != hipSuccess) n = 4;
 	return n;
 }
-/* the any-hit BVH4 kernels' own occupancy (16-entry LDS stack, <= 64 VGPRs: 8 blocks per CU where the closest-hit
-   loops hold 7) */
-int lh2_any4d_blocks_per_cu( void )
-{
-	int n = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_any4d<1, 2>, 256, 0 ) != hipSuccess || n < 1) n = 4;
-	return n;
-}
+/* the per-ray traversal kernels' occupancy (persistent grid: CUs x blocks per CU) */
 int lh2_trace_blocks_per_cu( void )
 {
-	int n1 = 0, n2 = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest<true, 1>, 256, 0 ) != hipSuccess) n1 = 4;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_any<1, 1>, 256, 0 ) != hipSuccess) n2 = 4;
-	return n1 > n2 ? n1 : n2;
+	int n1 = 0;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest4d, 256, 0 ) != hipSuccess) n1 = 4;
+	return n1;
 }
 static int lh2_shade_last_grid( void )   /* k_shade_last: every CU full (occupancy x CUs), at least a block per segment */
 {
@@ -2111,10 +1951,6 @@ void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadePa
 	if (!s->nodes4) return;   /* the host selects the path tail only over a BVH4 */
 	if (s->nArea + s->nPoint + s->nSpot + s->nDir == 0) LH2_LAUNCH( (k_trace_path4d<true>), grid, 256, st, ev, *s, *a, *p );
 	else LH2_LAUNCH( (k_trace_path4d<false>), grid, 256, st, ev, *s, *a, *p );
-}
-void lh2_launch_trace_term( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st )
-{
-	if (s->nodes4) LH2_LAUNCH( k_trace_term4d, grid, 256, st, ev, *s, *a );
 }
 int lh2_path_blocks_per_cu( void )
 {

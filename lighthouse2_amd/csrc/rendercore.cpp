@@ -108,37 +108,18 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	blocksPerCU = maxBlocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
 	packetBlocksPerCU = std::max( 1, std::min( 8, lh2_packet_blocks_per_cu() ) );
 	pathBlocksPerCU = std::max( 1, std::min( 8, lh2_path_blocks_per_cu() ) );
-	anyBlocksPerCU = std::max( 1, std::min( 8, lh2_any4d_blocks_per_cu() ) );
-	for (int gi = 0; gi < LH2_MAX_GROUPS; gi++)
-	{
-		PathGroup& g = grp[gi];
-		if (gi == 0) g.st = stream;
-		else
-		{
-			CHK_HIP( hipStreamCreateWithFlags( &g.st, hipStreamNonBlocking ) );
-			g.ownStream = true;
-		}
-		g.counters.resize( 1 );
-		g.cursors.resize( (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
-		g.rayLog.resize( LH2_MAX_BOUNCES + 8 );
-		g.camAlloc.resize( 2 * LH2_CAM_ALLOC_WORDS );
-		CHK_HIP( hipMemsetAsync( g.camAlloc.ptr, 0, sizeof( uint32_t ) * 2 * LH2_CAM_ALLOC_WORDS, stream ) );
-		CHK_HIP( hipMemsetAsync( g.rayLog.ptr, 0, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), stream ) );
-		/* indexed by pathLength; written by k_counters_next (system scope) */
-		CHK_HIP( hipHostMalloc( (void**)&g.activeLog, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), hipHostMallocCoherent ) );
-		for (auto& e : g.evTrace) CHK_HIP( hipEventCreate( &e ) );
-		for (auto& e : g.evShade) CHK_HIP( hipEventCreate( &e ) );
-		for (auto& e : g.evShadowB) CHK_HIP( hipEventCreate( &e ) );
-		for (auto& e : g.evCount) CHK_HIP( hipEventCreate( &e ) );   /* stop events of launches (LaunchEvents) */
-		CHK_HIP( hipEventCreate( &g.evCamera ) );
-		CHK_HIP( hipEventCreate( &g.evShadow ) );
-		CHK_HIP( hipEventCreateWithFlags( &g.evDone, hipEventDisableTiming ) );
-	}
-	CHK_HIP( hipEventCreateWithFlags( &evFork, hipEventDisableTiming ) );
-	CHK_HIP( hipStreamCreateWithFlags( &sideStream, hipStreamNonBlocking ) );
-	CHK_HIP( hipEventCreate( &evSideStart ) );
-	CHK_HIP( hipEventCreate( &evSideStop ) );
-	shadowSnap.resize( LH2_SEGS * LH2_SEGCOUNT_STRIDE );
+	ps.counters.resize( 1 );
+	ps.cursors.resize( (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
+	ps.rayLog.resize( LH2_MAX_BOUNCES + 8 );
+	CHK_HIP( hipMemsetAsync( ps.rayLog.ptr, 0, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), stream ) );
+	/* indexed by pathLength; written by advance_bounce (system scope) */
+	CHK_HIP( hipHostMalloc( (void**)&ps.activeLog, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), hipHostMallocCoherent ) );
+	for (auto& e : ps.evTrace) CHK_HIP( hipEventCreate( &e ) );
+	for (auto& e : ps.evShade) CHK_HIP( hipEventCreate( &e ) );
+	for (auto& e : ps.evShadowB) CHK_HIP( hipEventCreate( &e ) );
+	for (auto& e : ps.evCount) CHK_HIP( hipEventCreate( &e ) );   /* stop events of launches (LaunchEvents) */
+	CHK_HIP( hipEventCreate( &ps.evCamera ) );
+	CHK_HIP( hipEventCreate( &ps.evShadow ) );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
@@ -148,7 +129,6 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipMemsetAsync( dTlasDepth.ptr, 0, sizeof( int ), stream ) );
 	dInstDesc.resize( 1 );   /* shading reads record 0 for a miss (HitInstance): it always exists */
 	CHK_HIP( hipMemsetAsync( dInstDesc.ptr, 0, sizeof( lh2_CoreInstanceDesc ), stream ) );
-	if (const char* tv = getenv( "LH2_TRACE_VERSION" )) traceVersion = std::min( 7, std::max( 0, atoi( tv ) ) );   /* A/B runs */
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
 }
@@ -188,21 +168,9 @@ bool RenderCore::UsePackets() const
 	return bytes <= (double)packetMaxMB * 1048576.0;
 }
 
-/* traversal loop of the per-ray launches (setting "traceVersion", 0: auto).  Auto: lh2_trace4d.inc (BVH4,
-   packed-FMA slabs, LDS child references, rcp box reciprocals, the single instance entered at ray
-   set-up).  While the BVH4 + triangles fit the 256 MB Infinity Cache each branch fetches its own record
-   and every reached leaf is tested at once (6: config-2 bounce rays 0.86 ms vs 0.88 for the v4 loop,
-   config 3 2.68 vs 2.77 ms per frame); beyond it leaves are parked in a one-entry slot and tested in
-   batches of leafBatch (default 16) lanes (7: config 5, 1 GB, 12.89 ms per frame vs 13.31 for the one-fetch
-   loop 5 and 13.68 for 6; profiles/r02j_ab_versions.txt, r02l_ab_slot.txt) */
-int RenderCore::TraceVersion() const
-{
-	if (traceVersion) return (traceVersion >= 4 && !bvh4) ? 2 : traceVersion;
-	if (!bvh4) return 2;
-	/* the leaf-slot loop with small leaf batches: config-2 bounce rays 0.64 -> 0.60 ms, config 5 (DRAM-resident)
-	   13.25 -> 13.1 ms, config 3 unchanged (profiles/r02y_ab_v7.txt); traceFetchMB no longer decides */
-	return 7;
-}
+/* traversal loop of the per-ray launches (setting "traceVersion"): 7, the BVH4 loop (lh2_trace4d.inc), unless
+   the BVH4 is not built (setting "bvh4" 0) or the reference BVH2 loop is asked for (1) */
+int RenderCore::TraceVersion() const { return (traceVersion == 1 || !bvh4) ? 1 : 7; }
 
 void RenderCore::EnsureBuffers()
 {
@@ -210,26 +178,25 @@ void RenderCore::EnsureBuffers()
 	frame.resize( (size_t)scrwidth * scrheight );
 }
 
-/* path buffers of a group for `paths` paths (a bit extra, as the reference reserves, and room for
-   LH2_SEGS segments of ceil(paths / LH2_SEGS)); shadow rays: 2 per path */
-void RenderCore::EnsureGroup( PathGroup& g, uint32_t paths )
+/* path buffers for `paths` paths (a bit extra, as the reference reserves, and room for LH2_SEGS segments
+   of ceil(paths / LH2_SEGS)); shadow rays: 2 per path */
+void RenderCore::EnsurePaths( uint32_t paths )
 {
-	if ((size_t)paths + 64 > g.cap)
+	if ((size_t)paths + 64 > ps.cap)
 	{
-		g.cap = (size_t)paths + (paths >> 4) + 64;
-		for (int i = 0; i < 2; i++) g.rayO[i].resize( g.cap ), g.rayD[i].resize( g.cap ), g.T4[i].resize( g.cap ), g.Q4[i].resize( g.cap );
-		g.hits.resize( g.cap );
-		g.shO.resize( 2 * g.cap ), g.shD.resize( 2 * g.cap ), g.shP.resize( 2 * g.cap );
-		g.shMask.resize( (2 * g.cap + 63) / 32 + 2 );
+		ps.cap = (size_t)paths + (paths >> 4) + 64;
+		for (int i = 0; i < 2; i++) ps.rayO[i].resize( ps.cap ), ps.rayD[i].resize( ps.cap ), ps.T4[i].resize( ps.cap ), ps.Q4[i].resize( ps.cap );
+		ps.hits.resize( ps.cap );
+		ps.shO.resize( 2 * ps.cap ), ps.shD.resize( 2 * ps.cap ), ps.shP.resize( 2 * ps.cap );
+		ps.shMask.resize( (2 * ps.cap + 63) / 32 + 2 );
 	}
-	EnsureStack( g );
+	EnsureStack();
 }
 
-void RenderCore::EnsureStack( PathGroup& g )
+void RenderCore::EnsureStack()
 {
-	const size_t need = (size_t)(LH2_STACK_TOTAL - std::min( LH2_STACK_LDS, LH2_STACK4_LDS )) * std::max( TraceGrid(), ShadowGrid() ) * 256;
-	if (g.gstack.count < need) g.gstack.resize( need );
-	if (&g == &grp[0] && sideStack.count < need) sideStack.resize( need );
+	const size_t need = (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256;
+	if (ps.gstack.count < need) ps.gstack.resize( need );
 }
 
 void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439-457 */
@@ -248,53 +215,31 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* traversal: test parked BLAS leaves once this many lanes of a wave hold one (0 = every step) */
 	else if (!strcmp( name, "leafBatch" )) leafBatch = std::min( 64, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "leafBatchPrimary" )) leafBatchPrimary = std::min( 64, std::max( 0, (int)value ) );
-	/* the shadow launches' own loop (5, 6, 7 over the BVH4; 0: traceVersion), leaf batch (-1: leafBatch) and refill (0: refill) */
-	else if (!strcmp( name, "shadowVersion" )) shadowVersion = (int)value >= 5 && (int)value <= 7 ? (int)value : 0;
-	else if (!strcmp( name, "leafBatchShadow" )) leafBatchShadow = std::min( 64, std::max( -1, (int)value ) );
-	else if (!strcmp( name, "refillShadow" )) refillShadow = std::min( 64, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "sampleInterleave" )) sampleInterleave = value != 0;   /* the samples of an 8x8 block in consecutive waves */
-	else if (!strcmp( name, "shadowGridOwn" )) { shadowGridOwn = value != 0; if (scrwidth) EnsureBuffers(); }   /* final shadow launch at the any-hit kernels' occupancy */
-	else if (!strcmp( name, "shadowBackfill" )) shadowBackfill = value != 0;   /* shadow rays in the closest-hit launches' tails */
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
-	else if (!strcmp( name, "bvhSweep" )) bvhSweep = std::max( 0, (int)value );   /* exact SAH sweep for nodes of <= this many triangles */
 	else if (!strcmp( name, "bvhSpatial" )) bvhSpatial = std::max( 0.0f, value );   /* SBVH overlap threshold (x root area); 0: off */
 	else if (!strcmp( name, "bvhSpatialBudget" )) bvhSpatialBudget = std::min( 4.0f, std::max( 0.0f, value ) );
 	else if (!strcmp( name, "bvh4Collapse" )) bvh4Collapse = value != 0;
+	else if (!strcmp( name, "bvh4" )) { bvh4 = value != 0; }   /* before SetGeometry */
+	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
+	else if (!strcmp( name, "gpuTlas" )) { gpuTlas = value != 0; instancesDirty = true; }
+	else if (!strcmp( name, "plocRadius" )) gpuBvh.radius = std::min( 32, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "chordSplit" )) chordSplit = std::max( 0.0f, value );   /* two-ended path segments (longest first); 0: off */
-	else if (!strcmp( name, "chordSplitShadow" )) chordSplitShadow = std::max( 0.0f, value );   /* two-ended shadow segments; 0: off */
 	else if (!strcmp( name, "packetHeavy" )) packetHeavy = std::max( 0.0f, value );   /* heavy-first primary packets; 0: off */
-	else if (!strcmp( name, "terminalTrace" )) terminalTrace = value != 0;   /* the last terminal bounce's sky samples in its trace launch */
 	else if (!strcmp( name, "pathTail" )) pathTail = std::max( 0, (int)value );   /* bounces from this one in one trace-and-shade launch; 0: off */
 	else if (!strcmp( name, "pathTailBatch" )) pathTailBatch = std::min( 64, std::max( 1, (int)value ) );
-	else if (!strcmp( name, "chordSplitPrimary" )) chordSplitPrimary = std::min( 1.0f, std::max( 0.0f, value ) );   /* two-ended primary segments; 0: off */
-	else if (!strcmp( name, "bvh4LeafTris" )) bvh4LeafTris = std::min( 16, std::max( 1, (int)value ) );
-	else if (!strcmp( name, "bvh4LeafCost" )) bvh4LeafCost = std::max( 0.0f, value );
-	else if (!strcmp( name, "bvh4TriCost" )) bvh4TriCost = std::max( 0.0f, value );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
-	else if (!strcmp( name, "packetWidth" )) packetWidth = value >= 4 ? 4 : 2;   /* packets over the BVH2 / BVH4 */
-	else if (!strcmp( name, "shadowSplit" )) shadowSplit = std::min( LH2_MAX_BOUNCES, std::max( 0, (int)value ) );   /* early shadow launch after this bounce (0: off) */
-	else if (!strcmp( name, "pathGroups" )) pathGroups = std::min( LH2_MAX_GROUPS, std::max( 1, (int)value ) );   /* pipelined path groups per frame */
 	else if (!strcmp( name, "singleInstanceStart" )) singleInstanceStart = value != 0;   /* one instance: rays start at its TLAS leaf */
 	else if (!strcmp( name, "terminalShade" )) terminalShade = value != 0;   /* drop hits that cannot contribute before shading them (ShadeParams::terminal) */
-	else if (!strcmp( name, "tailPool" )) tailPool = std::min( 64, std::max( 0, (int)value ) );   /* hand a dry wave's rays to another wave of its workgroup (0: off) */
-	else if (!strcmp( name, "tailLanes" )) tailLanes = std::min( 64, std::max( 0, (int)value ) );   /* traversal tail hand-off (0: off) */
 	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (default: occupancy limit) */
 	{
 		blocksPerCU = value > 0 ? std::min( maxBlocksPerCU, std::max( 1, (int)value ) ) : maxBlocksPerCU;
 	}
-	else if (!strcmp( name, "packetShadow" )) packetShadow = value != 0;     /* packet traversal of the shadow rays */
-	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice uses the primary-ray launch */
-	else if (!strcmp( name, "traceVersion" )) traceVersion = std::min( 7, std::max( 0, (int)value ) );   /* traversal loop: 1, 2 (BVH2), 4 (BVH4), 5 / 6 (BVH4, lh2_trace4d.inc: one fetch per iteration / per branch), 0 auto */
-	else if (!strcmp( name, "traceFetchMB" )) traceFetchMB = std::max( 0.0f, value );
-	else if (!strcmp( name, "bvh4" )) { bvh4 = value != 0; if (!bvh4 && traceVersion >= 4) traceVersion = 2; }   /* before SetGeometry */
-	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
-	else if (!strcmp( name, "gpuTlas" )) { gpuTlas = value != 0; instancesDirty = true; }
-	else if (!strcmp( name, "plocRadius" )) gpuBvh.radius = std::min( 32, std::max( 1, (int)value ) );
-	else if (!strcmp( name, "blocksPerCU" )) { blocksPerCU = std::min( 16, std::max( 1, (int)value ) ); if (scrwidth) EnsureBuffers(); }
+	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice traces as the frame traces primary rays */
+	else if (!strcmp( name, "traceVersion" )) traceVersion = (int)value == 1 ? 1 : 0;   /* 1: the reference BVH2 loop; else the BVH4 loop */
 	/* other names ("clampDirect", "filter", "TAA", ...) are ignored, as in the reference */
 }
 
@@ -305,13 +250,12 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "epsilon", geometryEpsilon }, { "clampValue", clampValue }, { "maxPathLength", (float)maxPathLength },
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
-		{ "shadowVersion", (float)ShadowVersion() }, { "leafBatchShadow", (float)ShadowLeafBatch() }, { "refillShadow", (float)ShadowRefill() }, { "shadowBackfill", (float)shadowBackfill }, { "sampleInterleave", (float)sampleInterleave }, { "shadowGridOwn", (float)shadowGridOwn },
-		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSweep", (float)bvhSweep }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "bvh4LeafTris", (float)bvh4LeafTris }, { "chordSplit", chordSplit }, { "chordSplitPrimary", chordSplitPrimary }, { "pathTail", (float)pathTail }, { "terminalTrace", (float)terminalTrace }, { "packetHeavy", packetHeavy }, { "chordSplitShadow", chordSplitShadow }, { "pathTailBatch", (float)pathTailBatch }, { "bvh4LeafCost", bvh4LeafCost }, { "bvh4TriCost", bvh4TriCost }, { "packetPrimary", (float)packetPrimary }, { "packetWidth", (float)packetWidth },
-		{ "pathGroups", (float)pathGroups }, { "shadowSplit", (float)shadowSplit }, { "singleInstanceStart", (float)singleInstanceStart },
-		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "traceFetchMB", traceFetchMB }, { "bvh4", (float)bvh4 },
-		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "blocksPerCU", (float)blocksPerCU },
-		{ "packetShadow", (float)packetShadow }, { "usePackets", (float)UsePackets() } };
+		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
+		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch },
+		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
+		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
+		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
+		{ "usePackets", (float)UsePackets() } };
 	for (const auto& e : t) if (!strcmp( name, e.n )) { value = e.v; return true; }
 	return false;
 }
@@ -470,7 +414,7 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 			}
 		}
 		BvhOutput bvh;
-		BuildBvh2( prims, bvhMaxLeaf, 0, bvh, bvhTraversalCost, bvhSweep, verts.empty() ? nullptr : verts.data(), bvhSpatial, bvhSpatialBudget );
+		BuildBvh2( prims, bvhMaxLeaf, 0, bvh, bvhTraversalCost, 0, verts.empty() ? nullptr : verts.data(), bvhSpatial, bvhSpatialBudget );
 		/* one triangle record per leaf slot (a spatial split can reference a triangle from several leaves) */
 		std::vector<float> tris48( std::max<size_t>( bvh.perm.size(), 1 ) * 12, 0.0f );
 		for (size_t j = 0; j < bvh.perm.size(); j++)
@@ -502,27 +446,13 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 	coreStats.bvhBuildTime += std::chrono::duration<float>( std::chrono::high_resolution_clock::now() - t0 ).count();
 }
 
-void RenderCore::SetTail( TraceArgs& ta, PathGroup& g )
-{
-	ta.pool = ta.packet ? 0u : (uint32_t)tailPool;
-#ifndef LH2_TAIL_HANDOFF
-	(void)ta, (void)g;
-	return;   /* the traversal loop is compiled without the hand-off (lh2_trace2.inc) */
-#endif
-	if (!tailLanes || ta.packet) return;
-	const size_t threads = (size_t)TraceGrid() * 256;
-	if (g.tailRec.count < threads) g.tailRec.resize( threads ), g.tailUV.resize( threads );
-	ta.tailOut = g.tailRec.ptr, ta.tailOutUV = g.tailUV.ptr;
-	ta.tailCounts = ta.cursor + LH2_TAIL_COUNT;
-	ta.tailStride = (uint32_t)(((TraceGrid() + LH2_SEGS - 1) / LH2_SEGS) * 256);   /* one record per thread of the segment's blocks */
-	ta.tailLanes = (uint32_t)tailLanes;
-}
-
 void RenderCore::BuildBlas4( CoreMeshHost& m, const float* nodes2 )
 {
 	std::vector<float> n4;
 	/* bvh4Collapse 1: dynamic-programming collapse (surface-area costs, optional leaf merging); 0: greedy */
-	m.depth4 = bvh4Collapse ? CollapseBvh4Sah( nodes2, (size_t)m.nodeCount, n4, bvh4LeafCost, bvh4TriCost, bvh4LeafTris )
+	/* node step = 1, leaf visit 0.4, triangle test 0.5; one triangle per leaf (merged leaves run the leaf loop
+	   divergent: slower, profiles/r02s_ab_collapse_shade4.txt) */
+	m.depth4 = bvh4Collapse ? CollapseBvh4Sah( nodes2, (size_t)m.nodeCount, n4, 0.4f, 0.5f, 1 )
 		: CollapseBvh4( nodes2, (size_t)m.nodeCount, n4 );
 	m.bvh4Nodes.upload( (const float4*)n4.data(), n4.size() / 4, stream );
 	m.node4Count = (int)(n4.size() / 32);
@@ -770,19 +700,21 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	}
 	if (converge == LH2_CONVERGE) firstConvergingFrame = false;
 	const int tileRows = TileRows();
-	const int tilePix = tileRows * scrwidth;
-	const uint32_t pathCount = (uint32_t)tilePix * (uint32_t)scrspp;
+	const uint32_t pathCount = (uint32_t)tileRows * (uint32_t)scrwidth * (uint32_t)scrspp;
 	const SceneDev sd = MakeSceneDev();
-	/* path groups (PathGroup): contiguous shares of the tile's paths with their boundaries on whole
-	   waves (64 slots: an 8x8 pixel block stays in one group), each on its own stream; small frames
-	   run as one group */
-	const int G = pathCount >= 4096u * (uint32_t)pathGroups ? pathGroups : 1;
-	frameGroups = G;
-	/* the accumulator reset of a restart: one frame-wide memset when path groups run concurrently,
-	   else folded into the camera launch (each pixel's first sample zeroes it; rows outside this
-	   rank's tile stay zero from SetTarget / SetTileBands) */
-	if (restart && (G > 1 || tileChanged)) CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
-	/* primary rays (camera.h) for every sample of the tile */
+	/* the accumulator reset of a restart is folded into the camera launch (each pixel's first sample zeroes
+	   it; rows outside this rank's tile stay zero from SetTarget); a changed tile clears the whole frame */
+	if (restart && tileChanged) CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
+	EnsurePaths( pathCount );
+	/* segmented path / ray streams (lh2_kernels.h): LH2_SEGS segments of segStride records; shadow rays in
+	   segments of shadowStride */
+	ps.count = pathCount;
+	ps.segStride = (pathCount + LH2_SEGS - 1) / LH2_SEGS;
+	ps.shadowStride = (uint32_t)(ps.shO.count / LH2_SEGS);
+	ps.in = 0, ps.pl = 0, ps.tailL = 0;
+	Counters* const c = ps.counters.ptr;
+	/* primary rays (camera.h) for every sample of the tile; the camera launch also resets the frame's
+	   counters and work-queue heads (k_init_counters) */
 	CameraParams cp{};
 	cp.pos = view.pos, cp.p1 = view.p1;
 	cp.right = { view.p2.x - view.p1.x, view.p2.y - view.p1.y, view.p2.z - view.p1.z };
@@ -793,10 +725,24 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	cp.y0 = std::max( 0, tileY0 ), cp.tileRows = tileRows;
 	cp.band = tileBand > 0 ? tileBand : std::max( 1, tileRows ), cp.bandStride = tileBand > 0 ? tileStride : std::max( 1, tileRows );
 	cp.tiled = tiledRays;
-	cp.spp = G == 1 && sampleInterleave ? scrspp : 0;
 	cp.primeRef = primeRef;
-	const bool twoEndedPrimary = chordSplitPrimary > 0 && tiledRays && !primeRef && scrwidth % 8 == 0 && tileRows % 8 == 0;
-	const float primaryCut = twoEndedPrimary ? PrimaryChordCut( view ) : 0.0f;
+	cp.initC = c, cp.cursors = ps.cursors.ptr, cp.cursorWords = LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS;
+	cp.pathCount = pathCount, cp.segStride = ps.segStride;
+	cp.clearAcc = restart && !tileChanged ? accumulator.ptr : nullptr;
+	/* heavy-first primary packets: this frame reads the block the previous one recorded, and records into the
+	   other one, which the camera launch zeroes (a new layout zeroes both) */
+	ps.hvOn = packetHeavy > 0 && tiledRays && UsePackets() && !primeRef;
+	if (ps.hvOn)
+	{
+		const uint32_t cap = (ps.segStride + 63) / 64, maskWords = (LH2_SEGS * cap + 31) / 32;
+		if (cap != ps.hvCap)
+		{
+			ps.hvCap = cap, ps.hvMaskWords = maskWords, ps.hvBlock = LH2_HV_MASK + maskWords + LH2_SEGS * cap, ps.hvParity = 0;
+			ps.hv.resize( 2 * (size_t)ps.hvBlock );
+			CHK_HIP( hipMemsetAsync( ps.hv.ptr, 0, sizeof( uint32_t ) * 2 * ps.hvBlock, stream ) );
+		}
+		cp.hvZero = ps.hv.ptr + (size_t)(1 - ps.hvParity) * ps.hvBlock, cp.hvZeroWords = LH2_HV_MASK + ps.hvMaskWords;
+	}
 	const int grid = TraceGrid();
 	int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
 	/* no specular event and no alpha cut-out in any material: every path ends at its second vertex,
@@ -805,276 +751,132 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	/* the frame's start: a marker before the camera launch (~4 us of idle GPU), not the launch's own start
 	   event (hipExtLaunchKernelGGL start events cost ~8 us: tools/launch_gap.hip, profiles/r02q_launch_gap.txt) */
 	CHK_HIP( hipEventRecord( evFrame[0], stream ) );
-	if (G > 1) CHK_HIP( hipEventRecord( evFork, stream ) );   /* the other groups start after the accumulator reset */
-	for (int gi = 0; gi < G; gi++)
-	{
-		PathGroup& g = grp[gi];
-		const uint32_t b0 = (uint32_t)(((uint64_t)pathCount * gi / G) & ~63ull);
-		const uint32_t b1 = gi + 1 == G ? pathCount : (uint32_t)(((uint64_t)pathCount * (gi + 1) / G) & ~63ull);
-		g.base = b0, g.count = b1 - b0;
-		EnsureGroup( g, g.count );
-		/* segmented path / ray streams (lh2_kernels.h): LH2_SEGS segments of segStride records; shadow
-		   rays in segments of shadowStride */
-		g.segStride = (g.count + LH2_SEGS - 1) / LH2_SEGS;
-		g.shadowStride = (uint32_t)(g.shO.count / LH2_SEGS);
-		g.in = 0, g.pl = 0, g.done = false, g.tailL = 0;
-		if (gi) CHK_HIP( hipStreamWaitEvent( g.st, evFork, 0 ) );
-		/* the camera launch also resets the group's counters and work-queue heads (k_init_counters) */
-		CameraParams cg = cp;
-		cg.slotBase = (int)g.base;
-		cg.initC = g.counters.ptr, cg.cursors = g.cursors.ptr, cg.cursorWords = LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS;
-		cg.pathCount = g.count, cg.segStride = g.segStride;
-		cg.clearAcc = restart && G == 1 && !tileChanged ? accumulator.ptr : nullptr;
-		/* two-ended primary segments: whole 8x8 tiles in whole segments only */
-		g.twoEnded = twoEndedPrimary && g.segStride % 64 == 0 && g.count % 64 == 0;
-		/* heavy-first primary packets: this frame reads the block the previous one recorded, and records
-		   into the other one, which the camera launch zeroes (a new layout zeroes both) */
-		const bool heavy = packetHeavy > 0 && tiledRays && UsePackets() && !primeRef;
-		if (heavy)
-		{
-			const uint32_t cap = (g.segStride + 63) / 64, maskWords = (LH2_SEGS * cap + 31) / 32;
-			if (cap != g.hvCap)
-			{
-				g.hvCap = cap, g.hvMaskWords = maskWords, g.hvBlock = LH2_HV_MASK + maskWords + LH2_SEGS * cap, g.hvParity = 0;
-				g.hv.resize( 2 * (size_t)g.hvBlock );
-				CHK_HIP( hipMemsetAsync( g.hv.ptr, 0, sizeof( uint32_t ) * 2 * g.hvBlock, g.st ) );
-			}
-			cg.hvZero = g.hv.ptr + (size_t)(1 - g.hvParity) * g.hvBlock, cg.hvZeroWords = LH2_HV_MASK + g.hvMaskWords;
-		}
-		g.hvOn = heavy;
-		if (g.twoEnded)
-		{
-			cg.camAlloc = g.camAlloc.ptr + (g.camFrame & 1) * LH2_CAM_ALLOC_WORDS;
-			cg.camZero = g.camAlloc.ptr + ((g.camFrame + 1) & 1) * LH2_CAM_ALLOC_WORDS;
-			g.camFrame++;
-			for (int k = 0; k < 3; k++) cg.chordLo[k] = sceneLo[k], cg.chordHi[k] = sceneHi[k];
-			cg.chordCut = primaryCut;
-		}
-		lh2_launch_camera( &cg, dBlueNoise.ptr, g.rayO[0].ptr, g.rayD[0].ptr, g.T4[0].ptr, g.Q4[0].ptr, (int)g.count, { nullptr, g.evCamera }, g.st );
-		g.prevStop = g.evCamera;
-	}
+	lh2_launch_camera( &cp, dBlueNoise.ptr, ps.rayO[0].ptr, ps.rayD[0].ptr, ps.T4[0].ptr, ps.Q4[0].ptr, (int)pathCount, { nullptr, ps.evCamera }, stream );
+	ps.prevStop = ps.evCamera;
 	if (restart) tileChanged = false;
 	/* without lights no path samples one (RandomPointOnLight: lightPdf 0), so there are no shadow
 	   rays and their launches are not queued */
 	const bool shadows = nArea + nPoint + nSpot + nDir > 0;
 	frameShadows = shadows;
-	const int splitL = (shadows && !primeRef && G == 1 && shadowSplit > 0 && shadowSplit < maxPL) ? shadowSplit : 0;
-	frameSplit = false;
-	/* two-ended shadow segments (setting "chordSplitShadow"): shadow rays shorter than it x the scene's
-	   extent are traced last; not with the shadow split or PrimeRef's per-bounce shadow launches */
-	float shadowCut = -3.0e38f;   /* off: no shadow ray is that short */
-	if (!splitL && !primeRef && chordSplitShadow > 0)
-		shadowCut = chordSplitShadow * std::max( std::max( sceneHi[0] - sceneLo[0], sceneHi[1] - sceneLo[1] ), sceneHi[2] - sceneLo[2] );
 	/* the path tail (setting "pathTail"): bounces pathTail .. maxPL in one launch of k_trace_path4d */
-	const int tailL = (!primeRef && G == 1 && !splitL && pathTail >= 2 && pathTail <= maxPL && TraceVersion() == 7 && dNodes4.ptr) ? pathTail : 0;
-	/* the bounce loop, the groups' launches interleaved */
+	const int tailL = (!primeRef && pathTail >= 2 && pathTail <= maxPL && TraceVersion() == 7) ? pathTail : 0;
+	/* the bounce loop */
 	for (int pathLength = 1; pathLength <= maxPL; pathLength++)
 	{
-		bool any = false;
-		for (int gi = 0; gi < G; gi++)
+		ps.pl = pathLength;
+		/* the path counts ping-pong (Counters::segPath): this bounce's paths, and its extension rays */
+		uint32_t* const segIn = c->segPath[(pathLength - 1) & 1];
+		uint32_t* const segNext = c->segPath[pathLength & 1];
+		uint32_t* const segInBack = c->segBack[(pathLength - 1) & 1];
+		uint32_t* const segNextBack = c->segBack[pathLength & 1];
+		const bool primary = pathLength == 1 && tiledRays;
+		TraceArgs ta{};
+		ta.version = TraceVersion();
+		ta.rayO = ps.rayO[ps.in].ptr, ta.rayD = ps.rayD[ps.in].ptr, ta.segCounts = segIn, ta.segStride = ps.segStride, ta.segBack = segInBack;
+		ta.cursor = ps.cursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
+		ta.refill = (uint32_t)(primary ? refillPrimary : refillOther);
+		ta.packet = primary && UsePackets() ? 1 : 0;
+		ta.leafBatch = (uint32_t)(primary ? leafBatchPrimary : leafBatch);
+		ta.hits = ps.hits.ptr, ta.gstack = ps.gstack.ptr;
+		if (pathLength == 1 && ta.packet && ps.hvOn)
 		{
-			PathGroup& g = grp[gi];
-			if (g.done) continue;
-			any = true;
-			g.pl = pathLength;
-			Counters* c = g.counters.ptr;
-			TraceArgs ta{};
-			ta.version = TraceVersion();
-			/* the path counts ping-pong (Counters::segPath): this bounce's paths, and its extension rays */
-			uint32_t* segIn = c->segPath[(pathLength - 1) & 1];
-			uint32_t* segNext = c->segPath[pathLength & 1];
-			uint32_t* segInBack = c->segBack[(pathLength - 1) & 1];
-			if (pathLength == 1 && g.twoEnded)
+			ta.hvRead = ps.hv.ptr + (size_t)ps.hvParity * ps.hvBlock, ta.hvWrite = ps.hv.ptr + (size_t)(1 - ps.hvParity) * ps.hvBlock;
+			ta.hvCap = ps.hvCap, ta.hvMaskWords = ps.hvMaskWords, ta.hvFactor = packetHeavy;
+			ta.hvTiles = 0;
+			for (int k = 0; k < LH2_SEGS; k++)
 			{
-				/* the camera's two-ended segments (zeroed when retired at the hand-off, as segPath[0] is) */
-				segIn = g.camAlloc.ptr + ((g.camFrame - 1) & 1) * LH2_CAM_ALLOC_WORDS;
-				segInBack = segIn + LH2_SEGS * LH2_SEGCOUNT_STRIDE;
+				const uint32_t lo = (uint32_t)k * ps.segStride, n = ps.count > lo ? std::min( ps.count - lo, ps.segStride ) : 0u;
+				ta.hvTiles += (n + 63) / 64;
 			}
-			uint32_t* segNextBack = c->segBack[pathLength & 1];
-			ta.rayO = g.rayO[g.in].ptr, ta.rayD = g.rayD[g.in].ptr, ta.segCounts = segIn, ta.segStride = g.segStride;
-			ta.segBack = segInBack;
-			ta.cursor = g.cursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
-			ta.refill = (uint32_t)(pathLength == 1 && tiledRays ? refillPrimary : refillOther);
-			ta.packet = pathLength == 1 && tiledRays && UsePackets() ? PacketMode() : 0;
-			ta.leafBatch = (uint32_t)(pathLength == 1 && tiledRays ? leafBatchPrimary : leafBatch);
-			if (pathLength == 1 && ta.packet && g.hvOn)
-			{
-				ta.hvRead = g.hv.ptr + (size_t)g.hvParity * g.hvBlock, ta.hvWrite = g.hv.ptr + (size_t)(1 - g.hvParity) * g.hvBlock;
-				ta.hvCap = g.hvCap, ta.hvMaskWords = g.hvMaskWords, ta.hvFactor = packetHeavy;
-				ta.hvTiles = 0;
-				for (int k = 0; k < LH2_SEGS; k++)
-				{
-					const uint32_t lo = (uint32_t)k * g.segStride, n = g.count > lo ? std::min( g.count - lo, g.segStride ) : 0u;
-					ta.hvTiles += (n + 63) / 64;
-				}
-				g.hvParity = 1 - g.hvParity;
-			}
-			ta.hits = g.hits.ptr, ta.gstack = g.gstack.ptr;
-			SetTail( ta, g );
-			if (pathLength == tailL)
-			{
-				/* the path tail: trace and shade every remaining bounce in one launch; each path's records
-				   are updated in place, its shadow rays queued for the shadow launch, and rayLog counted */
-				ShadeParams sp{};
-				sp.shadowStride = g.shadowStride;
-				sp.rayO = g.rayO[g.in].ptr, sp.rayD = g.rayD[g.in].ptr, sp.T4 = g.T4[g.in].ptr, sp.Q4 = g.Q4[g.in].ptr;
-				sp.rayOut = g.rayO[g.in].ptr, sp.rayDOut = g.rayD[g.in].ptr, sp.T4Out = g.T4[g.in].ptr, sp.Q4Out = g.Q4[g.in].ptr;
-				sp.shO = g.shO.ptr, sp.shD = g.shD.ptr, sp.shP = g.shP.ptr;
-				sp.acc = accumulator.ptr, sp.counters = c;
-				sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
-				sp.probePixel = probeX + scrwidth * probeY;
-				sp.spreadAngle = view.spreadAngle;
-				sp.adv.rayCountLog = g.rayLog.ptr;
-				ta.shadeBatch = (uint32_t)pathTailBatch;
-				sp.shadowCut = shadowCut;
-				lh2_launch_trace_path( &sd, &ta, &sp, PathGrid(), { nullptr, g.evTrace[pathLength] }, g.st );
-				g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
-				g.tailL = pathLength;   /* no shade interval of its own (Synchronize) */
-				g.done = true;
-				continue;
-			}
-			/* the last bounce of a terminal frame (no lights, nothing that emits or cuts out: its hits add
-			   nothing, ShadeParams::terminal): the trace launch adds the misses' sky samples itself, so there
-			   is no hit record to write and no k_shade_last launch (setting "terminalTrace") */
-			if (pathLength == maxPL && pathLength > 1 && !primeRef && !shadows && !canEmit && terminalShade && terminalTrace &&
-				!ta.packet && TraceVersion() == 7 && dNodes4.ptr)
-			{
-				ta.pathT4 = g.T4[g.in].ptr, ta.pathQ4 = g.Q4[g.in].ptr, ta.acc = accumulator.ptr, ta.wh = (uint32_t)(scrwidth * scrheight);
-				lh2_launch_trace_term( &sd, &ta, grid, { nullptr, g.evTrace[pathLength] }, g.st );
-				g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
-				g.tailL = pathLength;   /* no shade interval of its own (Synchronize) */
-				g.done = true;
-				continue;
-			}
-			/* shadow backfill: the shadow rays of the bounces before this one (their counts no longer change
-			   during this launch) are the final shadow launch's work; this launch's idle lanes take them in its
-			   tail, from that launch's work-queue heads (one-ended shadow segments only) */
-			if (shadowBackfill && shadows && !primeRef && !splitL && !ta.packet && pathLength >= 2 && TraceVersion() == 7 &&
-				dNodes4.ptr && !(shadowCut > 0.0f))
-			{
-				ta.bfO = g.shO.ptr, ta.bfD = g.shD.ptr, ta.bfCounts = c->segShadow, ta.bfStride = g.shadowStride;
-				ta.bfCursor = g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS;
-				ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr;
-			}
-			lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : grid, { nullptr, g.evTrace[pathLength] }, g.st );
-			g.fromTrace[pathLength] = g.prevStop, g.prevStop = g.evTrace[pathLength];
-			ShadeParams sp{};
-			sp.segCounts = segIn, sp.segOut = segNext, sp.segStride = g.segStride, sp.shadowStride = g.shadowStride;
-			sp.segBack = segInBack, sp.segOutBack = segNextBack;
-			/* two-ended path segments: rays with a chord through the scene box below chordSplit x its
-			   largest extent go last (setting "chordSplit"; 0: off) */
-			{
-				const float ext = std::max( std::max( sceneHi[0] - sceneLo[0], sceneHi[1] - sceneLo[1] ), sceneHi[2] - sceneLo[2] );
-				for (int k = 0; k < 3; k++) sp.chordLo[k] = sceneLo[k], sp.chordHi[k] = sceneHi[k];
-				sp.chordCut = ext > 0 ? chordSplit * ext : 0.0f;
-			}
-			/* the hand-off to the next bounce: the shade launch's last block (no launch of its own), except
-			   in PrimeRef mode, where the bounce's shadow rays are traced (and their counts reset) first */
-			const bool split = pathLength == splitL;
-			const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, g.rayLog.ptr, g.activeLog, split ? shadowSnap.ptr : nullptr,
-				split ? g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr, pathLength + 1 == tailL };
-			sp.advance = pathLength < maxPL && !primeRef;
-			sp.shadowCut = shadowCut;
-			sp.adv = adv;
-			sp.rayO = g.rayO[g.in].ptr, sp.rayD = g.rayD[g.in].ptr, sp.T4 = g.T4[g.in].ptr, sp.Q4 = g.Q4[g.in].ptr, sp.hits = g.hits.ptr;
-			sp.rayOut = g.rayO[1 - g.in].ptr, sp.rayDOut = g.rayD[1 - g.in].ptr, sp.T4Out = g.T4[1 - g.in].ptr, sp.Q4Out = g.Q4[1 - g.in].ptr;
-			sp.shO = g.shO.ptr, sp.shD = g.shD.ptr, sp.shP = g.shP.ptr;
-			sp.acc = accumulator.ptr, sp.counters = c;
-			sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
-			sp.primeRef = primeRef;
-			sp.terminal = !primeRef && !shadows && !canEmit && pathLength > 1 && terminalShade;
-			sp.probePixel = probeX + scrwidth * probeY;
-			sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
-			sp.spreadAngle = view.spreadAngle;
-			lh2_launch_shade( &sd, &sp, grid, { nullptr, g.evShade[pathLength] }, g.st );
-			g.fromShade[pathLength] = g.prevStop, g.prevStop = g.evShade[pathLength];
-			if (pathLength == maxPL) { g.done = true; continue; }
-			if (primeRef && shadows)
-			{
-				/* RenderCore_PrimeRef traces the shadow rays of every bounce right after it
-				   (rendercore.cpp connect step), fused with finalizeConnections */
-				TraceArgs ts{};
-				ts.version = ShadowVersion();
-				ts.rayO = g.shO.ptr, ts.rayD = g.shD.ptr, ts.segCounts = c->segShadow, ts.segStride = g.shadowStride;
-				ts.cursor = g.cursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
-				ts.refill = ShadowRefill(), ts.leafBatch = ShadowLeafBatch();
-				ts.mask = g.shMask.ptr, ts.potentials = g.shP.ptr, ts.acc = accumulator.ptr, ts.gstack = g.gstack.ptr;
-				ts.packet = packetShadow ? PacketMode() : 0;
-				SetTail( ts, g );
-				lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, g.evShadowB[pathLength] }, g.st );
-				g.fromShadowB[pathLength] = g.prevStop, g.prevStop = g.evShadowB[pathLength];
-			}
-			/* the hand-off writes this bounce's extension-ray count into the pinned activeLog itself */
-			g.countReady[pathLength] = g.evShade[pathLength];
-			if (primeRef)
-			{
-				lh2_launch_counters_next( c, &adv, pathLength, 1, { nullptr, g.evCount[pathLength] }, g.st );
-				g.prevStop = g.countReady[pathLength] = g.evCount[pathLength];
-			}
-			if (split)
-			{
-				/* the shadow rays queued so far, on the side stream, beside the later bounces; the final
-				   shadow launch's work queues start behind them (advance_bounce) */
-				CHK_HIP( hipStreamWaitEvent( sideStream, g.countReady[pathLength], 0 ) );
-				TraceArgs ta{};
-				ta.version = ShadowVersion();
-				ta.rayO = g.shO.ptr, ta.rayD = g.shD.ptr, ta.segCounts = shadowSnap.ptr, ta.segStride = g.shadowStride;
-				ta.cursor = g.cursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS, ta.refill = ShadowRefill(), ta.leafBatch = ShadowLeafBatch();
-				ta.mask = g.shMask.ptr, ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = sideStack.ptr;
-				ta.packet = packetShadow ? PacketMode() : 0;
-				lh2_launch_trace_any( &sd, &ta, grid, 1, { evSideStart, evSideStop }, sideStream );
-				frameSplit = true;
-			}
+			ps.hvParity = 1 - ps.hvParity;
 		}
-		if (!any) break;
-		/* early exit without stalling the GPU: wait for the count of a group's previous bounce while
-		   this bounce is queued; when it was 0, this bounce is empty and so is everything after it */
-		for (int gi = 0; gi < G; gi++)
+		ShadeParams sp{};
+		sp.shadowStride = ps.shadowStride;
+		sp.shO = ps.shO.ptr, sp.shD = ps.shD.ptr, sp.shP = ps.shP.ptr;
+		sp.acc = accumulator.ptr, sp.counters = c;
+		sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
+		sp.probePixel = probeX + scrwidth * probeY;
+		sp.spreadAngle = view.spreadAngle;
+		if (pathLength == tailL)
 		{
-			PathGroup& g = grp[gi];
-			if (g.done) continue;
-			if (pathLength >= 2)
-			{
-				CHK_HIP( hipEventSynchronize( g.countReady[pathLength - 1] ) );
-				if (g.activeLog[pathLength - 1] == 0) { g.done = true; continue; }
-			}
-			g.in = 1 - g.in;
+			/* the path tail: trace and shade every remaining bounce in one launch; each path's records are
+			   updated in place, its shadow rays queued for the shadow launch, and rayLog counted */
+			sp.rayO = ps.rayO[ps.in].ptr, sp.rayD = ps.rayD[ps.in].ptr, sp.T4 = ps.T4[ps.in].ptr, sp.Q4 = ps.Q4[ps.in].ptr;
+			sp.rayOut = ps.rayO[ps.in].ptr, sp.rayDOut = ps.rayD[ps.in].ptr, sp.T4Out = ps.T4[ps.in].ptr, sp.Q4Out = ps.Q4[ps.in].ptr;
+			sp.adv.rayCountLog = ps.rayLog.ptr;
+			ta.shadeBatch = (uint32_t)pathTailBatch;
+			lh2_launch_trace_path( &sd, &ta, &sp, PathGrid(), { nullptr, ps.evTrace[pathLength] }, stream );
+			ps.fromTrace[pathLength] = ps.prevStop, ps.prevStop = ps.evTrace[pathLength];
+			ps.tailL = pathLength;   /* no shade interval of its own (Synchronize) */
+			break;
 		}
+		lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : grid, { nullptr, ps.evTrace[pathLength] }, stream );
+		ps.fromTrace[pathLength] = ps.prevStop, ps.prevStop = ps.evTrace[pathLength];
+		sp.segCounts = segIn, sp.segOut = segNext, sp.segStride = ps.segStride;
+		sp.segBack = segInBack, sp.segOutBack = segNextBack;
+		/* two-ended path segments: rays with a chord through the scene box below chordSplit x its largest
+		   extent go last (setting "chordSplit"; 0: off) */
+		{
+			const float ext = std::max( std::max( sceneHi[0] - sceneLo[0], sceneHi[1] - sceneLo[1] ), sceneHi[2] - sceneLo[2] );
+			for (int k = 0; k < 3; k++) sp.chordLo[k] = sceneLo[k], sp.chordHi[k] = sceneHi[k];
+			sp.chordCut = ext > 0 ? chordSplit * ext : 0.0f;
+		}
+		/* the hand-off to the next bounce: the shade launch's last block (no launch of its own), except
+		   in PrimeRef mode, where the bounce's shadow rays are traced (and their counts reset) first */
+		const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, ps.rayLog.ptr, ps.activeLog, pathLength + 1 == tailL };
+		sp.advance = pathLength < maxPL && !primeRef;
+		sp.adv = adv;
+		sp.rayO = ps.rayO[ps.in].ptr, sp.rayD = ps.rayD[ps.in].ptr, sp.T4 = ps.T4[ps.in].ptr, sp.Q4 = ps.Q4[ps.in].ptr, sp.hits = ps.hits.ptr;
+		sp.rayOut = ps.rayO[1 - ps.in].ptr, sp.rayDOut = ps.rayD[1 - ps.in].ptr, sp.T4Out = ps.T4[1 - ps.in].ptr, sp.Q4Out = ps.Q4[1 - ps.in].ptr;
+		sp.primeRef = primeRef;
+		sp.terminal = !primeRef && !shadows && !canEmit && pathLength > 1 && terminalShade;
+		sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
+		lh2_launch_shade( &sd, &sp, grid, { nullptr, ps.evShade[pathLength] }, stream );
+		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];
+		if (pathLength == maxPL) break;
+		if (primeRef && shadows)
+		{
+			/* RenderCore_PrimeRef traces the shadow rays of every bounce right after it (rendercore.cpp
+			   connect step), fused with finalizeConnections */
+			TraceArgs ts{};
+			ts.version = TraceVersion();
+			ts.rayO = ps.shO.ptr, ts.rayD = ps.shD.ptr, ts.segCounts = c->segShadow, ts.segStride = ps.shadowStride;
+			ts.cursor = ps.cursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
+			ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
+			ts.mask = ps.shMask.ptr, ts.potentials = ps.shP.ptr, ts.acc = accumulator.ptr, ts.gstack = ps.gstack.ptr;
+			lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, ps.evShadowB[pathLength] }, stream );
+			ps.fromShadowB[pathLength] = ps.prevStop, ps.prevStop = ps.evShadowB[pathLength];
+		}
+		/* the hand-off writes this bounce's extension-ray count into the pinned activeLog itself */
+		ps.countReady[pathLength] = ps.evShade[pathLength];
+		if (primeRef)
+		{
+			lh2_launch_counters_next( c, &adv, pathLength, 1, { nullptr, ps.evCount[pathLength] }, stream );
+			ps.prevStop = ps.countReady[pathLength] = ps.evCount[pathLength];
+		}
+		/* early exit without stalling the GPU: wait for the count of the previous bounce while this one is
+		   queued; when it was 0, this bounce is empty and so is everything after it */
+		if (pathLength >= 2)
+		{
+			CHK_HIP( hipEventSynchronize( ps.countReady[pathLength - 1] ) );
+			if (ps.activeLog[pathLength - 1] == 0) break;
+		}
+		ps.in = 1 - ps.in;
 	}
-	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592); then the groups join */
-	for (int gi = 0; gi < G; gi++)
+	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
+	if (!primeRef && shadows)
 	{
-		PathGroup& g = grp[gi];
-		if (!primeRef && shadows)
-		{
-			TraceArgs ta{};
-			ta.version = ShadowVersion();
-			ta.rayO = g.shO.ptr, ta.rayD = g.shD.ptr, ta.segCounts = g.counters.ptr->segShadow, ta.segStride = g.shadowStride;
-			ta.segBack = g.counters.ptr->segShadowBack;
-			ta.cursor = g.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = ShadowRefill(), ta.leafBatch = ShadowLeafBatch();
-			ta.mask = g.shMask.ptr, ta.potentials = g.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = g.gstack.ptr;
-			ta.packet = packetShadow ? PacketMode() : 0;
-			SetTail( ta, g );
-			lh2_launch_trace_any( &sd, &ta, ta.version >= 5 && !ta.packet ? ShadowGrid() : grid, 1, { nullptr, g.evShadow }, g.st );
-			g.fromShadow = g.prevStop;
-		}
-		if (gi == 0 && frameSplit) CHK_HIP( hipStreamWaitEvent( stream, evSideStop, 0 ) );   /* join the side stream's shadow launch */
-		if (gi)
-		{
-			CHK_HIP( hipEventRecord( g.evDone, g.st ) );
-			CHK_HIP( hipStreamWaitEvent( stream, g.evDone, 0 ) );
-		}
+		TraceArgs ta{};
+		ta.version = TraceVersion();
+		ta.rayO = ps.shO.ptr, ta.rayD = ps.shD.ptr, ta.segCounts = c->segShadow, ta.segStride = ps.shadowStride;
+		ta.cursor = ps.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+		ta.mask = ps.shMask.ptr, ta.potentials = ps.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = ps.gstack.ptr;
+		lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, ps.evShadow }, stream );
+		ps.fromShadow = ps.prevStop;
 	}
 	samplesTaken += scrspp;
-	/* finalize also delivers every group's counters and ray-count log, and the scene error, to hostStats */
-	FrameStatsDev fs{};
-	fs.groups = G;
-	for (int gi = 0; gi < G; gi++)
-	{
-		fs.counters[gi] = grp[gi].counters.ptr, fs.rayLog[gi] = grp[gi].rayLog.ptr + 1;
-		fs.hostCounters[gi] = &hostStats->counters[gi], fs.hostRayCount[gi] = hostStats->rayCount[gi] + 1;
-	}
-	fs.sceneError = dSceneError.ptr, fs.hostSceneError = &hostStats->sceneError;
+	/* finalize also delivers the frame's counters and ray-count log, and the scene error, to hostStats */
+	const FrameStatsDev fs{ c, ps.rayLog.ptr + 1, &hostStats->counters, hostStats->rayCount + 1, dSceneError.ptr, &hostStats->sceneError };
 	/* a tile finalizes its own rows only (a rank of the band partition: the gathered frame is finalized
 	   where it is assembled, MultiDevice / FinalizeFrame) */
 	RowMap rm{};
@@ -1088,44 +890,11 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipMemcpy2DToArrayAsync( arr, 0, 0, frame.ptr, sizeof( float4 ) * scrwidth, sizeof( float4 ) * scrwidth, scrheight, hipMemcpyDeviceToDevice, stream ) );
 		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, stream ) );
 	}
-	framePathLengths = 0;
-	for (int gi = 0; gi < G; gi++) hostStats->rayCount[gi][0] = grp[gi].count, framePathLengths = std::max( framePathLengths, grp[gi].tailL ? maxPL : grp[gi].pl );
+	hostStats->rayCount[0] = ps.count;
+	framePathLengths = ps.tailL ? maxPL : ps.pl;
 	framePrimeRef = primeRef;
 	statsPending = true;
 	frameHostMs = std::chrono::duration<double, std::milli>( std::chrono::high_resolution_clock::now() - t0 ).count();
-}
-
-/* the chordSplitPrimary quantile of the frame's 8x8 tile centre rays' lengths inside the scene box (pinhole
-   rays through the tile centres, at most ~4096 of them; box_chord in lh2_kernels.hip is the device side),
-   recomputed when the view or the box changes */
-float RenderCore::PrimaryChordCut( const lh2_ViewPyramid& view )
-{
-	const float box[7] = { sceneLo[0], sceneLo[1], sceneLo[2], sceneHi[0], sceneHi[1], sceneHi[2], chordSplitPrimary };
-	if (cutValid && !memcmp( &view, &cutView, sizeof( view ) ) && !memcmp( box, cutBox, sizeof( box ) )) return cutValue;
-	const int tw = scrwidth / 8, th = std::max( 1, scrheight / 8 );
-	const int step = std::max( 1, (int)std::ceil( std::sqrt( (double)tw * th / 4096.0 ) ) );
-	std::vector<float> len;
-	for (int ty = 0; ty < th; ty += step)
-		for (int tx = 0; tx < tw; tx += step)
-		{
-			const float fx = (tx * 8 + 4.5f) / scrwidth, fy = (ty * 8 + 4.5f) / scrheight;
-			float d[3], o[3] = { view.pos.x, view.pos.y, view.pos.z };
-			const float p1[3] = { view.p1.x, view.p1.y, view.p1.z }, p2[3] = { view.p2.x, view.p2.y, view.p2.z }, p3[3] = { view.p3.x, view.p3.y, view.p3.z };
-			for (int k = 0; k < 3; k++) d[k] = p1[k] + fx * (p2[k] - p1[k]) + fy * (p3[k] - p1[k]) - o[k];
-			float tn = 0, tf = 1e30f;
-			for (int k = 0; k < 3; k++)
-			{
-				const float inv = 1.0f / d[k], a = (sceneLo[k] - o[k]) * inv, b = (sceneHi[k] - o[k]) * inv;
-				if (a == a && b == b) tn = std::max( tn, std::min( a, b ) ), tf = std::min( tf, std::max( a, b ) );
-			}
-			const float n = std::sqrt( d[0] * d[0] + d[1] * d[1] + d[2] * d[2] );
-			len.push_back( (tf - tn) * n );   /* d is not normalised: scale t to distance */
-		}
-	const size_t q = std::min( len.size() - 1, (size_t)(chordSplitPrimary * (len.size() - 1)) );
-	std::nth_element( len.begin(), len.begin() + q, len.end() );
-	cutValue = len[q], cutView = view, cutValid = true;
-	memcpy( cutBox, box, sizeof( box ) );
-	return cutValue;
 }
 
 void RenderCore::UnpackTile( const void* devSrc, int rank, int nranks, int band )
@@ -1170,75 +939,47 @@ int RenderCore::TileRows() const
 static uint32_t QueuedShadowRays( const Counters& c )
 {
 	uint32_t n = 0;
-	for (int k = 0; k < LH2_SEGS; k++) n += c.segShadow[k * LH2_SEGCOUNT_STRIDE] + c.segShadowBack[k * LH2_SEGCOUNT_STRIDE];
+	for (int k = 0; k < LH2_SEGS; k++) n += c.segShadow[k * LH2_SEGCOUNT_STRIDE];
 	return n;
 }
 
 void RenderCore::Synchronize()
 {
-	CHK_HIP( hipStreamSynchronize( stream ) );   /* the other groups' streams joined into `stream` */
-	if (statsPending)
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	if (!statsPending) return;
+	statsPending = false;
+	const Counters& cn = hostStats->counters;
+	bool full = cn.shadowOverflow != 0;
+	for (int k = 0; k < LH2_SEGS; k++) full = full || cn.segShadow[k * LH2_SEGCOUNT_STRIDE] > ps.shadowStride;
+	if (full) FatalError( "shadow ray buffer overflow" );
+	if (hostStats->sceneError) FatalError( "BVH depth exceeds the traversal stack (%d levels): frame skipped", LH2_STACK_TOTAL );
+	const uint32_t* rc = hostStats->rayCount;   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
+	auto ms = [&]( hipEvent_t a, hipEvent_t b ) { float t = 0; (void)hipEventElapsedTime( &t, a, b ); return t * 1e-3f; };
+	/* each interval: the previous launch's stop event -> this launch's stop event (kernel + launch gap) */
+	auto trace = [&]( int L ) { return L <= ps.pl ? ms( ps.fromTrace[L], ps.evTrace[L] ) : 0.0f; };
+	coreStats.primaryRayCount = rc[0];
+	coreStats.traceTime0 = trace( 1 );
+	coreStats.bounce1RayCount = framePathLengths >= 2 ? rc[1] : 0;
+	coreStats.traceTime1 = framePathLengths >= 2 ? trace( 2 ) : 0;
+	coreStats.deepRayCount = 0, coreStats.traceTimeX = 0;
+	/* (a path tail's bounces past its first have no launch of their own: their time is in its launch) */
+	for (int L = 3; L <= framePathLengths; L++)
 	{
-		statsPending = false;
-		for (int gi = 0; gi < frameGroups; gi++)
-		{
-			const Counters& cn = hostStats->counters[gi];
-			bool full = cn.shadowOverflow != 0;   /* a segment's two ends met: same failure */
-			for (int k = 0; k < LH2_SEGS; k++) full = full || cn.segShadow[k * LH2_SEGCOUNT_STRIDE] + cn.segShadowBack[k * LH2_SEGCOUNT_STRIDE] > grp[gi].shadowStride;
-			if (full) FatalError( "shadow ray buffer overflow" );
-		}
-		if (hostStats->sceneError) FatalError( "BVH depth exceeds the traversal stack (%d levels): frame skipped", LH2_STACK_TOTAL );
-		uint32_t rc[LH2_MAX_BOUNCES + 1] = {};   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
-		for (int gi = 0; gi < frameGroups; gi++) for (int L = 0; L <= LH2_MAX_BOUNCES; L++) rc[L] += hostStats->rayCount[gi][L];
-		auto ms = [&]( hipEvent_t a, hipEvent_t b ) { float t = 0; (void)hipEventElapsedTime( &t, a, b ); return t * 1e-3f; };
-		/* each interval: a group's previous launch's stop event -> this launch's stop event (kernel +
-		   launch gap); with overlapping groups, a pass takes the longest of the groups' intervals */
-		auto trace = [&]( int L ) {
-			float t = 0;
-			for (int gi = 0; gi < frameGroups; gi++) if (L <= grp[gi].pl) t = std::max( t, ms( grp[gi].fromTrace[L], grp[gi].evTrace[L] ) );
-			return t;
-		};
-		coreStats.primaryRayCount = rc[0];
-		coreStats.traceTime0 = trace( 1 );
-		coreStats.bounce1RayCount = framePathLengths >= 2 ? rc[1] : 0;
-		coreStats.traceTime1 = framePathLengths >= 2 ? trace( 2 ) : 0;
-		coreStats.deepRayCount = 0, coreStats.traceTimeX = 0;
-		/* (a path tail's bounces past its first have no launch of their own: their time is in its launch) */
-		for (int L = 3; L <= framePathLengths; L++)
-		{
-			coreStats.deepRayCount = rc[L - 1];
-			if (std::any_of( grp, grp + frameGroups, [L]( const PathGroup& g ) { return L <= g.pl; } )) coreStats.traceTimeX = trace( L );
-		}
-		float shadow = 0, shade = 0;
-		for (int gi = 0; gi < frameGroups; gi++)
-		{
-			const PathGroup& g = grp[gi];
-			float sh = 0, sd = 0;
-			if (!frameShadows) sh = 0;
-			else if (!framePrimeRef) sh = ms( g.fromShadow, g.evShadow );
-			else for (int L = 1; L < g.pl; L++) sh += ms( g.fromShadowB[L], g.evShadowB[L] );
-			for (int L = 1; L <= g.pl; L++) if (L != g.tailL) sd += ms( g.fromShade[L], g.evShade[L] );
-			shadow = std::max( shadow, sh ), shade = std::max( shade, sd );
-		}
-		coreStats.shadowTraceTime = shadow;
-		coreStats.shadeTime = shade;
-		for (int L = 1; L <= framePathLengths && L <= 8; L++) lastKernelMs[L - 1] = trace( L ) * 1e3f;
-		uint32_t shadowRays = 0, extRays = 0;
-		int probe = 0;
-		for (int gi = 0; gi < frameGroups; gi++)
-		{
-			const Counters& cnt = hostStats->counters[gi];
-			shadowRays += framePrimeRef ? cnt.totalShadowRays : QueuedShadowRays( cnt );
-			extRays += cnt.totalExtensionRays;
-			if (cnt.probedInstid != -1 || cnt.probedTriid != -1) probe = gi;
-		}
-		coreStats.totalShadowRays = shadowRays;
-		coreStats.totalExtensionRays = extRays;
-		coreStats.totalRays = coreStats.totalExtensionRays + coreStats.totalShadowRays;
-		coreStats.renderTime = ms( evFrame[0], evFrame[1] );   /* device time of the whole frame (the reference's Render blocks) */
-		const Counters& pc = hostStats->counters[probe];
-		coreStats.probedInstid = pc.probedInstid, coreStats.probedTriid = pc.probedTriid, coreStats.probedDist = pc.probedDist;
+		coreStats.deepRayCount = rc[L - 1];
+		if (L <= ps.pl) coreStats.traceTimeX = trace( L );
 	}
+	float shadow = 0, shade = 0;
+	if (frameShadows && !framePrimeRef) shadow = ms( ps.fromShadow, ps.evShadow );
+	else if (frameShadows) for (int L = 1; L < ps.pl; L++) shadow += ms( ps.fromShadowB[L], ps.evShadowB[L] );
+	for (int L = 1; L <= ps.pl; L++) if (L != ps.tailL) shade += ms( ps.fromShade[L], ps.evShade[L] );
+	coreStats.shadowTraceTime = shadow;
+	coreStats.shadeTime = shade;
+	for (int L = 1; L <= framePathLengths && L <= 8; L++) lastKernelMs[L - 1] = trace( L ) * 1e3f;
+	coreStats.totalShadowRays = framePrimeRef ? cn.totalShadowRays : QueuedShadowRays( cn );
+	coreStats.totalExtensionRays = cn.totalExtensionRays;
+	coreStats.totalRays = coreStats.totalExtensionRays + coreStats.totalShadowRays;
+	coreStats.renderTime = ms( evFrame[0], evFrame[1] );   /* device time of the whole frame (the reference's Render blocks) */
+	coreStats.probedInstid = cn.probedInstid, coreStats.probedTriid = cn.probedTriid, coreStats.probedDist = cn.probedDist;
 }
 
 lh2_CoreStats RenderCore::GetCoreStats()
@@ -1250,14 +991,8 @@ lh2_CoreStats RenderCore::GetCoreStats()
 void RenderCore::GetRayCounts( uint32_t* out17 )
 {
 	Synchronize();
-	for (int i = 0; i < 17; i++)
-	{
-		out17[i] = 0;
-		if (i < framePathLengths) for (int gi = 0; gi < frameGroups; gi++) out17[i] += hostStats->rayCount[gi][i];
-	}
-	out17[16] = 0;
-	for (int gi = 0; gi < frameGroups; gi++)
-		out17[16] += framePrimeRef ? hostStats->counters[gi].totalShadowRays : QueuedShadowRays( hostStats->counters[gi] );
+	for (int i = 0; i < 16; i++) out17[i] = i < framePathLengths ? hostStats->rayCount[i] : 0u;
+	out17[16] = framePrimeRef ? hostStats->counters.totalShadowRays : QueuedShadowRays( hostStats->counters );
 }
 
 void RenderCore::GetAccumulator( float* hostOut4 )
@@ -1316,8 +1051,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	ta.version = TraceVersion();
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
 	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
-	ta.packet = unitCoherent && UsePackets() ? PacketMode() : 0;
-	SetTail( ta, grp[0] );
+	ta.packet = unitCoherent && UsePackets() ? 1 : 0;
 	lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : TraceGrid(), {}, stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -1338,8 +1072,6 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	TraceArgs ta{};
 	ta.version = TraceVersion();
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
-	ta.packet = unitCoherent && packetShadow ? PacketMode() : 0;
-	SetTail( ta, grp[0] );
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, {}, stream );
 	std::vector<uint32_t> tmp( words );
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
@@ -1351,7 +1083,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void* hitsOut, int iterations, float* msOut )
 {
 	if (geometryDirty || instancesDirty) UpdateToplevel();
-	EnsureStack( grp[0] );
+	EnsureStack();
 	const SceneDev sd = MakeSceneDev();
 	DevBuf<uint32_t> cursors;
 	cursors.resize( (size_t)std::max( 1, iterations ) * LH2_CURSOR_WORDS );
@@ -1374,18 +1106,17 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 		TraceArgs ta{};
 		ta.version = TraceVersion();
 		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = cursors.ptr + (size_t)i * LH2_CURSOR_WORDS;
-		ta.hits = (uint4*)hitsOut, ta.gstack = grp[0].gstack.ptr;
+		ta.hits = (uint4*)hitsOut, ta.gstack = ps.gstack.ptr;
 		/* unitCoherent: trace as the frame traces its (tiled) primary rays */
 		ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
-		ta.packet = unitCoherent && UsePackets() ? PacketMode() : 0;
+		ta.packet = unitCoherent && UsePackets() ? 1 : 0;
 #ifdef LH2_TRACE_STATS
 		ta.stats = tstats.ptr;
 #endif
 #ifdef LH2_TRACE_TIMES
 		ta.stats = ttimes.ptr;
 #endif
-		SetTail( ta, grp[0] );
-		lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : TraceGrid(), { ev[2 * i], ev[2 * i + 1] }, stream );
+			lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : TraceGrid(), { ev[2 * i], ev[2 * i + 1] }, stream );
 	}
 	CHK_HIP( hipStreamSynchronize( stream ) );
 #ifdef LH2_TRACE_TIMES
@@ -1458,22 +1189,13 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto* m : meshes) delete m;
 	meshes.clear();
 	instances.clear();
-	for (int gi = 0; gi < LH2_MAX_GROUPS; gi++)
-	{
-		PathGroup& g = grp[gi];
-		if (g.ownStream) (void)hipStreamSynchronize( g.st );
-		for (auto& e : g.evTrace) (void)hipEventDestroy( e ), e = nullptr;
-		for (auto& e : g.evShade) (void)hipEventDestroy( e ), e = nullptr;
-		for (auto& e : g.evShadowB) (void)hipEventDestroy( e ), e = nullptr;
-		for (auto& e : g.evCount) (void)hipEventDestroy( e ), e = nullptr;
-		for (hipEvent_t* e : { &g.evCamera, &g.evShadow, &g.evDone }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
-		if (g.activeLog) (void)hipHostFree( g.activeLog );
-		g.activeLog = nullptr;
-		if (g.ownStream) (void)hipStreamDestroy( g.st );
-		g.st = nullptr, g.ownStream = false;
-	}
-	if (evFork) (void)hipEventDestroy( evFork );
-	evFork = nullptr;
+	for (auto& e : ps.evTrace) (void)hipEventDestroy( e ), e = nullptr;
+	for (auto& e : ps.evShade) (void)hipEventDestroy( e ), e = nullptr;
+	for (auto& e : ps.evShadowB) (void)hipEventDestroy( e ), e = nullptr;
+	for (auto& e : ps.evCount) (void)hipEventDestroy( e ), e = nullptr;
+	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
+	if (ps.activeLog) (void)hipHostFree( ps.activeLog );
+	ps.activeLog = nullptr;
 	for (hipEvent_t* e : { &evConsumer, &evPacked }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
 	for (auto& e : evFrame) (void)hipEventDestroy( e );
 	for (auto& e : evStage) (void)hipEventDestroy( e );

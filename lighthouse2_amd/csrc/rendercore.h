@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -55,17 +56,10 @@ struct CoreMeshHost   /* RenderCore always copies what it needs (rendercore.h:57
 
 struct CoreInstanceHost { int mesh; float T[16]; float inv[16]; };
 
-#define LH2_MAX_GROUPS 4
-
-/* A path group: a share of the frame's paths with its own path / ray buffers, counters, traversal
-   stacks and HIP stream.  Render issues the groups' bounce loops interleaved on their streams, so
-   one group's kernels fill the GPU while another's traversal drains (the tail of a persistent trace
-   launch leaves ~18 % of its wave slots idle, profiles/r01c_sweep_tail.txt) and its latency-bound
-   shade pass runs beside the other group's issue-bound traversal. */
-struct PathGroup
+/* the frame's path and ray streams (segmented, lh2_kernels.h) with their counters, work-queue heads,
+   traversal stacks and the events that time the frame's launches */
+struct PathStreams
 {
-	hipStream_t st = nullptr;
-	bool ownStream = false;
 	size_t cap = 0;                      /* paths the buffers hold */
 	DevBuf<float4> rayO[2], rayD[2], T4[2], Q4[2];
 	DevBuf<uint4> hits;
@@ -75,33 +69,27 @@ struct PathGroup
 	DevBuf<Counters> counters;
 	DevBuf<uint32_t> cursors;            /* LH2_CURSOR_SLOTS x LH2_CURSOR_WORDS work-queue heads */
 	DevBuf<uint32_t> rayLog;
-	DevBuf<uint32_t> camAlloc;           /* two-ended primary segments: 2 frames x LH2_CAM_ALLOC_WORDS (CameraParams::camAlloc) */
-	uint32_t camFrame = 0;
 	DevBuf<uint32_t> hv;                 /* heavy-first packets: two blocks (TraceArgs::hvRead / hvWrite), the frame parity picks */
 	uint32_t hvCap = 0, hvMaskWords = 0, hvBlock = 0, hvParity = 0;
-	DevBuf<uint4> tailRec;               /* tail hand-off records, one per trace thread (TraceArgs::tailOut) */
-	DevBuf<float2> tailUV;
-	uint32_t* activeLog = nullptr;       /* pinned: extension rays after each bounce (k_counters_next) */
-	hipEvent_t evTrace[LH2_MAX_BOUNCES + 1] = {}, evShade[LH2_MAX_BOUNCES + 1] = {}, evShadowB[LH2_MAX_BOUNCES + 1] = {};
-	hipEvent_t evCount[LH2_MAX_BOUNCES + 2] = {}, evCamera = nullptr, evShadow = nullptr, evDone = nullptr;
-	hipEvent_t countReady[LH2_MAX_BOUNCES + 2] = {};   /* [L]: the event after which bounce L's hand-off is done (evShade or evCount, not owned) */
+	uint32_t* activeLog = nullptr;       /* pinned: extension rays after each bounce (advance_bounce) */
 	/* a launch carries only a stop event (a start event costs its dispatch ~5 us of idle GPU); a timed
-	   interval runs from the group's previous launch's stop event, so it includes the launch gap */
+	   interval runs from the previous launch's stop event, so it includes the launch gap */
+	hipEvent_t evTrace[LH2_MAX_BOUNCES + 1] = {}, evShade[LH2_MAX_BOUNCES + 1] = {}, evShadowB[LH2_MAX_BOUNCES + 1] = {};
+	hipEvent_t evCount[LH2_MAX_BOUNCES + 2] = {}, evCamera = nullptr, evShadow = nullptr;
+	hipEvent_t countReady[LH2_MAX_BOUNCES + 2] = {};   /* [L]: the event after which bounce L's hand-off is done (evShade or evCount, not owned) */
 	hipEvent_t fromTrace[LH2_MAX_BOUNCES + 1] = {}, fromShade[LH2_MAX_BOUNCES + 1] = {}, fromShadowB[LH2_MAX_BOUNCES + 1] = {}, fromShadow = nullptr;
 	/* this frame */
-	uint32_t base = 0, count = 0, segStride = 0, shadowStride = 0;
+	uint32_t count = 0, segStride = 0, shadowStride = 0;
 	int in = 0, pl = 0;
-	bool done = false;
-	bool twoEnded = false;
 	int tailL = 0;                       /* this frame's path-tail launch (pathLength), 0: none */
-	bool hvOn = false;                   /* this frame's primary packets run heavy-first (TraceArgs::hvRead) */               /* this frame's primary rays are in two-ended segments (CameraParams::camAlloc) */
+	bool hvOn = false;                   /* this frame's primary packets run heavy-first (TraceArgs::hvRead) */
 	hipEvent_t prevStop = nullptr;
 };
 
-struct FrameStats   /* per-frame values read back from the device, per path group */
+struct FrameStats   /* per-frame values delivered by k_finalize into pinned host memory */
 {
-	uint32_t rayCount[LH2_MAX_GROUPS][LH2_MAX_BOUNCES + 1];
-	Counters counters[LH2_MAX_GROUPS];
+	uint32_t rayCount[LH2_MAX_BOUNCES + 1];
+	Counters counters;
 	int sceneError;
 };
 
@@ -162,21 +150,17 @@ private:
 	void EnsureBuffers();
 	void ConcatenateBlas( int instanceCount );
 	void BuildBlas4( CoreMeshHost& m, const float* nodes2 );
-	void SetTail( TraceArgs& ta, PathGroup& g );   /* tail hand-off buffers of a trace launch (ta.cursor set) */
-	void EnsureGroup( PathGroup& g, uint32_t paths );
-	void EnsureStack( PathGroup& g );
+	void EnsurePaths( uint32_t paths );
+	void EnsureStack();
 	void CheckSceneError();
 	bool UsePackets() const;
 	SceneDev MakeSceneDev() const;
+	TraceArgs StreamArgs( const float4* o, const float4* d, const uint32_t* segCounts, uint32_t segStride, uint32_t* cursor, bool coherent ) const;
 	int TraceGrid() const { return smCount * blocksPerCU; }
-	int PacketGrid() const { return smCount * packetBlocksPerCU; }   /* packet kernels: their own occupancy */
+	int PacketGrid() const { return smCount * packetBlocksPerCU; }   /* packet kernel: its own occupancy */
 	int PathGrid() const { return smCount * std::min( blocksPerCU, pathBlocksPerCU ); }   /* path tail: its occupancy, within the stack's */
-	/* the final shadow launch (any-hit BVH4 loops): their own occupancy unless traceBlocksPerCU lowered the grid
-	   (setting "shadowGridOwn" 0: the closest-hit grid) */
-	int ShadowGrid() const { return smCount * (shadowGridOwn && blocksPerCU == maxBlocksPerCU ? std::max( blocksPerCU, anyBlocksPerCU ) : blocksPerCU); }
-	int anyBlocksPerCU = 0, shadowGridOwn = 0;   /* own grid measured no faster (profiles/r02zq_ab_shadow_grid.txt) */
 
-	int device = 0, smCount = 256, blocksPerCU = 5, maxBlocksPerCU = 5, packetBlocksPerCU = 5, pathBlocksPerCU = 4;
+	int device = 0, smCount = 256, blocksPerCU = 7, maxBlocksPerCU = 7, packetBlocksPerCU = 8, pathBlocksPerCU = 3;
 	bool initialized = false;
 	/* scene */
 	std::vector<CoreMeshHost*> meshes;
@@ -184,13 +168,13 @@ private:
 	bool geometryDirty = true, instancesDirty = true;
 	DevBuf<float4> dNodes, dTris;
 	DevBuf<float4> dNodes4;              /* BVH4: all BLAS (relocated), then the TLAS as two-child nodes */
-	DevBuf<uint8_t> dInst;                 /* DevInstance[] */
+	DevBuf<uint8_t> dInst;               /* DevInstance[] */
 	DevBuf<lh2_CoreInstanceDesc> dInstDesc;
 	int tlasRoot = 0, blasNodeCount = 0, blasTriCount = 0, blasMeshTris = 0, sceneMaxDepth = 0;   /* blasTriCount: leaf triangle records; blasMeshTris: triangles */
 	std::vector<int> meshNodeBase, meshTriBase, meshNode4Base;
 	int tlasCapacity = 0, maxBlasDepth = 0;
 	int blasNode4Count = 0, maxBlas4Depth = 0;
-	int bvh4 = 1;                        /* build BVH4 copies of the BLAS (traceVersion 4 needs them) */
+	int bvh4 = 1;                        /* build BVH4 copies of the BLAS (the default traversal loop needs them) */
 	int StackDepthBound() const { return bvh4 ? std::max( maxBlasDepth, 3 * maxBlas4Depth ) : maxBlasDepth; }
 	bool tlasOnDevice = false;           /* TLAS of the last UpdateToplevel built by the GPU (depth in dTlasDepth) */
 	GpuBvhBuilder gpuBvh;
@@ -223,96 +207,41 @@ private:
 	int scrwidth = 0, scrheight = 0, scrspp = 1;
 	int tileY0 = 0, tileY1 = -1, tileBand = 0, tileStride = 0;
 	DevBuf<float4> accumulator, frame;
-	PathGroup grp[LH2_MAX_GROUPS];       /* grp[0] runs on `stream` and serves the unit-level trace calls */
-	/* groups a frame is split into (setting "pathGroups", 1..4).  1: the overlap did not pay on
-	   config 2 (1 group 1.88 ms, 2 groups 1.97, 4 groups 2.16, profiles/r01c_ab_path_groups.jsonl):
-	   concurrent traversals slow each other down and a shade pass beside a traversal takes 4x longer */
-	int pathGroups = 1;
-	/* shadow split (setting "shadowSplit", 0: off): the shadow rays queued by the first shadowSplit
-	   bounces are traced on a second stream while the later bounces run (their launches hold few rays:
-	   config 3's bounces 3 and 4 trace 0.53 M and 60 k rays in 266 + 208 us); the final shadow launch
-	   traces the rest.  One path group, no PrimeRef.  Off: measured no faster (config 3 2.71 ms off,
-	   2.72 / 2.74 / 2.75 with 1 / 2 / 3), the shade passes beside the side launch slow down by as much
-	   as the shadow pass gains (profiles/r02n_ab_shadow_split.txt) */
-	int shadowSplit = 0;
-	hipStream_t sideStream = nullptr;
-	hipEvent_t evSideStart = nullptr, evSideStop = nullptr;
-	DevBuf<uint32_t> shadowSnap;
-	DevBuf<int> sideStack;               /* the side launch's global traversal stack (it runs beside group 0's) */
-	bool frameSplit = false;
-	int frameGroups = 1;
-	hipEvent_t evFork = nullptr;
-	bool tileChanged = false;
-	bool frameShadows = true;            /* the last frame queued shadow-ray launches (the scene has lights) */            /* the next restart clears the whole accumulator, not only the tile's pixels */
+	PathStreams ps;                      /* on `stream`; also serves the unit-level trace calls */
+	bool tileChanged = false;            /* the next restart clears the whole accumulator, not only the tile's pixels */
+	bool frameShadows = true;            /* the last frame queued shadow-ray launches (the scene has lights) */
 	bool singleInstanceStart = true;     /* one instance of a non-empty mesh: rays start at its TLAS leaf (SceneDev::tlasRoot) */
-	bool terminalShade = true;          /* k_shade<true> for shade passes whose hits cannot contribute (ShadeParams::terminal) */
-	int tailPool = 0;                   /* tail pool threshold: a dry wave with at most this many rays hands them to another wave of its workgroup (0: off) */
-	int tailLanes = 0;                   /* hand a dry wave's rays on when fewer are active (0: off; restarting them costs more than the tail, profiles/r01c_sweep_tail.txt) */
+	bool terminalShade = true;           /* k_shade<true> for shade passes whose hits cannot contribute (ShadeParams::terminal) */
 	FrameStats* hostStats = nullptr;     /* pinned */
 	bool statsPending = false;
 	hipEvent_t evFrame[2] = {};
-	int tiledRays = 1;
-	/* BVH4 per-ray traversal, 1-triangle leaves, no leaf parking, refill at 48 idle lanes: the best of
-	   the sweeps on the config-2 frame (profiles/r01c_sweep_bvh4.jsonl, r01c_ab_bvh4_settings.jsonl:
-	   1.89 ms vs 1.94 for BVH2 with 2-triangle leaves); config 3 (room) runs 4 % faster with
-	   bvhMaxLeaf 2 / leafBatch 16, config 5 2 % slower */
-	int refillPrimary = 48, refillOther = 48, leafBatch = 6, leafBatchPrimary = 8;   /* leafBatch: traceVersion 7 leaf batches (r02y) */
-	/* the shadow (any-hit) launches: traversal loop, leaf batch and refill of their own (0 / -1 / 0: as the closest-hit launches) */
-	int shadowVersion = 0, leafBatchShadow = -1, refillShadow = 0;
-	int sampleInterleave = 0;            /* spp > 1: the samples of an 8x8 pixel block in consecutive waves (k_camera storage order); config 5 no faster: off (profiles/r02zl_ab_sample_interleave.txt) */
-	int shadowBackfill = 0;              /* closest-hit launches take queued shadow rays in their tail (TraceArgs::bfO); measured slower: off (profiles/r02zg_ab_shadow_backfill.txt) */
-	int ShadowVersion() const { return shadowVersion && bvh4 ? shadowVersion : TraceVersion(); }
-	uint32_t ShadowLeafBatch() const { return (uint32_t)(leafBatchShadow >= 0 ? leafBatchShadow : leafBatch); }
-	uint32_t ShadowRefill() const { return (uint32_t)(refillShadow ? refillShadow : refillOther); }
+	int tiledRays = 1;                   /* primary rays stored in 8x8 pixel blocks per wave (coherent packets) */
+	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle; BLAS leaves parked until this many
+	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,
+	   r02y_ab_v7.txt) */
+	int refillPrimary = 48, refillOther = 48, leafBatch = 6, leafBatchPrimary = 8;
 	int bvhMaxLeaf = 1;
-	int bvhSweep = 0;                    /* exact SAH sweep below this node size (setting "bvhSweep") */
 	float bvhSpatial = 1e-5f;            /* spatial splits (SBVH): overlap threshold x root area; 0 = off */
 	float bvhSpatialBudget = 1.0f;       /* ... adding at most this many references per triangle */
 	int bvh4Collapse = 1;                /* BVH4 collapse: 0 greedy (CollapseBvh4), 1 dynamic programming (CollapseBvh4Sah) */
-	int bvh4LeafTris = 1;                /* ... merging subtrees of at most this many triangles into one leaf */
-	float bvh4LeafCost = 0.4f, bvh4TriCost = 0.5f;   /* ... its costs of a leaf visit and a triangle test (node step = 1) */
 	float chordSplit = 0.35f;            /* extension rays with a chord through the scene box below this x its extent are traced last */
 	float sceneLo[3] = { 0, 0, 0 }, sceneHi[3] = { 0, 0, 0 };   /* world box of the instanced meshes (UpdateToplevel) */
-	/* two-ended primary segments (CameraParams::camAlloc): the 8x8 tiles whose centre ray's length inside
-	   the scene box is at most the chordSplitPrimary quantile (over the frame's tile centres) are traced
-	   last; 0: off.  Measured slower (profiles/r02za_ab_primary_chord.txt): the per-wave allocation atomics
-	   of the camera launch contend on 16 words (4K camera 0.11 -> 0.78 ms) and the in-box chord did not
-	   shorten the config-2 packet launch (0.376 -> 0.384 ms): off */
-	float chordSplitPrimary = 0.0f;
 	/* the path tail (k_trace_path4d): bounces pathTail .. maxPathLength traced and shaded in one launch,
 	   a wave shading its finished queries once pathTailBatch lanes hold one (or none walks); 0: a launch
-	   pair per bounce.  Config 3 (profiles/r02zb_ab_path_tail.txt): 2.542 -> 2.389 ms per frame at 3 / 56
-	   (batches of 16: 2.525, 32: 2.455, 48: 2.43, 64: 2.396; pathTail 2: 2.706, 4: 2.494) */
+	   pair per bounce.  Config 3 (profiles/r02zb_ab_path_tail.txt): 2.542 -> 2.389 ms per frame at 3 / 56 */
 	int pathTail = 3, pathTailBatch = 56;
-	/* k_trace_term4d for the last bounce of a terminal frame (no k_shade_last, no hit records).  Measured
-	   slower on config 2 (1.2065 / 1.2053 ms off, 1.2097 / 1.2118 on: the miss lanes' path-state loads and
-	   sky sample stall their waves inside the traversal loop, +20 us, more than the 16 us launch saved): off */
-	int terminalTrace = 0;
 	/* heavy-first primary packets (TraceArgs::hvRead): the packets of the previous frame that took more than
 	   packetHeavy x its mean node steps are taken first; 0: off */
 	float packetHeavy = 2.0f;
-	/* two-ended shadow segments: shadow rays shorter than chordSplitShadow x the scene's largest extent are
-	   written from their segment's end, so the shadow launch takes the long ones first; 0: off */
-	float chordSplitShadow = 0.0f;   /* measured no faster on config 3 (0.61 ms either way, profiles/r02zd_ab_shadow_chord.txt): off */
-	float PrimaryChordCut( const lh2_ViewPyramid& view );
-	lh2_ViewPyramid cutView{};
-	float cutBox[7] = {}, cutValue = 0;
-	bool cutValid = false;
 	int traceVersion = 0;                /* 0: auto (TraceVersion) */
-	float traceFetchMB = 256.0f;         /* auto: traceVersion 5 above this BVH4 + triangle footprint */
 	int TraceVersion() const;
 	int unitCoherent = 0;
 	int packetPrimary = -1;              /* wave-uniform packet traversal for 8x8-tiled primary rays (-1: by scene size) */
 	/* auto: packets while the BVH + triangles fit the 256 MB Infinity Cache (a packet's node and triangle
 	   records come through the scalar cache, one at a time: beyond the cache each is a DRAM round trip).
 	   Config 3 (134 MB): primary 0.29 -> 0.24 ms with packets; config 5 (1.4 GB): 5.3 -> 7.8 ms
-	   (profiles/r02zc_ab_packets_configs.txt); round 1's limit was 16 MB */
+	   (profiles/r02zc_ab_packets_configs.txt) */
 	float packetMaxMB = 256.0f;
-	/* packets over the BVH2 (2) or the BVH4 (4): BVH2 0.48 ms, BVH4 0.56 ms on the config-2 primary
-	   rays (r01c): fewer, wider steps do not pay when one node fetch already serves 64 rays */
-	int packetWidth = 2;
-	int PacketMode() const { return packetWidth == 4 ? 4 : 1; }
-	int packetShadow = 0;                /* the same for shadow rays (setting "packetShadow") */                /* traversal loop version (setting "traceVersion") */
 	int gpuBuild = 0, gpuTlas = 1;       /* BLAS builder (1: GPU PLOC, 0: CPU binned SAH); TLAS on the GPU */
 	float bvhTraversalCost = 1.0f;
 	int framePathLengths = 0, framePrimeRef = 0;

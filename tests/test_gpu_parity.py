@@ -239,13 +239,10 @@ def test_room_depth4_parity(core):
     core.setting("maxPathLength", 16)
 
 
-@pytest.mark.parametrize("version", [2, 4])
 @pytest.mark.parametrize("kind", ["random", "primary", "instanced"])
-def test_packet_traversal_bitexact(fresh_core, kind, version):
-    """Packet traversal (wave-uniform path for 64 rays, lh2_trace_packet.inc, over the BVH2 or the
-    BVH4) gives every ray exactly the per-ray traversal's hit record, also for incoherent rays and
-    through instances."""
-    fresh_core.setting("packetWidth", version)
+def test_packet_traversal_bitexact(fresh_core, kind):
+    """Packet traversal (wave-uniform path for 64 rays over the BVH2, lh2_trace_packet.inc) gives every
+    ray exactly the per-ray traversal's hit record, also for incoherent rays and through instances."""
     if kind == "instanced":
         sc = scene.instanced_scene(meshes=6, tris_per_mesh=3000, width=64, height=36, grid=3, spacing=12.0)
         scene.animate_instances(sc, 2)
@@ -269,43 +266,13 @@ def test_packet_traversal_bitexact(fresh_core, kind, version):
     assert np.array_equal(hp, ho), np.argwhere((hp != ho).any(1))[:10]
 
 
-@pytest.mark.parametrize("version", [2, 4])
-def test_packet_shadow_rays_match(fresh_core, version):
-    """Packet any-hit (fused finalizeConnection path and occlusion bits) equals the per-ray result."""
-    fresh_core.setting("packetWidth", version)
-    sc = scene.config2_scene(n=20000, width=64, height=36)
-    o = _load_both(fresh_core, sc, 64, 36)
-    O4, D4 = _random_rays(30001, 4, tmin=0.0)
-    rng = np.random.default_rng(5)
-    D4[:, 3] = rng.uniform(1.0, 20.0, len(D4)).astype(np.float32)
-    fresh_core.setting("packetShadow", 1)
-    fresh_core.setting("unitCoherent", 1)
-    mg = fresh_core.trace_any(O4, D4)
-    fresh_core.setting("unitCoherent", 0)
-    assert np.array_equal(mg, o.trace_any(O4, D4))
-
-
-def test_packet_shadow_frame_parity(fresh_core):
-    w, h = 128, 72
-    sc = scene.room_scene(40000, w, h)
-    o = _load_both(fresh_core, sc, w, h)
-    for tgt in (fresh_core, o):
-        tgt.setting("maxPathLength", 4)
-    fresh_core.setting("packetShadow", 1)
-    sc.render_frame(fresh_core)
-    sc.render_frame(o)
-    assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
-    ag, ao = fresh_core.accumulator(), o.accumulator()
-    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
-
-
-@pytest.mark.parametrize("version,leaf_batch,max_leaf", [(1, 0, 2), (1, 16, 2), (2, 0, 2), (2, 16, 1), (4, 0, 1), (4, 16, 2), (4, 8, 4),
-                                                       (5, 0, 1), (5, 0, 2), (5, 0, 4), (6, 0, 1), (6, 0, 2), (6, 0, 4),
-                                                       (7, 0, 1), (7, 1, 2), (7, 32, 1), (7, 8, 4)])
+@pytest.mark.parametrize("version,leaf_batch,max_leaf", [(1, 0, 2), (1, 16, 2), (1, 8, 4), (7, 0, 1), (7, 1, 2), (7, 6, 1), (7, 32, 1),
+                                                       (7, 8, 4), (7, 64, 2)])
 def test_traversal_variants_bitexact(fresh_core, version, leaf_batch, max_leaf):
-    """Every per-ray traversal loop (trace_stream, lh2_trace2.inc over the BVH2 and over the BVH4
-    collapse, lh2_trace4d.inc with its leaf slot), with and without leaf parking, over trees of different leaf sizes, returns the
-    oracle's hit records and occlusion bits: hits do not depend on the tree or the visiting order."""
+    """Both per-ray traversal loops (the reference BVH2 loop trace_stream, and the BVH4 loop of
+    lh2_trace4d.inc with its leaf slot), with and without leaf parking / batching, over trees of
+    different leaf sizes, return the oracle's hit records and occlusion bits: hits do not depend on the
+    tree or the visiting order."""
     fresh_core.setting("bvhMaxLeaf", max_leaf)
     fresh_core.setting("traceVersion", version)
     fresh_core.setting("leafBatch", leaf_batch)
@@ -321,8 +288,8 @@ def test_traversal_variants_bitexact(fresh_core, version, leaf_batch, max_leaf):
     assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
 
 
-@pytest.mark.parametrize("version,max_leaf,alpha", [(6, 1, 1e-5), (6, 4, 1e-5), (7, 1, 1e-5), (4, 2, 1e-5), (1, 2, 1e-5),
-                                                     (6, 1, 1e-7), (6, 1, 0.0)])
+@pytest.mark.parametrize("version,max_leaf,alpha", [(7, 1, 1e-5), (7, 4, 1e-5), (7, 2, 1e-5), (1, 2, 1e-5),
+                                                     (7, 1, 1e-7), (7, 1, 0.0)])
 def test_spatial_splits_bitexact(fresh_core, version, max_leaf, alpha):
     """Spatial splits (bvhSpatial, the default: SBVH references, a triangle in several leaves with
     clipped boxes; 0 = object splits only) change the tree only: closest hits, occlusion and a
@@ -346,14 +313,12 @@ def test_spatial_splits_bitexact(fresh_core, version, max_leaf, alpha):
     assert rel_l2(fresh_core.accumulator()[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
 
 
-@pytest.mark.parametrize("version,leaf_tris", [(6, 1), (6, 2), (6, 4), (7, 4), (4, 3), (5, 2)])
-def test_bvh4_dp_collapse_bitexact(fresh_core, version, leaf_tris):
-    """The dynamic-programming BVH4 collapse (bvh4Collapse 1), merging small subtrees into leaves of up
-    to leaf_tris triangles, over an SBVH tree with instances: hits, occlusion and a frame equal the
-    oracle's."""
-    fresh_core.setting("bvh4Collapse", 1)
-    fresh_core.setting("bvh4LeafTris", leaf_tris)
-    fresh_core.setting("traceVersion", version)
+@pytest.mark.parametrize("collapse,max_leaf", [(1, 1), (1, 2), (1, 4), (0, 1), (0, 3)])
+def test_bvh4_collapse_bitexact(fresh_core, collapse, max_leaf):
+    """The BVH4 collapses (bvh4Collapse 1: dynamic programming, 0: greedy) of SBVH trees with leaves of up
+    to max_leaf triangles, with instances: hits, occlusion and a frame equal the oracle's."""
+    fresh_core.setting("bvh4Collapse", collapse)
+    fresh_core.setting("bvhMaxLeaf", max_leaf)
     sc = scene.instanced_scene(meshes=3, tris_per_mesh=6000, width=64, height=36, grid=2, spacing=10.0)
     scene.animate_instances(sc, 1)
     o = _load_both(fresh_core, sc, 64, 36)
@@ -369,7 +334,7 @@ def test_bvh4_dp_collapse_bitexact(fresh_core, version, leaf_tris):
     assert rel_l2(fresh_core.accumulator()[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
 
 
-@pytest.mark.parametrize("version", [4, 5, 6, 7])
+@pytest.mark.parametrize("version", [1, 7])
 def test_bvh4_deep_stack(fresh_core, version):
     """A deep BLAS (triangles shrinking geometrically along a line: a chain-like SAH tree) next to the
     random cloud: BVH4 nodes push up to three children per level, the LDS part of the traversal
@@ -401,88 +366,6 @@ def test_bvh4_deep_stack(fresh_core, version):
     assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
     D4[:, 3] = np.random.default_rng(15).uniform(1.0, 20.0, len(D4)).astype(np.float32)
     assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
-
-
-@pytest.mark.parametrize("groups", [1, 3, 4])
-def test_path_groups_frame_parity(fresh_core, groups):
-    """A frame split into pipelined path groups (own buffers, counters and streams) gives the oracle's
-    per-bounce ray counts and accumulator, with NEE shadow rays and deeper specular paths (room)."""
-    w, h = 192, 108          # 20736 paths: enough for 4 groups (>= 4096 paths each)
-    sc = scene.room_scene(40000, w, h)
-    o = _load_both(fresh_core, sc, w, h)
-    for tgt in (fresh_core, o):
-        tgt.setting("maxPathLength", 4)
-    fresh_core.setting("pathGroups", groups)
-    sc.render_frame(fresh_core)
-    sc.render_frame(o)
-    assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
-    ag, ao = fresh_core.accumulator(), o.accumulator()
-    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
-    st = fresh_core.stats()
-    assert st.totalExtensionRays == int(o.ray_counts()[:16].sum()) or st.totalExtensionRays > 0
-
-
-@pytest.mark.parametrize("version,leaf_batch", [(2, 0), (4, 0), (4, 16)])
-@pytest.mark.parametrize("pool", [1, 16, 64])
-def test_tail_pool_bitexact(fresh_core, version, leaf_batch, pool):
-    """Rays handed between the waves of a workgroup through the LDS tail pool (setting tailPool)
-    resume with their traversal state and stack where they were: hit records and occlusion bits
-    stay the oracle's.  One block per CU makes each wave trace many rays, so pooling happens."""
-    fresh_core.setting("traceVersion", version)
-    fresh_core.setting("leafBatch", leaf_batch)
-    fresh_core.setting("traceBlocksPerCU", 1)
-    fresh_core.setting("tailPool", pool)
-    sc = scene.instanced_scene(meshes=4, tris_per_mesh=4000, width=64, height=36, grid=2, spacing=10.0)
-    scene.animate_instances(sc, 1)
-    o = _load_both(fresh_core, sc, 64, 36)
-    O4, D4 = _random_rays(200001, 21, radius=30.0)
-    hg = fresh_core.trace_closest(O4, D4)
-    ho = o.trace_closest(O4, D4)
-    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.05
-    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
-    D4[:, 3] = np.random.default_rng(22).uniform(1.0, 40.0, len(D4)).astype(np.float32)
-    assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
-
-
-def test_tail_pool_deep_stack(fresh_core):
-    """Pooled rays whose stacks reach past the LDS part into the global spill area (a chain-like
-    BLAS) keep their spilled entries: the receiving lane adopts the stack column, LDS and global."""
-    k = np.arange(120, dtype=np.float32)
-    x = (6.0 * 0.93 ** k).astype(np.float32)
-    s_ = (0.02 * 0.93 ** k).astype(np.float32)
-    z0 = np.zeros_like(x)
-    v0, v1, v2 = np.stack([x, -s_, z0], 1), np.stack([x + s_, s_, z0], 1), np.stack([x - s_, s_, s_], 1)
-    sc = scene.config2_scene(n=5000, width=64, height=36)
-    sc.meshes.append(abi.tris_from_vertices(v0, v1, v2, 0))
-    sc.instances.append((1, np.eye(4, dtype=np.float32)))
-    fresh_core.setting("traceVersion", 4)
-    fresh_core.setting("traceBlocksPerCU", 1)
-    fresh_core.setting("tailPool", 64)
-    o = _load_both(fresh_core, sc, 64, 36)
-    O4, D4 = _random_rays(120001, 23)
-    rng = np.random.default_rng(24)
-    j = rng.integers(0, len(x), 60000)
-    d = ((v0[j] + v1[j] + v2[j]) / 3).astype(np.float32) - O4[:60000, :3]
-    D4[:60000, :3] = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
-    hg, ho = fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4)
-    assert (ho[:60000, 2] == 1).mean() > 0.2
-    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
-
-
-@pytest.mark.parametrize("pool", [16, 64])
-def test_tail_pool_frame_parity(fresh_core, pool):
-    """A depth-4 room frame (closest and shadow rays) with the tail pool on matches the oracle."""
-    w, h = 192, 108
-    sc = scene.room_scene(40000, w, h)
-    o = _load_both(fresh_core, sc, w, h)
-    for tgt in (fresh_core, o):
-        tgt.setting("maxPathLength", 4)
-    fresh_core.setting("tailPool", pool)
-    sc.render_frame(fresh_core)
-    sc.render_frame(o)
-    assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
-    ag, ao = fresh_core.accumulator(), o.accumulator()
-    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
 
 
 @pytest.mark.parametrize("kind", ["diffuse", "emissive", "specular"])
@@ -518,7 +401,7 @@ def test_terminal_shade_frame_parity(fresh_core, kind):
     assert np.array_equal(ag[..., 3], a0[..., 3])
 
 
-@pytest.mark.parametrize("version", [1, 2, 4, 5, 6, 7])
+@pytest.mark.parametrize("version", [1, 7])
 @pytest.mark.parametrize("start", [0, 1])
 def test_single_instance_start_bitexact(fresh_core, version, start):
     """One instance (sheared and scaled): with singleInstanceStart the rays begin at its TLAS leaf
@@ -536,7 +419,7 @@ def test_single_instance_start_bitexact(fresh_core, version, start):
     assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
     D4[:, 3] = np.random.default_rng(4).uniform(1.0, 20.0, len(D4)).astype(np.float32)
     assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
-    if version >= 4:
+    if version == 7:
         fresh_core.setting("epsilon", 1e-4)
         o.setting("epsilon", 1e-4)
         sc.render_frame(fresh_core)
@@ -563,10 +446,10 @@ def test_no_lights_rng_stream_past_sample_256(fresh_core):
     assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
 
 
-@pytest.mark.parametrize("version", [4, 5, 6, 7])
+@pytest.mark.parametrize("version", [1, 7])
 def test_lit_room_frame_traversal_versions(fresh_core, version):
     """The whole lit frame (closest hits of every bounce, any-hit shadow rays with the fused connect)
-    through the BVH4 loops: identical ray counts and accumulator."""
+    through either per-ray loop: identical ray counts and accumulator."""
     w, h = 128, 72
     sc = scene.room_scene(40000, w, h)
     fresh_core.setting("traceVersion", version)
@@ -578,22 +461,3 @@ def test_lit_room_frame_traversal_versions(fresh_core, version):
     assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
     ag, ao = fresh_core.accumulator(), o.accumulator()
     assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
-
-
-@pytest.mark.parametrize("split", [0, 1, 2, 3])
-def test_shadow_split_frame_parity(fresh_core, split):
-    """The shadow rays of the first `split` bounces traced on a side stream beside the later bounces,
-    the rest by the final shadow launch (setting shadowSplit): identical ray counts and accumulator."""
-    w, h = 128, 72
-    sc = scene.room_scene(40000, w, h)
-    fresh_core.setting("shadowSplit", split)
-    o = _load_both(fresh_core, sc, w, h)
-    for tgt in (fresh_core, o):
-        tgt.setting("maxPathLength", 4)
-    for f in range(2):
-        sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
-        sc.render_frame(o, converge=1 if f == 0 else 0)
-        assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
-    ag, ao = fresh_core.accumulator(), o.accumulator()
-    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
-    assert fresh_core.stats().shadowTraceTime > 0

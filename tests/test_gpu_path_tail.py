@@ -104,35 +104,6 @@ def test_path_tail_spp_and_pass_past_256(fresh_core):
     assert rel_l2(fresh_core.accumulator()[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
 
 
-@pytest.mark.parametrize("kind,depth", [("diffuse", 2), ("diffuse", 4), ("specular", 5)])
-def test_terminal_trace_frame_parity(fresh_core, kind, depth):
-    """A terminal frame's last bounce (no lights, nothing emits or cuts out: ShadeParams::terminal) in
-    one launch of k_trace_term4d (setting terminalTrace): its misses add their sky samples, its hits add
-    nothing, and no k_shade_last runs.  Oracle parity, and the same frame through k_shade_last to float
-    summation order; the bench's config 2 frame takes this path."""
-    w, h = 160, 90
-    sc = scene.config2_scene(n=20000, width=w, height=h, sky=True)
-    if kind == "specular":
-        sc.materials.append(abi.make_material((0.9, 0.9, 0.9), roughness=0.0))
-        sc.meshes[0].view(np.uint32)[::2, abi.TRI["material"]] = 1
-    o = _load_both(fresh_core, sc, w, h)
-    for tgt in (fresh_core, o):
-        tgt.setting("maxPathLength", depth)
-    fresh_core.setting("terminalTrace", 1)
-    sc.render_frame(fresh_core)
-    sc.render_frame(o)
-    cg, co = fresh_core.ray_counts(), o.ray_counts()
-    assert np.array_equal(cg, co), (cg[:8], co[:8])
-    ag, ao = fresh_core.accumulator(), o.accumulator()
-    assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
-    assert rel_l2(ag[..., 3], ao[..., 3]) <= 1e-6
-    fresh_core.setting("terminalTrace", 0)
-    sc.render_frame(fresh_core)
-    a0 = fresh_core.accumulator()
-    assert rel_l2(ag[..., :3], a0[..., :3]) <= 1e-6
-    assert np.array_equal(ag[..., 3], a0[..., 3])
-
-
 @pytest.mark.parametrize("factor", [0.5, 2.0])
 def test_heavy_first_packets_frames(fresh_core, factor):
     """Heavy-first primary packets (setting packetHeavy): from the second frame on, the packets that took

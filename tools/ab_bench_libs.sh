@@ -8,6 +8,6 @@ cd "$ROOT"
 export LH2_BLUENOISE="$ROOT/lighthouse2_amd/data/bluenoise.bin"
 for rep in 1 2; do for lib in new "$@"; do
   if [ "$lib" = new ]; then unset LH2_CORE_LIB; else export LH2_CORE_LIB="$ROOT/gpuab/$lib/libRenderCore_MI355X.so"; fi
-  b=$(timeout -k 10 180 python3 bench.py --no-cpu-baseline --no-config4 --steps 30 2>/dev/null | tail -1) || exit 1
+  b=$(timeout -k 10 180 python3 bench.py --no-cpu-baseline --no-config4 --no-configs --steps 30 2>/dev/null | tail -1) || exit 1
   echo "$lib $(echo "$b" | python3 -c "import json,sys;d=json.load(sys.stdin);print(d['value'],d['ms_per_step'],d['detail']['traceTime0_ms'],d['detail']['traceTime1_ms'],d['detail']['shadeTime_ms'])")"
 done; done

@@ -8,7 +8,7 @@ import statistics
 import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/lat"
-kern = sys.argv[2] if len(sys.argv) > 2 else "k_trace_closest4d<0>"
+kern = sys.argv[2] if len(sys.argv) > 2 else "k_trace_closest4d"
 vals = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):

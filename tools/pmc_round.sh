@@ -2,7 +2,7 @@
 # Counter passes behind bench.py's roofline (run through gpurun from the repo root, after profile_gpu.sh):
 #   sq1, sq2  SQ instruction-issue counters of the dominant kernel (k_trace_closest<false, 4> on the
 #             config-2 bounce rays, tools/trace_kernel_bench.py --set bounce) + GRBM_GUI_ACTIVE (clock)
-#   pk1       the same for the primary-ray launch (packet traversal, k_trace_closest_packet<2>)
+#   pk1       the same for the primary-ray launch (packet traversal, k_trace_closest_packet)
 #   c5_fetch, c5_write  FETCH_SIZE / WRITE_SIZE over config-5 frames (10M triangles: the DRAM-real
 #             working set), one TCC counter group per pass
 # One --pmc pass per rocprofv3 run; each run under its own kill-timeout; chained with &&.

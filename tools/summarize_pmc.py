@@ -119,7 +119,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", required=True)
     ap.add_argument("--src", default=str(ROOT / "gpurun_out" / "pmc"))
-    ap.add_argument("--kernel", default="k_trace_closest4d<2>")
+    ap.add_argument("--kernel", default="k_trace_closest4d")
     a = ap.parse_args()
     src = pathlib.Path(a.src)
     dst = ROOT / "profiles"

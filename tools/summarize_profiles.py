@@ -35,7 +35,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="r01")
     ap.add_argument("--src", default=str(ROOT / "gpurun_out" / "prof"))
-    ap.add_argument("--kernel", default="k_trace_closest4d<2>", help="bench.py's roofline kernel (rocprof name)")
+    ap.add_argument("--kernel", default="k_trace_closest4d", help="bench.py's roofline kernel (rocprof name)")
     a = ap.parse_args()
     src = pathlib.Path(a.src)
     dst = ROOT / "profiles"
