@@ -80,6 +80,7 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
         "lh2_core_generate_eye_rays": [_P, C.POINTER(abi.ViewPyramid), C.c_uint32, C.c_int, _F, _F, _F],
         "lh2_core_scene_info": [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)],
         "lh2_xorshift_floats": [C.c_uint32, _F, C.c_uint64],
+        "lh2_core_debug_shadow_rays": [_P, _F, _F, _F, C.c_int, C.POINTER(C.c_int)],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -288,6 +289,14 @@ class RenderCore:
         self._chk(self.lib.lh2_core_generate_eye_rays(self.h, C.byref(view), R0 & 0xffffffff, int(pass_), _fp(o), _fp(d),
                                                       _fp(s)))
         return o, d, s
+
+    def debug_shadow_rays(self, cap: int):
+        """Diagnostics: the last frame's queued shadow rays (O4, D4, potentials; potential.w holds the pixel
+        index bits)."""
+        o, d, p = (np.zeros((cap, 4), np.float32) for _ in range(3))
+        n = C.c_int(0)
+        self._chk(self.lib.lh2_core_debug_shadow_rays(self.h, _fp(o), _fp(d), _fp(p), int(cap), C.byref(n)))
+        return o[:n.value], d[:n.value], p[:n.value]
 
     def scene_info(self) -> dict:
         v = [C.c_int(0) for _ in range(4)]

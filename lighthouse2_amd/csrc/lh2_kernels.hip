@@ -237,12 +237,15 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 
 LH2_DEV float safe_inv( float d ) { return (d > -1e-30f && d < 1e-30f) ? (d < 0 ? -1e30f : 1e30f) : 1.0f / d; }
 
-struct TRay { v3 O, D, invD, oinv; };
+/* oinv = -O / D; oerr: its rounding per axis (|oinv| 2^-22, lh2_box4.inc slab_offsets), subtracted from the entry
+   and added to the exit slab of that axis */
+struct TRay { v3 O, D, invD, oinv, oerr; };
 LH2_DEV void setup_ray( TRay& r, v3 O, v3 D )
 {
 	r.O = O, r.D = D;
 	r.invD = mk3( safe_inv( D.x ), safe_inv( D.y ), safe_inv( D.z ) );
 	r.oinv = mk3( -O.x * r.invD.x, -O.y * r.invD.y, -O.z * r.invD.z );
+	r.oerr = mk3( fabsf( r.oinv.x ) * 0x1p-22f, fabsf( r.oinv.y ) * 0x1p-22f, fabsf( r.oinv.z ) * 0x1p-22f );
 }
 
 /* conservative slab test of one child box; culling only (padded, FMA allowed) */
@@ -252,8 +255,8 @@ LH2_DEV bool box_test( float lox, float hix, float loy, float hiy, float loz, fl
 	const float t1x = __builtin_fmaf( lox, r.invD.x, r.oinv.x ), t2x = __builtin_fmaf( hix, r.invD.x, r.oinv.x );
 	const float t1y = __builtin_fmaf( loy, r.invD.y, r.oinv.y ), t2y = __builtin_fmaf( hiy, r.invD.y, r.oinv.y );
 	const float t1z = __builtin_fmaf( loz, r.invD.z, r.oinv.z ), t2z = __builtin_fmaf( hiz, r.invD.z, r.oinv.z );
-	tn = fmaxf( fmaxf( fminf( t1x, t2x ), fminf( t1y, t2y ) ), fminf( t1z, t2z ) );
-	const float tf = fminf( fminf( fmaxf( t1x, t2x ), fmaxf( t1y, t2y ) ), fmaxf( t1z, t2z ) );
+	tn = fmaxf( fmaxf( fminf( t1x, t2x ) - r.oerr.x, fminf( t1y, t2y ) - r.oerr.y ), fminf( t1z, t2z ) - r.oerr.z );
+	const float tf = fminf( fminf( fmaxf( t1x, t2x ) + r.oerr.x, fmaxf( t1y, t2y ) + r.oerr.y ), fmaxf( t1z, t2z ) + r.oerr.z );
 	const float tfp = tf * 1.00001f + 1e-30f;
 	return tn <= tfp && tfp >= tmin && tn <= tmax * 1.00001f + 1e-30f;
 }

@@ -23,6 +23,8 @@
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
+#include <atomic>
+#include <functional>
 #include <thread>
 
 #include "../../include/lh2_detmath.h"
@@ -223,6 +225,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "bvh4Collapse" )) bvh4Collapse = value != 0;
 	else if (!strcmp( name, "bvh4" )) { bvh4 = value != 0; }   /* before SetGeometry */
 	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
+	else if (!strcmp( name, "buildThreads" )) buildThreads = std::max( 0, (int)value );   /* host threads of the deferred CPU builds */
 	else if (!strcmp( name, "gpuTlas" )) { gpuTlas = value != 0; instancesDirty = true; }
 	else if (!strcmp( name, "plocRadius" )) gpuBvh.radius = std::min( 32, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "chordSplit" )) chordSplit = std::max( 0.0f, value );   /* two-ended path segments (longest first); 0: off */
@@ -365,6 +368,7 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 	if (meshIdx < 0 || meshIdx > (int)meshes.size()) FatalError( "SetGeometry: mesh index %d out of sequence", meshIdx );
 	if (meshIdx == (int)meshes.size()) meshes.push_back( new CoreMeshHost() );
 	CoreMeshHost& m = *meshes[meshIdx];
+	m.build = nullptr;   /* a build of earlier data not run yet is superseded */
 	const auto t0 = std::chrono::high_resolution_clock::now();
 	m.triCount = triangleCount;
 	m.shadeTris.upload( (const float4*)tris, (size_t)triangleCount * 11, stream );
@@ -387,51 +391,53 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 	}
 	if (cpuBuild)
 	{
-		/* CPU binned-SAH build (bvh_build.cpp) */
+		/* CPU binned-SAH build (bvh_build.cpp), deferred: the inputs are copied now (the caller's triangle
+		   array is borrowed for this call only) and the builds of all meshes set since the last one run in
+		   parallel over the meshes when the scene is first needed (FlushBuilds) */
 		std::vector<Aabb> prims( triangleCount );
+		std::vector<float> verts( (size_t)triangleCount * 9 );
 		for (int k = 0; k < 3; k++) m.aabbLo[k] = 1e30f, m.aabbHi[k] = -1e30f;
 		for (int i = 0; i < triangleCount; i++)
 		{
 			const lh2_CoreTri& t = tris[i];
-			const float v[3][3] = { { t.vertex0.x, t.vertex0.y, t.vertex0.z }, { t.vertex1.x, t.vertex1.y, t.vertex1.z }, { t.vertex2.x, t.vertex2.y, t.vertex2.z } };
+			const float v[9] = { t.vertex0.x, t.vertex0.y, t.vertex0.z, t.vertex1.x, t.vertex1.y, t.vertex1.z, t.vertex2.x, t.vertex2.y, t.vertex2.z };
+			memcpy( &verts[(size_t)i * 9], v, sizeof( v ) );
 			for (int k = 0; k < 3; k++)
 			{
-				prims[i].lo[k] = std::min( std::min( v[0][k], v[1][k] ), v[2][k] );
-				prims[i].hi[k] = std::max( std::max( v[0][k], v[1][k] ), v[2][k] );
+				prims[i].lo[k] = std::min( std::min( v[k], v[3 + k] ), v[6 + k] );
+				prims[i].hi[k] = std::max( std::max( v[k], v[3 + k] ), v[6 + k] );
 				m.aabbLo[k] = std::min( m.aabbLo[k], prims[i].lo[k] ), m.aabbHi[k] = std::max( m.aabbHi[k], prims[i].hi[k] );
 			}
 		}
-		/* spatial splits (bvhSpatial > 0) clip triangles: the builder gets their vertices */
-		std::vector<float> verts;
-		if (bvhSpatial > 0)
-		{
-			verts.resize( (size_t)triangleCount * 9 );
-			for (int i = 0; i < triangleCount; i++)
+		const int maxLeaf = bvhMaxLeaf, collapse = bvh4Collapse, wide = bvh4;
+		const float cost = bvhTraversalCost, spatial = bvhSpatial, budget = bvhSpatialBudget;
+		CoreMeshHost* mp = &m;
+		m.build = [mp, prims = std::move( prims ), verts = std::move( verts ), maxLeaf, collapse, wide, cost, spatial, budget]( int threads ) {
+			BvhOutput bvh;
+			BuildBvh2( prims, maxLeaf, threads, bvh, cost, 0, spatial > 0 ? verts.data() : nullptr, spatial, budget );
+			/* one triangle record per leaf slot (a spatial split can reference a triangle from several leaves):
+			   v0, e1 = v1 - v0, e2 = v2 - v0 in fp32, exactly as the oracle's intersect_tri */
+			std::vector<float>& t48 = mp->hostTris48;
+			t48.assign( std::max<size_t>( bvh.perm.size(), 1 ) * 12, 0.0f );
+			for (size_t j = 0; j < bvh.perm.size(); j++)
 			{
-				const lh2_CoreTri& t = tris[i];
-				const float v[9] = { t.vertex0.x, t.vertex0.y, t.vertex0.z, t.vertex1.x, t.vertex1.y, t.vertex1.z, t.vertex2.x, t.vertex2.y, t.vertex2.z };
-				memcpy( &verts[(size_t)i * 9], v, sizeof( v ) );
+				const uint32_t ti = bvh.perm[j];
+				const float* v = &verts[(size_t)ti * 9];
+				float* o = &t48[j * 12];
+				o[0] = v[0], o[1] = v[1], o[2] = v[2]; memcpy( &o[3], &ti, 4 );
+				o[4] = v[3] - v[0], o[5] = v[4] - v[1], o[6] = v[5] - v[2], o[7] = 0;
+				o[8] = v[6] - v[0], o[9] = v[7] - v[1], o[10] = v[8] - v[2], o[11] = 0;
 			}
-		}
-		BvhOutput bvh;
-		BuildBvh2( prims, bvhMaxLeaf, 0, bvh, bvhTraversalCost, 0, verts.empty() ? nullptr : verts.data(), bvhSpatial, bvhSpatialBudget );
-		/* one triangle record per leaf slot (a spatial split can reference a triangle from several leaves) */
-		std::vector<float> tris48( std::max<size_t>( bvh.perm.size(), 1 ) * 12, 0.0f );
-		for (size_t j = 0; j < bvh.perm.size(); j++)
-		{
-			const uint32_t ti = bvh.perm[j];
-			const lh2_CoreTri& t = tris[ti];
-			float* o = &tris48[j * 12];
-			/* v0, e1 = v1 - v0, e2 = v2 - v0 in fp32, exactly as the oracle's intersect_tri */
-			o[0] = t.vertex0.x, o[1] = t.vertex0.y, o[2] = t.vertex0.z; memcpy( &o[3], &ti, 4 );
-			o[4] = t.vertex1.x - t.vertex0.x, o[5] = t.vertex1.y - t.vertex0.y, o[6] = t.vertex1.z - t.vertex0.z, o[7] = 0;
-			o[8] = t.vertex2.x - t.vertex0.x, o[9] = t.vertex2.y - t.vertex0.y, o[10] = t.vertex2.z - t.vertex0.z, o[11] = 0;
-		}
-		m.bvhNodes.upload( (const float4*)bvh.nodes.data(), bvh.nodes.size() / 4, stream );
-		m.bvhTris.upload( (const float4*)tris48.data(), tris48.size() / 4, stream );
-		m.leafTris = (int)bvh.perm.size();
-		m.nodeCount = (int)(bvh.nodes.size() / 16), m.maxDepth = bvh.maxDepth;
-		if (bvh4) BuildBlas4( m, bvh.nodes.data() );
+			mp->leafTris = (int)bvh.perm.size();
+			mp->nodeCount = (int)(bvh.nodes.size() / 16), mp->maxDepth = bvh.maxDepth;
+			mp->hostNodes4.clear(), mp->depth4 = 0;
+			/* BVH4 collapse: dynamic programming (surface-area costs: node step 1, leaf visit 0.4, triangle test 0.5,
+			   one triangle per leaf; merged leaves run the leaf loop divergent: slower, r02s) or greedy */
+			if (wide) mp->depth4 = collapse ? CollapseBvh4Sah( bvh.nodes.data(), (size_t)mp->nodeCount, mp->hostNodes4, 0.4f, 0.5f, 1 )
+				: CollapseBvh4( bvh.nodes.data(), (size_t)mp->nodeCount, mp->hostNodes4 );
+			mp->hostNodes2 = std::move( bvh.nodes );
+		};
+		pendingBuilds = true;
 	}
 	else if (bvh4)
 	{
@@ -443,6 +449,48 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 	}
 	CHK_HIP( hipStreamSynchronize( stream ) );   /* the caller's triangle array is borrowed for this call only */
 	geometryDirty = true;
+	coreStats.bvhBuildTime += std::chrono::duration<float>( std::chrono::high_resolution_clock::now() - t0 ).count();
+}
+
+/* the deferred CPU BLAS builds (SetGeometry), in parallel over the meshes on up to `buildThreads` host threads
+   (a mesh's own build gets the threads left over when there are fewer meshes than threads), then their upload */
+void RenderCore::FlushBuilds()
+{
+	if (!pendingBuilds) return;
+	pendingBuilds = false;
+	const auto t0 = std::chrono::high_resolution_clock::now();
+	std::vector<CoreMeshHost*> jobs;
+	for (auto* m : meshes) if (m->build) jobs.push_back( m );
+	int workers = buildThreads;
+	if (workers <= 0)
+	{
+		const char* e = getenv( "LH2_BUILD_THREADS" );
+		if (!e) e = getenv( "OMP_NUM_THREADS" );
+		const unsigned hw = std::thread::hardware_concurrency();
+		workers = e && atoi( e ) > 0 ? atoi( e ) : (int)std::min( 16u, hw ? hw : 4u );
+	}
+	const int nthreads = std::max( 1, std::min( workers, (int)jobs.size() ) );
+	const int perJob = std::max( 1, workers / std::max( 1, (int)jobs.size() ) );
+	std::atomic<int> next{ 0 };
+	std::vector<std::string> errors( nthreads );
+	auto work = [&]( int w ) {
+		try { for (int j; (j = next.fetch_add( 1 )) < (int)jobs.size();) jobs[j]->build( perJob ); }
+		catch (const std::exception& e) { errors[w] = e.what(); }
+	};
+	std::vector<std::thread> pool;
+	for (int w = 1; w < nthreads; w++) pool.emplace_back( work, w );
+	work( 0 );
+	for (auto& t : pool) t.join();
+	for (auto& e : errors) if (!e.empty()) FatalError( "BLAS build: %s", e.c_str() );
+	for (auto* m : jobs)
+	{
+		m->bvhNodes.upload( (const float4*)m->hostNodes2.data(), m->hostNodes2.size() / 4, stream );
+		m->bvhTris.upload( (const float4*)m->hostTris48.data(), m->hostTris48.size() / 4, stream );
+		if (bvh4) m->bvh4Nodes.upload( (const float4*)m->hostNodes4.data(), m->hostNodes4.size() / 4, stream ), m->node4Count = (int)(m->hostNodes4.size() / 32);
+		CHK_HIP( hipStreamSynchronize( stream ) );
+		m->hostNodes2 = std::vector<float>(), m->hostTris48 = std::vector<float>(), m->hostNodes4 = std::vector<float>();
+		m->build = nullptr;
+	}
 	coreStats.bvhBuildTime += std::chrono::duration<float>( std::chrono::high_resolution_clock::now() - t0 ).count();
 }
 
@@ -471,6 +519,7 @@ void RenderCore::SetInstance( int instanceIdx, int meshIdx, const float* M )   /
 /* scene node array = all BLAS (relocated, device to device) followed by room for the TLAS */
 void RenderCore::ConcatenateBlas( int ni )
 {
+	FlushBuilds();
 	meshNodeBase.assign( meshes.size(), 0 ), meshTriBase.assign( meshes.size(), 0 ), meshNode4Base.assign( meshes.size(), 0 );
 	int nodeTotal = 0, triTotal = 0, node4Total = 0, meshTris = 0;
 	maxBlasDepth = 0, maxBlas4Depth = 0;
@@ -993,6 +1042,24 @@ void RenderCore::GetRayCounts( uint32_t* out17 )
 	Synchronize();
 	for (int i = 0; i < 16; i++) out17[i] = i < framePathLengths ? hostStats->rayCount[i] : 0u;
 	out17[16] = framePrimeRef ? hostStats->counters.totalShadowRays : QueuedShadowRays( hostStats->counters );
+}
+
+int RenderCore::DebugShadowRays( float* o4, float* d4, float* p4, int cap )
+{
+	Synchronize();
+	int n = 0;
+	for (int k = 0; k < LH2_SEGS; k++)
+	{
+		const uint32_t cnt = std::min( hostStats->counters.segShadow[k * LH2_SEGCOUNT_STRIDE], ps.shadowStride );
+		const int m = std::min( (int)cnt, cap - n );
+		if (m <= 0) break;
+		const size_t at = (size_t)k * ps.shadowStride;
+		CHK_HIP( hipMemcpy( o4 + 4 * (size_t)n, ps.shO.ptr + at, 16 * (size_t)m, hipMemcpyDeviceToHost ) );
+		CHK_HIP( hipMemcpy( d4 + 4 * (size_t)n, ps.shD.ptr + at, 16 * (size_t)m, hipMemcpyDeviceToHost ) );
+		CHK_HIP( hipMemcpy( p4 + 4 * (size_t)n, ps.shP.ptr + at, 16 * (size_t)m, hipMemcpyDeviceToHost ) );
+		n += m;
+	}
+	return n;
 }
 
 void RenderCore::GetAccumulator( float* hostOut4 )

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -52,6 +53,9 @@ struct CoreMeshHost   /* RenderCore always copies what it needs (rendercore.h:57
 	int nodeCount = 0, maxDepth = 0;
 	DevBuf<float4> bvh4Nodes;            /* the same BLAS collapsed to BVH4 (CollapseBvh4), mesh-local refs */
 	int node4Count = 0, depth4 = 0;
+	/* a deferred CPU build (RenderCore::FlushBuilds): the job (its argument: threads for the build) and its results */
+	std::function<void( int )> build;
+	std::vector<float> hostNodes2, hostTris48, hostNodes4;
 };
 
 struct CoreInstanceHost { int mesh; float T[16]; float inv[16]; };
@@ -136,6 +140,8 @@ public:
 	int Device() const { return device; }
 	int SamplesTaken() const { return samplesTaken; }
 	void GetRayCounts( uint32_t* out17 );
+	/* diagnostics: the last frame's queued shadow rays {O, tmin} {D, tmax} {potential rgb, pixel bits}, segment by segment */
+	int DebugShadowRays( float* o4, float* d4, float* p4, int cap );
 	void TraceClosest( const float* orgTmin4, const float* dirTmax4, int n, uint32_t* hits4 );   /* host in/out */
 	void TraceAny( const float* orgTmin4, const float* dirTmax4, int n, uint32_t* occluded );
 	void TraceClosestDevice( const void* rayO, const void* rayD, int n, void* hits, int iterations, float* msOut );
@@ -150,6 +156,10 @@ private:
 	void EnsureBuffers();
 	void ConcatenateBlas( int instanceCount );
 	void BuildBlas4( CoreMeshHost& m, const float* nodes2 );
+	void FlushBuilds();
+	bool pendingBuilds = false;
+	int buildThreads = 0;                /* host threads of the deferred BLAS builds (setting "buildThreads"; 0: LH2_BUILD_THREADS,
+	                                        OMP_NUM_THREADS or min(16, cores)) */
 	void EnsurePaths( uint32_t paths );
 	void EnsureStack();
 	void CheckSceneError();

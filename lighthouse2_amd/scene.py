@@ -755,3 +755,140 @@ def bounce_rays(tris, O4, D4, hits, seed=1):
     O = np.concatenate([o, np.zeros((len(o), 1))], 1).astype(np.float32)
     D = np.concatenate([d, np.full((len(d), 1), 1e34)], 1).astype(np.float32)
     return O, D
+
+
+# ---------------------------------------------------------------------------------------------
+# config 1: tinyapp's default scene (BASELINE.json configs[0], apps/tinyapp/main.cpp:34-45)
+# ---------------------------------------------------------------------------------------------
+TINYAPP_FIXTURE = __import__("pathlib").Path(__file__).resolve().parents[1] / "tests" / "golden" / "config1_tinyapp.npz"
+
+
+def _normalize_rows(v: np.ndarray) -> np.ndarray:
+    """helper_math.h normalize on the host: v * (1 / sqrtf(dot(v, v))), float32."""
+    d = (v * v).sum(1, dtype=np.float32).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return (v * (np.float32(1) / np.sqrt(d))[:, None]).astype(np.float32)
+
+
+def _consistent_alpha(nnv: np.ndarray) -> np.ndarray:
+    """The consistent-normal parameter per vertex: acosf(nnv) * (1 + 0.03632 (1 - nnv)^2) (host_mesh.cpp:190-196, 499-503)."""
+    nnv = nnv.astype(np.float32)
+    return (np.arccos(nnv).astype(np.float32) * (np.float32(1) + np.float32(0.03632) * (np.float32(1) - nnv) * (np.float32(1) - nnv))).astype(np.float32)
+
+
+def _gltf_primitive_tris(P, Nv, U, ind, material: int) -> np.ndarray:
+    """HostMesh::BuildFromIndexedData (host_mesh.cpp:477-569) for one glTF primitive with normals and uvs."""
+    i0, i1, i2 = ind[0::3], ind[1::3], ind[2::3]
+    v0, v1, v2 = P[i0], P[i1], P[i2]
+    N = _normalize_rows(np.cross(v1 - v0, v2 - v0).astype(np.float32))
+    vN0, vN1, vN2 = Nv[i0], Nv[i1], Nv[i2]
+    d = lambda a, b: (a * b).sum(1, dtype=np.float32).astype(np.float32)
+    flip = (d(N, vN0) < 0) & (d(N, vN1) < 0) & (d(N, vN2) < 0)
+    Nf = np.where(flip[:, None], -N, N).astype(np.float32)        # flipped for the alphas only
+    m0 = np.fmax(np.float32(0.7), d(vN0, Nf))   # fmaxf: a NaN dot (degenerate face) gives 0.7
+    m1 = np.fmax(np.float32(0.7), d(vN1, Nf))
+    m2 = np.fmax(np.float32(0.7), d(vN2, Nf))
+    alpha = np.ones(len(P), np.float32)
+    # sequential, with the reference's update of vertices 1 and 2 from vertex 0's value (host_mesh.cpp:497-499)
+    for t in range(len(i0)):
+        a0 = min(alpha[i0[t]], m0[t])
+        alpha[i0[t]] = a0
+        alpha[i1[t]] = min(a0, m1[t])
+        alpha[i2[t]] = min(a0, m2[t])
+    alpha = _consistent_alpha(alpha)
+    t = abi.new_tris(len(i0))
+    for k, vn in zip(("vN0", "vN1", "vN2"), (vN0, vN1, vN2)):
+        t[:, abi.TRI[k]:abi.TRI[k] + 3] = vn
+    t[:, abi.TRI["Nx"]], t[:, abi.TRI["Ny"]], t[:, abi.TRI["Nz"]] = N[:, 0], N[:, 1], N[:, 2]
+    t[:, 32:35], t[:, 36:39], t[:, 40:43] = v0, v1, v2
+    t[:, abi.TRI["alpha"]], t[:, abi.TRI["alpha"] + 1], t[:, abi.TRI["alpha"] + 2] = alpha[i0], alpha[i1], alpha[i2]
+    uv0, uv1, uv2 = U[i0], U[i1], U[i2]
+    # CoreTri u / v fields: (u0, u1, u2) at TRI["u"], (v0, v1, v2) at TRI["v"] (common_classes.h:126-154)
+    t[:, abi.TRI["u"]:abi.TRI["u"] + 3] = np.stack([uv0[:, 0], uv1[:, 0], uv2[:, 0]], 1)
+    t[:, abi.TRI["v"]:abi.TRI["v"] + 3] = np.stack([uv0[:, 1], uv1[:, 1], uv2[:, 1]], 1)
+    uv01, uv02 = (uv1 - uv0).astype(np.float32), (uv2 - uv0).astype(np.float32)
+    e1, e2 = (v1 - v0).astype(np.float32), (v2 - v0).astype(np.float32)
+    edges = (d(uv01, uv01) == 0) | (d(uv02, uv02) == 0)
+    T_e = _normalize_rows(e1)
+    B_e = _normalize_rows(np.cross(N, T_e).astype(np.float32))
+    T_u = _normalize_rows((e1 * uv02[:, 1:2] - e2 * uv01[:, 1:2]).astype(np.float32))
+    B_u = _normalize_rows((e2 * uv01[:, 0:1] - e1 * uv02[:, 0:1]).astype(np.float32))
+    t[:, abi.TRI["T"]:abi.TRI["T"] + 3] = np.where(edges[:, None], T_e, T_u)
+    t[:, abi.TRI["B"]:abi.TRI["B"] + 3] = np.where(edges[:, None], B_e, B_u)
+    t.view(np.uint32)[:, abi.TRI["material"]] = material
+    return t
+
+
+def _obj_tris(P, Nrm, fv, fn, fmat) -> np.ndarray:
+    """HostMesh::LoadGeometryFromOBJ (host_mesh.cpp:131-305) for a smooth-shaded OBJ without texture coordinates."""
+    v0, v1, v2 = P[fv[:, 0]], P[fv[:, 1]], P[fv[:, 2]]
+    vN0, vN1, vN2 = Nrm[fn[:, 0]], Nrm[fn[:, 1]], Nrm[fn[:, 2]]
+    d = lambda a, b: (a * b).sum(1, dtype=np.float32).astype(np.float32)
+    # alphas per normal index: the face normal flipped when against all three vertex normals (:173-184)
+    N0 = _normalize_rows(np.cross(v1 - v0, v2 - v0).astype(np.float32))
+    flip = (d(N0, vN0) < 0) & (d(N0, vN1) < 0) & (d(N0, vN2) < 0)
+    Na = np.where(flip[:, None], -N0, N0).astype(np.float32)
+    alpha = np.ones(len(Nrm), np.float32)
+    for k, vn in enumerate((vN0, vN1, vN2)):
+        np.fmin.at(alpha, fn[:, k], np.fmax(np.float32(0.7), d(vn, Na)))
+    alpha = _consistent_alpha(alpha)
+    # the triangle records: face normal flipped when against vertex normal 0 (:253)
+    e1, e2 = (v1 - v0).astype(np.float32), (v2 - v0).astype(np.float32)
+    N = _normalize_rows(np.cross(e1, e2).astype(np.float32))
+    N = np.where((d(N, vN0) < 0)[:, None], -N, N).astype(np.float32)
+    t = abi.new_tris(len(fv))
+    for k, vn in zip(("vN0", "vN1", "vN2"), (vN0, vN1, vN2)):
+        t[:, abi.TRI[k]:abi.TRI[k] + 3] = vn
+    t[:, abi.TRI["Nx"]], t[:, abi.TRI["Ny"]], t[:, abi.TRI["Nz"]] = N[:, 0], N[:, 1], N[:, 2]
+    t[:, 32:35], t[:, 36:39], t[:, 40:43] = v0, v1, v2
+    T = _normalize_rows(e1)
+    t[:, abi.TRI["T"]:abi.TRI["T"] + 3] = T
+    t[:, abi.TRI["B"]:abi.TRI["B"] + 3] = _normalize_rows(np.cross(N, T).astype(np.float32))
+    t[:, abi.TRI["alpha"]], t[:, abi.TRI["alpha"] + 1], t[:, abi.TRI["alpha"] + 2] = alpha[fn[:, 0]], alpha[fn[:, 1]], alpha[fn[:, 2]]
+    t.view(np.uint32)[:, abi.TRI["material"]] = fmat.astype(np.uint32)
+    return t
+
+
+def tinyapp_scene(width: int = 640, height: int = 400, path=None) -> Scene:
+    """tinyapp's PrepareScene (apps/tinyapp/main.cpp:34-45) from the committed fixture
+    (tools/make_config1_fixture.py): the pica glTF diorama (170 meshes, one instance per node, the root node
+    rotated by RotateX(-pi/2)), legocar.obj at scale 10 (placed as the main loop's first frame places it:
+    Translate(0, 5, 0)), and the light quad (0, -1, 0) at (0, 26, 0), 6.9 x 6.9, radiance (100, 100, 80).
+    Materials: glTF base colour / metallic / roughness factors (host_material.cpp:77-103; the decal textures
+    are left out: untextured), the .mtl Kd colours with tinyobjloader's default shininess (roughness 0), the
+    light.  The camera is tinyapp's default (no camera.xml ships with the app: Camera's defaults, camera.h:33-44:
+    at the origin looking down +z, FOV 40, focal distance 5, aperture EPSILON, distortion 0.05)."""
+    f = np.load(path or TINYAPP_FIXTURE)
+    meshes, materials = [], []
+    for c, m, r in zip(f["pica_mat_color"], f["pica_mat_metallic"], f["pica_mat_roughness"]):
+        materials.append(abi.make_material(tuple(float(x) for x in c), roughness=None if np.isnan(r) else float(r),
+                                           metallic=None if np.isnan(m) else float(m)))
+    prim_mesh, prim_mat, prim_v, prim_i = f["pica_prim_mesh"], f["pica_prim_mat"], f["pica_prim_v"], f["pica_prim_i"]
+    P, Nv, U, I = f["pica_pos"], f["pica_nrm"], f["pica_uv"], f["pica_idx"]
+    per_mesh = [[] for _ in range(int(f["pica_meshes"]))]
+    for k in range(len(prim_mesh)):
+        vb, vc = prim_v[k]
+        ib, ic = prim_i[k]
+        per_mesh[prim_mesh[k]].append(_gltf_primitive_tris(P[vb:vb + vc], Nv[vb:vb + vc], U[vb:vb + vc], I[ib:ib + ic].astype(np.int64),
+                                                         int(prim_mat[k])))
+    meshes = [np.concatenate(x) for x in per_mesh]
+    car_base = len(materials)
+    materials += [abi.make_material(tuple(float(x) for x in c), roughness=0.0) for c in f["car_mat_color"]]
+    car = _obj_tris(f["car_pos"], f["car_nrm"], f["car_face_v"], f["car_face_n"], f["car_face_mat"] + car_base)
+    light_mat = len(materials)
+    materials.append(abi.make_material((100.0, 100.0, 80.0)))
+    quad = quad_tris((0, -1, 0), (0, 26.0, 0), 6.9, 6.9, light_mat)
+    quad.view(np.int32)[:, abi.TRI["ltriIdx"]] = [0, 1]
+    car_mesh, quad_mesh = len(meshes), len(meshes) + 1
+    meshes += [car, quad]
+    instances = [(int(m), T) for m, T in zip(f["pica_inst_mesh"], f["pica_inst_T"])]
+    light_inst = len(instances)
+    instances.append((quad_mesh, np.eye(4, dtype=np.float32)))
+    car_T = np.eye(4, dtype=np.float32)
+    car_T[1, 3] = 5.0
+    instances.append((car_mesh, car_T))
+    sc = Scene(meshes=meshes, instances=instances, materials=materials, name="tinyapp")
+    sc.area_lights = [light_from_tri(quad[i], i, light_inst, (100.0, 100.0, 80.0)) for i in range(2)]
+    sc.view = camera_view((0, 0, 0), (0, 0, 1), fov_deg=40, aspect=width / height, focal=5, aperture=1e-4, distortion=0.05,
+                          pixel_height=height)
+    return sc

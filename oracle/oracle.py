@@ -58,12 +58,14 @@ def lib() -> C.CDLL:
             "orc_generate_eye_rays": [_P, C.POINTER(abi.ViewPyramid), C.c_uint32, C.c_int, _F, _F, _F],
             "orc_trace_closest": [_P, _F, _F, C.c_int, _U, _U, C.c_int], "orc_trace_any": [_P, _F, _F, C.c_int, _U],
             "orc_unpack_normal": [C.c_uint32, _F], "orc_mat4_inverse": [_F, _F],
-            "orc_detmath_eval": [C.c_int, _F, _F, C.c_int, _F],
+            "orc_detmath_eval": [C.c_int, _F, _F, C.c_int, _F], "orc_debug_pixel": [_P, C.c_int, C.c_int],
         }
         for k, v in sig.items():
             getattr(L, k).argtypes = v
             getattr(L, k).restype = None
         L.orc_fetch_texel.restype = C.c_int
+        L.orc_debug_log.argtypes = [_P, _F, C.c_int]
+        L.orc_debug_log.restype = C.c_int
         L.orc_samples_taken.argtypes = [_P]
         L.orc_samples_taken.restype = C.c_int
         for k in ("orc_wanghash", "orc_xorshift"):
@@ -120,6 +122,17 @@ class Oracle:
 
     def set_probe(self, x, y):
         self.L.orc_set_probe(self.o, x, y)
+
+    def debug_pixel(self, px, cap=256):
+        """Diagnostics: the next renders log pixel px's path vertices and shadow rays (debug_log)."""
+        self.L.orc_debug_pixel(self.o, int(px), int(cap))
+
+    def debug_log(self, cap=256):
+        """Records of debug_pixel: float32 (n, 16); kind 0 = vertex [kind, pathLength, hit t, tri (bits),
+        inst (bits), O, D, tmin, tmax], kind 1 = shadow ray [kind, pathLength, occluded, O, D, tmax, rgb]."""
+        out = np.zeros((cap, 16), np.float32)
+        n = self.L.orc_debug_log(self.o, _fp(out), cap)
+        return out[:n]
 
     def set_tile(self, y0, y1):
         self.L.orc_set_tile(self.o, y0, y1)

@@ -130,7 +130,17 @@ struct Oracle
 	int tileY0, tileY1;
 	int bandRank, bandCount, band;   /* band partition (0 bands = contiguous tile) */
 	OracleStats stats;
+	/* diagnostics (orc_debug_pixel): every path vertex and shadow ray of one pixel, 16 floats per record */
+	int debugPixel;
+	float* debugLog; int debugCount, debugCap;
 };
+/* one debug record: kind (0 vertex: pathLength, hit t, tri, inst, ray O, D; 1 shadow ray: pathLength,
+   occluded, O, D, tmax, contribution) */
+static void debug_log( const Oracle* o, const float* rec )
+{
+	Oracle* m = (Oracle*)o;   /* one thread renders the debug pixel */
+	if (m->debugCount < m->debugCap) memcpy( m->debugLog + 16 * m->debugCount++, rec, 16 * sizeof( float ) );
+}
 
 Oracle* orc_create( void )
 {
@@ -141,6 +151,7 @@ Oracle* orc_create( void )
 	o->camRNGseed = 0x12345678;
 	o->firstConvergingFrame = 0;
 	o->tileY0 = 0, o->tileY1 = -1;
+	o->debugPixel = -1;
 	return o;
 }
 
@@ -155,7 +166,7 @@ void orc_destroy( Oracle* o )
 	for (int i = 0; i < o->meshCount; i++) free_mesh( &o->meshes[i] );
 	free( o->meshes ); free( o->inst ); free( o->mats ); free( o->area ); free( o->point ); free( o->spot );
 	free( o->dirl ); free( o->sky ); free( o->acc ); free( o->blueNoise );
-	free( o->tex ); free( o->argb32 ); free( o->nrm32 );
+	free( o->tex ); free( o->argb32 ); free( o->nrm32 ); free( o->debugLog );
 	free( o );
 }
 
@@ -684,6 +695,19 @@ void orc_set_target( Oracle* o, int w, int h, int spp ) /* rendercore.cpp:149-20
 }
 
 void orc_set_probe( Oracle* o, int x, int y ) { o->probeX = x, o->probeY = y; }
+/* diagnostics: log the path vertices and shadow rays of pixel px (-1: none) of the next renders */
+void orc_debug_pixel( Oracle* o, int px, int cap )
+{
+	free( o->debugLog );
+	o->debugPixel = px, o->debugCount = 0, o->debugCap = px >= 0 ? cap : 0;
+	o->debugLog = px >= 0 ? (float*)calloc( (size_t)cap * 16, sizeof( float ) ) : 0;
+}
+int orc_debug_log( const Oracle* o, float* out, int cap )
+{
+	const int n = o->debugCount < cap ? o->debugCount : cap;
+	if (n > 0) memcpy( out, o->debugLog, (size_t)n * 16 * sizeof( float ) );
+	return n;
+}
 
 /* ------------------------------------------------------------------------------------- */
 /* tools: tools_shared.h                                                                   */
@@ -1628,6 +1652,12 @@ static int shade_one( const Oracle* o, ThreadCtx* ctx, const PathSeg* in, const 
 				THit sh; uint32_t nn = 0, tt = 0; int occluded;
 				trace_ray( o, SO, L, 0.0f, dist - 2 * o->geometryEpsilon, 1, &sh, &nn, &tt, &occluded );
 				if (!occluded) acc_add( ctx->acc, pixelIdx, contribution, 0 );
+				if ((int)pixelIdx == o->debugPixel)
+				{
+					const float rec[16] = { 1, (float)pathLength, (float)occluded, SO.x, SO.y, SO.z, L.x, L.y, L.z, dist - 2 * o->geometryEpsilon,
+						contribution.x, contribution.y, contribution.z, 0, 0, 0 };
+					debug_log( o, rec );
+				}
 			}
 		}
 	}
@@ -1837,6 +1867,12 @@ static void* render_worker( void* arg )
 			THit hit; uint32_t nn = 0, tt = 0; int occ;
 			trace_ray( o, cur.O, cur.D, cur.tmin, cur.tmax, 0, &hit, &nn, &tt, &occ );
 			if (hit.tri == -1) hit.t = -1.0f, hit.inst = -1;
+			if (px == o->debugPixel)
+			{
+				float rec[16] = { 0, (float)pathLength, hit.t, 0, 0, cur.O.x, cur.O.y, cur.O.z, cur.D.x, cur.D.y, cur.D.z, cur.tmin, cur.tmax, 0, 0, 0 };
+				memcpy( &rec[3], &hit.tri, 4 ), memcpy( &rec[4], &hit.inst, 4 );
+				debug_log( o, rec );
+			}
 			if (pathLength <= 16) j->ctx.st.rayCount[pathLength - 1]++;
 			if (pathLength > (int)j->ctx.st.maxPathLength) j->ctx.st.maxPathLength = pathLength;
 			const uint32_t R0 = (uint32_t)j->pass * 7907u + (uint32_t)pathLength * 91771u;

@@ -48,6 +48,8 @@ int orc_fetch_texel( const Oracle* o, int storage, float u, float v, int offset,
 void orc_setting( Oracle* o, const char* name, float value );
 void orc_set_target( Oracle* o, int w, int h, int spp );
 void orc_set_probe( Oracle* o, int x, int y );
+void orc_debug_pixel( Oracle* o, int px, int cap );       /* diagnostics: log pixel px's path vertices and shadow rays */
+int orc_debug_log( const Oracle* o, float* out, int cap );  /* 16 floats per record; returns the records written */
 void orc_set_tile( Oracle* o, int y0, int y1 );   /* render rows [y0, y1) only (-1 = all) */
 void orc_set_tile_bands( Oracle* o, int rank, int nranks, int band );   /* rows in bands, round-robin */
 void orc_render( Oracle* o, const lh2_ViewPyramid* view, int converge, int nthreads );

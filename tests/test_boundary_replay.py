@@ -123,3 +123,31 @@ def test_reference_header_host_frame_matches_oracle(tmp_path, devices):
     assert (st["probedInstid"], st["probedTriid"]) == (ost.probedInstid, ost.probedTriid)
     rel = np.linalg.norm(acc[..., :3] - ref[..., :3]) / np.linalg.norm(ref[..., :3])
     assert rel <= 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_config1_tinyapp_scene_through_reference_header(tmp_path):
+    """BASELINE config 1: tinyapp's default scene (apps/tinyapp/main.cpp:34-45: the pica glTF diorama, the lego
+    car at scale 10, the light quad; tests/golden/config1_tinyapp.npz) at 640 x 400, driven through the
+    reference's own CoreAPI_Base declaration as RenderSystem drives it (172 meshes, 172 instances, SetLights
+    with the quad's two emissive triangles), two frames (restart, converge): identical primary and bounce-1
+    ray counts, accumulator within 1e-4 of the oracle."""
+    assert REF_HOST.exists(), "oracle/_ref/reference_rendersystem missing: build it where /root/reference exists"
+    w, h = 640, 400
+    sc = scene.tinyapp_scene(w, h)
+    calls = tmp_path / "calls.bin"
+    _record(calls, sc, w, h, frames=2)
+    res = subprocess.run([str(REF_HOST), str(LIB), str(calls), str(tmp_path / "acc.bin")], capture_output=True,
+                         text=True, timeout=240)
+    assert res.returncode == 0 and res.stdout.strip(), (res.returncode, res.stdout, res.stderr)
+    st = json.loads(res.stdout.strip().splitlines()[-1])
+    acc = np.fromfile(tmp_path / "acc.bin", np.float32).reshape(h, w, 4)
+    ref, counts, ost = _oracle_frames(sc, w, h, 2)
+    assert st["frames"] == 2
+    assert st["primaryRayCount"] == counts[0] == w * h and st["bounce1RayCount"] == counts[1] > 0
+    assert (st["probedInstid"], st["probedTriid"]) == (ost.probedInstid, ost.probedTriid)
+    assert (ref[..., :3].sum(-1) > 0).mean() > 0.05        # the default camera sees lit geometry
+    rel = np.linalg.norm(acc[..., :3] - ref[..., :3]) / np.linalg.norm(ref[..., :3])
+    print(f"config1 tinyapp 640x400: rays {counts[:3].tolist()} shadow {int(counts[16])} rel-L2 {rel:.2e}")
+    assert rel <= 1e-4

@@ -198,3 +198,20 @@ def test_camera_view_matches_reference(cam):
                           pixel_height=py)
     ours = np.frombuffer(bytes(v), np.float32)
     assert np.array_equal(ours.view(np.uint32), ref.view(np.uint32)), (ours, ref)
+
+
+def test_config1_tinyapp_fixture():
+    """The committed tinyapp scene (tools/make_config1_fixture.py, from apps/tinyapp/data): pica's 76,274
+    glTF triangles in 170 meshes / instances, the car's 10,992 OBJ triangles scaled by 10, the 2-triangle light
+    quad at y = 26 (main.cpp:34-45); converted with the reference's mesh builders (scene.tinyapp_scene)."""
+    from lighthouse2_amd import abi, scene
+    sc = scene.tinyapp_scene(640, 400)
+    assert sc.tri_count == 76_274 + 10_992 + 2
+    assert len(sc.meshes) == 172 and len(sc.instances) == 172 and len(sc.materials) == 28 + 8 + 1
+    quad = sc.meshes[-1]
+    assert np.allclose(quad[:, [33, 37, 41]], 26.0) and len(sc.area_lights) == 2
+    car_mesh, car_T = sc.instances[-1]
+    assert car_T[1, 3] == 5.0 and len(sc.meshes[car_mesh]) == 10_992
+    # consistent-normal alphas in [0, acos(0.7) * (1 + 0.03632 * 0.09)], finite
+    alpha = np.concatenate([m[:, abi.TRI["alpha"]:abi.TRI["alpha"] + 3] for m in sc.meshes[:-1]])
+    assert np.isfinite(alpha).all() and alpha.min() >= 0 and alpha.max() <= 0.7981

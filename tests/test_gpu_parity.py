@@ -461,3 +461,61 @@ def test_lit_room_frame_traversal_versions(fresh_core, version):
     assert np.array_equal(fresh_core.ray_counts(), o.ray_counts())
     ag, ao = fresh_core.accumulator(), o.accumulator()
     assert rel_l2(ag[..., :3], ao[..., :3]) <= REL_L2_TOL
+
+
+def _grazing_scene():
+    """Two light-like quads at y = 15.95 (the room's lights, tessellated by the SBVH's spatial splits too) among
+    a few thousand random triangles, far from the coordinate origin."""
+    sc = scene.config2_scene(n=4000, width=64, height=36)
+    tris = sc.meshes[0].copy()
+    tris[:, 32:35] += np.float32(8.0)
+    tris[:, 36:39] += np.float32(8.0)
+    tris[:, 40:43] += np.float32(8.0)
+    q1 = scene.quad_tris((0, -1, 0), (-8, 15.95, 0), 4, 4, 0)
+    q2 = scene.quad_tris((0, -1, 0), (8, 15.95, 0), 4, 4, 0)
+    sc.meshes[0] = np.concatenate([tris, q1, q2])
+    return sc
+
+
+def _grazing_rays(n, seed):
+    """Shadow-ray-like queries from points just below the quads' plane (|y| ~ 16, so -o / d is large) to random
+    points on a quad, at grazing angles; tmax within 2e-6 relative of the distance, so the quad's triangle lies
+    just inside or just outside [tmin, tmax] (the room's light samples: SafeOrigin moves the origin, and a
+    grazing ray meets the light's plane a little before distance - 2 epsilon, pathtracer.h:203-204)."""
+    rng = np.random.default_rng(seed)
+    o = np.stack([rng.uniform(-19, 19, n), 15.95 - rng.uniform(1e-3, 0.2, n), rng.uniform(-11.9, 11.9, n)], 1).astype(np.float32)
+    side = np.where(rng.uniform(size=n) < 0.5, -8.0, 8.0)
+    p = np.stack([side + rng.uniform(-2, 2, n), np.full(n, 15.95), rng.uniform(-2, 2, n)], 1).astype(np.float32)
+    L = p - o
+    dist = np.sqrt((L * L).sum(1, dtype=np.float32)).astype(np.float32)
+    d = (L * (np.float32(1) / dist)[:, None]).astype(np.float32)
+    O4 = np.concatenate([o, np.zeros((n, 1), np.float32)], 1)
+    tmax = (dist * (1 + rng.uniform(-2e-6, 2e-6, n))).astype(np.float32)
+    D4 = np.concatenate([d, tmax[:, None]], 1)
+    return O4, D4
+
+
+@pytest.mark.parametrize("version", [1, 7])
+def test_grazing_rays_box_rounding(fresh_core, version):
+    """Rays nearly parallel to a plane close to their origin's coordinate (shadow rays grazing the room's light
+    quads): the slab distance (pl - o) / d is small while -o / d is large, so the rounding of the per-ray offset
+    is an absolute error the boxes' relative pad does not cover; the offsets are rounded outward per axis
+    (lh2_box4.inc slab_offsets).  Occlusion and closest hits, per-ray loops and packets, equal the oracle's,
+    which tests (pl - o) * (1 / d) (RenderCore_Bart bvh.cpp:7-42).  Config 3 at 1080p lost 10 light samples to
+    this before (tools/residual_config3.py)."""
+    sc = _grazing_scene()
+    fresh_core.setting("traceVersion", version)
+    o = _load_both(fresh_core, sc, 64, 36)
+    O4, D4 = _grazing_rays(60000, 41)
+    og, oo = fresh_core.trace_any(O4, D4), o.trace_any(O4, D4)
+    bits = np.unpackbits(oo.view(np.uint8), bitorder="little")[:len(O4)]
+    assert 0 < bits.sum() < len(O4)
+    assert np.array_equal(og, oo), np.nonzero(np.unpackbits((og ^ oo).view(np.uint8), bitorder="little"))[0][:10]
+    D4[:, 3] = 1e34
+    hg, ho = fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4)
+    assert np.array_equal(hg, ho), np.argwhere((hg != ho).any(1))[:10]
+    fresh_core.setting("packetPrimary", 1)
+    fresh_core.setting("unitCoherent", 1)
+    hp = fresh_core.trace_closest(O4, D4)
+    fresh_core.setting("unitCoherent", 0)
+    assert np.array_equal(hp, ho), np.argwhere((hp != ho).any(1))[:10]

@@ -1,11 +1,13 @@
 """BASELINE config 1: tinyapp + RenderCore_SoftRasterizer, default scene at
 640 x 400, on the CPU - plumbing, frame time, no Mrays/s.
 
-tinyapp's PrepareScene (apps/tinyapp/main.cpp:34-45) loads the pica glTF (76,274 triangles), the
-legocar OBJ (10,992 faces, scale 10) and a light quad (2 triangles, radiance 100, 100, 80).  The
-assets are missing from the reference (.MISSING_LARGE_BLOBS), so the scene here is synthetic with
-the same triangle counts: a 76,274-triangle cloud (the config-2 generator), a 10,992-triangle cloud
-of 1/10 the size instanced at scale 10, and the light quad.
+The scene is tinyapp's own (apps/tinyapp/main.cpp:34-45): the pica glTF diorama (76,274 triangles in 170
+meshes, the root node rotated by RotateX(-pi/2)), the lego car OBJ (10,992 triangles, scale 10) and the
+light quad (2 triangles, radiance 100, 100, 80, at y = 26, 6.9 x 6.9), read from the reference's assets
+(apps/tinyapp/data) into tests/golden/config1_tinyapp.npz by tools/make_config1_fixture.py and converted
+by scene.tinyapp_scene with the reference's mesh builders; the camera is tinyapp's default (no camera.xml
+ships with the app).  The decal textures are left out (one of the six images is missing from the
+reference, .MISSING_LARGE_BLOBS).
 
 Measured, one JSON line:
   - the reference CPU rasterizer (RenderCore_SoftRasterizer/rasterizer.cpp, oracle/_ref/
@@ -29,25 +31,6 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 from lighthouse2_amd import abi, scene  # noqa: E402
-
-
-def tinyapp_scene(width: int = 640, height: int = 400) -> scene.Scene:
-    body = scene.random_triangles(76_274, seed=0x2468ACE1, edge=0.5, spread=10.0)
-    car = scene.random_triangles(10_992, seed=0x13579BDF, edge=0.05, spread=1.0)
-    car.view(np.uint32)[:, abi.TRI["material"]] = 1
-    mats = [abi.make_material((0.8, 0.8, 0.8), roughness=1.0), abi.make_material((0.8, 0.2, 0.1), roughness=1.0),
-            abi.make_material((100.0, 100.0, 80.0))]
-    quad = scene.quad_tris((0, -1, 0), (0, 9.0, 0), 4, 4, 2)
-    quad.view(np.int32)[:, abi.TRI["ltriIdx"]] = [0, 1]
-    S = np.diag([10.0, 10.0, 10.0, 1.0]).astype(np.float32)
-    S[:3, 3] = (0.0, -2.0, 0.0)
-    sc = scene.Scene(meshes=[body, car, quad],
-                     instances=[(0, np.eye(4, dtype=np.float32)), (1, S), (2, np.eye(4, dtype=np.float32))],
-                     materials=mats, name="tinyapp-like")
-    sc.area_lights = [scene.light_from_tri(quad[i], i, 2, (100.0, 100.0, 80.0)) for i in range(2)]
-    sc.view = scene.camera_view((0, 0, -14), (0, 0, 1), fov_deg=40, aspect=width / height, focal=5,
-                                pixel_height=height)
-    return sc
 
 
 def soft_rasterizer(sc: scene.Scene, width: int, height: int, seconds: float) -> dict:
@@ -124,9 +107,9 @@ def main():
     ap.add_argument("--frames", type=int, default=50)
     ap.add_argument("--no-gpu", action="store_true")
     args = ap.parse_args()
-    sc = tinyapp_scene(args.width, args.height)
-    out = {"config": "config1", "workload": f"tinyapp-like scene, {sc.tri_count} tris "
-           f"(76,274 + 10,992 at scale 10 + 2-tri light quad; synthetic: the assets are missing), {args.width}x{args.height}",
+    sc = scene.tinyapp_scene(args.width, args.height)
+    out = {"config": "config1", "workload": f"tinyapp default scene, {sc.tri_count} tris (pica glTF 76,274 in 170 "
+           f"instances + legocar.obj 10,992 at scale 10 + 2-tri light quad; untextured), {args.width}x{args.height}",
            "soft_rasterizer_reference": soft_rasterizer(sc, args.width, args.height, args.cpu_seconds)}
     if not args.no_gpu:
         out["mi355x_core"] = mi355x_core(sc, args.width, args.height, args.frames)
