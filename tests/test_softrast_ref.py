@@ -1,6 +1,6 @@
 """BASELINE config 1 plumbing: the reference CPU rasterizer (RenderCore_SoftRasterizer/rasterizer.cpp,
-built from the reference sources by oracle/Makefile.ref) renders the tinyapp-like scene of
-tools/config1_plumbing.py headless.  CPU only; skipped where the reference was not built."""
+built from the reference sources by oracle/Makefile.ref) renders tinyapp's default scene
+(scene.tinyapp_scene, tests/golden/config1_tinyapp.npz) headless.  CPU only; skipped where the reference was not built."""
 import pathlib
 import sys
 
@@ -14,10 +14,11 @@ sys.path.insert(0, str(ROOT / "tools"))
 @pytest.mark.skipif(not LIB.exists(), reason="oracle/_ref not built (needs /root/reference)")
 def test_soft_rasterizer_renders_config1_scene():
     import config1_plumbing as c1
-    sc = c1.tinyapp_scene(160, 100)
+    from lighthouse2_amd import scene
+    sc = scene.tinyapp_scene(160, 100)
     r = c1.soft_rasterizer(sc, 160, 100, seconds=0.2)
     assert r["frames"] >= 1
-    assert r["covered_pixel_share"] > 0.5, r
+    assert r["covered_pixel_share"] > 0.08, r      # tinyapp's default camera: the diorama fills ~12 % of the view
 
 
 @pytest.mark.skipif(not LIB.exists(), reason="oracle/_ref not built (needs /root/reference)")
