@@ -87,9 +87,24 @@ def trace_sq(src, kernel, p1="sq1", p2="sq2", what="config-2 bounce rays from th
     }
 
 
-def config5_traffic(src):
-    f = dispatches(src / "c5_fetch" / "run_counter_collection.csv")
-    w = dispatches(src / "c5_write" / "run_counter_collection.csv")
+def frame_sq(src, p1, p2, what):
+    """Per kernel of a frame workload: the SQ issue summary of trace_sq (medians over that kernel's launches)."""
+    names = sorted({d["kernel"] for d in dispatches(src / p1 / "run_counter_collection.csv").values()})
+    rows = []
+    for k in names:
+        n = sum(1 for d in dispatches(src / p1 / "run_counter_collection.csv", k).values() if d["kernel"] == k)
+        if n < 2:
+            continue
+        r = trace_sq(src, k, p1, p2, what)
+        r["kernel"] = k
+        rows.append(r)
+    rows.sort(key=lambda r: -r["launch_ms_median"] * r["launches"])
+    return {"workload": what, "kernels": rows}
+
+
+def traffic(src, fetch, write, what):
+    f = dispatches(src / fetch / "run_counter_collection.csv")
+    w = dispatches(src / write / "run_counter_collection.csv")
     per = collections.defaultdict(lambda: {"fetch": [], "write": [], "ns": []})
     for d in f.values():
         per[d["kernel"]]["fetch"].append(2.0 * d["FETCH_SIZE"] * 1024.0)
@@ -107,8 +122,7 @@ def config5_traffic(src):
                      "fetch_bytes": statistics.median(v["fetch"]), "write_bytes": statistics.median(v["write"]),
                      "launch_ms_median": ns / 1e6, "hbm_gb_s": round(b / ns, 1), "hbm_frac": round(b / ns / 8000.0, 4)})
     rows.sort(key=lambda r: -r["launch_ms_median"] * r["launches"])
-    return {"workload": "config 5: 100 x 100k-triangle instanced meshes, per-frame TLAS, 1920x1080 8 spp "
-                        "(tools/bench_configs.py --configs 5 --frames 3 --warmup 1)",
+    return {"workload": what,
             "kernels": rows,
             "note": "HBM bytes = 2 x FETCH_SIZE (gfx950 calibration) + WRITE_SIZE per launch (medians over "
                     "launches, separate --pmc passes); FETCH_SIZE also counts Infinity-Cache hits, so this "
@@ -131,10 +145,18 @@ def main():
                                                                    "order, tools/trace_kernel_bench.py --set primary")
         (dst / f"{a.tag}_pmc_packet_sq.json").write_text(json.dumps(pk, indent=1) + "\n")
         print(json.dumps(pk, indent=1))
-    if (src / "c5_fetch").exists():
-        c5 = config5_traffic(src)
-        (dst / f"{a.tag}_pmc_config5_traffic.json").write_text(json.dumps(c5, indent=1) + "\n")
-        print(json.dumps(c5, indent=1))
+    C5 = "config 5: 100 x 100k-triangle instanced meshes, per-frame TLAS, 1920x1080 8 spp (tools/bench_configs.py --configs 5)"
+    C3 = "config 3: 1M-triangle lit room, maxPathLength 4, 1920x1080 1 spp (tools/bench_configs.py --configs 3)"
+    for tag, f, w, what in (("config5_traffic", "c5_fetch", "c5_write", C5), ("config3_traffic", "c3_fetch", "c3_write", C3)):
+        if (src / f).exists() and (src / w).exists():
+            t = traffic(src, f, w, what)
+            (dst / f"{a.tag}_pmc_{tag}.json").write_text(json.dumps(t, indent=1) + "\n")
+            print(json.dumps(t, indent=1))
+    for tag, p1, p2, what in (("config5_sq", "c5_sq1", "c5_sq2", C5), ("config3_sq", "c3_sq1", "c3_sq2", C3)):
+        if (src / p1).exists():
+            t = frame_sq(src, p1, p2 if (src / p2).exists() else None, what)
+            (dst / f"{a.tag}_pmc_{tag}.json").write_text(json.dumps(t, indent=1) + "\n")
+            print(json.dumps(t, indent=1)[:2000])
 
 
 if __name__ == "__main__":
