@@ -44,6 +44,8 @@ from lighthouse2_amd import build_info, scene  # noqa: E402
 from lighthouse2_amd.core import RenderCore  # noqa: E402
 from lighthouse2_amd.parallel import BAND, TileGather  # noqa: E402
 
+LH2_CONVERGE, LH2_RESTART = 0, 1   # include/lh2_core_types.h (Convergence, core_api_base.h)
+
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SIMDS, CLOCK_GHZ = 256 * 4, 2.4
 # the per-ray closest-hit kernel of incoherent rays per traversal loop version (rocprofv3 names)
@@ -129,8 +131,14 @@ def timed_frames(core, sc, gather, steps, warmup, world, dev, per_frame=None):
     """warmup + steps frames (render; N > 1: pack the owned rows, gather); returns (max-over-ranks
     seconds, rays of all ranks per frame [primary + bounce 1, deeper, shadow], this rank's counts).
     With one rank the finished frame is the core's own frame buffer: there is nothing to exchange."""
+    first = [True]
+
     def step():
-        sc.render_frame(core, converge=1)     # Restart: the same paths every step
+        # a still camera converging, as tinyapp renders it (apps/tinyapp/main.cpp:102-103: Restart only when the
+        # camera moved): the first frame restarts, every later one accumulates a new sample with new random numbers,
+        # so no frame repeats the previous one's paths (the heavy-first packet order is last frame's costs)
+        sc.render_frame(core, converge=LH2_RESTART if first[0] else LH2_CONVERGE)
+        first[0] = False
         if world == 1:
             return None
         core.pack_tile(gather.send.data_ptr())    # owned accumulator rows (ordered with torch's stream)
@@ -185,12 +193,12 @@ def config4(args, rank, world, local, dev):
 
 def single_gpu_frames(core, sc, steps, warmup, per_frame=None):
     """frames timed like the step loop (K frames between two synchronisations, the host queueing frame
-    i + 1 while the GPU renders frame i); Restart frames, or per_frame(i) first (config 5's instance
+    i + 1 while the GPU renders frame i); a converging still camera (frame 0 restarts), per_frame(i) first (config 5's instance
     updates).  Returns (seconds per frame, ray counts of the last frame)."""
     def frame(i):
         if per_frame:
             per_frame(i)
-        sc.render_frame(core, converge=1)
+        sc.render_frame(core, converge=LH2_RESTART if i == 0 else LH2_CONVERGE)   # as timed_frames
     for i in range(warmup):
         frame(i)
     core.sync()
@@ -272,19 +280,19 @@ def config4_incore(args, ndev):
     core.set_target(W4, H4, 1)
     setup = time.perf_counter() - t0
 
-    def frame():
+    def frame(i):
         for name, v in (("epsilon", 1e-4), ("clampValue", 10.0), ("clampDirect", 1.0), ("clampIndirect", 1.0),
                         ("filter", 0.0), ("TAA", 0.0)):
             core.setting(name, v)
-        core.render(sc.view, 1)
+        core.render(sc.view, LH2_RESTART if i == 0 else LH2_CONVERGE)   # as timed_frames
 
-    for _ in range(args.warmup):
-        frame()
+    for i in range(args.warmup):
+        frame(i)
     core.sync()
     counts = core.ray_counts()
     t0 = time.perf_counter()
-    for _ in range(args.config4_steps):
-        frame()
+    for i in range(args.config4_steps):
+        frame(args.warmup + i)
     core.sync()
     el = (time.perf_counter() - t0) / args.config4_steps
     core.close()
@@ -447,7 +455,8 @@ def main():
                                    f"({args.width}x{args.height} paths per GPU, {BAND}-row bands), 1 spp, "
                                    f"full wavefront frame (primary + bounce-1 rays); strong scaling of config 4 "
                                    f"(4K, frame split across the GPUs) in 'config4'",
-                       "frame": [W, H], "spp": 1, "tris": args.tris, "parallelism": f"tiles{world}"},
+                       "frame": [W, H], "spp": 1, "tris": args.tris, "parallelism": f"tiles{world}",
+                       "frames": "a still camera converging: one Restart, then Converge (new samples every step)"},
             "roofline": roof,
             "roofline_primary": prim,
             "detail": {"primary_rays": int(counts[0]), "secondary_rays": int(counts[1]),

@@ -328,10 +328,10 @@ struct SpatialBuilder
 		std::vector<Ref> left, right;
 		left.reserve( count ), right.reserve( count );
 		bool spatial = spAxis >= 0 && spCost < bestCost;
+		int64_t straddle = 0;
 		if (spatial)
 		{
 			/* the straddling references come out of the duplication budget (reserved before the split) */
-			int64_t straddle = 0;
 			for (const Ref& r : refs) straddle += r.box.lo[spAxis] < spPos && r.box.hi[spAxis] > spPos;
 			if (refBudget.fetch_sub( straddle ) < straddle) refBudget.fetch_add( straddle ), spatial = false;
 		}
@@ -353,6 +353,10 @@ struct SpatialBuilder
 			}
 			/* a split that does not shrink both sides could recurse forever: take the object split */
 			if (left.size() >= count || right.size() >= count) left.clear(), right.clear(), spatial = false;
+			/* give back the reservation the split did not use: all of it when abandoned, else the straddlers
+			   whose one side clipped away */
+			const int64_t added = spatial ? (int64_t)(left.size() + right.size()) - (int64_t)count : 0;
+			if (straddle > added) refBudget.fetch_add( straddle - added );
 		}
 		if (!spatial && bestAxis >= 0)
 		{

@@ -1579,7 +1579,7 @@ template <bool NL>
 __global__ __launch_bounds__( 256, LH2_PATH_MINWAVES ) void k_trace_path4d( const SceneDev s, const TraceArgs a, const ShadeParams p )
 {
 	__shared__ int lstack[LH2_STACK_LDS * 256];
-	__shared__ int lrefs[4 * 256];
+	__shared__ __attribute__( (aligned( 4096 )) ) int lrefs[4 * 256];
 	trace_stream4d<3, NL>( s, a, lstack + threadIdx.x, lrefs + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &p );
 }
 

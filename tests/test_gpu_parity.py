@@ -288,14 +288,16 @@ def test_traversal_variants_bitexact(fresh_core, version, leaf_batch, max_leaf):
     assert np.array_equal(fresh_core.trace_any(O4, D4), o.trace_any(O4, D4))
 
 
-@pytest.mark.parametrize("version,max_leaf,alpha", [(7, 1, 1e-5), (7, 4, 1e-5), (7, 2, 1e-5), (1, 2, 1e-5),
-                                                     (7, 1, 1e-7), (7, 1, 0.0)])
-def test_spatial_splits_bitexact(fresh_core, version, max_leaf, alpha):
+@pytest.mark.parametrize("version,max_leaf,alpha,budget", [(7, 1, 1e-5, 1.0), (7, 4, 1e-5, 1.0), (7, 2, 1e-5, 1.0),
+                                                            (1, 2, 1e-5, 1.0), (7, 1, 1e-7, 1.0), (7, 1, 0.0, 1.0),
+                                                            (7, 1, 1e-7, 0.002)])
+def test_spatial_splits_bitexact(fresh_core, version, max_leaf, alpha, budget):
     """Spatial splits (bvhSpatial, the default: SBVH references, a triangle in several leaves with
     clipped boxes; 0 = object splits only) change the tree only: closest hits, occlusion and a
-    packet-traced frame equal the oracle's."""
+    packet-traced frame equal the oracle's.  A small bvhSpatialBudget runs the duplication budget dry
+    (splits abandoned and reservations returned part-way through the build)."""
     fresh_core.setting("bvhSpatial", alpha)
-    fresh_core.setting("bvhSpatialBudget", 1.0)
+    fresh_core.setting("bvhSpatialBudget", budget)
     fresh_core.setting("bvhMaxLeaf", max_leaf)
     fresh_core.setting("traceVersion", version)
     sc = scene.config2_scene(n=20000, width=64, height=36)

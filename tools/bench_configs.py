@@ -29,7 +29,7 @@ from lighthouse2_amd import scene  # noqa: E402
 from lighthouse2_amd.core import RenderCore  # noqa: E402
 
 
-def measure(core, sc, frames, warmup, per_frame=None, converge_each=True):
+def measure(core, sc, frames, warmup, per_frame=None, converge_each=False):
     """frames timed like bench.py's step loop: one synchronize before and after the K frames (the host
     queues frame i+1 while the GPU renders frame i); the per-frame-synchronised time (the host's launch
     latency exposed every frame) is reported beside it"""

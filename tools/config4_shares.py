@@ -42,12 +42,12 @@ def main():
         sc.load_into(core)
         core.set_target(W4, H4, 1)
         core.set_tile_bands(0, n, BAND)
-        for _ in range(args.warmup):
-            sc.render_frame(core, converge=1)
+        for i in range(args.warmup):
+            sc.render_frame(core, converge=1 if i == 0 else 0)   # a converging still camera, as bench.py
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.frames):
-            sc.render_frame(core, converge=1)
+            sc.render_frame(core, converge=0)
         core.sync()
         ms = (time.perf_counter() - t0) / args.frames * 1e3
         counts = core.ray_counts()

@@ -12,13 +12,13 @@ import sys, re
 cur = {}
 rows = []
 for line in sys.stdin:
-    m = re.match(r"\s*\.(name|vgpr_count|sgpr_count|vgpr_spill_count|sgpr_spill_count|group_segment_fixed_size|private_segment_fixed_size|agpr_count):\s+(.*)", line)
+    # a kernel record starts with "- .<first key>" (keys are sorted: .group_segment_fixed_size precedes .name)
+    if re.match(r"\s*-\s+\.", line) and cur.get("name"):
+        rows.append(cur)
+        cur = {}
+    m = re.match(r"\s*-?\s*\.(name|vgpr_count|sgpr_count|vgpr_spill_count|sgpr_spill_count|group_segment_fixed_size|private_segment_fixed_size|agpr_count):\s+(.*)", line)
     if not m: continue
-    k, v = m.group(1), m.group(2).strip()
-    if k == "name":
-        if cur: rows.append(cur)
-        cur = {"name": v}
-    else: cur[k] = v
+    cur[m.group(1)] = m.group(2).strip()
 if cur: rows.append(cur)
 for r in rows:
     if "vgpr_count" not in r: continue
