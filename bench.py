@@ -70,8 +70,11 @@ def newest(pattern, pred=lambda d: True):
 
 
 def valu_cycles_per_instruction():
-    """Measured SIMD cycles per wave64 v_fma_f32 at full occupancy (tools/valu_rate, committed under
-    profiles/); 2 (SIMD-32, MI355X_MICROARCH.md per-instruction constants) when absent."""
+    """Measured SIMD cycles per wave64 VALU instruction at >= 4 waves per SIMD (tools/valu_rate, committed
+    under profiles/): the fastest of its instruction mixes (v_fma_f32 chains, v_pk_fma_f32 chains, and the
+    node step's mix of packed FMA, max3 / min3, compares, selects and integer key ops, whose count comes
+    from SQ_INSTS_VALU), so the peak is the highest issue rate measured; 2 (SIMD-32, MI355X_MICROARCH.md
+    per-instruction constants) when absent."""
     files = sorted(glob.glob(str(ROOT / "profiles" / "*valu_rate*.jsonl")))
     if files:
         rows = [json.loads(line) for line in open(files[-1]) if line.strip().startswith("{")]

@@ -5,7 +5,8 @@
                                          effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration), and the
                                          VALU issue rate against the chip's VALU issue peak (1024
                                          SIMDs x 2.4 GHz / the cycles per wave64 VALU instruction that
-                                         tools/valu_rate measured: 4.1 at 4-8 waves per SIMD).
+                                         tools/valu_rate measured: the fastest of its mixes at 4-8 waves
+                                         per SIMD, 3.58 for the node step's mix in round 3).
   profiles/<tag>_pmc_packet_sq.json      the same for the primary-ray packet launch.
   profiles/<tag>_pmc_config5_traffic.json  HBM bytes per launch of every kernel of config-5 frames
                                          (2 x FETCH_SIZE per the gfx950 calibration + WRITE_SIZE, KiB ->
@@ -82,7 +83,7 @@ def trace_sq(src, kernel, p1="sq1", p2="sq2", what="config-2 bounce rays from th
         "wave_cycles_waiting_frac": round(counters["SQ_WAIT_ANY"] / counters["SQ_WAVE_CYCLES"], 4)
         if "SQ_WAIT_ANY" in counters else None,
         "note": "VALU issue peak = 1024 SIMDs x 2.4 GHz / cycles per wave64 VALU instruction, measured by "
-                "tools/valu_rate (profiles/*valu_rate*.jsonl: 4.1 at 4-8 waves/SIMD); SQ_ACTIVE_INST_* and "
+                "tools/valu_rate (profiles/*valu_rate*.jsonl: the fastest instruction mix at 4-8 waves/SIMD); SQ_ACTIVE_INST_* and "
                 "SQ_WAVE_CYCLES count quad-cycles (MI355X_MICROARCH.md)",
     }
 
