@@ -1575,12 +1575,12 @@ __global__ __launch_bounds__( 256 ) void k_shade_last( const SceneDev s, const S
 #ifndef LH2_PATH_MINWAVES
 #define LH2_PATH_MINWAVES 3   /* 4: 128 VGPRs + 176 B of spills (lit); config 3 tail 0.655 ms at 4, 0.558 ms at 3 */
 #endif
-template <bool NL>
+template <bool NL, bool SINGLE>
 __global__ __launch_bounds__( 256, LH2_PATH_MINWAVES ) void k_trace_path4d( const SceneDev s, const TraceArgs a, const ShadeParams p )
 {
 	__shared__ int lstack[LH2_STACK_LDS * 256];
 	__shared__ __attribute__( (aligned( 4096 )) ) int lrefs[4 * 256];
-	trace_stream4d<3, NL>( s, a, lstack + threadIdx.x, lrefs + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &p );
+	trace_stream4d<3, SINGLE, NL>( s, a, lstack + threadIdx.x, lrefs + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &p );
 }
 
 /* counters: .cuda.cu:64-84 */
@@ -1910,7 +1910,12 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
 	/* coherent primary rays: packets over the BVH2 (lh2_trace_packet.inc); incoherent rays: the BVH4 loop
 	   (lh2_trace4d.inc), or the reference BVH2 loop (traceVersion 1, or no BVH4) */
 	if (a->packet) LH2_LAUNCH( k_trace_closest_packet, grid, 256, st, ev, *s, *a );
-	else if (a->version == 7 && s->nodes4) LH2_LAUNCH( k_trace_closest4d, grid, 256, st, ev, *s, *a );
+	else if (a->version == 7 && s->nodes4)
+	{
+		/* a single-instance scene (tlasRoot4 < 0): the loop without instance state (lh2_trace4d.inc SINGLE) */
+		if (s->tlasRoot4 < 0) LH2_LAUNCH( k_trace_closest4d<true>, grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( k_trace_closest4d<false>, grid, 256, st, ev, *s, *a );
+	}
 	else if (a->leafBatch) LH2_LAUNCH( k_trace_closest<true>, grid, 256, st, ev, *s, *a );
 	else LH2_LAUNCH( k_trace_closest<false>, grid, 256, st, ev, *s, *a );
 }
@@ -1918,8 +1923,11 @@ void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int 
 {
 	if (a->version == 7 && s->nodes4)
 	{
-		if (fused) LH2_LAUNCH( k_trace_any4d<1>, grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( k_trace_any4d<0>, grid, 256, st, ev, *s, *a );
+		const bool single = s->tlasRoot4 < 0;
+		if (fused && single) LH2_LAUNCH( (k_trace_any4d<1, true>), grid, 256, st, ev, *s, *a );
+		else if (fused) LH2_LAUNCH( (k_trace_any4d<1, false>), grid, 256, st, ev, *s, *a );
+		else if (single) LH2_LAUNCH( (k_trace_any4d<0, true>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_any4d<0, false>), grid, 256, st, ev, *s, *a );
 	}
 	else if (fused) LH2_LAUNCH( k_trace_any<1>, grid, 256, st, ev, *s, *a );
 	else LH2_LAUNCH( k_trace_any<0>, grid, 256, st, ev, *s, *a );
@@ -1933,9 +1941,11 @@ int lh2_packet_blocks_per_cu( void )
 /* the per-ray traversal kernels' occupancy (persistent grid: CUs x blocks per CU) */
 int lh2_trace_blocks_per_cu( void )
 {
-	int n1 = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest4d, 256, 0 ) != hipSuccess) n1 = 4;
-	return n1;
+	/* the smaller of the variants' (the global stack is sized for this grid) */
+	int n1 = 0, n2 = 0;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest4d<false>, 256, 0 ) != hipSuccess) n1 = 4;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_closest4d<true>, 256, 0 ) != hipSuccess) n2 = 4;
+	return n1 < n2 ? n1 : n2;
 }
 static int lh2_shade_last_grid( void )   /* k_shade_last: every CU full (occupancy x CUs), at least a block per segment */
 {
@@ -1952,14 +1962,18 @@ static int lh2_shade_last_grid( void )   /* k_shade_last: every CU full (occupan
 void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st )
 {
 	if (!s->nodes4) return;   /* the host selects the path tail only over a BVH4 */
-	if (s->nArea + s->nPoint + s->nSpot + s->nDir == 0) LH2_LAUNCH( (k_trace_path4d<true>), grid, 256, st, ev, *s, *a, *p );
-	else LH2_LAUNCH( (k_trace_path4d<false>), grid, 256, st, ev, *s, *a, *p );
+	const bool nl = s->nArea + s->nPoint + s->nSpot + s->nDir == 0, single = s->tlasRoot4 < 0;
+	if (nl && single) LH2_LAUNCH( (k_trace_path4d<true, true>), grid, 256, st, ev, *s, *a, *p );
+	else if (nl) LH2_LAUNCH( (k_trace_path4d<true, false>), grid, 256, st, ev, *s, *a, *p );
+	else if (single) LH2_LAUNCH( (k_trace_path4d<false, true>), grid, 256, st, ev, *s, *a, *p );
+	else LH2_LAUNCH( (k_trace_path4d<false, false>), grid, 256, st, ev, *s, *a, *p );
 }
 int lh2_path_blocks_per_cu( void )
 {
-	int n = 0;
-	(void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_path4d<false>, 256, 0 );
-	return n;
+	int n = 0, n2 = 0;
+	(void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_path4d<false, false>, 256, 0 );
+	(void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_path4d<false, true>, 256, 0 );
+	return n < n2 ? n : n2;
 }
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st )
 {
