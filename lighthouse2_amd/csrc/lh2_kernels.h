@@ -60,6 +60,11 @@ struct BounceAdvance  /* the hand-off to the next bounce (advance_bounce, lh2_ke
 	uint32_t* rayCountLog;           /* [pathLength] = rays of the next bounce */
 	uint32_t* hostActiveLog;         /* pinned host copy of the same (the host's early exit), or null */
 	int zeroLog;                     /* nonzero: also zero rayCountLog past pathLength (the path tail counts into it) */
+	/* shadow overlap (RenderCore setting "shadowOverlap"): the shadow rays queued so far, per segment, into
+	   shadowSnap (the side launch's segment counts) and into the final shadow launch's work-queue heads
+	   (shadowCursor, LH2_CURSOR_STRIDE apart), which then start behind them; null: off */
+	uint32_t* shadowSnap;
+	uint32_t* shadowCursor;
 };
 
 struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path state */

@@ -1791,6 +1791,12 @@ LH2_DEV void advance_bounce( Counters* c, const BounceAdvance& a, const int path
 		sh += c->segShadow[k * LH2_SEGCOUNT_STRIDE];
 		if (resetShadow) c->segShadow[k * LH2_SEGCOUNT_STRIDE] = 0;
 	}
+	if (a.shadowSnap)
+		for (int k = 0; k < LH2_SEGS; k++)
+		{
+			const uint32_t n = __hip_atomic_load( &c->segShadow[k * LH2_SEGCOUNT_STRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+			a.shadowSnap[k * LH2_SEGCOUNT_STRIDE] = n, a.shadowCursor[k * LH2_CURSOR_STRIDE] = n;
+		}
 	a.rayCountLog[pathLength] = ext;     /* rays traced at pathLength + 1 */
 	if (a.zeroLog) for (int k = pathLength + 1; k <= LH2_MAX_BOUNCES; k++) a.rayCountLog[k] = 0;
 	c->totalExtensionRays += ext;

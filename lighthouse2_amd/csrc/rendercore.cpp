@@ -96,6 +96,11 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	coreStats.deviceName = new char[strlen( name ) + 1];   /* owned (and leaked) by the core: core_api_base.h:33 */
 	memcpy( coreStats.deviceName, name, strlen( name ) + 1 );
 	CHK_HIP( hipStreamCreateWithFlags( &stream, hipStreamNonBlocking ) );
+	{
+		int least = 0, greatest = 0;
+		CHK_HIP( hipDeviceGetStreamPriorityRange( &least, &greatest ) );
+		CHK_HIP( hipStreamCreateWithPriority( &sideStream, hipStreamNonBlocking, least ) );
+	}
 	/* blue noise sampler tables (rendercore.cpp:125-134), shipped as data/bluenoise.bin */
 	std::string path = getenv( "LH2_BLUENOISE" ) ? getenv( "LH2_BLUENOISE" ) : LibraryDir() + "/data/bluenoise.bin";
 	FILE* f = fopen( path.c_str(), "rb" );
@@ -122,6 +127,8 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	for (auto& e : ps.evCount) CHK_HIP( hipEventCreate( &e ) );   /* stop events of launches (LaunchEvents) */
 	CHK_HIP( hipEventCreate( &ps.evCamera ) );
 	CHK_HIP( hipEventCreate( &ps.evShadow ) );
+	CHK_HIP( hipEventCreate( &ps.evSide ) );
+	ps.shSnap.resize( LH2_SEGS * LH2_SEGCOUNT_STRIDE );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
@@ -199,6 +206,7 @@ void RenderCore::EnsureStack()
 {
 	const size_t need = (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256;
 	if (ps.gstack.count < need) ps.gstack.resize( need );
+	if (shadowOverlap && ps.sideStack.count < need) ps.sideStack.resize( need );
 }
 
 void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439-457 */
@@ -232,6 +240,8 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "packetHeavy" )) packetHeavy = std::max( 0.0f, value );   /* heavy-first primary packets; 0: off */
 	else if (!strcmp( name, "pathTail" )) pathTail = std::max( 0, (int)value );   /* bounces from this one in one trace-and-shade launch; 0: off */
 	else if (!strcmp( name, "pathTailBatch" )) pathTailBatch = std::min( 64, std::max( 1, (int)value ) );
+	else if (!strcmp( name, "shadowOverlap" )) shadowOverlap = value != 0;
+	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
@@ -254,7 +264,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch },
+		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "pathTailBlocks", (float)pathTailBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -809,6 +819,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	frameShadows = shadows;
 	/* the path tail (setting "pathTail"): bounces pathTail .. maxPL in one launch of k_trace_path4d */
 	const int tailL = (!primeRef && pathTail >= 2 && pathTail <= maxPL && TraceVersion() == 7) ? pathTail : 0;
+	/* shadow overlap: the shade launch before the tail snapshots the queued shadow rays (advance_bounce) */
+	const bool overlap = shadows && tailL && shadowOverlap;
+	bool snapped = false;
+	ps.sideOn = false;
 	/* the bounce loop */
 	for (int pathLength = 1; pathLength <= maxPL; pathLength++)
 	{
@@ -854,7 +868,26 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			sp.rayOut = ps.rayO[ps.in].ptr, sp.rayDOut = ps.rayD[ps.in].ptr, sp.T4Out = ps.T4[ps.in].ptr, sp.Q4Out = ps.Q4[ps.in].ptr;
 			sp.adv.rayCountLog = ps.rayLog.ptr;
 			ta.shadeBatch = (uint32_t)pathTailBatch;
-			lh2_launch_trace_path( &sd, &ta, &sp, PathGrid(), { nullptr, ps.evTrace[pathLength] }, stream );
+			/* with the overlap the path tail runs fewer blocks per CU (pathTailBlocks, default 2) and leaves
+			   registers for the side launch's waves */
+			const bool side = overlap && snapped;
+			const int ptBlocks = pathTailBlocks > 0 ? pathTailBlocks : side ? 2 : pathBlocksPerCU;
+			lh2_launch_trace_path( &sd, &ta, &sp, smCount * std::min( std::min( blocksPerCU, pathBlocksPerCU ), ptBlocks ), { nullptr, ps.evTrace[pathLength] }, stream );
+			if (side)
+			{
+				/* the shadow rays of the bounces before the tail, beside it on the side stream (segment counts:
+				   the snapshot; the final launch's work-queue heads start behind them) */
+				CHK_HIP( hipStreamWaitEvent( sideStream, ps.prevStop, 0 ) );
+				TraceArgs ts{};
+				ts.version = TraceVersion();
+				ts.rayO = ps.shO.ptr, ts.rayD = ps.shD.ptr, ts.segCounts = ps.shSnap.ptr, ts.segStride = ps.shadowStride;
+				ts.cursor = ps.cursors.ptr + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS;
+				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
+				ts.mask = ps.shMask.ptr, ts.potentials = ps.shP.ptr, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
+				lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, ps.evSide }, sideStream );
+				ps.fromSide = ps.prevStop;
+				ps.sideOn = true;
+			}
 			ps.fromTrace[pathLength] = ps.prevStop, ps.prevStop = ps.evTrace[pathLength];
 			ps.tailL = pathLength;   /* no shade interval of its own (Synchronize) */
 			break;
@@ -872,7 +905,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		}
 		/* the hand-off to the next bounce: the shade launch's last block (no launch of its own), except
 		   in PrimeRef mode, where the bounce's shadow rays are traced (and their counts reset) first */
-		const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, ps.rayLog.ptr, ps.activeLog, pathLength + 1 == tailL };
+		const bool snap = overlap && pathLength + 1 == tailL;
+		const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, ps.rayLog.ptr, ps.activeLog, pathLength + 1 == tailL,
+			snap ? ps.shSnap.ptr : nullptr, snap ? ps.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr };
+		snapped = snapped || snap;
 		sp.advance = pathLength < maxPL && !primeRef;
 		sp.adv = adv;
 		sp.rayO = ps.rayO[ps.in].ptr, sp.rayD = ps.rayD[ps.in].ptr, sp.T4 = ps.T4[ps.in].ptr, sp.Q4 = ps.Q4[ps.in].ptr, sp.hits = ps.hits.ptr;
@@ -882,6 +918,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
 		lh2_launch_shade( &sd, &sp, grid, { nullptr, ps.evShade[pathLength] }, stream );
 		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];
+
 		if (pathLength == maxPL) break;
 		if (primeRef && shadows)
 		{
@@ -912,6 +949,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		}
 		ps.in = 1 - ps.in;
 	}
+	/* a snapshot whose side launch did not happen (the frame ended before its path tail): the final launch
+	   traces every shadow ray, from the first */
+	if (snapped && !ps.sideOn)
+		CHK_HIP( hipMemsetAsync( ps.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
 	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
 	if (!primeRef && shadows)
 	{
@@ -923,6 +964,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, ps.evShadow }, stream );
 		ps.fromShadow = ps.prevStop;
 	}
+	/* the side launch's contributions are in the accumulator before the frame is finalized */
+	if (ps.sideOn) CHK_HIP( hipStreamWaitEvent( stream, ps.evSide, 0 ) );
 	samplesTaken += scrspp;
 	/* finalize also delivers the frame's counters and ray-count log, and the scene error, to hostStats */
 	const FrameStatsDev fs{ c, ps.rayLog.ptr + 1, &hostStats->counters, hostStats->rayCount + 1, dSceneError.ptr, &hostStats->sceneError };
@@ -1018,7 +1061,7 @@ void RenderCore::Synchronize()
 		if (L <= ps.pl) coreStats.traceTimeX = trace( L );
 	}
 	float shadow = 0, shade = 0;
-	if (frameShadows && !framePrimeRef) shadow = ms( ps.fromShadow, ps.evShadow );
+	if (frameShadows && !framePrimeRef) shadow = ms( ps.fromShadow, ps.evShadow ) + (ps.sideOn ? ms( ps.fromSide, ps.evSide ) : 0.0f);
 	else if (frameShadows) for (int L = 1; L < ps.pl; L++) shadow += ms( ps.fromShadowB[L], ps.evShadowB[L] );
 	for (int L = 1; L <= ps.pl; L++) if (L != ps.tailL) shade += ms( ps.fromShade[L], ps.evShade[L] );
 	coreStats.shadowTraceTime = shadow;
@@ -1260,7 +1303,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto& e : ps.evShade) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evShadowB) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evCount) (void)hipEventDestroy( e ), e = nullptr;
-	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
+	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow, &ps.evSide }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
 	if (ps.activeLog) (void)hipHostFree( ps.activeLog );
 	ps.activeLog = nullptr;
 	for (hipEvent_t* e : { &evConsumer, &evPacked }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
@@ -1272,6 +1315,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	if (hostStats) (void)hipHostFree( hostStats );
 	hostStats = nullptr;
 	(void)hipStreamDestroy( stream );
+	if (sideStream) (void)hipStreamDestroy( sideStream ), sideStream = nullptr;
 	stream = nullptr;
 	initialized = false;
 }

@@ -70,6 +70,8 @@ struct PathStreams
 	DevBuf<float4> shO, shD, shP;
 	DevBuf<uint32_t> shMask;
 	DevBuf<int> gstack;
+	DevBuf<int> sideStack;               /* the side shadow launch's global stack (shadowOverlap) */
+	DevBuf<uint32_t> shSnap;             /* the shadow rays queued before the path tail, per segment (advance_bounce) */
 	DevBuf<Counters> counters;
 	DevBuf<uint32_t> cursors;            /* LH2_CURSOR_SLOTS x LH2_CURSOR_WORDS work-queue heads */
 	DevBuf<uint32_t> rayLog;
@@ -80,6 +82,8 @@ struct PathStreams
 	   interval runs from the previous launch's stop event, so it includes the launch gap */
 	hipEvent_t evTrace[LH2_MAX_BOUNCES + 1] = {}, evShade[LH2_MAX_BOUNCES + 1] = {}, evShadowB[LH2_MAX_BOUNCES + 1] = {};
 	hipEvent_t evCount[LH2_MAX_BOUNCES + 2] = {}, evCamera = nullptr, evShadow = nullptr;
+	hipEvent_t evSide = nullptr, fromSide = nullptr;   /* shadowOverlap: the side launch */
+	bool sideOn = false;                 /* this frame traced its early shadow rays on the side stream */
 	hipEvent_t countReady[LH2_MAX_BOUNCES + 2] = {};   /* [L]: the event after which bounce L's hand-off is done (evShade or evCount, not owned) */
 	hipEvent_t fromTrace[LH2_MAX_BOUNCES + 1] = {}, fromShade[LH2_MAX_BOUNCES + 1] = {}, fromShadowB[LH2_MAX_BOUNCES + 1] = {}, fromShadow = nullptr;
 	/* this frame */
@@ -151,6 +155,7 @@ public:
 
 	lh2_CoreStats coreStats{};
 	hipStream_t stream = nullptr;
+	hipStream_t sideStream = nullptr;    /* shadowOverlap: lowest priority */
 
 private:
 	void EnsureBuffers();
@@ -240,6 +245,13 @@ private:
 	   a wave shading its finished queries once pathTailBatch lanes hold one (or none walks); 0: a launch
 	   pair per bounce.  Config 3 (profiles/r02zb_ab_path_tail.txt): 2.542 -> 2.389 ms per frame at 3 / 56 */
 	int pathTail = 3, pathTailBatch = 56;
+	/* shadow overlap: the shadow rays queued before the path tail are traced on a low-priority side stream
+	   while the path tail runs (latency bound, it leaves much of the chip idle); the final shadow launch
+	   traces only the path tail's.  Config 3 2.29 -> 2.235 ms, config-4 rank share at N = 8 1.431 -> 1.363
+	   ms with the tail at 2 blocks per CU (profiles/r03g_overlap_sweep.txt); a side launch after every
+	   shade launch slows the bounces it overlaps (2.344 / 1.426 ms) */
+	bool shadowOverlap = true;
+	int pathTailBlocks = 0;              /* the path tail's blocks per CU; 0: 2 with the overlap, else its occupancy limit */
 	/* heavy-first primary packets (TraceArgs::hvRead): the packets of the previous frame that took more than
 	   packetHeavy x its mean node steps are taken first; 0: off */
 	float packetHeavy = 2.0f;

@@ -131,3 +131,34 @@ def test_heavy_first_packets_frames(fresh_core, factor):
         sc2.render_frame(o2, converge=1 if f == 0 else 0)
         assert np.array_equal(fresh_core.ray_counts(), o2.ray_counts()), f
     assert rel_l2(fresh_core.accumulator()[..., :3], o2.accumulator()[..., :3]) <= REL_L2_TOL
+
+
+@pytest.mark.parametrize("blocks", [0, 3])
+@pytest.mark.parametrize("tail", [2, 3])
+def test_shadow_overlap(fresh_core, blocks, tail):
+    """shadowOverlap: the shadow rays queued before the path tail are traced on the side stream beside it
+    (their segment counts snapshotted by the shade launch before the tail; the path tail at 2 blocks per CU,
+    or pathTailBlocks), and the final shadow launch starts behind them.  Every shadow ray is traced once:
+    the same ray counts and occlusion as the oracle, three converging frames within rel-L2 1e-4 of it, and
+    within float summation order of the frames traced with the overlap off."""
+    w, h = 128, 72
+    sc = _scene("room", w, h)
+    o = _load_both(fresh_core, sc, w, h)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", 4)
+    fresh_core.setting("pathTail", tail)
+    fresh_core.setting("pathTailBlocks", blocks)
+    res = {}
+    for ov in (1, 0):
+        fresh_core.setting("shadowOverlap", ov)
+        for f in range(3):
+            sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
+            if ov:
+                sc.render_frame(o, converge=1 if f == 0 else 0)
+                assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), f
+        res[ov] = (fresh_core.accumulator(), fresh_core.stats())
+    ag, st = res[1]
+    co = o.ray_counts()
+    assert co[16] > 0 and st.totalShadowRays == co[16], (st.totalShadowRays, co[16])
+    assert rel_l2(ag[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
+    assert rel_l2(ag[..., :3], res[0][0][..., :3]) <= 1e-6
