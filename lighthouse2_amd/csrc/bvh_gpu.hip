@@ -551,6 +551,83 @@ __global__ __launch_bounds__( 256 ) void k_tlas_to_bvh4( const float4* __restric
 	d[7] = make_float4( 0, 0, 0, 0 );
 }
 
+/* quantized BVH4 node (64 B, read by box4q in lh2_box4.inc):
+     uint4 [0]  origin x, y, z (f32 bits: the smallest lo of the node's children), then the grid exponents
+                e_x, e_y, e_z as signed bytes (plane = origin + q * 2^e)
+     uint4 [1]  x lo bytes of children 0..3, x hi bytes, y lo bytes, y hi bytes
+     uint4 [2]  z lo bytes, z hi bytes, 0, 0
+     uint4 [3]  the four child references (as the f32 node's)
+   Child planes round outward (lo down, hi up, computed in double, so the quantized box holds the f32 one
+   exactly); an empty slot (NaN planes) is the inverted box lo = 255, hi = 0 with the pop marker as its
+   reference.  A box the traversal enters by mistake only costs work: it holds no hit the f32 tree's boxes
+   do not hold (tests are exact per triangle).  Each exponent is at least the coordinate magnitude's - 28, so a plane's grid step is never
+   below the rounding of the slab arithmetic, and at least -100 (the scaled reciprocal stays normal). */
+__global__ __launch_bounds__( 256 ) void k_quantize4( const float4* __restrict__ nodes4, int first, int count, uint4* __restrict__ q )
+{
+	const int i = blockIdx.x * 256 + threadIdx.x;
+	if (i >= count) return;
+	const float4* s = nodes4 + (size_t)(first + i) * 8;
+	float lo[3][4], hi[3][4];
+	for (int a = 0; a < 3; a++)
+	{
+		const float4 l = s[2 * a], h = s[2 * a + 1];
+		lo[a][0] = l.x, lo[a][1] = l.y, lo[a][2] = l.z, lo[a][3] = l.w;
+		hi[a][0] = h.x, hi[a][1] = h.y, hi[a][2] = h.z, hi[a][3] = h.w;
+	}
+	bool valid[4];
+	for (int c = 0; c < 4; c++)
+	{
+		valid[c] = true;
+		for (int a = 0; a < 3; a++) valid[c] = valid[c] && isfinite( lo[a][c] ) && isfinite( hi[a][c] ) && lo[a][c] <= hi[a][c];
+	}
+	float origin[3];
+	int e[3];
+	uint32_t qlo[3] = { 0, 0, 0 }, qhi[3] = { 0, 0, 0 };
+	for (int a = 0; a < 3; a++)
+	{
+		float o = 0, m = 0;
+		bool any = false;
+		for (int c = 0; c < 4; c++)
+			if (valid[c]) o = any ? fminf( o, lo[a][c] ) : lo[a][c], m = any ? fmaxf( m, hi[a][c] ) : hi[a][c], any = true;
+		origin[a] = o;
+		const double ext = (double)m - (double)o;
+		const double mag = fmax( fabs( (double)o ), fabs( (double)m ) );
+		int ea = -100;
+		if (ext > 0) ea = max( ea, (int)ceil( log2( ext / 255.0 ) ) );
+		if (mag > 0) ea = max( ea, (int)floor( log2( mag ) ) - 28 );
+		while (ext > 255.0 * ldexp( 1.0, ea ) && ea < 127) ea++;   /* finite ext: ends well before the cap */
+		e[a] = ea;
+		const double step = ldexp( 1.0, ea );
+		for (int c = 0; c < 4; c++)
+		{
+			uint32_t l = 255, h = 0;
+			if (valid[c])
+			{
+				const double dl = floor( ((double)lo[a][c] - (double)o) / step ), dh = ceil( ((double)hi[a][c] - (double)o) / step );
+				l = (uint32_t)fmin( fmax( dl, 0.0 ), 255.0 ), h = (uint32_t)fmin( fmax( dh, 0.0 ), 255.0 );
+				/* outward in exact arithmetic: origin + l * step <= lo, origin + h * step >= hi */
+				while (l > 0 && (double)o + (double)l * step > (double)lo[a][c]) l--;
+				while (h < 255 && (double)o + (double)h * step < (double)hi[a][c]) h++;
+			}
+			qlo[a] |= l << (8 * c), qhi[a] |= h << (8 * c);
+		}
+	}
+	uint4* d = q + (size_t)(first + i) * 4;
+	d[0] = make_uint4( __float_as_uint( origin[0] ), __float_as_uint( origin[1] ), __float_as_uint( origin[2] ),
+		(uint32_t)(e[0] & 255) | ((uint32_t)(e[1] & 255) << 8) | ((uint32_t)(e[2] & 255) << 16) );
+	d[1] = make_uint4( qlo[0], qhi[0], qlo[1], qhi[1] );
+	d[2] = make_uint4( qlo[2], qhi[2], 0u, 0u );
+	/* an empty slot's reference is the traversal's pop marker (INT_MIN, LH2_POP in lh2_kernels.hip): if the
+	   inverted box is ever entered (a small node far down the ray, where the exit pad exceeds its grid), the
+	   ray just pops on (the f32 nodes keep 0 there, a real node, behind boxes of NaN that never hit) */
+	int4 r = *(const int4*)(s + 6);
+	if (!valid[0]) r.x = INT_MIN;
+	if (!valid[1]) r.y = INT_MIN;
+	if (!valid[2]) r.z = INT_MIN;
+	if (!valid[3]) r.w = INT_MIN;
+	d[3] = make_uint4( (uint32_t)r.x, (uint32_t)r.y, (uint32_t)r.z, (uint32_t)r.w );
+}
+
 inline int blocks( long n, int bs = 256 ) { return (int)std::max<long>( 1, (n + bs - 1) / bs ); }
 
 }  // namespace
@@ -683,6 +760,13 @@ void GpuBvhBuilder::Relocate4( const float4* src, int nodeCount, int nodeBase, u
 	if (nodeCount <= 0) return;
 	k_relocate4<<<blocks( nodeCount ), 256, 0, st>>>( src, nodeCount, nodeBase, triBase, dst );
 }
+void GpuBvhBuilder::Quantize4( const float4* nodes4, int first, int count, uint4* q, hipStream_t st )
+{
+	if (count <= 0) return;
+	k_quantize4<<<blocks( count ), 256, 0, st>>>( nodes4, first, count, q );
+	CHK( hipGetLastError() );
+}
+
 void GpuBvhBuilder::TlasToBvh4( const float4* nodes2, int base2, int count, int base4, float4* nodes4, hipStream_t st )
 {
 	if (count <= 0) return;

@@ -545,12 +545,12 @@ void RenderCore::ConcatenateBlas( int ni )
 	}
 	tlasCapacity = std::max( 64, 2 * ni + 16 );
 	CHK_HIP( hipStreamSynchronize( stream ) );   /* frames in flight may still read the old arrays */
-	dNodes.free(), dTris.free(), dNodes4.free();
+	dNodes.free(), dTris.free(), dNodes4.free(), dNodes4q.free();
 	dNodes.resize( ((size_t)nodeTotal + tlasCapacity) * 4 );
 	/* the BVH4 loops address nodes with 32-bit buffer offsets (lh2_trace4d.inc): the array stays below 2 GiB */
 	if (bvh4 && ((size_t)node4Total + tlasCapacity) * 128 > 0x7fffffffull)
 		FatalError( "BVH4 of %zu nodes exceeds the 2 GiB the traversal addresses", (size_t)node4Total + tlasCapacity );
-	if (bvh4) dNodes4.resize( ((size_t)node4Total + tlasCapacity) * 8 );
+	if (bvh4) dNodes4.resize( ((size_t)node4Total + tlasCapacity) * 8 ), dNodes4q.resize( ((size_t)node4Total + tlasCapacity) * 4 );
 	dTris.resize( (size_t)std::max( triTotal, 1 ) * 3 );
 	for (size_t mi = 0; mi < meshes.size(); mi++)
 	{
@@ -559,6 +559,7 @@ void RenderCore::ConcatenateBlas( int ni )
 		if (bvh4) GpuBvhBuilder::Relocate4( m.bvh4Nodes.ptr, m.node4Count, meshNode4Base[mi], (uint32_t)meshTriBase[mi], dNodes4.ptr, stream );
 		if (m.leafTris) CHK_HIP( hipMemcpyAsync( dTris.ptr + (size_t)meshTriBase[mi] * 3, m.bvhTris.ptr, sizeof( float4 ) * 3 * (size_t)m.leafTris, hipMemcpyDeviceToDevice, stream ) );
 	}
+	if (bvh4) GpuBvhBuilder::Quantize4( dNodes4.ptr, 0, node4Total, dNodes4q.ptr, stream );
 	dMeshBounds.upload( bounds.data(), bounds.size(), stream );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	blasNodeCount = nodeTotal, blasTriCount = triTotal, blasNode4Count = node4Total, blasMeshTris = meshTris;
@@ -698,7 +699,11 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		if (sceneMaxDepth >= LH2_STACK_TOTAL - 1) FatalError( "BVH depth %d exceeds the traversal stack (%d)", sceneMaxDepth, LH2_STACK_TOTAL );
 	}
 	/* the TLAS in the BVH4 array: its BVH2 nodes as two-child BVH4 nodes (one short launch) */
-	if (bvh4) GpuBvhBuilder::TlasToBvh4( dNodes.ptr, blasNodeCount, tlasCapacity, blasNode4Count, dNodes4.ptr, stream );
+	if (bvh4)
+	{
+		GpuBvhBuilder::TlasToBvh4( dNodes.ptr, blasNodeCount, tlasCapacity, blasNode4Count, dNodes4.ptr, stream );
+		GpuBvhBuilder::Quantize4( dNodes4.ptr, blasNode4Count, tlasCapacity, dNodes4q.ptr, stream );
+	}
 	CHK_HIP( hipEventRecord( evStage[slot], stream ) );
 	instancesDirty = false;
 }
@@ -723,7 +728,7 @@ SceneDev RenderCore::MakeSceneDev() const
 	s.argb32 = dArgb32.ptr, s.nrm32 = dNrm32.ptr;
 	s.argb32Count = (uint32_t)dArgb32.count, s.nrm32Count = (uint32_t)dNrm32.count;
 	s.tlasRoot = tlasRoot, s.instCount = (int)instances.size();
-	s.nodes4 = dNodes4.ptr, s.tlasRoot4 = blasNode4Count;
+	s.nodes4 = dNodes4.ptr, s.nodes4q = dNodes4q.ptr, s.tlasRoot4 = blasNode4Count;
 	/* one instance of a non-empty mesh: rays start at its TLAS leaf (MAKE_LEAF( 0, 1 ) = ~0) and skip
 	   the TLAS root's box test, which can only cull (TopLevelBVH::Traverse bvh.cpp:594-649); the
 	   instance transform runs as at the leaf, so the hits are unchanged: one loop iteration less per ray */

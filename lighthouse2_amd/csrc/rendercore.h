@@ -183,6 +183,7 @@ private:
 	bool geometryDirty = true, instancesDirty = true;
 	DevBuf<float4> dNodes, dTris;
 	DevBuf<float4> dNodes4;              /* BVH4: all BLAS (relocated), then the TLAS as two-child nodes */
+	DevBuf<uint4> dNodes4q;              /* the same nodes with quantized child boxes (GpuBvhBuilder::Quantize4) */
 	DevBuf<uint8_t> dInst;               /* DevInstance[] */
 	DevBuf<lh2_CoreInstanceDesc> dInstDesc;
 	int tlasRoot = 0, blasNodeCount = 0, blasTriCount = 0, blasMeshTris = 0, sceneMaxDepth = 0;   /* blasTriCount: leaf triangle records; blasMeshTris: triangles */
