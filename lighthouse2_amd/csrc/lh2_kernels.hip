@@ -231,7 +231,9 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 /* =====================================================================================
    traversal: two-level BVH2, ordered, t-culled, LDS short stack + global spill
    ===================================================================================== */
+#ifndef LH2_TRACE_MINWAVES
 #define LH2_TRACE_MINWAVES 7   /* min waves per SIMD the traversal kernels are compiled for (VGPR cap 72) */
+#endif
 #define STACK_LDS LH2_STACK_LDS   /* entries per lane kept in LDS: 16 x 256 x 4 B = 16 KB / block */
 #define STACK_TOTAL LH2_STACK_TOTAL /* + global spill; the host checks the tree depth against it */
 
