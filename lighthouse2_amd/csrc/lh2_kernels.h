@@ -34,6 +34,7 @@ struct SceneDev       /* everything the traversal and shading kernels read, by v
 	int tlasRoot, instCount;
 	const float4* nodes4;            /* BVH4 of the same scene (traceVersion 4; null when not built) */
 	const uint4* nodes4q;            /* the same BVH4 with quantized child boxes, 64 B per node (lh2_box4.inc, box4q) */
+	float qBound;                    /* >= |coordinate| of every node origin, world and mesh space (slab_offsets) */
 	int tlasRoot4;
 	const lh2_CoreInstanceDesc* instDesc;
 	const uint4* materials;          /* 128 B CUDAMaterial records (core_settings.h:94-104) */

@@ -626,6 +626,13 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 			}
 		}
 	}
+	/* the quantized nodes' origins lie in these boxes (TLAS: world; BLAS: mesh space); 1 % slack for the
+	   device-side TLAS bounds' own rounding */
+	qBound = 0;
+	for (int k = 0; k < 3; k++) qBound = std::max( qBound, std::max( fabsf( sceneLo[k] ), fabsf( sceneHi[k] ) ) );
+	for (const auto& m : meshes)
+		if (m->triCount) for (int k = 0; k < 3; k++) qBound = std::max( qBound, std::max( fabsf( m->aabbLo[k] ), fabsf( m->aabbHi[k] ) ) );
+	qBound = qBound * 1.01f + 1e-30f;
 	dInst.resize( nRec * sizeof( DevInstance ) ), dInstDesc.resize( nRec ), dInstT.resize( nRec * 16 ), dInstMesh.resize( nRec );
 	dSceneError.resize( 1 ), dTlasDepth.resize( 1 );
 	CHK_HIP( hipMemcpyAsync( dInst.ptr, di, nRec * sizeof( DevInstance ), hipMemcpyHostToDevice, stream ) );
@@ -728,7 +735,7 @@ SceneDev RenderCore::MakeSceneDev() const
 	s.argb32 = dArgb32.ptr, s.nrm32 = dNrm32.ptr;
 	s.argb32Count = (uint32_t)dArgb32.count, s.nrm32Count = (uint32_t)dNrm32.count;
 	s.tlasRoot = tlasRoot, s.instCount = (int)instances.size();
-	s.nodes4 = dNodes4.ptr, s.nodes4q = dNodes4q.ptr, s.tlasRoot4 = blasNode4Count;
+	s.nodes4 = dNodes4.ptr, s.nodes4q = dNodes4q.ptr, s.qBound = qBound, s.tlasRoot4 = blasNode4Count;
 	/* one instance of a non-empty mesh: rays start at its TLAS leaf (MAKE_LEAF( 0, 1 ) = ~0) and skip
 	   the TLAS root's box test, which can only cull (TopLevelBVH::Traverse bvh.cpp:594-649); the
 	   instance transform runs as at the leaf, so the hits are unchanged: one loop iteration less per ray */

@@ -242,6 +242,7 @@ private:
 	int bvh4Collapse = 1;                /* BVH4 collapse: 0 greedy (CollapseBvh4), 1 dynamic programming (CollapseBvh4Sah) */
 	float chordSplit = 0.35f;            /* extension rays with a chord through the scene box below this x its extent are traced last */
 	float sceneLo[3] = { 0, 0, 0 }, sceneHi[3] = { 0, 0, 0 };   /* world box of the instanced meshes (UpdateToplevel) */
+	float qBound = 0;                    /* |coordinate| bound of the world box and every mesh box, with slack (SceneDev::qBound) */
 	/* the path tail (k_trace_path4d): bounces pathTail .. maxPathLength traced and shaded in one launch,
 	   a wave shading its finished queries once pathTailBatch lanes hold one (or none walks); 0: a launch
 	   pair per bounce.  Config 3 (profiles/r02zb_ab_path_tail.txt): 2.542 -> 2.389 ms per frame at 3 / 56 */
