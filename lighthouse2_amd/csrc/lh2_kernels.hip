@@ -545,7 +545,9 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 /* 8 waves per SIMD (64 VGPRs, ~32 spilled outside the node loop): the packet loop is bound by the
    latency of its dependent node fetches, and 8 waves hide more of it than the unbounded 94-VGPR
    build's 5: 0.481 -> 0.437 ms on the config-2 primary rays (A/B 5/6/7/8 waves, r01c) */
+#ifndef LH2_PACKET_MINWAVES
 #define LH2_PACKET_MINWAVES 8
+#endif
 __global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet( s, a ); }
 
 /* the reference BVH2 loop (traceVersion 1; the BVH4 is not built with setting "bvh4" 0) */
