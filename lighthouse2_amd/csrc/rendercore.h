@@ -234,8 +234,9 @@ private:
 	int tiledRays = 1;                   /* primary rays stored in 8x8 pixel blocks per wave (coherent packets) */
 	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle; BLAS leaves parked until this many
 	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,
-	   r02y_ab_v7.txt) */
-	int refillPrimary = 48, refillOther = 48, leafBatch = 6, leafBatchPrimary = 8;
+	   r02y_ab_v7.txt); leafBatch 8 with the quantized nodes (bounce 0.492 -> 0.488 ms, N = 8 share 1.35 -> 1.32 ms,
+	   r03k_ab_leafbatch.txt) */
+	int refillPrimary = 48, refillOther = 48, leafBatch = 8, leafBatchPrimary = 8;
 	int bvhMaxLeaf = 1;
 	float bvhSpatial = 1e-5f;            /* spatial splits (SBVH): overlap threshold x root area; 0 = off */
 	float bvhSpatialBudget = 1.0f;       /* ... adding at most this many references per triangle */
