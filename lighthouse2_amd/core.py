@@ -81,6 +81,7 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
         "lh2_core_scene_info": [_P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)],
         "lh2_xorshift_floats": [C.c_uint32, _F, C.c_uint64],
         "lh2_core_debug_shadow_rays": [_P, _F, _F, _F, C.c_int, C.POINTER(C.c_int)],
+        "lh2_core_debug_bvh4": [_P, _F, C.c_void_p, C.c_int, C.POINTER(C.c_int)],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -297,6 +298,14 @@ class RenderCore:
         n = C.c_int(0)
         self._chk(self.lib.lh2_core_debug_shadow_rays(self.h, _fp(o), _fp(d), _fp(p), int(cap), C.byref(n)))
         return o[:n.value], d[:n.value], p[:n.value]
+
+    def debug_bvh4(self, cap: int = 1 << 22):
+        """Diagnostics: the scene's BVH4 nodes, (n, 32) float32 (f32 layout) and (n, 16) uint32 (quantized)."""
+        f = np.zeros((cap, 32), np.float32)
+        q = np.zeros((cap, 16), np.uint32)
+        n = C.c_int(0)
+        self._chk(self.lib.lh2_core_debug_bvh4(self.h, _fp(f), q.ctypes.data, int(cap), C.byref(n)))
+        return f[:n.value], q[:n.value]
 
     def scene_info(self) -> dict:
         v = [C.c_int(0) for _ in range(4)]

@@ -1117,6 +1117,17 @@ int RenderCore::DebugShadowRays( float* o4, float* d4, float* p4, int cap )
 	return n;
 }
 
+int RenderCore::DebugBvh4( float* f32Nodes, uint32_t* qNodes, int cap )
+{
+	if (geometryDirty || instancesDirty) UpdateToplevel();
+	Synchronize();
+	const int n = std::min( cap, blasNode4Count + tlasCapacity );
+	if (n <= 0 || !dNodes4.ptr || !dNodes4q.ptr) return 0;
+	CHK_HIP( hipMemcpy( f32Nodes, dNodes4.ptr, 128 * (size_t)n, hipMemcpyDeviceToHost ) );
+	CHK_HIP( hipMemcpy( qNodes, dNodes4q.ptr, 64 * (size_t)n, hipMemcpyDeviceToHost ) );
+	return n;
+}
+
 void RenderCore::GetAccumulator( float* hostOut4 )
 {
 	Synchronize();

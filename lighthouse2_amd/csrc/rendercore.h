@@ -146,6 +146,7 @@ public:
 	void GetRayCounts( uint32_t* out17 );
 	/* diagnostics: the last frame's queued shadow rays {O, tmin} {D, tmax} {potential rgb, pixel bits}, segment by segment */
 	int DebugShadowRays( float* o4, float* d4, float* p4, int cap );
+	int DebugBvh4( float* f32Nodes, uint32_t* qNodes, int cap );   /* the BVH4 nodes, f32 (32 floats) and quantized (16 words) */
 	void TraceClosest( const float* orgTmin4, const float* dirTmax4, int n, uint32_t* hits4 );   /* host in/out */
 	void TraceAny( const float* orgTmin4, const float* dirTmax4, int n, uint32_t* occluded );
 	void TraceClosestDevice( const void* rayO, const void* rayD, int n, void* hits, int iterations, float* msOut );

@@ -521,3 +521,44 @@ def test_grazing_rays_box_rounding(fresh_core, version):
     hp = fresh_core.trace_closest(O4, D4)
     fresh_core.setting("unitCoherent", 0)
     assert np.array_equal(hp, ho), np.argwhere((hp != ho).any(1))[:10]
+
+
+def test_quantized_nodes_hold_the_f32_boxes(fresh_core):
+    """k_quantize4 (bvh_gpu.hip): every child box of every BVH4 node (BLAS and TLAS, a mesh far from the origin
+    and a chain of tiny triangles among them) is inside its quantized box in exact arithmetic, an empty slot is
+    the inverted box with the pop marker as its reference, and the references are the f32 node's."""
+    k = np.arange(60, dtype=np.float32)
+    x = (6.0 * 0.9 ** k).astype(np.float32)
+    s_ = (0.02 * 0.9 ** k).astype(np.float32)
+    z0 = np.zeros_like(x)
+    chain = abi.tris_from_vertices(np.stack([x, -s_, z0], 1), np.stack([x + s_, s_, z0], 1), np.stack([x - s_, s_, s_], 1), 0)
+    sc = scene.config2_scene(n=4000, width=64, height=36)
+    sc.meshes.append(chain)
+    far = np.eye(4, dtype=np.float32)
+    far[:3, 3] = (1000.0, -500.0, 250.0)
+    sc.instances.append((1, far))
+    sc.instances.append((0, far))
+    sc.load_into(fresh_core)
+    fresh_core.set_target(64, 36, 1)
+    f, q = fresh_core.debug_bvh4()
+    assert len(f) > 100
+    lo = np.stack([f[:, 0:4], f[:, 8:12], f[:, 16:20]], 1).astype(np.float64)    # (n, axis, child)
+    hi = np.stack([f[:, 4:8], f[:, 12:16], f[:, 20:24]], 1).astype(np.float64)
+    valid = (np.isfinite(lo) & np.isfinite(hi) & (lo <= hi)).all(1)              # (n, child)
+    origin = q[:, 0:3].view(np.float32).astype(np.float64)
+    exps = ((q[:, 3:4] >> np.array([0, 8, 16], np.uint32)) & 255).astype(np.int8).astype(np.int64)
+    step = np.ldexp(1.0, exps)                                                     # (n, axis)
+    shifts = np.array([0, 8, 16, 24], np.uint32)
+    qlo = np.stack([(q[:, 4 + 2 * a, None] >> shifts) & 255 for a in range(3)], 1).astype(np.float64)
+    qhi = np.stack([(q[:, 5 + 2 * a, None] >> shifts) & 255 for a in range(3)], 1).astype(np.float64)
+    dlo = origin[:, :, None] + qlo * step[:, :, None]
+    dhi = origin[:, :, None] + qhi * step[:, :, None]
+    v3 = np.broadcast_to(valid[:, None, :], lo.shape)
+    assert np.all(dlo[v3] <= lo[v3]) and np.all(dhi[v3] >= hi[v3])
+    assert np.all(qlo[~v3] == 255) and np.all(qhi[~v3] == 0)
+    ref32 = f[:, 24:28].view(np.int32)
+    refq = q[:, 12:16].view(np.int32)
+    assert np.array_equal(refq[valid], ref32[valid])
+    assert np.all(refq[~valid] == np.iinfo(np.int32).min)
+    # the grid is fine where the boxes are: a valid child's quantized box is at most 2 grid steps wider per side
+    assert np.all((lo - dlo)[v3] <= 2 * np.broadcast_to(step[:, :, None], lo.shape)[v3])
