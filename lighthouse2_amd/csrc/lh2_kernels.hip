@@ -286,6 +286,7 @@ LH2_DEV bool mt_test( const float4 a, const float4 b, const float4 c, const TRay
 }
 
 #define LH2_POP INT_MIN   /* "pop the stack next" marker in cur (no valid node or leaf ref) */
+#define LH2_FIN (INT_MIN + 1)   /* the BVH4 loop: "this ray is done" (no leaf ref is this: it would start at triangle 2^27 - 1) */
 
 /* Ray-stream traversal with dynamic ray fetch (persistent waves, Aila & Laine 2009 "speculative
    fetch").  Each lane carries one ray's traversal state across loop iterations.  Every iteration
