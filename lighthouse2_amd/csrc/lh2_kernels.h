@@ -22,6 +22,8 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	   reset (initC non-null: what k_init_counters does), and the accumulator reset of a restart
 	   (clearAcc non-null: each pixel's first sample zeroes it; the memset of rendercore.cpp:465) */
 	Counters* initC; uint32_t* cursors; int cursorWords; uint32_t pathCount, segStride;
+	int keepCursor;   /* the camera fused into the primary packet launch: the first of the LH2_CURSOR_WORDS words the
+	                     launch itself uses, left alone by its reset (-1: reset every word) */
 	float4* clearAcc;
 	uint32_t* hvZero; uint32_t hvZeroWords;   /* heavy-first packets: the block this frame records into (TraceArgs::hvWrite) */
 };
@@ -93,6 +95,9 @@ struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path st
 	   on a path that cannot extend (ENOUGH_BOUNCES or the last vertex) adds and emits nothing, so
 	   k_shade<true> drops it after reading its hit and flags (misses still sample the sky) */
 	int terminal;
+	/* the camera fused into the primary packet launch (RenderCore::Render): the first shade launch zeroes the first
+	   hvZeroWords words of the heavy-packet block the frame read, the block the next frame records into */
+	uint32_t* hvZero; uint32_t hvZeroWords;
 };
 
 struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (any) out */
@@ -148,6 +153,9 @@ void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStri
 void lh2_launch_counters_next( Counters* c, const BounceAdvance* a, int pathLength, int resetShadow, LaunchEvents ev, hipStream_t st );
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st );
+/* the camera (k_camera's rays, path state and resets) fused into the primary packet launch: a->rayO / rayD and T4 / Q4
+   are written, a->segCounts must be null (the paths are dense: countFixed) */
+void lh2_launch_trace_primary( const SceneDev* s, const TraceArgs* a, const CameraParams* cp, float4* T4, float4* Q4, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st );
 int lh2_trace_blocks_per_cu( void );
 int lh2_packet_blocks_per_cu( void );
@@ -180,7 +188,8 @@ void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, co
 #define LH2_CURSOR_WORDS (2 * LH2_CHUNKS * LH2_CURSOR_STRIDE)
 #define LH2_HEAVY_CURSOR (LH2_CHUNKS * LH2_CURSOR_STRIDE)
 #define LH2_MAX_BOUNCES 64                                   /* RenderCore_PrimeRef MAXPATHLENGTH (core_settings.h:25) */
-#define LH2_CURSOR_SLOTS (2 * LH2_MAX_BOUNCES + 4)           /* launches per frame: [L] bounce L, [64 + L] shadow after bounce L, [130] shadow */
+#define LH2_CURSOR_SLOTS (2 * LH2_MAX_BOUNCES + 5)           /* launches per frame: [L] bounce L, [64 + L] shadow after bounce L, [130] shadow, [131] side shadow, [132] primary (odd fused frames) */
+#define LH2_PRIMARY_ALT_SLOT (2 * LH2_MAX_BOUNCES + 4)       /* the camera fused into the primary packet launch: its heads alternate between slot 1 and this one */
 #define LH2_SHADOW_SLOT (2 * LH2_MAX_BOUNCES + 2)
 /* traversal stacks: LH2_STACK_LDS entries per lane in LDS (16 x 256 x 4 B = 16 KiB per block), the rest in global memory */
 #ifndef LH2_STACK_LDS

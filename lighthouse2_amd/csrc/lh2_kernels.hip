@@ -139,9 +139,10 @@ LH2_DEV v3 RandomPointOnLens( const float r0, float r1, const v3 pos, const floa
 }
 
 /* InitCountersForExtend (.cuda.cu:64-74) plus the frame's work-queue heads; thread i of the launch */
-LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_t segStride, uint32_t* cursors, const int cursorWords, const int i )
+LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_t segStride, uint32_t* cursors, const int cursorWords, const int i,
+	const int keep = -1 )
 {
-	if (i < cursorWords) cursors[i] = 0;
+	if (i < cursorWords && (i < keep || i >= keep + LH2_CURSOR_WORDS)) cursors[i] = 0;
 	if (i < LH2_SEGS)
 	{
 		/* the camera writes the paths densely: segment i is [i * segStride, (i + 1) * segStride) */
@@ -157,14 +158,11 @@ LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_
 	c->reserved0 = 0, c->shadowOverflow = 0, c->shadeDone = 0;
 }
 
-__global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const uint8_t* __restrict__ bn, float4* __restrict__ rayO,
-	float4* __restrict__ rayD, float4* __restrict__ T4, float4* __restrict__ Q4, const int jobCount )
+/* the primary ray and path state of path slot `slot` (generateEyeRays, camera.h:39-111): rayO / rayD / T4 / Q4[slot]
+   written, the accumulator pixel of a restart's first sample zeroed; O, D: the ray */
+LH2_DEV void camera_path( const CameraParams& p, const uint8_t* __restrict__ bn, const uint32_t slot, float4* __restrict__ rayO,
+	float4* __restrict__ rayD, float4* __restrict__ T4, float4* __restrict__ Q4, float4& O, float4& D )
 {
-	const int local = threadIdx.x + blockIdx.x * blockDim.x;
-	if (p.initC) init_counters( p.initC, p.pathCount, p.segStride, p.cursors, p.cursorWords, local );
-	if (p.hvZero && (uint32_t)local < p.hvZeroWords) p.hvZero[local] = 0;
-	if (local >= jobCount) return;
-	const int slot = local;
 	/* slot -> (sample, tile row, x) -> global jobIndex = x + (y + s * h) * w, as camera.h:48-53 */
 	const uint32_t w = (uint32_t)p.w, h = (uint32_t)p.h;
 	const uint32_t tilePix = (uint32_t)p.tileRows * w;
@@ -220,12 +218,24 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 	}
 	const v3 posOnLens = RandomPointOnLens( r2, r3, mk3( p.pos.x, p.pos.y, p.pos.z ), p.aperture, right, up );
 	const v3 rayDir = normalize3( sub3( posOnPixel, posOnLens ) );
-	const uint32_t out = (uint32_t)local;
-	rayO[out] = make_float4( posOnLens.x, posOnLens.y, posOnLens.z, p.geometryEpsilon );
-	rayD[out] = make_float4( rayDir.x, rayDir.y, rayDir.z, 1e34f );
+	const uint32_t out = slot;
+	O = make_float4( posOnLens.x, posOnLens.y, posOnLens.z, p.geometryEpsilon );
+	D = make_float4( rayDir.x, rayDir.y, rayDir.z, 1e34f );
+	rayO[out] = O, rayD[out] = D;
 	T4[out] = make_float4( 1, 1, 1, bitsf( ((x + (y + (sampleIndex - (uint32_t)p.pass) * h) * w) << 8) + 1 /* S_SPECULAR */ ) );
 	Q4[out] = make_float4( 1, 0, 0, 0 );
 	if (p.clearAcc && sampleIndex == (uint32_t)p.pass) p.clearAcc[x + y * w] = make_float4( 0, 0, 0, 0 );
+}
+
+__global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const uint8_t* __restrict__ bn, float4* __restrict__ rayO,
+	float4* __restrict__ rayD, float4* __restrict__ T4, float4* __restrict__ Q4, const int jobCount )
+{
+	const int local = threadIdx.x + blockIdx.x * blockDim.x;
+	if (p.initC) init_counters( p.initC, p.pathCount, p.segStride, p.cursors, p.cursorWords, local );
+	if (p.hvZero && (uint32_t)local < p.hvZeroWords) p.hvZero[local] = 0;
+	if (local >= jobCount) return;
+	float4 O, D;
+	camera_path( p, bn, (uint32_t)local, rayO, rayD, T4, Q4, O, D );
 }
 
 /* =====================================================================================
@@ -549,7 +559,21 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 #ifndef LH2_PACKET_MINWAVES
 #define LH2_PACKET_MINWAVES 8
 #endif
-__global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet( s, a ); }
+__global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet<false>( s, a ); }
+#ifndef LH2_PRIMARY_MINWAVES
+#define LH2_PRIMARY_MINWAVES 7
+#endif
+/* the camera fused into the primary packet launch: each lane makes its path's primary ray (camera_path) and traces it,
+   and the launch does the camera launch's frame resets (counters; every work-queue head but its own, the heads of
+   the next frame's launch alternating between two slots); no camera launch, no ray round trip through HBM */
+__global__ __launch_bounds__( 256, LH2_PRIMARY_MINWAVES ) void k_trace_primary_packet( const CameraParams cp, const SceneDev s,
+	const TraceArgs a, float4* T4, float4* Q4 )
+{
+	/* cp first: trace_packet<true> reloads it from the start of the kernel arguments for each packet */
+	for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < (uint32_t)max( cp.cursorWords, LH2_SEGS ); i += gridDim.x * 256u)
+		init_counters( cp.initC, cp.pathCount, cp.segStride, cp.cursors, cp.cursorWords, (int)i, cp.keepCursor );
+	trace_packet<true>( s, a, T4, Q4 );
+}
 
 /* the reference BVH2 loop (traceVersion 1; the BVH4 is not built with setting "bvh4" 0) */
 template <bool PARK>
@@ -1501,6 +1525,8 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 	const uint32_t segBase = seg * p.segStride;
 	const uint32_t gstride = ((gridDim.x - seg + LH2_SEGS - 1) / LH2_SEGS) * 256u;
 	const int w = p.w, h = p.h;
+	if (p.hvZero)
+		for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < p.hvZeroWords; i += gridDim.x * 256u) p.hvZero[i] = 0;
 	for (uint32_t base = (blockIdx.x / LH2_SEGS) * 256u; base < count; base += gstride)
 	{
 		const uint32_t jobIndex = segBase + seg_pos( base + threadIdx.x, front, gap );
@@ -1915,6 +1941,10 @@ void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, 
 {
 	const int threads = std::max( std::max( jobCount, 1 ), p->initC ? std::max( p->cursorWords, LH2_SEGS ) : 0 );
 	LH2_LAUNCH( k_camera, (threads + 255) / 256, 256, st, ev, *p, bn, rayO, rayD, T4, Q4, jobCount );
+}
+void lh2_launch_trace_primary( const SceneDev* s, const TraceArgs* a, const CameraParams* cp, float4* T4, float4* Q4, int grid, LaunchEvents ev, hipStream_t st )
+{
+	LH2_LAUNCH( k_trace_primary_packet, grid, 256, st, ev, *cp, *s, *a, T4, Q4 );
 }
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st )
 {

@@ -117,6 +117,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	pathBlocksPerCU = std::max( 1, std::min( 8, lh2_path_blocks_per_cu() ) );
 	ps.counters.resize( 1 );
 	ps.cursors.resize( (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
+	CHK_HIP( hipMemsetAsync( ps.cursors.ptr, 0, sizeof( uint32_t ) * (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, stream ) );
 	ps.rayLog.resize( LH2_MAX_BOUNCES + 8 );
 	CHK_HIP( hipMemsetAsync( ps.rayLog.ptr, 0, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), stream ) );
 	/* indexed by pathLength; written by advance_bounce (system scope) */
@@ -241,6 +242,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "pathTail" )) pathTail = std::max( 0, (int)value );   /* bounces from this one in one trace-and-shade launch; 0: off */
 	else if (!strcmp( name, "pathTailBatch" )) pathTailBatch = std::min( 64, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "shadowOverlap" )) shadowOverlap = value != 0;
+	else if (!strcmp( name, "cameraFused" )) cameraFused = value != 0;
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
@@ -264,7 +266,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "pathTailBlocks", (float)pathTailBlocks },
+		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "pathTailBlocks", (float)pathTailBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -815,6 +817,19 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		cp.hvZero = ps.hv.ptr + (size_t)(1 - ps.hvParity) * ps.hvBlock, cp.hvZeroWords = LH2_HV_MASK + ps.hvMaskWords;
 	}
 	const int grid = TraceGrid();
+	/* the camera fused into the primary packet launch: this frame's heads are slot 1 or LH2_PRIMARY_ALT_SLOT; the
+	   heavy-packet block it records into must be zero (the previous fused frame's first shade launch zeroed it) */
+	const bool fusedCam = cameraFused && tiledRays && UsePackets() && !primeRef;
+	const uint32_t primSlot = fusedCam && ps.primParity ? LH2_PRIMARY_ALT_SLOT : 1u;
+	if (fusedCam)
+	{
+		cp.keepCursor = (int)(primSlot * LH2_CURSOR_WORDS);
+		if (ps.hvOn && !ps.hvNextZeroed) CHK_HIP( hipMemsetAsync( cp.hvZero, 0, sizeof( uint32_t ) * cp.hvZeroWords, stream ) );
+		cp.hvZero = nullptr, cp.hvZeroWords = 0;
+	}
+	else cp.keepCursor = -1;
+	ps.hvNextZeroed = false;
+	uint32_t* hvReadBlock = nullptr;
 	int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
 	/* no specular event and no alpha cut-out in any material: every path ends at its second vertex,
 	   so the bounce after it would be empty; not launching it saves three launches (~25 us) */
@@ -822,8 +837,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	/* the frame's start: a marker before the camera launch (~4 us of idle GPU), not the launch's own start
 	   event (hipExtLaunchKernelGGL start events cost ~8 us: tools/launch_gap.hip, profiles/r02q_launch_gap.txt) */
 	CHK_HIP( hipEventRecord( evFrame[0], stream ) );
-	lh2_launch_camera( &cp, dBlueNoise.ptr, ps.rayO[0].ptr, ps.rayD[0].ptr, ps.T4[0].ptr, ps.Q4[0].ptr, (int)pathCount, { nullptr, ps.evCamera }, stream );
-	ps.prevStop = ps.evCamera;
+	if (fusedCam) ps.prevStop = evFrame[0];
+	else
+	{
+		lh2_launch_camera( &cp, dBlueNoise.ptr, ps.rayO[0].ptr, ps.rayD[0].ptr, ps.T4[0].ptr, ps.Q4[0].ptr, (int)pathCount, { nullptr, ps.evCamera }, stream );
+		ps.prevStop = ps.evCamera;
+	}
 	if (restart) tileChanged = false;
 	/* without lights no path samples one (RandomPointOnLight: lightPdf 0), so there are no shadow
 	   rays and their launches are not queued */
@@ -848,7 +867,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		TraceArgs ta{};
 		ta.version = TraceVersion();
 		ta.rayO = ps.rayO[ps.in].ptr, ta.rayD = ps.rayD[ps.in].ptr, ta.segCounts = segIn, ta.segStride = ps.segStride, ta.segBack = segInBack;
-		ta.cursor = ps.cursors.ptr + (size_t)pathLength * LH2_CURSOR_WORDS;
+		ta.cursor = ps.cursors.ptr + (size_t)(pathLength == 1 ? primSlot : (uint32_t)pathLength) * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)(primary ? refillPrimary : refillOther);
 		ta.packet = primary && UsePackets() ? 1 : 0;
 		ta.leafBatch = (uint32_t)(primary ? leafBatchPrimary : leafBatch);
@@ -857,6 +876,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		{
 			ta.hvRead = ps.hv.ptr + (size_t)ps.hvParity * ps.hvBlock, ta.hvWrite = ps.hv.ptr + (size_t)(1 - ps.hvParity) * ps.hvBlock;
 			ta.hvCap = ps.hvCap, ta.hvMaskWords = ps.hvMaskWords, ta.hvFactor = packetHeavy;
+			hvReadBlock = (uint32_t*)ta.hvRead;
 			ta.hvTiles = 0;
 			for (int k = 0; k < LH2_SEGS; k++)
 			{
@@ -904,7 +924,14 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ps.tailL = pathLength;   /* no shade interval of its own (Synchronize) */
 			break;
 		}
-		lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : grid, { nullptr, ps.evTrace[pathLength] }, stream );
+		if (pathLength == 1 && fusedCam)
+		{
+			/* the paths are dense (camera order): fixed counts, no segment counters */
+			ta.segCounts = nullptr, ta.segBack = nullptr, ta.countFixed = pathCount;
+			lh2_launch_trace_primary( &sd, &ta, &cp, ps.T4[ps.in].ptr, ps.Q4[ps.in].ptr, PacketGrid(), { nullptr, ps.evTrace[pathLength] }, stream );
+			ps.primParity ^= 1;
+		}
+		else lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : grid, { nullptr, ps.evTrace[pathLength] }, stream );
 		ps.fromTrace[pathLength] = ps.prevStop, ps.prevStop = ps.evTrace[pathLength];
 		sp.segCounts = segIn, sp.segOut = segNext, sp.segStride = ps.segStride;
 		sp.segBack = segInBack, sp.segOutBack = segNextBack;
@@ -928,6 +955,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		sp.primeRef = primeRef;
 		sp.terminal = !primeRef && !shadows && !canEmit && pathLength > 1 && terminalShade;
 		sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
+		if (pathLength == 1 && fusedCam && hvReadBlock)
+		{
+			/* the block this frame's packets read is the one the next frame records into */
+			sp.hvZero = hvReadBlock, sp.hvZeroWords = LH2_HV_MASK + ps.hvMaskWords;
+			ps.hvNextZeroed = true;
+		}
 		lh2_launch_shade( &sd, &sp, grid, { nullptr, ps.evShade[pathLength] }, stream );
 		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];
 

@@ -91,6 +91,11 @@ struct PathStreams
 	int in = 0, pl = 0;
 	int tailL = 0;                       /* this frame's path-tail launch (pathLength), 0: none */
 	bool hvOn = false;                   /* this frame's primary packets run heavy-first (TraceArgs::hvRead) */
+	/* the camera fused into the primary packet launch (setting "cameraFused"): the launch's work-queue heads alternate
+	   between slot 1 and LH2_PRIMARY_ALT_SLOT (each launch zeroes the other), and the heavy-packet block the next frame
+	   records into is zeroed by the frame's first shade launch (hvNextZeroed: it was) */
+	int primParity = 0;
+	bool hvNextZeroed = false;
 	hipEvent_t prevStop = nullptr;
 };
 
@@ -233,6 +238,7 @@ private:
 	bool statsPending = false;
 	hipEvent_t evFrame[2] = {};
 	int tiledRays = 1;                   /* primary rays stored in 8x8 pixel blocks per wave (coherent packets) */
+	int cameraFused = 1;                 /* primary rays made by the packet launch itself (k_trace_primary_packet), no camera launch */
 	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle; BLAS leaves parked until this many
 	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,
 	   r02y_ab_v7.txt); leafBatch 8 with the quantized nodes (bounce 0.492 -> 0.488 ms, N = 8 share 1.35 -> 1.32 ms,
