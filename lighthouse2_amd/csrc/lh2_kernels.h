@@ -22,8 +22,6 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	   reset (initC non-null: what k_init_counters does), and the accumulator reset of a restart
 	   (clearAcc non-null: each pixel's first sample zeroes it; the memset of rendercore.cpp:465) */
 	Counters* initC; uint32_t* cursors; int cursorWords; uint32_t pathCount, segStride;
-	int keepCursor;   /* the camera fused into the primary packet launch: the first of the LH2_CURSOR_WORDS words the
-	                     launch itself uses, left alone by its reset (-1: reset every word) */
 	float4* clearAcc;
 	uint32_t* hvZero; uint32_t hvZeroWords;   /* heavy-first packets: the block this frame records into (TraceArgs::hvWrite) */
 };
@@ -149,12 +147,14 @@ struct FrameStatsDev
 };
 
 extern "C" {
-void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, LaunchEvents ev, hipStream_t st );
+void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, LaunchEvents ev, hipStream_t st,
+	int keepCursor = -1 );
 void lh2_launch_counters_next( Counters* c, const BounceAdvance* a, int pathLength, int resetShadow, LaunchEvents ev, hipStream_t st );
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st );
-/* the camera (k_camera's rays, path state and resets) fused into the primary packet launch: a->rayO / rayD and T4 / Q4
-   are written, a->segCounts must be null (the paths are dense: countFixed) */
+/* the camera (k_camera's rays and path state) fused into the primary packet launch: a->rayO / rayD and T4 / Q4 are
+   written, a->segCounts must be null (the paths are dense: countFixed); the frame's counters and work-queue heads are
+   reset by k_init_counters on the core stream (the launch itself may run beside the previous frame's tail) */
 void lh2_launch_trace_primary( const SceneDev* s, const TraceArgs* a, const CameraParams* cp, float4* T4, float4* Q4, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st );
 int lh2_trace_blocks_per_cu( void );

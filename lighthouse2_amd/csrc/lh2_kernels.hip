@@ -563,15 +563,13 @@ __global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_pa
 #ifndef LH2_PRIMARY_MINWAVES
 #define LH2_PRIMARY_MINWAVES 7
 #endif
-/* the camera fused into the primary packet launch: each lane makes its path's primary ray (camera_path) and traces it,
-   and the launch does the camera launch's frame resets (counters; every work-queue head but its own, the heads of
-   the next frame's launch alternating between two slots); no camera launch, no ray round trip through HBM */
+/* the camera fused into the primary packet launch: each lane makes its path's primary ray (camera_path) and traces it;
+   no camera launch, no ray round trip through HBM.  The frame's resets are k_init_counters' on the core stream (the
+   launch's own work-queue heads alternate between two slots, so it may run beside the previous frame's tail) */
 __global__ __launch_bounds__( 256, LH2_PRIMARY_MINWAVES ) void k_trace_primary_packet( const CameraParams cp, const SceneDev s,
 	const TraceArgs a, float4* T4, float4* Q4 )
 {
 	/* cp first: trace_packet<true> reloads it from the start of the kernel arguments for each packet */
-	for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < (uint32_t)max( cp.cursorWords, LH2_SEGS ); i += gridDim.x * 256u)
-		init_counters( cp.initC, cp.pathCount, cp.segStride, cp.cursors, cp.cursorWords, (int)i, cp.keepCursor );
 	trace_packet<true>( s, a, T4, Q4 );
 }
 
@@ -1803,9 +1801,9 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const 
 	}
 }
 
-__global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords )
+__global__ void k_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, int keep )
 {
-	init_counters( c, pathCount, segStride, cursors, cursorWords, blockIdx.x * blockDim.x + threadIdx.x );
+	init_counters( c, pathCount, segStride, cursors, cursorWords, blockIdx.x * blockDim.x + threadIdx.x, keep );
 }
 /* the hand-off from bounce L to bounce L + 1 (InitCountersSubsequent, .cuda.cu:76-84): the extension
    rays counted into segNext become the next bounce's paths (the counts ping-pong, Counters::segPath),
@@ -1929,9 +1927,10 @@ __global__ void k_spin( const unsigned long long ticks )
 	hipExtLaunchKernelGGL( kernel, dim3( grid ), dim3( block ), 0, st, (ev).start, (ev).stop, 0, __VA_ARGS__ )
 
 extern "C" {
-void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, LaunchEvents ev, hipStream_t st )
+void lh2_launch_init_counters( Counters* c, uint32_t pathCount, uint32_t segStride, uint32_t* cursors, int cursorWords, LaunchEvents ev, hipStream_t st,
+	int keepCursor )
 {
-	LH2_LAUNCH( k_init_counters, (cursorWords + 255) / 256 + 1, 256, st, ev, c, pathCount, segStride, cursors, cursorWords );
+	LH2_LAUNCH( k_init_counters, (cursorWords + 255) / 256 + 1, 256, st, ev, c, pathCount, segStride, cursors, cursorWords, keepCursor );
 }
 void lh2_launch_counters_next( Counters* c, const BounceAdvance* a, int pathLength, int resetShadow, LaunchEvents ev, hipStream_t st )
 {

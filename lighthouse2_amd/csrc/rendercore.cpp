@@ -101,6 +101,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 		CHK_HIP( hipDeviceGetStreamPriorityRange( &least, &greatest ) );
 		CHK_HIP( hipStreamCreateWithPriority( &sideStream, hipStreamNonBlocking, least ) );
 	}
+	CHK_HIP( hipStreamCreateWithFlags( &aheadStream, hipStreamNonBlocking ) );
 	/* blue noise sampler tables (rendercore.cpp:125-134), shipped as data/bluenoise.bin */
 	std::string path = getenv( "LH2_BLUENOISE" ) ? getenv( "LH2_BLUENOISE" ) : LibraryDir() + "/data/bluenoise.bin";
 	FILE* f = fopen( path.c_str(), "rb" );
@@ -129,6 +130,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipEventCreate( &ps.evCamera ) );
 	CHK_HIP( hipEventCreate( &ps.evShadow ) );
 	CHK_HIP( hipEventCreate( &ps.evSide ) );
+	CHK_HIP( hipEventCreateWithFlags( &ps.evMainTail, hipEventDisableTiming ) );
 	ps.shSnap.resize( LH2_SEGS * LH2_SEGCOUNT_STRIDE );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
@@ -148,6 +150,7 @@ void RenderCore::SetTarget( uint32_t w, uint32_t h, uint32_t spp )  /* rendercor
 	if (spp < 1) spp = 1;
 	if ((uint64_t)w * h * spp > (1u << 24)) FatalError( "path index exceeds 24 bits (camera.h:92): %ux%u x %u spp", w, h, spp );
 	scrwidth = (int)w, scrheight = (int)h, scrspp = (int)spp;
+	sceneVersion++;
 	EnsureBuffers();
 	CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)w * h, stream ) );
 	samplesTaken = 0;
@@ -197,6 +200,8 @@ void RenderCore::EnsurePaths( uint32_t paths )
 		ps.cap = (size_t)paths + (paths >> 4) + 64;
 		for (int i = 0; i < 2; i++) ps.rayO[i].resize( ps.cap ), ps.rayD[i].resize( ps.cap ), ps.T4[i].resize( ps.cap ), ps.Q4[i].resize( ps.cap );
 		ps.hits.resize( ps.cap );
+		ps.rayOP.resize( ps.cap ), ps.rayDP.resize( ps.cap ), ps.T4P.resize( ps.cap ), ps.Q4P.resize( ps.cap ), ps.hitsP.resize( ps.cap );
+		ps.relaid = true;
 		ps.shO.resize( 2 * ps.cap ), ps.shD.resize( 2 * ps.cap ), ps.shP.resize( 2 * ps.cap );
 		ps.shMask.resize( (2 * ps.cap + 63) / 32 + 2 );
 	}
@@ -243,6 +248,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "pathTailBatch" )) pathTailBatch = std::min( 64, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "shadowOverlap" )) shadowOverlap = value != 0;
 	else if (!strcmp( name, "cameraFused" )) cameraFused = value != 0;
+	else if (!strcmp( name, "frameOverlap" )) frameOverlap = value != 0;
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
@@ -266,7 +272,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "pathTailBlocks", (float)pathTailBlocks },
+		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "pathTailBlocks", (float)pathTailBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -277,6 +283,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 
 void RenderCore::SetTextures( const lh2_CoreTexDesc* tex, int textureCount )   /* rendercore.cpp:276-292 */
 {
+	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	texDescs.assign( tex, tex + std::max( 0, textureCount ) );
 	/* SyncStorageType (rendercore.cpp:299-336) for ARGB32, ARGB128 and NRM32: one continuous array per
 	   storage type, textures in descriptor order, at least 16 texels.  ARGB128 texels are copied whole
@@ -311,6 +318,7 @@ void RenderCore::SetTextures( const lh2_CoreTexDesc* tex, int textureCount )   /
 #define TOUINT4(a,b,c,d) (TOCHAR(a)+(TOCHAR(b)<<8)+(TOCHAR(c)<<16)+(TOCHAR(d)<<24))
 void RenderCore::SetMaterials( const lh2_CoreMaterial* mat, int n )   /* rendercore.cpp:353-399 */
 {
+	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	std::vector<uint4> recs( (size_t)std::max( n, 1 ) * 8 );
 	memset( recs.data(), 0, recs.size() * sizeof( uint4 ) );
 	diffuseOnly = true, canEmit = false;
@@ -360,6 +368,7 @@ void RenderCore::SetMaterials( const lh2_CoreMaterial* mat, int n )   /* renderc
 void RenderCore::SetLights( const lh2_CoreLightTri* a, int na, const lh2_CorePointLight* p, int np, const lh2_CoreSpotLight* s, int ns,
 	const lh2_CoreDirectionalLight* d, int nd )   /* rendercore.cpp:405-419 */
 {
+	sceneVersion++;
 	dArea.upload( a, na, stream ), dPoint.upload( p, np, stream ), dSpot.upload( s, ns, stream ), dDir.upload( d, nd, stream );
 	dArea.resize( 1 ), dPoint.resize( 1 ), dSpot.resize( 1 ), dDir.resize( 1 );
 	nArea = na, nPoint = np, nSpot = ns, nDir = nd;
@@ -368,6 +377,7 @@ void RenderCore::SetLights( const lh2_CoreLightTri* a, int na, const lh2_CorePoi
 
 void RenderCore::SetSkyData( const float* pixels, uint32_t width, uint32_t height )   /* rendercore.cpp:425-433 */
 {
+	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	dSky.upload( pixels, (size_t)width * height * 3, stream );
 	dSky.resize( 1 );
 	skyW = (int)width, skyH = (int)height;
@@ -376,6 +386,7 @@ void RenderCore::SetSkyData( const float* pixels, uint32_t width, uint32_t heigh
 
 void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount, const lh2_CoreTri* tris, const uint32_t* )
 {
+	sceneVersion++;
 	/* rendercore.cpp:215-223 + core_mesh.cpp:36-67: meshes arrive first-time in sequential order */
 	if (meshIdx < 0 || meshIdx > (int)meshes.size()) FatalError( "SetGeometry: mesh index %d out of sequence", meshIdx );
 	if (meshIdx == (int)meshes.size()) meshes.push_back( new CoreMeshHost() );
@@ -520,6 +531,7 @@ void RenderCore::BuildBlas4( CoreMeshHost& m, const float* nodes2 )
 
 void RenderCore::SetInstance( int instanceIdx, int meshIdx, const float* M )   /* rendercore.cpp:229-243 */
 {
+	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	if (meshIdx == -1) { if ((int)instances.size() > instanceIdx) instances.resize( instanceIdx ); instancesDirty = true; return; }
 	if (meshIdx < 0 || meshIdx >= (int)meshes.size()) FatalError( "SetInstance: unknown mesh %d", meshIdx );
 	if (instanceIdx >= (int)instances.size()) instances.resize( instanceIdx + 1 );
@@ -570,6 +582,7 @@ void RenderCore::ConcatenateBlas( int ni )
 
 void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 (instance descriptors) */
 {
+	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	const int ni = (int)instances.size();
 	if (geometryDirty || ni + 1 > tlasCapacity) ConcatenateBlas( ni );
 	tlasRoot = blasNodeCount;
@@ -813,6 +826,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ps.hvCap = cap, ps.hvMaskWords = maskWords, ps.hvBlock = LH2_HV_MASK + maskWords + LH2_SEGS * cap, ps.hvParity = 0;
 			ps.hv.resize( 2 * (size_t)ps.hvBlock );
 			CHK_HIP( hipMemsetAsync( ps.hv.ptr, 0, sizeof( uint32_t ) * 2 * ps.hvBlock, stream ) );
+			ps.relaid = true;
 		}
 		cp.hvZero = ps.hv.ptr + (size_t)(1 - ps.hvParity) * ps.hvBlock, cp.hvZeroWords = LH2_HV_MASK + ps.hvMaskWords;
 	}
@@ -823,11 +837,24 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const uint32_t primSlot = fusedCam && ps.primParity ? LH2_PRIMARY_ALT_SLOT : 1u;
 	if (fusedCam)
 	{
-		cp.keepCursor = (int)(primSlot * LH2_CURSOR_WORDS);
-		if (ps.hvOn && !ps.hvNextZeroed) CHK_HIP( hipMemsetAsync( cp.hvZero, 0, sizeof( uint32_t ) * cp.hvZeroWords, stream ) );
-		cp.hvZero = nullptr, cp.hvZeroWords = 0;
+		/* the frame's resets on the core stream (every work-queue head but the primary launch's own); the primary launch
+		   on the ahead stream, beside the previous frame's later bounces once that frame's first shade launch (the last
+		   reader of the primary buffers and of the heavy-packet block this frame records into) is done, or behind
+		   everything queued so far: on a restart (the launch zeroes accumulator pixels), after a change of scene data,
+		   buffers or tile, or when the previous frame had no fused primary launch */
+		lh2_launch_init_counters( c, pathCount, ps.segStride, ps.cursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, {}, stream,
+			(int)(primSlot * LH2_CURSOR_WORDS) );
+		const bool serialize = !frameOverlap || restart || !ps.lastFused || ps.relaid || tileChanged || sceneVersion != ps.lastSceneVersion;
+		if (serialize)
+		{
+			CHK_HIP( hipEventRecord( ps.evMainTail, stream ) );
+			CHK_HIP( hipStreamWaitEvent( aheadStream, ps.evMainTail, 0 ) );
+		}
+		else CHK_HIP( hipStreamWaitEvent( aheadStream, ps.evShade[1], 0 ) );
+		if (ps.hvOn && !ps.hvNextZeroed) CHK_HIP( hipMemsetAsync( cp.hvZero, 0, sizeof( uint32_t ) * cp.hvZeroWords, aheadStream ) );
+		cp.hvZero = nullptr, cp.hvZeroWords = 0, cp.initC = nullptr;
+		ps.relaid = false;
 	}
-	else cp.keepCursor = -1;
 	ps.hvNextZeroed = false;
 	uint32_t* hvReadBlock = nullptr;
 	int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
@@ -836,7 +863,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	if (!primeRef && diffuseOnly) maxPL = std::min( maxPL, 2 );
 	/* the frame's start: a marker before the camera launch (~4 us of idle GPU), not the launch's own start
 	   event (hipExtLaunchKernelGGL start events cost ~8 us: tools/launch_gap.hip, profiles/r02q_launch_gap.txt) */
-	CHK_HIP( hipEventRecord( evFrame[0], stream ) );
+	CHK_HIP( hipEventRecord( evFrame[0], fusedCam ? aheadStream : stream ) );
 	if (fusedCam) ps.prevStop = evFrame[0];
 	else
 	{
@@ -872,6 +899,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.packet = primary && UsePackets() ? 1 : 0;
 		ta.leafBatch = (uint32_t)(primary ? leafBatchPrimary : leafBatch);
 		ta.hits = ps.hits.ptr, ta.gstack = ps.gstack.ptr;
+		const bool fusedPrimary = pathLength == 1 && fusedCam;   /* the primary buffers (PathStreams::rayOP ..) */
+		if (fusedPrimary) ta.rayO = ps.rayOP.ptr, ta.rayD = ps.rayDP.ptr, ta.hits = ps.hitsP.ptr;
 		if (pathLength == 1 && ta.packet && ps.hvOn)
 		{
 			ta.hvRead = ps.hv.ptr + (size_t)ps.hvParity * ps.hvBlock, ta.hvWrite = ps.hv.ptr + (size_t)(1 - ps.hvParity) * ps.hvBlock;
@@ -924,11 +953,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ps.tailL = pathLength;   /* no shade interval of its own (Synchronize) */
 			break;
 		}
-		if (pathLength == 1 && fusedCam)
+		if (fusedPrimary)
 		{
-			/* the paths are dense (camera order): fixed counts, no segment counters */
+			/* the paths are dense (camera order): fixed counts, no segment counters; the core stream waits for it */
 			ta.segCounts = nullptr, ta.segBack = nullptr, ta.countFixed = pathCount;
-			lh2_launch_trace_primary( &sd, &ta, &cp, ps.T4[ps.in].ptr, ps.Q4[ps.in].ptr, PacketGrid(), { nullptr, ps.evTrace[pathLength] }, stream );
+			lh2_launch_trace_primary( &sd, &ta, &cp, ps.T4P.ptr, ps.Q4P.ptr, PacketGrid(), { nullptr, ps.evTrace[pathLength] }, aheadStream );
+			CHK_HIP( hipStreamWaitEvent( stream, ps.evTrace[pathLength], 0 ) );
 			ps.primParity ^= 1;
 		}
 		else lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : grid, { nullptr, ps.evTrace[pathLength] }, stream );
@@ -951,6 +981,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		sp.advance = pathLength < maxPL && !primeRef;
 		sp.adv = adv;
 		sp.rayO = ps.rayO[ps.in].ptr, sp.rayD = ps.rayD[ps.in].ptr, sp.T4 = ps.T4[ps.in].ptr, sp.Q4 = ps.Q4[ps.in].ptr, sp.hits = ps.hits.ptr;
+		if (fusedPrimary) sp.rayO = ps.rayOP.ptr, sp.rayD = ps.rayDP.ptr, sp.T4 = ps.T4P.ptr, sp.Q4 = ps.Q4P.ptr, sp.hits = ps.hitsP.ptr;
 		sp.rayOut = ps.rayO[1 - ps.in].ptr, sp.rayDOut = ps.rayD[1 - ps.in].ptr, sp.T4Out = ps.T4[1 - ps.in].ptr, sp.Q4Out = ps.Q4[1 - ps.in].ptr;
 		sp.primeRef = primeRef;
 		sp.terminal = !primeRef && !shadows && !canEmit && pathLength > 1 && terminalShade;
@@ -1028,6 +1059,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, stream ) );
 	}
 	hostStats->rayCount[0] = ps.count;
+	ps.lastFused = fusedCam, ps.lastSceneVersion = sceneVersion;
 	framePathLengths = ps.tailL ? maxPL : ps.pl;
 	framePrimeRef = primeRef;
 	statsPending = true;
@@ -1082,6 +1114,7 @@ static uint32_t QueuedShadowRays( const Counters& c )
 
 void RenderCore::Synchronize()
 {
+	CHK_HIP( hipStreamSynchronize( aheadStream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	if (!statsPending) return;
 	statsPending = false;
@@ -1372,6 +1405,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	hostStats = nullptr;
 	(void)hipStreamDestroy( stream );
 	if (sideStream) (void)hipStreamDestroy( sideStream ), sideStream = nullptr;
+	if (aheadStream) (void)hipStreamDestroy( aheadStream ), aheadStream = nullptr;
 	stream = nullptr;
 	initialized = false;
 }

@@ -67,6 +67,11 @@ struct PathStreams
 	size_t cap = 0;                      /* paths the buffers hold */
 	DevBuf<float4> rayO[2], rayD[2], T4[2], Q4[2];
 	DevBuf<uint4> hits;
+	/* the primary rays, path state and hits of a fused frame (k_trace_primary_packet writes them, its first shade
+	   launch reads them): apart from the bounce ping-pong, so the next frame's primary launch can run beside this
+	   frame's later bounces */
+	DevBuf<float4> rayOP, rayDP, T4P, Q4P;
+	DevBuf<uint4> hitsP;
 	DevBuf<float4> shO, shD, shP;
 	DevBuf<uint32_t> shMask;
 	DevBuf<int> gstack;
@@ -96,6 +101,11 @@ struct PathStreams
 	   records into is zeroed by the frame's first shade launch (hvNextZeroed: it was) */
 	int primParity = 0;
 	bool hvNextZeroed = false;
+	/* frame overlap (setting "frameOverlap"): the primary launch of a fused frame runs on the ahead stream after the
+	   previous frame's first shade launch, unless something since then needs it to wait for the whole previous frame */
+	bool lastFused = false, relaid = true;
+	uint64_t lastSceneVersion = 0;
+	hipEvent_t evMainTail = nullptr;
 	hipEvent_t prevStop = nullptr;
 };
 
@@ -162,6 +172,7 @@ public:
 	lh2_CoreStats coreStats{};
 	hipStream_t stream = nullptr;
 	hipStream_t sideStream = nullptr;    /* shadowOverlap: lowest priority */
+	hipStream_t aheadStream = nullptr;   /* frameOverlap: the fused primary launch */
 
 private:
 	void EnsureBuffers();
@@ -239,6 +250,8 @@ private:
 	hipEvent_t evFrame[2] = {};
 	int tiledRays = 1;                   /* primary rays stored in 8x8 pixel blocks per wave (coherent packets) */
 	int cameraFused = 1;                 /* primary rays made by the packet launch itself (k_trace_primary_packet), no camera launch */
+	int frameOverlap = 1;                /* a fused frame's primary launch beside the previous frame's tail (aheadStream) */
+	uint64_t sceneVersion = 0;           /* incremented by every change of device-resident scene data or buffers */
 	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle; BLAS leaves parked until this many
 	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,
 	   r02y_ab_v7.txt); leafBatch 8 with the quantized nodes (bounce 0.492 -> 0.488 ms, N = 8 share 1.35 -> 1.32 ms,

@@ -1,10 +1,15 @@
-"""GPU parity of the camera fused into the primary packet launch (setting cameraFused, k_trace_primary_packet):
-the packet launch makes each path's primary ray itself (camera.h:39-111, the code of k_camera) and does the
-camera launch's frame resets, its work-queue heads alternating between two slots from frame to frame, and the
-heavy-packet block the next frame records into zeroed by the first shade launch.  Against the CPU oracle
-(pathtracer.h:54-245 after generateEyeRays): identical per-bounce ray counts every frame, accumulator rel-L2
-<= 1e-4, and the same frames with the camera launch (cameraFused 0) to float summation order; a restart in
-the middle of the sequence exercises the accumulator reset of each pixel's first sample."""
+"""GPU parity of the camera fused into the primary packet launch (setting cameraFused, k_trace_primary_packet) and
+of the frame overlap (setting frameOverlap).  The packet launch makes each path's primary ray itself (camera.h:39-111,
+the code of k_camera) into primary buffers of its own, and runs on the core's ahead stream: beside the previous
+frame's later bounces once that frame's first shade launch is done, or behind the whole previous frame after a
+restart or a scene change.  Its work-queue heads alternate between two slots from frame to frame; the frame's resets
+are a k_init_counters launch on the core stream; the heavy-packet block the next frame records into is zeroed by the
+first shade launch.
+
+Against the CPU oracle (pathtracer.h:54-245 after generateEyeRays): identical per-bounce ray counts every frame,
+accumulator rel-L2 <= 1e-4; and frames queued back to back (no host synchronisation between them, so the primary
+launches overlap the previous frames' tails) equal, to float summation order, the same frames without the overlap
+and without the fusion.  Restarts in the sequence exercise the accumulator reset of each pixel's first sample."""
 import numpy as np
 import pytest
 
@@ -20,19 +25,32 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-# restart, converge, converge, restart, converge, converge: both head slots, each twice, and two restarts
-SEQUENCE = (1, 0, 0, 1, 0, 0)
+# restart, converge x2, restart, converge x3: both head slots, each several times, and two restarts
+SEQUENCE = (1, 0, 0, 1, 0, 0, 0)
 
 
-@pytest.mark.parametrize("kind", ["room", "config2"])
+def _scene(kind, w, h):
+    if kind == "room":
+        return scene.room_scene(40000, w, h), 4
+    if kind == "instanced":
+        sc = scene.instanced_scene(meshes=4, tris_per_mesh=4000, width=w, height=h, grid=2, spacing=10.0)
+        sc.sky = scene.gradient_sky(64, 32)
+        return sc, 3
+    return scene.config2_scene(n=20000, width=w, height=h), 2
+
+
+def _animate(sc, tgt, f):
+    scene.animate_instances(sc, f)
+    for k, (mesh, T) in enumerate(sc.instances):
+        tgt.set_instance(k, mesh, T)
+    tgt.update_toplevel()
+
+
+@pytest.mark.parametrize("kind", ["room", "config2", "instanced"])
 def test_camera_fused_frames(fresh_core, kind):
     w, h = 128, 72
-    if kind == "room":
-        sc = scene.room_scene(40000, w, h)
-        depth = 4
-    else:
-        sc = scene.config2_scene(n=20000, width=w, height=h)
-        depth = 2
+    sc, depth = _scene(kind, w, h)
+    anim = kind == "instanced"            # instances move every frame: each primary launch waits for the update
     sc.load_into(fresh_core)
     fresh_core.set_target(w, h, 1)
     o = Oracle()
@@ -40,17 +58,27 @@ def test_camera_fused_frames(fresh_core, kind):
     o.set_target(w, h, 1)
     for tgt in (fresh_core, o):
         tgt.setting("maxPathLength", depth)
-    assert fresh_core.get_setting("cameraFused") == 1
+    assert fresh_core.get_setting("cameraFused") == 1 and fresh_core.get_setting("frameOverlap") == 1
+    # per-frame ray counts against the oracle (synchronised after every frame)
+    for f, conv in enumerate(SEQUENCE):
+        if anim:
+            _animate(sc, fresh_core, f), _animate(sc, o, f)
+        sc.render_frame(fresh_core, converge=conv)
+        sc.render_frame(o, converge=conv)
+        assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (f, fresh_core.ray_counts()[:6], o.ray_counts()[:6])
+    ref = o.accumulator()
     res = {}
-    for fused in (1, 0):
+    for fused, overlap in ((1, 1), (1, 0), (0, 0)):
         fresh_core.setting("cameraFused", fused)
-        for f, conv in enumerate(SEQUENCE):
+        fresh_core.setting("frameOverlap", overlap)
+        for f, conv in enumerate(SEQUENCE):   # queued back to back: no synchronisation between frames
+            if anim:
+                _animate(sc, fresh_core, f)
             sc.render_frame(fresh_core, converge=conv)
-            if fused:
-                sc.render_frame(o, converge=conv)
-                assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (f, fresh_core.ray_counts()[:6], o.ray_counts()[:6])
-        res[fused] = fresh_core.accumulator()
-    assert rel_l2(res[1][..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
-    assert rel_l2(res[1][..., :3], res[0][..., :3]) <= 1e-6
-    # the primary hit distances (the accumulator's w: first-vertex distance sum) are order-free sums of identical values
-    assert np.array_equal(res[1][..., 3], res[0][..., 3])
+        res[(fused, overlap)] = fresh_core.accumulator()
+    a = res[(1, 1)]
+    assert rel_l2(a[..., :3], ref[..., :3]) <= REL_L2_TOL
+    for k in ((1, 0), (0, 0)):
+        assert rel_l2(a[..., :3], res[k][..., :3]) <= 1e-6, k
+        # the first-vertex distances (w): one addition per pixel per frame, in frame order: bit-identical
+        assert np.array_equal(a[..., 3], res[k][..., 3]), k
