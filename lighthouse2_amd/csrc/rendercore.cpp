@@ -100,8 +100,10 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 		int least = 0, greatest = 0;
 		CHK_HIP( hipDeviceGetStreamPriorityRange( &least, &greatest ) );
 		CHK_HIP( hipStreamCreateWithPriority( &sideStream, hipStreamNonBlocking, least ) );
+		/* frameOverlap: the next frame's primary launch yields to the current frame's launches (lowest priority): config 3
+		   1.98 -> 1.96 ms, config-4 N = 8 share 1.19 -> 1.17 ms (profiles/r03m_ab_overlap_policy.txt) */
+		CHK_HIP( hipStreamCreateWithPriority( &aheadStream, hipStreamNonBlocking, least ) );
 	}
-	CHK_HIP( hipStreamCreateWithFlags( &aheadStream, hipStreamNonBlocking ) );
 	/* blue noise sampler tables (rendercore.cpp:125-134), shipped as data/bluenoise.bin */
 	std::string path = getenv( "LH2_BLUENOISE" ) ? getenv( "LH2_BLUENOISE" ) : LibraryDir() + "/data/bluenoise.bin";
 	FILE* f = fopen( path.c_str(), "rb" );
@@ -248,7 +250,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "pathTailBatch" )) pathTailBatch = std::min( 64, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "shadowOverlap" )) shadowOverlap = value != 0;
 	else if (!strcmp( name, "cameraFused" )) cameraFused = value != 0;
-	else if (!strcmp( name, "frameOverlap" )) frameOverlap = value != 0;
+	else if (!strcmp( name, "frameOverlap" )) frameOverlap = (int)value;
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
@@ -850,7 +852,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			CHK_HIP( hipEventRecord( ps.evMainTail, stream ) );
 			CHK_HIP( hipStreamWaitEvent( aheadStream, ps.evMainTail, 0 ) );
 		}
-		else CHK_HIP( hipStreamWaitEvent( aheadStream, ps.evShade[1], 0 ) );
+		else CHK_HIP( hipStreamWaitEvent( aheadStream, ps.overlapEv, 0 ) );
 		if (ps.hvOn && !ps.hvNextZeroed) CHK_HIP( hipMemsetAsync( cp.hvZero, 0, sizeof( uint32_t ) * cp.hvZeroWords, aheadStream ) );
 		cp.hvZero = nullptr, cp.hvZeroWords = 0, cp.initC = nullptr;
 		ps.relaid = false;
@@ -994,6 +996,9 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		}
 		lh2_launch_shade( &sd, &sp, grid, { nullptr, ps.evShade[pathLength] }, stream );
 		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];
+		/* the next frame's primary launch starts after this frame's first shade launch (the last reader of the primary
+		   buffers), or (frameOverlap 1) after the shade launch before the path tail: beside the latency-bound tail */
+		if (pathLength == 1 || (frameOverlap == 1 && tailL && pathLength == tailL - 1)) ps.overlapEv = ps.evShade[pathLength];
 
 		if (pathLength == maxPL) break;
 		if (primeRef && shadows)

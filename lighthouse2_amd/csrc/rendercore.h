@@ -106,6 +106,7 @@ struct PathStreams
 	bool lastFused = false, relaid = true;
 	uint64_t lastSceneVersion = 0;
 	hipEvent_t evMainTail = nullptr;
+	hipEvent_t overlapEv = nullptr;      /* the last frame's shade launch the next primary launch waits for (not owned) */
 	hipEvent_t prevStop = nullptr;
 };
 
@@ -250,7 +251,9 @@ private:
 	hipEvent_t evFrame[2] = {};
 	int tiledRays = 1;                   /* primary rays stored in 8x8 pixel blocks per wave (coherent packets) */
 	int cameraFused = 1;                 /* primary rays made by the packet launch itself (k_trace_primary_packet), no camera launch */
-	int frameOverlap = 1;                /* a fused frame's primary launch beside the previous frame's tail (aheadStream) */
+	/* a fused frame's primary launch beside the previous frame's later bounces (aheadStream): 1, after its shade launch
+	   before the path tail (its first without one); 2, after its first shade launch; 0: off */
+	int frameOverlap = 1;
 	uint64_t sceneVersion = 0;           /* incremented by every change of device-resident scene data or buffers */
 	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle; BLAS leaves parked until this many
 	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,
