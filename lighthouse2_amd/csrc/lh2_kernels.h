@@ -22,6 +22,8 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	   reset (initC non-null: what k_init_counters does), and the accumulator reset of a restart
 	   (clearAcc non-null: each pixel's first sample zeroes it; the memset of rendercore.cpp:465) */
 	Counters* initC; uint32_t* cursors; int cursorWords; uint32_t pathCount, segStride;
+	int keepCursor;   /* the fused primary launch (initC non-null): the first of the LH2_CURSOR_WORDS words it uses itself,
+	                     left alone by its reset */
 	float4* clearAcc;
 	uint32_t* hvZero; uint32_t hvZeroWords;   /* heavy-first packets: the block this frame records into (TraceArgs::hvWrite) */
 };

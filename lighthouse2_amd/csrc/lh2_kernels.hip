@@ -569,6 +569,11 @@ __global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_pa
 __global__ __launch_bounds__( 256, LH2_PRIMARY_MINWAVES ) void k_trace_primary_packet( const CameraParams cp, const SceneDev s,
 	const TraceArgs a, float4* T4, float4* Q4 )
 {
+	/* behind the previous frame (on the core stream, RenderCore::Render): the frame's resets, the camera launch's (every
+	   work-queue head but the launch's own); beside it: k_init_counters on the core stream, initC null */
+	if (cp.initC)
+		for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < (uint32_t)max( cp.cursorWords, LH2_SEGS ); i += gridDim.x * 256u)
+			init_counters( cp.initC, cp.pathCount, cp.segStride, cp.cursors, cp.cursorWords, (int)i, cp.keepCursor );
 	/* cp first: trace_packet<true> reloads it from the start of the kernel arguments for each packet */
 	trace_packet<true>( s, a, T4, Q4 );
 }

@@ -132,7 +132,6 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipEventCreate( &ps.evCamera ) );
 	CHK_HIP( hipEventCreate( &ps.evShadow ) );
 	CHK_HIP( hipEventCreate( &ps.evSide ) );
-	CHK_HIP( hipEventCreateWithFlags( &ps.evMainTail, hipEventDisableTiming ) );
 	ps.shSnap.resize( LH2_SEGS * LH2_SEGCOUNT_STRIDE );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
@@ -836,25 +835,30 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	/* the camera fused into the primary packet launch: this frame's heads are slot 1 or LH2_PRIMARY_ALT_SLOT; the
 	   heavy-packet block it records into must be zero (the previous fused frame's first shade launch zeroed it) */
 	const bool fusedCam = cameraFused && tiledRays && UsePackets() && !primeRef;
+	/* the fused primary launch beside the previous frame (frame overlap), or behind it on the core stream: on a restart
+	   (the launch zeroes accumulator pixels), after a change of scene data, buffers or tile, or when the previous frame
+	   had no fused primary launch */
+	const bool serialize = !frameOverlap || restart || !ps.lastFused || ps.relaid || tileChanged || sceneVersion != ps.lastSceneVersion;
+	hipStream_t primStream = stream;
 	const uint32_t primSlot = fusedCam && ps.primParity ? LH2_PRIMARY_ALT_SLOT : 1u;
 	if (fusedCam)
 	{
-		/* the frame's resets on the core stream (every work-queue head but the primary launch's own); the primary launch
-		   on the ahead stream, beside the previous frame's later bounces once that frame's first shade launch (the last
-		   reader of the primary buffers and of the heavy-packet block this frame records into) is done, or behind
-		   everything queued so far: on a restart (the launch zeroes accumulator pixels), after a change of scene data,
-		   buffers or tile, or when the previous frame had no fused primary launch */
-		lh2_launch_init_counters( c, pathCount, ps.segStride, ps.cursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, {}, stream,
-			(int)(primSlot * LH2_CURSOR_WORDS) );
-		const bool serialize = !frameOverlap || restart || !ps.lastFused || ps.relaid || tileChanged || sceneVersion != ps.lastSceneVersion;
-		if (serialize)
+		/* beside the previous frame (on the ahead stream, after the previous frame's shade launch before its path tail, or
+		   its first without one: the last reader of the primary buffers and of the heavy-packet block this frame records
+		   into), the frame's resets are a k_init_counters launch on the core stream (behind the previous frame); behind
+		   it, on the core stream, the primary launch does them itself.  Its own work-queue heads are left alone: they
+		   alternate between two slots, and the resets zero the other */
+		primStream = serialize ? stream : aheadStream;
+		cp.keepCursor = (int)(primSlot * LH2_CURSOR_WORDS);
+		if (serialize) cp.initC = c;
+		else
 		{
-			CHK_HIP( hipEventRecord( ps.evMainTail, stream ) );
-			CHK_HIP( hipStreamWaitEvent( aheadStream, ps.evMainTail, 0 ) );
+			lh2_launch_init_counters( c, pathCount, ps.segStride, ps.cursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, {}, stream, cp.keepCursor );
+			CHK_HIP( hipStreamWaitEvent( aheadStream, ps.overlapEv, 0 ) );
+			cp.initC = nullptr;
 		}
-		else CHK_HIP( hipStreamWaitEvent( aheadStream, ps.overlapEv, 0 ) );
-		if (ps.hvOn && !ps.hvNextZeroed) CHK_HIP( hipMemsetAsync( cp.hvZero, 0, sizeof( uint32_t ) * cp.hvZeroWords, aheadStream ) );
-		cp.hvZero = nullptr, cp.hvZeroWords = 0, cp.initC = nullptr;
+		if (ps.hvOn && !ps.hvNextZeroed) CHK_HIP( hipMemsetAsync( cp.hvZero, 0, sizeof( uint32_t ) * cp.hvZeroWords, primStream ) );
+		cp.hvZero = nullptr, cp.hvZeroWords = 0;
 		ps.relaid = false;
 	}
 	ps.hvNextZeroed = false;
@@ -865,7 +869,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	if (!primeRef && diffuseOnly) maxPL = std::min( maxPL, 2 );
 	/* the frame's start: a marker before the camera launch (~4 us of idle GPU), not the launch's own start
 	   event (hipExtLaunchKernelGGL start events cost ~8 us: tools/launch_gap.hip, profiles/r02q_launch_gap.txt) */
-	CHK_HIP( hipEventRecord( evFrame[0], fusedCam ? aheadStream : stream ) );
+	CHK_HIP( hipEventRecord( evFrame[0], fusedCam ? primStream : stream ) );
 	if (fusedCam) ps.prevStop = evFrame[0];
 	else
 	{
@@ -959,8 +963,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		{
 			/* the paths are dense (camera order): fixed counts, no segment counters; the core stream waits for it */
 			ta.segCounts = nullptr, ta.segBack = nullptr, ta.countFixed = pathCount;
-			lh2_launch_trace_primary( &sd, &ta, &cp, ps.T4P.ptr, ps.Q4P.ptr, PacketGrid(), { nullptr, ps.evTrace[pathLength] }, aheadStream );
-			CHK_HIP( hipStreamWaitEvent( stream, ps.evTrace[pathLength], 0 ) );
+			lh2_launch_trace_primary( &sd, &ta, &cp, ps.T4P.ptr, ps.Q4P.ptr, PacketGrid(), { nullptr, ps.evTrace[pathLength] }, primStream );
+			if (primStream != stream) CHK_HIP( hipStreamWaitEvent( stream, ps.evTrace[pathLength], 0 ) );
 			ps.primParity ^= 1;
 		}
 		else lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : grid, { nullptr, ps.evTrace[pathLength] }, stream );

@@ -105,7 +105,6 @@ struct PathStreams
 	   previous frame's first shade launch, unless something since then needs it to wait for the whole previous frame */
 	bool lastFused = false, relaid = true;
 	uint64_t lastSceneVersion = 0;
-	hipEvent_t evMainTail = nullptr;
 	hipEvent_t overlapEv = nullptr;      /* the last frame's shade launch the next primary launch waits for (not owned) */
 	hipEvent_t prevStop = nullptr;
 };

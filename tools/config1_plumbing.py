@@ -73,11 +73,14 @@ def soft_rasterizer(sc: scene.Scene, width: int, height: int, seconds: float) ->
             "covered_pixel_share": round(float((px != 0).mean()), 4)}
 
 
-def mi355x_core(sc: scene.Scene, width: int, height: int, frames: int) -> dict:
+def mi355x_core(sc: scene.Scene, width: int, height: int, frames: int, settings=()) -> dict:
     import torch  # noqa: F401  (one HIP runtime in the process)
     from lighthouse2_amd.core import RenderCore
     t0 = time.perf_counter()
     core = RenderCore(device=0)
+    for kv in settings:
+        k, v = kv.split("=")
+        core.setting(k, float(v))
     sc.load_into(core)
     core.set_target(width, height, 1)
     setup = time.perf_counter() - t0
@@ -106,13 +109,14 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--frames", type=int, default=50)
     ap.add_argument("--no-gpu", action="store_true")
+    ap.add_argument("--setting", action="append", default=[], help="name=value core setting")
     args = ap.parse_args()
     sc = scene.tinyapp_scene(args.width, args.height)
     out = {"config": "config1", "workload": f"tinyapp default scene, {sc.tri_count} tris (pica glTF 76,274 in 170 "
            f"instances + legocar.obj 10,992 at scale 10 + 2-tri light quad; untextured), {args.width}x{args.height}",
            "soft_rasterizer_reference": soft_rasterizer(sc, args.width, args.height, args.cpu_seconds)}
     if not args.no_gpu:
-        out["mi355x_core"] = mi355x_core(sc, args.width, args.height, args.frames)
+        out["mi355x_core"] = mi355x_core(sc, args.width, args.height, args.frames, args.setting)
     print(json.dumps(out), flush=True)
 
 
