@@ -26,6 +26,11 @@ struct CameraParams   /* camera.h:39-43 arguments (pos, right, up, p1, aperture,
 	                     left alone by its reset */
 	float4* clearAcc;
 	uint32_t* hvZero; uint32_t hvZeroWords;   /* heavy-first packets: the block this frame records into (TraceArgs::hvWrite) */
+	/* set by the launchers (lh2_camera_derive), not by callers: right / w and up / h (IEEE division on the host: the
+	   device's correctly rounded quotients), and division by the invariant divisors tileRows x w, w and band as
+	   multiply-high + shifts (lh2_udiv) */
+	lh2_float3 rightW, upH;
+	uint32_t divTile[3], divW[3], divBand[3];
 };
 
 struct SceneDev       /* everything the traversal and shading kernels read, by value (kernarg) */

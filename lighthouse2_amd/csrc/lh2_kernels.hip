@@ -158,6 +158,14 @@ LH2_DEV void init_counters( Counters* c, const uint32_t pathCount, const uint32_
 	c->reserved0 = 0, c->shadowOverflow = 0, c->shadeDone = 0;
 }
 
+/* n / d for a divisor fixed for the launch (Granlund & Montgomery 1994, the round-up multiplier with the add step):
+   exact for every 32-bit n.  dv = { m, a, s } from lh2_div_magic; d == 1 is m = 0, a = 0, s = 0 */
+LH2_DEV uint32_t lh2_udiv( const uint32_t n, const uint32_t dv[3] )
+{
+	const uint32_t t = __umulhi( n, dv[0] );
+	return (t + ((n - t) >> dv[1])) >> dv[2];
+}
+
 /* the primary ray and path state of path slot `slot` (generateEyeRays, camera.h:39-111): rayO / rayD / T4 / Q4[slot]
    written, the accumulator pixel of a restart's first sample zeroed; O, D: the ray */
 LH2_DEV void camera_path( const CameraParams& p, const uint8_t* __restrict__ bn, const uint32_t slot, float4* __restrict__ rayO,
@@ -166,31 +174,32 @@ LH2_DEV void camera_path( const CameraParams& p, const uint8_t* __restrict__ bn,
 	/* slot -> (sample, tile row, x) -> global jobIndex = x + (y + s * h) * w, as camera.h:48-53 */
 	const uint32_t w = (uint32_t)p.w, h = (uint32_t)p.h;
 	const uint32_t tilePix = (uint32_t)p.tileRows * w;
-	const uint32_t s = (uint32_t)slot / tilePix, r = (uint32_t)slot % tilePix;
-	uint32_t lr = r / w, x = r % w;
+	const uint32_t s = lh2_udiv( slot, p.divTile ), r = slot - s * tilePix;
+	uint32_t lr = lh2_udiv( r, p.divW ), x = r - lr * w;
 	if (p.tiled && (w & 7u) == 0)
 	{
 		/* storage order only: each wave (64 slots) holds an 8x8 pixel block, so a wave's rays are
 		   coherent; the path index (and therefore every random number) is unchanged */
-		const uint32_t rb = r / (8u * w);
+		const uint32_t rb = lr >> 3;   /* r / (8 w) */
 		if (rb < (uint32_t)p.tileRows / 8u)
 		{
 			const uint32_t q = r - rb * 8u * w, k = q & 63u;
 			x = (q >> 6) * 8u + (k & 7u), lr = rb * 8u + (k >> 3);
 		}
 	}
-	const uint32_t gy = (uint32_t)p.y0 + (lr / (uint32_t)p.band) * (uint32_t)p.bandStride + lr % (uint32_t)p.band;
+	const uint32_t lb = lh2_udiv( lr, p.divBand );
+	const uint32_t gy = (uint32_t)p.y0 + lb * (uint32_t)p.bandStride + (lr - lb * (uint32_t)p.band);
 	const uint32_t jobIndex = x + (gy + s * h) * w;
-	uint32_t y = jobIndex / w;
-	const uint32_t sampleIndex = (uint32_t)p.pass + y / h;
-	y %= h;
+	/* jobIndex / w = gy + s h (x < w), so the sample is s + gy / h and the row gy % h (gy < h but for odd tilings) */
+	uint32_t y = gy, sampleIndex = (uint32_t)p.pass + s;
+	if (gy >= h) sampleIndex += gy / h, y = gy % h;
 	float r0, r1, r2, r3;
 	if (sampleIndex < 256 && !p.primeRef)
 	{
-		r0 = blueNoiseSampler( bn, x, y, sampleIndex, 0 );
-		r1 = blueNoiseSampler( bn, x, y, sampleIndex, 1 );
-		r2 = blueNoiseSampler( bn, x, y, sampleIndex, 2 );
-		r3 = blueNoiseSampler( bn, x, y, sampleIndex, 3 );
+		/* dimensions 0..3: blueNoiseSampler's values, the four ranking and scrambling bytes in one dword each */
+		float bnv[4];
+		blueNoiseFinish4( bn, blueNoiseFetch4( bn, (int)x, (int)y, (int)sampleIndex, 0 ), bnv );
+		r0 = bnv[0], r1 = bnv[1], r2 = bnv[2], r3 = bnv[3];
 	}
 	else
 	{
@@ -199,10 +208,11 @@ LH2_DEV void camera_path( const CameraParams& p, const uint8_t* __restrict__ bn,
 		r2 = RandomFloat( seed ), r3 = RandomFloat( seed );
 	}
 	const v3 p1 = mk3( p.p1.x, p.p1.y, p.p1.z ), right = mk3( p.right.x, p.right.y, p.right.z ), up = mk3( p.up.x, p.up.y, p.up.z );
+	const v3 rightW = mk3( p.rightW.x, p.rightW.y, p.rightW.z ), upH = mk3( p.upH.x, p.upH.y, p.upH.z );   /* divs( right, w ), divs( up, h ) */
 	v3 posOnPixel;
 	if (p.distortion == 0 || p.primeRef)
 	{
-		posOnPixel = add3( add3( p1, smul( (float)x + r0, divs( right, (float)w ) ) ), smul( (float)y + r1, divs( up, (float)h ) ) );
+		posOnPixel = add3( add3( p1, smul( (float)x + r0, rightW ) ), smul( (float)y + r1, upH ) );
 	}
 	else
 	{
@@ -214,7 +224,7 @@ LH2_DEV void camera_path( const CameraParams& p, const uint8_t* __restrict__ bn,
 		lh2_sincosf( theta, &st, &ct );
 		const float bx = (st * rq + 0.5f) * (float)w;
 		const float by = (ct * rq + 0.5f) * (float)h;
-		posOnPixel = add3( add3( p1, smul( bx + r0, divs( right, (float)w ) ) ), smul( by + r1, divs( up, (float)h ) ) );
+		posOnPixel = add3( add3( p1, smul( bx + r0, rightW ) ), smul( by + r1, upH ) );
 	}
 	const v3 posOnLens = RandomPointOnLens( r2, r3, mk3( p.pos.x, p.pos.y, p.pos.z ), p.aperture, right, up );
 	const v3 rayDir = normalize3( sub3( posOnPixel, posOnLens ) );
@@ -1941,14 +1951,35 @@ void lh2_launch_counters_next( Counters* c, const BounceAdvance* a, int pathLeng
 {
 	LH2_LAUNCH( k_counters_next, 1, 64, st, ev, c, *a, pathLength, resetShadow );
 }
+/* lh2_udiv's { m, a, s } for divisor d >= 1: m = floor( 2^32 (2^l - d) / d ) + 1 with l = ceil( log2 d ), a = 1, s = l - 1 */
+static void lh2_div_magic( const uint32_t d, uint32_t dv[3] )
+{
+	if (d <= 1) { dv[0] = 0, dv[1] = 0, dv[2] = 0; return; }
+	const uint32_t l = 32u - (uint32_t)__builtin_clz( d - 1u );
+	dv[0] = (uint32_t)((((uint64_t)1 << l) - d) * ((uint64_t)1 << 32) / d + 1u), dv[1] = 1, dv[2] = l - 1u;
+}
+/* the launch-invariant quantities camera_path reads (CameraParams, last fields) */
+static CameraParams lh2_camera_derive( const CameraParams& in )
+{
+	CameraParams c = in;
+	const float fw = (float)c.w, fh = (float)c.h;
+	c.rightW = { c.right.x / fw, c.right.y / fw, c.right.z / fw };
+	c.upH = { c.up.x / fh, c.up.y / fh, c.up.z / fh };
+	lh2_div_magic( (uint32_t)c.tileRows * (uint32_t)c.w, c.divTile );
+	lh2_div_magic( (uint32_t)c.w, c.divW );
+	lh2_div_magic( (uint32_t)c.band, c.divBand );
+	return c;
+}
 void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, float4* rayD, float4* T4, float4* Q4, int jobCount, LaunchEvents ev, hipStream_t st )
 {
+	const CameraParams c = lh2_camera_derive( *p );
 	const int threads = std::max( std::max( jobCount, 1 ), p->initC ? std::max( p->cursorWords, LH2_SEGS ) : 0 );
-	LH2_LAUNCH( k_camera, (threads + 255) / 256, 256, st, ev, *p, bn, rayO, rayD, T4, Q4, jobCount );
+	LH2_LAUNCH( k_camera, (threads + 255) / 256, 256, st, ev, c, bn, rayO, rayD, T4, Q4, jobCount );
 }
 void lh2_launch_trace_primary( const SceneDev* s, const TraceArgs* a, const CameraParams* cp, float4* T4, float4* Q4, int grid, LaunchEvents ev, hipStream_t st )
 {
-	LH2_LAUNCH( k_trace_primary_packet, grid, 256, st, ev, *cp, *s, *a, T4, Q4 );
+	const CameraParams c = lh2_camera_derive( *cp );
+	LH2_LAUNCH( k_trace_primary_packet, grid, 256, st, ev, c, *s, *a, T4, Q4 );
 }
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st )
 {
