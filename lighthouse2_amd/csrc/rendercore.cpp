@@ -251,6 +251,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "cameraFused" )) cameraFused = value != 0;
 	else if (!strcmp( name, "frameOverlap" )) frameOverlap = (int)value;
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
@@ -273,7 +274,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "pathTailBlocks", (float)pathTailBlocks },
+		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -886,6 +887,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	/* shadow overlap: the shade launch before the tail snapshots the queued shadow rays (advance_bounce) */
 	const bool overlap = shadows && tailL && shadowOverlap;
 	bool snapped = false;
+	bool besideNext = false;   /* the next frame's primary launch may run beside the launches from here on */
 	ps.sideOn = false;
 	/* the bounce loop */
 	for (int pathLength = 1; pathLength <= maxPL; pathLength++)
@@ -967,7 +969,15 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			if (primStream != stream) CHK_HIP( hipStreamWaitEvent( stream, ps.evTrace[pathLength], 0 ) );
 			ps.primParity ^= 1;
 		}
-		else lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : grid, { nullptr, ps.evTrace[pathLength] }, stream );
+		else
+		{
+			/* a bounce launch the next frame's primary launch will likely run beside (this frame overlapped: the next one
+			   probably does too): fewer blocks per CU, so the packets' latency-bound waves get slots from the start instead
+			   of the bounce launch's tail (config 2: 4262-4296 -> 4437-4442 Mrays/s at 5, r03q_ab_trace_blocks.txt) */
+			const bool beside = besideNext && !ta.packet && overlapTraceBlocks > 0;
+			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, overlapTraceBlocks ) : grid;
+			lh2_launch_trace_closest( &sd, &ta, g, { nullptr, ps.evTrace[pathLength] }, stream );
+		}
 		ps.fromTrace[pathLength] = ps.prevStop, ps.prevStop = ps.evTrace[pathLength];
 		sp.segCounts = segIn, sp.segOut = segNext, sp.segStride = ps.segStride;
 		sp.segBack = segInBack, sp.segOutBack = segNextBack;
@@ -1002,7 +1012,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];
 		/* the next frame's primary launch starts after this frame's first shade launch (the last reader of the primary
 		   buffers), or (frameOverlap 1) after the shade launch before the path tail: beside the latency-bound tail */
-		if (pathLength == 1 || (frameOverlap == 1 && tailL && pathLength == tailL - 1)) ps.overlapEv = ps.evShade[pathLength];
+		if (pathLength == 1 || (frameOverlap == 1 && tailL && pathLength == tailL - 1)) ps.overlapEv = ps.evShade[pathLength],
+			besideNext = !serialize && fusedCam && !(frameOverlap == 1 && tailL && pathLength + 1 < tailL);   /* the final overlapEv */
 
 		if (pathLength == maxPL) break;
 		if (primeRef && shadows)

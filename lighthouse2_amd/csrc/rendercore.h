@@ -277,6 +277,8 @@ private:
 	   shade launch slows the bounces it overlaps (2.344 / 1.426 ms) */
 	bool shadowOverlap = true;
 	int pathTailBlocks = 0;              /* the path tail's blocks per CU; 0: 2 with the overlap, else its occupancy limit */
+	int overlapTraceBlocks = 5;          /* blocks per CU of a closest-hit launch that the next frame's primary launch runs
+	                                        beside (an overlapped frame's later bounces, no path tail); 0: the trace grid's */
 	/* heavy-first primary packets (TraceArgs::hvRead): the packets of the previous frame that took more than
 	   packetHeavy x its mean node steps are taken first; 0: off */
 	float packetHeavy = 2.0f;
