@@ -137,9 +137,11 @@ def timed_frames(core, sc, gather, steps, warmup, world, dev, per_frame=None):
     first = [True]
 
     def step():
-        # a still camera converging, as tinyapp renders it (apps/tinyapp/main.cpp:102-103: Restart only when the
-        # camera moved): the first frame restarts, every later one accumulates a new sample with new random numbers,
-        # so no frame repeats the previous one's paths (the heavy-first packet order is last frame's costs)
+        # a still camera converging, as imguiapp renders a still scene (apps/imguiapp/main.cpp:188-204: Restart only
+        # when the camera moved, a material changed or an animation ran): the first frame restarts, every later one
+        # accumulates a new sample with new random numbers, so no frame repeats the previous one's paths (the
+        # heavy-first packet order is last frame's costs).  tinyapp's animated loop (a Restart every frame) is
+        # timed beside it: "config2_restart
         sc.render_frame(core, converge=LH2_RESTART if first[0] else LH2_CONVERGE)
         first[0] = False
         if world == 1:
@@ -211,6 +213,44 @@ def single_gpu_frames(core, sc, steps, warmup, per_frame=None):
         frame(warmup + i)
     core.sync()
     return (time.perf_counter() - t0) / steps, counts
+
+
+def config2_restart(args, local):
+    """The config-2 frame as tinyapp's animated main loop renders it (apps/tinyapp/main.cpp:98-118): every frame a
+    SetNodeTransform of one node (here the scene's one instance: a small rotation, SetInstance + UpdateToplevel,
+    rendersystem.cpp:143-174) and Render(Restart) (camMoved is set every frame).  A restart zeroes the accumulator
+    and a changed scene must not be traversed by the previous frame's rays, so the frame cannot start beside the
+    previous one the way a converging frame does."""
+    t0 = time.perf_counter()
+    sc = scene.config2_scene(n=args.tris, width=args.width, height=args.height)
+    core = RenderCore(device=local)
+    for kv in args.setting:
+        k, v = kv.split("=")
+        core.setting(k, float(v))
+    sc.load_into(core)
+    core.set_target(args.width, args.height, 1)
+    setup = time.perf_counter() - t0
+    mesh0 = sc.instances[0][0]
+
+    def frame(i):
+        core.set_instance(0, mesh0, scene.rotation_y(1e-3 * i))   # tinyapp: r += deltaTime * 0.3 per frame
+        core.set_instance(1, -1, None)                             # UpdateSceneGraph's end of the instance list
+        core.update_toplevel()
+        sc.render_frame(core, converge=LH2_RESTART)
+
+    for i in range(args.warmup):
+        frame(i)
+    core.sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        frame(args.warmup + i)
+    core.sync()
+    el = (time.perf_counter() - t0) / args.steps
+    counts = core.ray_counts()
+    r = frame_record(f"config2_restart: {args.tris} random tris, {args.width}x{args.height} 1 spp, Restart + "
+                     f"SetInstance + UpdateToplevel every frame (tinyapp's animated loop)", el, counts, core.stats(), setup)
+    core.close()
+    return r
 
 
 def frame_record(workload, el, counts, st, setup_s):
@@ -473,7 +513,7 @@ def main():
         }
     core.close()
     c4 = None if args.no_config4 else config4(args, rank, world, local, dev)
-    c4in = c3 = c5 = None
+    c4in = c3 = c5 = c2r = None
     if not args.no_configs:
         # the in-core multi-device run uses the node's first `world` GPUs from rank 0 alone: the other ranks
         # wait at a host-side (gloo) barrier, so no collective kernel occupies their GPUs meanwhile
@@ -483,11 +523,13 @@ def main():
         if rank == 0:
             c4in = config4_incore(args, world)
             if world == 1:
+                c2r = config2_restart(args, local)
                 c3 = config3(args, local)
                 c5 = None if args.no_config5 else config5(args, local)
         if world > 1:
             dist.barrier(group=host)
     if rank == 0:
+        out["config2_restart"] = c2r
         out["config4"] = c4
         out["config4_incore"] = c4in
         out["config3"] = c3

@@ -96,6 +96,7 @@ int lh2_core_scene_info( lh2_core core, int* nodeCount, int* triCount, int* maxD
 int lh2_core_debug_shadow_rays( lh2_core core, float* o4, float* d4, float* p4, int cap, int* n );
 /* diagnostics: the scene's BVH4 nodes (BLAS then TLAS, at most cap): f32 (32 floats each) and quantized (16 words
    each, the layout of k_quantize4); *n = the nodes copied */
+/* cap 0 (or null arrays): *n = the node count, nothing copied */
 int lh2_core_debug_bvh4( lh2_core core, float* f32Nodes, uint32_t* qNodes, int cap, int* n );
 
 /* host utility: n successive RandomFloat() values of Marsaglia xorshift32 (platform/system.cpp:44-46) */

@@ -299,11 +299,15 @@ class RenderCore:
         self._chk(self.lib.lh2_core_debug_shadow_rays(self.h, _fp(o), _fp(d), _fp(p), int(cap), C.byref(n)))
         return o[:n.value], d[:n.value], p[:n.value]
 
-    def debug_bvh4(self, cap: int = 1 << 22):
-        """Diagnostics: the scene's BVH4 nodes, (n, 32) float32 (f32 layout) and (n, 16) uint32 (quantized)."""
-        f = np.zeros((cap, 32), np.float32)
-        q = np.zeros((cap, 16), np.uint32)
+    def debug_bvh4(self, cap: int | None = None):
+        """Diagnostics: the scene's BVH4 nodes, (n, 32) float32 (f32 layout) and (n, 16) uint32 (quantized).
+        Without cap the arrays are sized by a count-only call first (cap 0 returns the node count)."""
         n = C.c_int(0)
+        if cap is None:
+            self._chk(self.lib.lh2_core_debug_bvh4(self.h, None, None, 0, C.byref(n)))
+            cap = n.value
+        f = np.zeros((max(cap, 1), 32), np.float32)
+        q = np.zeros((max(cap, 1), 16), np.uint32)
         self._chk(self.lib.lh2_core_debug_bvh4(self.h, _fp(f), q.ctypes.data, int(cap), C.byref(n)))
         return f[:n.value], q[:n.value]
 

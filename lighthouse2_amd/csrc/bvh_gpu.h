@@ -73,8 +73,9 @@ public:
 	/* TLAS BVH2 nodes [base2, base2 + count) as two-child BVH4 nodes at base4 (interior refs remapped) */
 	static void TlasToBvh4( const float4* nodes2, int base2, int count, int base4, float4* nodes4, hipStream_t stream );
 	/* BVH4 nodes [first, first + count) with quantized child boxes (4 uint4 per node, lh2_box4.inc box4q):
-	   8-bit child planes on a per-node, per-axis power-of-two grid, rounded outward */
-	static void Quantize4( const float4* nodes4, int first, int count, uint4* q, hipStream_t stream );
+	   8-bit child planes on a per-node, per-axis power-of-two grid, rounded outward; a node beyond the grid's range
+	   sets LH2_SCENE_ERR_QRANGE in *sceneError */
+	static void Quantize4( const float4* nodes4, int first, int count, uint4* q, int* sceneError, hipStream_t stream );
 
 private:
 	void Reserve( int n );

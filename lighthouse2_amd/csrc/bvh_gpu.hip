@@ -351,7 +351,7 @@ __global__ void k_tlas_check( const uint32_t* red, int maxBlasDepth, int* sceneE
 {
 	const int d = (int)red[14];
 	*tlasDepth = d;
-	if (d + maxBlasDepth >= LH2_STACK_TOTAL - 1) atomicOr( sceneError, 1 );
+	if (d + maxBlasDepth >= LH2_STACK_TOTAL - 1) atomicOr( sceneError, LH2_SCENE_ERR_DEPTH );
 }
 
 /* ---- single-workgroup TLAS build (count <= LH2_TLAS_WG_MAX): no host round trip ---------- */
@@ -497,7 +497,7 @@ __global__ __launch_bounds__( 1024 ) void k_tlas_build_wg( const GpuTlasArgs a, 
 	if (t == 0)
 	{
 		*a.tlasDepth = (int)depthMax;
-		if ((int)depthMax + a.maxBlasDepth >= LH2_STACK_TOTAL - 1) atomicOr( a.sceneError, 1 );
+		if ((int)depthMax + a.maxBlasDepth >= LH2_STACK_TOTAL - 1) atomicOr( a.sceneError, LH2_SCENE_ERR_DEPTH );
 	}
 }
 
@@ -561,8 +561,13 @@ __global__ __launch_bounds__( 256 ) void k_tlas_to_bvh4( const float4* __restric
    exactly); an empty slot (NaN planes) is the inverted box lo = 255, hi = 0 with the pop marker as its
    reference.  A box the traversal enters by mistake only costs work: it holds no hit the f32 tree's boxes
    do not hold (tests are exact per triangle).  Each exponent is at least the coordinate magnitude's - 28, so a plane's grid step is never
-   below the rounding of the slab arithmetic, and at least -100 (the scaled reciprocal stays normal). */
-__global__ __launch_bounds__( 256 ) void k_quantize4( const float4* __restrict__ nodes4, int first, int count, uint4* __restrict__ q )
+   below the rounding of the slab arithmetic, and at least -100 (the scaled reciprocal stays normal).  It is at most
+   LH2_QEXP_MAX = 27: box4q scales the ray's reciprocal by 2^e, and an axis-parallel ray's reciprocal is clamped to
+   +-1e30 (fast_inv), so 1e30 * 2^27 = 1.3e38 stays finite (a larger e makes it inf, and a zero byte plane times
+   inf a NaN slab).  A node that would need more (extent > 255 * 2^27 = 3.4e10, or coordinates beyond 2^55) sets
+   bit LH2_SCENE_ERR_QRANGE of the scene error flag, and the traversal kernels refuse the scene. */
+#define LH2_QEXP_MAX 27
+__global__ __launch_bounds__( 256 ) void k_quantize4( const float4* __restrict__ nodes4, int first, int count, uint4* __restrict__ q, int* __restrict__ err )
 {
 	const int i = blockIdx.x * 256 + threadIdx.x;
 	if (i >= count) return;
@@ -595,7 +600,8 @@ __global__ __launch_bounds__( 256 ) void k_quantize4( const float4* __restrict__
 		int ea = -100;
 		if (ext > 0) ea = max( ea, (int)ceil( log2( ext / 255.0 ) ) );
 		if (mag > 0) ea = max( ea, (int)floor( log2( mag ) ) - 28 );
-		while (ext > 255.0 * ldexp( 1.0, ea ) && ea < 127) ea++;   /* finite ext: ends well before the cap */
+		while (ext > 255.0 * ldexp( 1.0, ea ) && ea <= LH2_QEXP_MAX) ea++;   /* finite ext: ends at the cap at the latest */
+		if (ea > LH2_QEXP_MAX) atomicOr( err, LH2_SCENE_ERR_QRANGE ), ea = LH2_QEXP_MAX;
 		e[a] = ea;
 		const double step = ldexp( 1.0, ea );
 		for (int c = 0; c < 4; c++)
@@ -760,10 +766,10 @@ void GpuBvhBuilder::Relocate4( const float4* src, int nodeCount, int nodeBase, u
 	if (nodeCount <= 0) return;
 	k_relocate4<<<blocks( nodeCount ), 256, 0, st>>>( src, nodeCount, nodeBase, triBase, dst );
 }
-void GpuBvhBuilder::Quantize4( const float4* nodes4, int first, int count, uint4* q, hipStream_t st )
+void GpuBvhBuilder::Quantize4( const float4* nodes4, int first, int count, uint4* q, int* sceneError, hipStream_t st )
 {
 	if (count <= 0) return;
-	k_quantize4<<<blocks( count ), 256, 0, st>>>( nodes4, first, count, q );
+	k_quantize4<<<blocks( count ), 256, 0, st>>>( nodes4, first, count, q, sceneError );
 	CHK( hipGetLastError() );
 }
 

@@ -203,3 +203,6 @@ void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, co
 #define LH2_STACK_LDS 16
 #endif
 #define LH2_STACK_TOTAL 96
+/* bits of the scene error flag (SceneDev::sceneError; any bit set: the trace kernels exit and the host raises FatalError) */
+#define LH2_SCENE_ERR_DEPTH 1    /* BVH depth exceeds the traversal stack */
+#define LH2_SCENE_ERR_QRANGE 2   /* a BVH4 node beyond the quantized grid's range (k_quantize4) */

@@ -575,7 +575,7 @@ void RenderCore::ConcatenateBlas( int ni )
 		if (bvh4) GpuBvhBuilder::Relocate4( m.bvh4Nodes.ptr, m.node4Count, meshNode4Base[mi], (uint32_t)meshTriBase[mi], dNodes4.ptr, stream );
 		if (m.leafTris) CHK_HIP( hipMemcpyAsync( dTris.ptr + (size_t)meshTriBase[mi] * 3, m.bvhTris.ptr, sizeof( float4 ) * 3 * (size_t)m.leafTris, hipMemcpyDeviceToDevice, stream ) );
 	}
-	if (bvh4) GpuBvhBuilder::Quantize4( dNodes4.ptr, 0, node4Total, dNodes4q.ptr, stream );
+	if (bvh4) GpuBvhBuilder::Quantize4( dNodes4.ptr, 0, node4Total, dNodes4q.ptr, dSceneError.ptr, stream );
 	dMeshBounds.upload( bounds.data(), bounds.size(), stream );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	blasNodeCount = nodeTotal, blasTriCount = triTotal, blasNode4Count = node4Total, blasMeshTris = meshTris;
@@ -726,7 +726,7 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 	if (bvh4)
 	{
 		GpuBvhBuilder::TlasToBvh4( dNodes.ptr, blasNodeCount, tlasCapacity, blasNode4Count, dNodes4.ptr, stream );
-		GpuBvhBuilder::Quantize4( dNodes4.ptr, blasNode4Count, tlasCapacity, dNodes4q.ptr, stream );
+		GpuBvhBuilder::Quantize4( dNodes4.ptr, blasNode4Count, tlasCapacity, dNodes4q.ptr, dSceneError.ptr, stream );
 	}
 	CHK_HIP( hipEventRecord( evStage[slot], stream ) );
 	instancesDirty = false;
@@ -734,6 +734,14 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 
 /* device-side scene errors (TLAS deeper than the traversal stack): the trace kernels skip the
    frame, and the host reports it here */
+#define LH2_STR_( x ) #x
+#define LH2_XSTR( x ) LH2_STR_( x )
+static const char* SceneErrorText( int e )
+{
+	if (e & LH2_SCENE_ERR_QRANGE) return "scene extent beyond the quantized BVH4 grid (a node wider than 255 * 2^27 or coordinates beyond 2^55)";
+	return "BVH depth exceeds the traversal stack (" LH2_XSTR( LH2_STACK_TOTAL ) " levels)";
+}
+
 void RenderCore::CheckSceneError()
 {
 	if (!dSceneError.ptr) return;
@@ -741,7 +749,7 @@ void RenderCore::CheckSceneError()
 	CHK_HIP( hipMemcpyAsync( &hostStats->sceneError, dSceneError.ptr, sizeof( int ), hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	e = hostStats->sceneError;
-	if (e) FatalError( "BVH depth exceeds the traversal stack (%d levels)", LH2_STACK_TOTAL );
+	if (e) FatalError( "%s", SceneErrorText( e ) );
 }
 
 SceneDev RenderCore::MakeSceneDev() const
@@ -1069,7 +1077,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	   where it is assembled, MultiDevice / FinalizeFrame) */
 	RowMap rm{};
 	if (tileRows < scrheight) rm = { scrwidth, cp.y0, cp.band, cp.bandStride, tileRows };
+	/* the previous frame's end stays recorded (evFrame[2]): an overlapped frame's render time starts at the later of
+	   its primary launch's start and the previous frame's end (Synchronize), so per-frame times sum to wall time */
+	std::swap( evFrame[1], evFrame[2] );
+	prevFrameEndValid = frameEndRecorded, frameWasOverlapped = fusedCam && !serialize;
 	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, &fs, { nullptr, evFrame[1] }, stream, &rm );
+	frameEndRecorded = true;
 	if (glResource && !displayAtFinalize)
 	{
 		hipArray_t arr = nullptr;
@@ -1142,7 +1155,7 @@ void RenderCore::Synchronize()
 	bool full = cn.shadowOverflow != 0;
 	for (int k = 0; k < LH2_SEGS; k++) full = full || cn.segShadow[k * LH2_SEGCOUNT_STRIDE] > ps.shadowStride;
 	if (full) FatalError( "shadow ray buffer overflow" );
-	if (hostStats->sceneError) FatalError( "BVH depth exceeds the traversal stack (%d levels): frame skipped", LH2_STACK_TOTAL );
+	if (hostStats->sceneError) FatalError( "%s: frame skipped", SceneErrorText( hostStats->sceneError ) );
 	const uint32_t* rc = hostStats->rayCount;   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
 	auto ms = [&]( hipEvent_t a, hipEvent_t b ) { float t = 0; (void)hipEventElapsedTime( &t, a, b ); return t * 1e-3f; };
 	/* each interval: the previous launch's stop event -> this launch's stop event (kernel + launch gap) */
@@ -1168,7 +1181,15 @@ void RenderCore::Synchronize()
 	coreStats.totalShadowRays = framePrimeRef ? cn.totalShadowRays : QueuedShadowRays( cn );
 	coreStats.totalExtensionRays = cn.totalExtensionRays;
 	coreStats.totalRays = coreStats.totalExtensionRays + coreStats.totalShadowRays;
-	coreStats.renderTime = ms( evFrame[0], evFrame[1] );   /* device time of the whole frame (the reference's Render blocks) */
+	/* device time of the whole frame (the reference's Render blocks).  Under frameOverlap the frame's primary launch
+	   starts beside the previous frame's tail: the part before the previous frame's end is the previous frame's
+	   (ADVICE r3).  traceTime0 stays the primary launch's own duration, stretched by what ran beside it */
+	coreStats.renderTime = ms( evFrame[0], evFrame[1] );
+	if (frameWasOverlapped && prevFrameEndValid)
+	{
+		const float shared = ms( evFrame[0], evFrame[2] );
+		if (shared > 0) coreStats.renderTime = std::max( 0.0f, coreStats.renderTime - shared );
+	}
 	coreStats.probedInstid = cn.probedInstid, coreStats.probedTriid = cn.probedTriid, coreStats.probedDist = cn.probedDist;
 }
 
@@ -1207,8 +1228,9 @@ int RenderCore::DebugBvh4( float* f32Nodes, uint32_t* qNodes, int cap )
 {
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	Synchronize();
+	if (!dNodes4.ptr || !dNodes4q.ptr) return 0;
+	if (cap <= 0 || !f32Nodes || !qNodes) return blasNode4Count + tlasCapacity;   /* a count-only call */
 	const int n = std::min( cap, blasNode4Count + tlasCapacity );
-	if (n <= 0 || !dNodes4.ptr || !dNodes4q.ptr) return 0;
 	CHK_HIP( hipMemcpy( f32Nodes, dNodes4.ptr, 128 * (size_t)n, hipMemcpyDeviceToHost ) );
 	CHK_HIP( hipMemcpy( qNodes, dNodes4q.ptr, 64 * (size_t)n, hipMemcpyDeviceToHost ) );
 	return n;

@@ -247,7 +247,8 @@ private:
 	bool terminalShade = true;           /* k_shade<true> for shade passes whose hits cannot contribute (ShadeParams::terminal) */
 	FrameStats* hostStats = nullptr;     /* pinned */
 	bool statsPending = false;
-	hipEvent_t evFrame[2] = {};
+	hipEvent_t evFrame[3] = {};          /* the frame's start marker, its end (finalize), the previous frame's end */
+	bool frameEndRecorded = false, prevFrameEndValid = false, frameWasOverlapped = false;
 	int tiledRays = 1;                   /* primary rays stored in 8x8 pixel blocks per wave (coherent packets) */
 	int cameraFused = 1;                 /* primary rays made by the packet launch itself (k_trace_primary_packet), no camera launch */
 	/* a fused frame's primary launch beside the previous frame's later bounces (aheadStream): 1, after its shade launch

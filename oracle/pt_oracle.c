@@ -138,8 +138,11 @@ struct Oracle
    occluded, O, D, tmax, contribution) */
 static void debug_log( const Oracle* o, const float* rec )
 {
-	Oracle* m = (Oracle*)o;   /* one thread renders the debug pixel */
-	if (m->debugCount < m->debugCap) memcpy( m->debugLog + 16 * m->debugCount++, rec, 16 * sizeof( float ) );
+	/* the debug pixel's samples and shadow rays may run on different render_worker threads (spp > 1, chunked
+	   jobs): the slot is claimed with an atomic fetch-add, the count clamped when read */
+	Oracle* m = (Oracle*)o;
+	const int slot = __atomic_fetch_add( &m->debugCount, 1, __ATOMIC_RELAXED );
+	if (slot < m->debugCap) memcpy( m->debugLog + 16 * slot, rec, 16 * sizeof( float ) );
 }
 
 Oracle* orc_create( void )
@@ -704,7 +707,8 @@ void orc_debug_pixel( Oracle* o, int px, int cap )
 }
 int orc_debug_log( const Oracle* o, float* out, int cap )
 {
-	const int n = o->debugCount < cap ? o->debugCount : cap;
+	int n = o->debugCount < o->debugCap ? o->debugCount : o->debugCap;
+	if (n > cap) n = cap;
 	if (n > 0) memcpy( out, o->debugLog, (size_t)n * 16 * sizeof( float ) );
 	return n;
 }
