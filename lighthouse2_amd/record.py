@@ -18,7 +18,7 @@ import numpy as np
 from . import abi
 
 OP = dict(SET_SKY=1, SET_MATERIALS=2, SET_GEOMETRY=3, SET_INSTANCE=4, UPDATE_TOPLEVEL=5, SET_LIGHTS=6,
-          SETTING=7, SET_TARGET=8, RENDER=9, SET_PROBE=10)
+          SETTING=7, SET_TARGET=8, RENDER=9, SET_PROBE=10, SET_TEXTURES=11)
 
 
 class CallRecorder:
@@ -49,6 +49,18 @@ class CallRecorder:
 
     def set_probe(self, x, y):
         self._rec("SET_PROBE", struct.pack("<ii", x, y))
+
+    def set_textures(self, textures):
+        """SetTextures( const CoreTexDesc*, int ) (core_api_base.h:100): per texture the descriptor's fields
+        (width, height, flags, pixelCount, MIPlevels, storage) and its texels; the replay host points the
+        descriptor at its copy of them (the core copies them during the call, rendercore.cpp:276-347)."""
+        out = [struct.pack("<i", len(textures))]
+        for t in textures:
+            px = np.ascontiguousarray(t.pixels)
+            d = t.desc(px)
+            out.append(struct.pack("<IIIIIiI", d.width, d.height, d.flags, d.pixelCount, d.MIPlevels, d.storage, px.nbytes))
+            out.append(px.tobytes())
+        self._rec("SET_TEXTURES", b"".join(out))
 
     def set_materials(self, mats):
         arr = abi.material_array(mats)

@@ -849,20 +849,53 @@ def _obj_tris(P, Nrm, fv, fn, fmat) -> np.ndarray:
     return t
 
 
+# the stand-in for the one pica texture image missing from the reference (Wax_Pastel_Label_02_baseColor.png,
+# .MISSING_LARGE_BLOBS): 512 x 512 texels of opaque white, so the material it colours (baseColorFactor 1) shades
+# as it would untextured; every other texture is the reference's own image
+MISSING_TEXTURE_RGBA = (512, 512, (255, 255, 255, 255))
+TEX_LDR = 4                # HostTexture::LDR (host_texture.h:42)
+
+
+def _gltf_texture(png: np.ndarray) -> Texture:
+    """HostScene::AddScene's texture conversion (host_scene.cpp:260-271): the glTF image as tinygltf decodes it
+    (stb_image, 8-bit RGBA with req_comp 4, first row first: tiny_gltf.h:2202-2286), memcpy'd into idata, flags
+    LDR, MIP levels by ConstructMIPmaps (no FLIPPED / LINEARIZED mods on this path).  PNG is lossless, so PIL's
+    decode (palette and transparency expanded to RGBA, like stb_image) gives the same bytes."""
+    if png.size == 0:
+        w, h, rgba = MISSING_TEXTURE_RGBA
+        img = np.empty((h, w, 4), np.uint8)
+        img[...] = np.array(rgba, np.uint8)
+    else:
+        import io
+        from PIL import Image
+        im = Image.open(io.BytesIO(png.tobytes()))
+        assert im.mode in ("P", "RGB", "RGBA", "L", "LA"), im.mode   # 8 bits per channel
+        img = np.asarray(im.convert("RGBA"), np.uint8)
+    t = make_texture(img)
+    t.flags = TEX_LDR
+    return t
+
+
 def tinyapp_scene(width: int = 640, height: int = 400, path=None) -> Scene:
     """tinyapp's PrepareScene (apps/tinyapp/main.cpp:34-45) from the committed fixture
     (tools/make_config1_fixture.py): the pica glTF diorama (170 meshes, one instance per node, the root node
     rotated by RotateX(-pi/2)), legocar.obj at scale 10 (placed as the main loop's first frame places it:
     Translate(0, 5, 0)), and the light quad (0, -1, 0) at (0, 26, 0), 6.9 x 6.9, radiance (100, 100, 80).
-    Materials: glTF base colour / metallic / roughness factors (host_material.cpp:77-103; the decal textures
-    are left out: untextured), the .mtl Kd colours with tinyobjloader's default shininess (roughness 0), the
+    Materials: glTF base colour / metallic / roughness factors and base colour textures (host_material.cpp:77-103;
+    the six glTF textures as AddScene converts them, _gltf_texture, one a documented stand-in for the image missing
+    from the reference), the .mtl Kd colours with tinyobjloader's default shininess (roughness 0), the
     light.  The camera is tinyapp's default (no camera.xml ships with the app: Camera's defaults, camera.h:33-44:
     at the origin looking down +z, FOV 40, focal distance 5, aperture EPSILON, distortion 0.05)."""
     f = np.load(path or TINYAPP_FIXTURE)
     meshes, materials = [], []
-    for c, m, r in zip(f["pica_mat_color"], f["pica_mat_metallic"], f["pica_mat_roughness"]):
-        materials.append(abi.make_material(tuple(float(x) for x in c), roughness=None if np.isnan(r) else float(r),
-                                           metallic=None if np.isnan(m) else float(m)))
+    # the glTF textures, in AddScene order (textureBase 0: the first scene loaded)
+    textures = [_gltf_texture(f[f"pica_tex_png_{i}"]) for i in range(int(f["pica_tex_count"]))]
+    for c, m, r, t in zip(f["pica_mat_color"], f["pica_mat_metallic"], f["pica_mat_roughness"], f["pica_mat_tex"]):
+        mat = abi.make_material(tuple(float(x) for x in c), roughness=None if np.isnan(r) else float(r),
+                                metallic=None if np.isnan(m) else float(m))
+        if t >= 0:
+            mat.color.textureID = int(t)      # baseColorTexture index + textureBase (host_material.cpp:95-98)
+        materials.append(mat)
     prim_mesh, prim_mat, prim_v, prim_i = f["pica_prim_mesh"], f["pica_prim_mat"], f["pica_prim_v"], f["pica_prim_i"]
     P, Nv, U, I = f["pica_pos"], f["pica_nrm"], f["pica_uv"], f["pica_idx"]
     per_mesh = [[] for _ in range(int(f["pica_meshes"]))]
@@ -887,7 +920,7 @@ def tinyapp_scene(width: int = 640, height: int = 400, path=None) -> Scene:
     car_T = np.eye(4, dtype=np.float32)
     car_T[1, 3] = 5.0
     instances.append((car_mesh, car_T))
-    sc = Scene(meshes=meshes, instances=instances, materials=materials, name="tinyapp")
+    sc = Scene(meshes=meshes, instances=instances, materials=materials, textures=textures, name="tinyapp")
     sc.area_lights = [light_from_tri(quad[i], i, light_inst, (100.0, 100.0, 80.0)) for i in range(2)]
     sc.view = camera_view((0, 0, 0), (0, 0, 1), fov_deg=40, aspect=width / height, focal=5, aperture=1e-4, distortion=0.05,
                           pixel_height=height)

@@ -86,8 +86,27 @@ SR_API int sr_set_instance( void* h, int instanceIdx, int meshIdx, const float* 
 	return 0;
 }
 
-/* RenderCore::SetMaterials (rendercore.cpp:147-172) for untextured materials: the diffuse colour
-   packed to 8 bits per channel */
+/* RenderCore::SetTextures (rendercore.cpp:128-141): each texture's texels copied (pixelCount 32-bit texels,
+   all MIP levels), its base size kept */
+SR_API int sr_set_textures( void* h, const CoreTexDesc* tex, int count )
+{
+	SoftRast* s = (SoftRast*)h;
+	std::vector<Texture*>& list = s->rasterizer.scene.texList;
+	for (int i = 0; i < count; i++)
+	{
+		Texture* t;
+		if (i < (int)list.size()) t = list[i];
+		else list.push_back( t = new Texture() );
+		t->pixels = (uint*)MALLOC64( tex[i].pixelCount * sizeof( uint ) );
+		if (!tex[i].idata) return -1;
+		memcpy( t->pixels, tex[i].idata, tex[i].pixelCount * sizeof( uint ) );
+		t->width = tex[i].width, t->height = tex[i].height;
+	}
+	return 0;
+}
+
+/* RenderCore::SetMaterials (rendercore.cpp:147-172): the diffuse colour packed to 8 bits per channel, or the
+   colour texture */
 SR_API int sr_set_materials( void* h, const CoreMaterial* mat, int count )
 {
 	SoftRast* s = (SoftRast*)h;
@@ -98,9 +117,17 @@ SR_API int sr_set_materials( void* h, const CoreMaterial* mat, int count )
 		if (i < (int)list.size()) m = list[i];
 		else list.push_back( m = new Material() );
 		m->texture = 0;
-		if (mat[i].color.textureID != -1) return -1;   /* textures: not used by the config-1 scene */
-		const float r = mat[i].color.value.x, g = mat[i].color.value.y, b = mat[i].color.value.z;
-		m->diffuse = ((int)(b * 255.0f) << 16) + ((int)(g * 255.0f) << 8) + (int)(r * 255.0f);
+		const int texID = mat[i].color.textureID;
+		if (texID == -1)
+		{
+			const float r = mat[i].color.value.x, g = mat[i].color.value.y, b = mat[i].color.value.z;
+			m->diffuse = ((int)(b * 255.0f) << 16) + ((int)(g * 255.0f) << 8) + (int)(r * 255.0f);
+		}
+		else
+		{
+			if (texID >= (int)s->rasterizer.scene.texList.size()) return -1;
+			m->texture = s->rasterizer.scene.texList[texID];
+		}
 	}
 	return 0;
 }

@@ -130,13 +130,14 @@ def test_reference_header_host_frame_matches_oracle(tmp_path, devices):
 def test_config1_tinyapp_scene_through_reference_header(tmp_path):
     """BASELINE config 1: tinyapp's default scene (apps/tinyapp/main.cpp:34-45: the pica glTF diorama, the lego
     car at scale 10, the light quad; tests/golden/config1_tinyapp.npz) at 640 x 400, driven through the
-    reference's own CoreAPI_Base declaration as RenderSystem drives it (172 meshes, 172 instances, SetLights
-    with the quad's two emissive triangles), two frames (restart, converge): identical primary and bounce-1
-    ray counts, accumulator within 1e-4 of the oracle."""
+    reference's own CoreAPI_Base declaration as RenderSystem drives it (SetTextures with the six glTF textures,
+    172 meshes, 172 instances, SetLights with the quad's two emissive triangles), two frames (restart,
+    converge): identical primary and bounce-1 ray counts, accumulator within 1e-4 of the oracle."""
     assert REF_HOST.exists(), "oracle/_ref/reference_rendersystem missing: build it where /root/reference exists"
     w, h = 640, 400
     sc = scene.tinyapp_scene(w, h)
     calls = tmp_path / "calls.bin"
+    assert len(sc.textures) == 6 and sum(m.color.textureID >= 0 for m in sc.materials) == 5
     _record(calls, sc, w, h, frames=2)
     res = subprocess.run([str(REF_HOST), str(LIB), str(calls), str(tmp_path / "acc.bin")], capture_output=True,
                          text=True, timeout=240)

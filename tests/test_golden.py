@@ -215,3 +215,25 @@ def test_config1_tinyapp_fixture():
     # consistent-normal alphas in [0, acos(0.7) * (1 + 0.03632 * 0.09)], finite
     alpha = np.concatenate([m[:, abi.TRI["alpha"]:abi.TRI["alpha"] + 3] for m in sc.meshes[:-1]])
     assert np.isfinite(alpha).all() and alpha.min() >= 0 and alpha.max() <= 0.7981
+
+
+def test_config1_tinyapp_textures():
+    """The pica glTF textures as HostScene::AddScene converts them (host_scene.cpp:260-271): six textures in glTF
+    order, 8-bit RGBA as tinygltf's stb_image decode (req_comp 4) gives them, flags LDR, MIP levels by
+    ConstructMIPmaps; materials point at them by baseColorTexture index (host_material.cpp:95-98).  Texture 2
+    (Wax_Pastel_Label_02_baseColor.png, missing from the reference) is the documented white stand-in.  The base
+    levels' hashes pin the PNG decode (lossless: any conforming decoder gives these bytes)."""
+    import hashlib
+
+    from lighthouse2_amd import scene
+    sc = scene.tinyapp_scene(64, 40)
+    want = [(512, 256, "b81a73cea0089fbb"), (512, 512, "087fd8907b9ec1f9"), (512, 512, "f5fb04aa5b882706"),
+            (2048, 2048, "1a7eb87feb1a9877"), (512, 512, "dccc8d13a9ea76d8"), (2048, 2048, "2f656f70c1035c44")]
+    assert len(sc.textures) == len(want)
+    for t, (w, h, sha) in zip(sc.textures, want):
+        assert (t.width, t.height, t.flags, t.storage) == (w, h, scene.TEX_LDR, 0)
+        assert t.pixels.size == scene.pixels_needed(w, h, scene.MIPLEVELCOUNT)
+        assert hashlib.sha256(t.pixels[:w * h].tobytes()).hexdigest()[:16] == sha
+    assert (sc.textures[2].pixels == 0xffffffff).all()          # the stand-in, every level
+    tex_of = {i: m.color.textureID for i, m in enumerate(sc.materials) if m.color.textureID >= 0}
+    assert tex_of == {10: 5, 12: 4, 17: 1, 19: 0, 24: 2}          # Decal_Note, First_Aid, Caution, Keyboard, Wax

@@ -6,8 +6,8 @@ meshes, the root node rotated by RotateX(-pi/2)), the lego car OBJ (10,992 trian
 light quad (2 triangles, radiance 100, 100, 80, at y = 26, 6.9 x 6.9), read from the reference's assets
 (apps/tinyapp/data) into tests/golden/config1_tinyapp.npz by tools/make_config1_fixture.py and converted
 by scene.tinyapp_scene with the reference's mesh builders; the camera is tinyapp's default (no camera.xml
-ships with the app).  The decal textures are left out (one of the six images is missing from the
-reference, .MISSING_LARGE_BLOBS).
+ships with the app).  The six glTF textures are applied as HostScene::AddScene converts them (one, missing from
+the reference (.MISSING_LARGE_BLOBS), is a documented stand-in: scene.MISSING_TEXTURE_RGBA).
 
 Measured, one JSON line:
   - the reference CPU rasterizer (RenderCore_SoftRasterizer/rasterizer.cpp, oracle/_ref/
@@ -59,6 +59,11 @@ def soft_rasterizer(sc: scene.Scene, width: int, height: int, seconds: float) ->
     for i, (m, T) in enumerate(sc.instances):
         M = np.ascontiguousarray(T, np.float32)
         assert L.sr_set_instance(h, i, m, M.ctypes.data) == 0
+    L.sr_set_textures.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    if sc.textures:
+        keep += [np.ascontiguousarray(t.pixels) for t in sc.textures]
+        descs = (abi.CoreTexDesc * len(sc.textures))(*[t.desc(k) for t, k in zip(sc.textures, keep[-len(sc.textures):])])
+        assert L.sr_set_textures(h, C.cast(descs, C.c_void_p), len(sc.textures)) == 0
     mats = (abi.CoreMaterial * len(sc.materials))(*sc.materials)
     assert L.sr_set_materials(h, mats, len(sc.materials)) == 0
     view = sc.view

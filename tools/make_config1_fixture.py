@@ -15,9 +15,14 @@ The fixture keeps the loaders' inputs in compact form (numpy, no parsing at test
     POSITION, NORMAL, TEXCOORD_0 (TANGENT is skipped by the reference), the material index;
   * the node hierarchy flattened into instances (mesh, world matrix), the root node's transform replaced by
     RotateX(-pi/2) as PrepareScene does;
-  * glTF materials' baseColorFactor / metallicFactor / roughnessFactor (HostMaterial::ConvertFrom,
-    host_material.cpp:77-103); texture references are recorded but not the texels (decals; one of the six
-    images is missing from the reference, .MISSING_LARGE_BLOBS): the scene is rendered untextured;
+  * glTF materials' baseColorFactor / metallicFactor / roughnessFactor and baseColorTexture index
+    (HostMaterial::ConvertFrom, host_material.cpp:77-103);
+  * the glTF textures in HostScene::AddScene's order (host_scene.cpp:260-271: one HostTexture per glTF texture,
+    from its image): the image files' own bytes (lossless PNG; decoded at load by scene.tinyapp_scene with PIL to
+    8-bit RGBA, as tinygltf's stb_image decode with req_comp 4 gives them, tiny_gltf.h:2202-2286).  One of the six
+    images, Wax_Pastel_Label_02_baseColor.png, is missing from the reference (.MISSING_LARGE_BLOBS; the reference
+    itself would stop at loading the glTF): its slot holds no bytes and the loader substitutes a documented
+    stand-in texel block (scene.MISSING_TEXTURE_RGBA);
   * the OBJ's polygon soup after LoadGeometryFromOBJ's scale (host_mesh.cpp:131-305): positions (x 10), the
     per-corner normal indices and normals, per-face material; the .mtl Kd colours; tinyobjloader's default
     shininess 1 gives roughness min(1 - 1, 1) = 0 (host_material.cpp:41).
@@ -124,12 +129,21 @@ def load_pica():
     metal = np.array([m.get("pbrMetallicRoughness", {}).get("metallicFactor", np.nan) for m in mats], np.float32)
     rough = np.array([m.get("pbrMetallicRoughness", {}).get("roughnessFactor", np.nan) for m in mats], np.float32)
     tex = np.array([m.get("pbrMetallicRoughness", {}).get("baseColorTexture", {}).get("index", -1) for m in mats], np.int32)
+    # the textures (AddScene order), each the bytes of its image file (empty: missing from the reference)
+    tex_png, tex_names = [], []
+    for t in g.get("textures", []):
+        uri = g["images"][t["source"]]["uri"]
+        f = REF / "pica" / uri
+        tex_png.append(np.frombuffer(f.read_bytes(), np.uint8) if f.exists() else np.zeros(0, np.uint8))
+        tex_names.append(uri)
+    png = {f"pica_tex_png_{i}": b for i, b in enumerate(tex_png)}
     return dict(pica_pos=np.concatenate(pos), pica_nrm=np.concatenate(nrm), pica_uv=np.concatenate(uv), pica_idx=np.concatenate(idx),
                 pica_prim_mesh=np.array(prim_mesh, np.int32), pica_prim_mat=np.array(prim_mat, np.int32),
                 pica_prim_v=np.array(prim_v, np.int64), pica_prim_i=np.array(prim_i, np.int64), pica_meshes=np.int32(len(g["meshes"])),
                 pica_inst_mesh=np.array(inst_mesh, np.int32), pica_inst_T=np.array(inst_T, np.float32),
                 pica_mat_color=color, pica_mat_metallic=metal, pica_mat_roughness=rough, pica_mat_tex=tex,
-                pica_mat_names=np.array([m.get("name", "") for m in mats]))
+                pica_mat_names=np.array([m.get("name", "") for m in mats]), pica_tex_count=np.int32(len(tex_png)),
+                pica_tex_names=np.array(tex_names), **png)
 
 
 def load_car(scale: float = 10.0):

@@ -36,7 +36,7 @@ using namespace lighthouse2;
 
 namespace {
 
-enum Op : uint32_t { SET_SKY = 1, SET_MATERIALS, SET_GEOMETRY, SET_INSTANCE, UPDATE_TOPLEVEL, SET_LIGHTS, SETTING, SET_TARGET, RENDER, SET_PROBE };
+enum Op : uint32_t { SET_SKY = 1, SET_MATERIALS, SET_GEOMETRY, SET_INSTANCE, UPDATE_TOPLEVEL, SET_LIGHTS, SETTING, SET_TARGET, RENDER, SET_PROBE, SET_TEXTURES };
 
 struct Reader
 {
@@ -124,6 +124,27 @@ int main( int argc, char** argv )
 		{
 			const int x = r.get<int>(), y = r.get<int>();
 			if (core) core->SetProbePos( make_int2( x, y ) );
+			break;
+		}
+		case SET_TEXTURES:
+		{
+			/* per texture: width, height, flags, pixelCount, MIPlevels, storage, texel bytes, texels (record.py); the
+			   descriptors point at this host's copies for the duration of the call (rendercore.cpp:276-347) */
+			const int n = r.get<int>();
+			std::vector<CoreTexDesc> d( n > 0 ? n : 1 );
+			std::vector<std::vector<uint8_t>> texels( n > 0 ? n : 1 );
+			for (int i = 0; i < n; i++)
+			{
+				d[i].width = r.get<uint32_t>(), d[i].height = r.get<uint32_t>(), d[i].flags = r.get<uint32_t>();
+				d[i].pixelCount = r.get<uint32_t>(), d[i].MIPlevels = r.get<uint32_t>();
+				d[i].storage = (TexelStorage)r.get<int32_t>();
+				d[i].firstPixel = 0;
+				const uint32_t bytes = r.get<uint32_t>();
+				const uint8_t* src = r.take( bytes );
+				texels[i].assign( src, src + bytes );
+				d[i].idata = (uchar4*)(void*)texels[i].data();
+			}
+			if (core) core->SetTextures( d.data(), n );
 			break;
 		}
 		case SET_MATERIALS:
