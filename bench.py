@@ -130,6 +130,14 @@ def cpu_baseline(sc, width, height, seconds):
                       f"{threads} threads, {el:.1f} s"}
 
 
+def apply_settings(core, args):
+    """--setting name=value (A/B runs): applied to every core the bench creates, before its scene is loaded."""
+    for kv in args.setting:
+        k, v = kv.split("=")
+        core.setting(k, float(v))
+    return core
+
+
 def timed_frames(core, sc, gather, steps, warmup, world, dev, per_frame=None):
     """warmup + steps frames (render; N > 1: pack the owned rows, gather); returns (max-over-ranks
     seconds, rays of all ranks per frame [primary + bounce 1, deeper, shadow], this rank's counts).
@@ -270,7 +278,7 @@ def config3(args, local):
     (specular chains, glass, two area lights: NEE + shadow rays), 1080p 1 spp, one GPU."""
     t0 = time.perf_counter()
     sc = scene.room_scene(args.room_tris, 1920, 1080)
-    core = RenderCore(device=local)
+    core = apply_settings(RenderCore(device=local), args)
     core.setting("maxPathLength", 4)
     sc.load_into(core)
     core.set_target(1920, 1080, 1)
@@ -288,9 +296,13 @@ def config5(args, local):
     frame), 1080p 8 spp (16,588,800 paths), one GPU."""
     t0 = time.perf_counter()
     sc = scene.instanced_scene(meshes=100, tris_per_mesh=100_000, width=1920, height=1080)
-    core = RenderCore(device=local)
+    gen = time.perf_counter() - t0
+    core = apply_settings(RenderCore(device=local), args)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()      # the core's setup (SynchronizeSceneData: SetGeometry x 100, BLAS builds, TLAS)
     sc.load_into(core)
     core.set_target(1920, 1080, 8)
+    core.sync()
     setup = time.perf_counter() - t0
 
     def per_frame(i):
@@ -302,6 +314,7 @@ def config5(args, local):
     el, counts = single_gpu_frames(core, sc, args.config_steps, args.warmup, per_frame)
     r = frame_record("config5: 100 meshes x 100k tris, per-frame instance rotations + TLAS rebuild, 1920x1080 8 spp",
                      el, counts, core.stats(), setup)
+    r["scene_gen_s"] = round(gen, 2)   # the synthetic scene's generation in Python (not the core's)
     core.close()
     return r
 
@@ -315,7 +328,7 @@ def config4_incore(args, ndev):
     W4, H4 = 3840, 2160
     t0 = time.perf_counter()
     sc = scene.room_scene(args.room_tris, W4, H4)
-    core = RenderCore(device=0)
+    core = apply_settings(RenderCore(device=0), args)
     if ndev > 1:
         core.setting("deviceCount", ndev)
     core.setting("maxPathLength", 4)

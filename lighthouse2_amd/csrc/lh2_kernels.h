@@ -151,6 +151,10 @@ struct FrameStatsDev
 	const Counters* counters; const uint32_t* rayLog;
 	Counters* hostCounters; uint32_t* hostRayCount;
 	const int* sceneError; int* hostSceneError;
+	uint32_t* zeroHeads;    /* LH2_CURSOR_WORDS work-queue heads zeroed by the finalize (the primary launch's slot of the frame
+	                           parity's block: its next user's launch may reset the rest while it runs, never its own) */
+	float4* delta;          /* early shade: the frame's first-vertex contributions, added into the accumulator (and zeroed) by
+	                           the finalize, so the previous frame's finalize never sees them */
 };
 
 extern "C" {
@@ -174,7 +178,7 @@ void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int ba
 void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
 /* the rows of a band partition (k_pack_rows' mapping); rows 0: every pixel */
 struct RowMap { int w, y0, band, bandStride, rows; };
-void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st,
+void lh2_launch_finalize( float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st,
 	const RowMap* rm = nullptr );
 }
 
@@ -195,14 +199,14 @@ void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, co
 #define LH2_CURSOR_WORDS (2 * LH2_CHUNKS * LH2_CURSOR_STRIDE)
 #define LH2_HEAVY_CURSOR (LH2_CHUNKS * LH2_CURSOR_STRIDE)
 #define LH2_MAX_BOUNCES 64                                   /* RenderCore_PrimeRef MAXPATHLENGTH (core_settings.h:25) */
-#define LH2_CURSOR_SLOTS (2 * LH2_MAX_BOUNCES + 5)           /* launches per frame: [L] bounce L, [64 + L] shadow after bounce L, [130] shadow, [131] side shadow, [132] primary (odd fused frames) */
-#define LH2_PRIMARY_ALT_SLOT (2 * LH2_MAX_BOUNCES + 4)       /* the camera fused into the primary packet launch: its heads alternate between slot 1 and this one */
+#define LH2_CURSOR_SLOTS (2 * LH2_MAX_BOUNCES + 5)           /* launches per frame: [L] bounce L, [64 + L] shadow after bounce L, [130] shadow, [131] side shadow, [132] unused */
 #define LH2_SHADOW_SLOT (2 * LH2_MAX_BOUNCES + 2)
 /* traversal stacks: LH2_STACK_LDS entries per lane in LDS (16 x 256 x 4 B = 16 KiB per block), the rest in global memory */
 #ifndef LH2_STACK_LDS
 #define LH2_STACK_LDS 16
 #endif
 #define LH2_STACK_TOTAL 96
+#define LH2_RAYLOG (LH2_MAX_BOUNCES + 8)   /* ray-count log words per frame parity (RenderCore::FrameRayLog) */
 /* bits of the scene error flag (SceneDev::sceneError; any bit set: the trace kernels exit and the host raises FatalError) */
 #define LH2_SCENE_ERR_DEPTH 1    /* BVH depth exceeds the traversal stack */
 #define LH2_SCENE_ERR_QRANGE 2   /* a BVH4 node beyond the quantized grid's range (k_quantize4) */

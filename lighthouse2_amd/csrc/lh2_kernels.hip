@@ -1535,6 +1535,7 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 	const uint32_t seg = blockIdx.x % LH2_SEGS;
 	uint32_t count, front, gap;
 	shade_segment( p, seg, count, front, gap );
+	if (*s.sceneError) count = 0;   /* the trace kernels refused the scene (they exited): no hit record is this frame's */
 	const uint32_t segBase = seg * p.segStride;
 	const uint32_t gstride = ((gridDim.x - seg + LH2_SEGS - 1) / LH2_SEGS) * 256u;
 	const int w = p.w, h = p.h;
@@ -1595,6 +1596,7 @@ __global__ __launch_bounds__( 256 ) void k_shade_last( const SceneDev s, const S
 	const uint32_t seg = blockIdx.x % LH2_SEGS;
 	uint32_t count, front, gap;
 	shade_segment( p, seg, count, front, gap );
+	if (*s.sceneError) count = 0;   /* the trace kernels refused the scene (they exited): no hit record is this frame's */
 	const uint32_t segBase = seg * p.segStride;
 	const uint32_t gstride = ((gridDim.x - seg + LH2_SEGS - 1) / LH2_SEGS) * 256u;
 	const uint32_t wh = (uint32_t)(p.w * p.h);
@@ -1710,6 +1712,7 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const 
 	const uint32_t seg = blockIdx.x % LH2_SEGS;
 	uint32_t count, front, gap;
 	shade_segment( p, seg, count, front, gap );
+	if (*s.sceneError) count = 0;   /* the trace kernels refused the scene (they exited): no hit record is this frame's */
 	const uint32_t segBase = seg * p.segStride;
 	const uint32_t gstride = ((gridDim.x - seg + LH2_SEGS - 1) / LH2_SEGS) * 256u;
 	const int w = p.w, h = p.h;
@@ -1875,7 +1878,7 @@ __global__ void k_counters_next( Counters* c, const BounceAdvance a, int pathLen
 }
 /* rm.rows > 0: only the rows a tile owns (a rank's bands, the k_pack_rows mapping): the other rows are
    other ranks' and are finalized where the frame is gathered */
-__global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale, const FrameStatsDev fs,
+__global__ void k_finalize( float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale, const FrameStatsDev fs,
 	const RowMap rm )
 {
 	const int i = threadIdx.x + blockIdx.x * blockDim.x;
@@ -1891,6 +1894,8 @@ __global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__
 			__hip_atomic_store( fs.hostRayCount + k, fs.rayLog[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
 		if (threadIdx.x == 0) __hip_atomic_store( fs.hostSceneError, *fs.sceneError, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
 	}
+	if (blockIdx.x == 0 && fs.zeroHeads)
+		for (int k = threadIdx.x; k < LH2_CURSOR_WORDS; k += blockDim.x) fs.zeroHeads[k] = 0;
 	if (i >= n) return;
 	int p = i;
 	if (rm.rows > 0)
@@ -1898,7 +1903,16 @@ __global__ void k_finalize( const float4* __restrict__ acc, float4* __restrict__
 		const int lr = i / rm.w, x = i % rm.w;
 		p = (rm.y0 + (lr / rm.band) * rm.bandStride + lr % rm.band) * rm.w + x;
 	}
-	const float4 a = acc[p];
+	float4 a = acc[p];
+	if (fs.delta)
+	{
+		/* early shade: this frame's first-vertex contributions join the accumulator now (the depth w: one addition per
+		   pixel per frame, as in frame order) */
+		const float4 d = fs.delta[p];
+		a = make_float4( a.x + d.x, a.y + d.y, a.z + d.z, a.w + d.w );
+		acc[p] = a;
+		fs.delta[p] = make_float4( 0, 0, 0, 0 );
+	}
 	out[p] = make_float4( a.x * scale, a.y * scale, a.z * scale, a.w * scale );
 }
 
@@ -2071,7 +2085,7 @@ void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int 
 	LH2_LAUNCH( k_unpack_rows, (rows * w + 255) / 256, 256, st, ev, src, acc, w, y0, band, bandStride, rows );
 }
 void lh2_launch_spin( unsigned long long ticks, hipStream_t st ) { hipLaunchKernelGGL( k_spin, dim3( 1 ), dim3( 64 ), 0, st, ticks ); }
-void lh2_launch_finalize( const float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st, const RowMap* rm )
+void lh2_launch_finalize( float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st, const RowMap* rm )
 {
 	const FrameStatsDev none{};
 	const RowMap all{};

@@ -118,11 +118,12 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	blocksPerCU = maxBlocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
 	packetBlocksPerCU = std::max( 1, std::min( 8, lh2_packet_blocks_per_cu() ) );
 	pathBlocksPerCU = std::max( 1, std::min( 8, lh2_path_blocks_per_cu() ) );
-	ps.counters.resize( 1 );
-	ps.cursors.resize( (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
-	CHK_HIP( hipMemsetAsync( ps.cursors.ptr, 0, sizeof( uint32_t ) * (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, stream ) );
-	ps.rayLog.resize( LH2_MAX_BOUNCES + 8 );
-	CHK_HIP( hipMemsetAsync( ps.rayLog.ptr, 0, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), stream ) );
+	ps.counters.resize( 2 );
+	CHK_HIP( hipMemsetAsync( ps.counters.ptr, 0, sizeof( Counters ) * 2, stream ) );
+	ps.cursors.resize( 2 * (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
+	CHK_HIP( hipMemsetAsync( ps.cursors.ptr, 0, sizeof( uint32_t ) * 2 * (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, stream ) );
+	ps.rayLog.resize( 2 * LH2_RAYLOG );
+	CHK_HIP( hipMemsetAsync( ps.rayLog.ptr, 0, sizeof( uint32_t ) * 2 * LH2_RAYLOG, stream ) );
 	/* indexed by pathLength; written by advance_bounce (system scope) */
 	CHK_HIP( hipHostMalloc( (void**)&ps.activeLog, sizeof( uint32_t ) * (LH2_MAX_BOUNCES + 8), hipHostMallocCoherent ) );
 	for (auto& e : ps.evTrace) CHK_HIP( hipEventCreate( &e ) );
@@ -132,14 +133,15 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipEventCreate( &ps.evCamera ) );
 	CHK_HIP( hipEventCreate( &ps.evShadow ) );
 	CHK_HIP( hipEventCreate( &ps.evSide ) );
-	ps.shSnap.resize( LH2_SEGS * LH2_SEGCOUNT_STRIDE );
+	ps.shSnap.resize( 2 * LH2_SEGS * LH2_SEGCOUNT_STRIDE );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evStage) CHK_HIP( hipEventCreateWithFlags( &e, hipEventDisableTiming ) );
-	dSceneError.resize( 1 ), dTlasDepth.resize( 1 );
+	dSceneError.resize( 1 ), dTlasDepth.resize( 1 ), dBlasQError.resize( 1 );
 	CHK_HIP( hipMemsetAsync( dSceneError.ptr, 0, sizeof( int ), stream ) );
 	CHK_HIP( hipMemsetAsync( dTlasDepth.ptr, 0, sizeof( int ), stream ) );
+	CHK_HIP( hipMemsetAsync( dBlasQError.ptr, 0, sizeof( int ), stream ) );
 	dInstDesc.resize( 1 );   /* shading reads record 0 for a miss (HitInstance): it always exists */
 	CHK_HIP( hipMemsetAsync( dInstDesc.ptr, 0, sizeof( lh2_CoreInstanceDesc ), stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -154,6 +156,7 @@ void RenderCore::SetTarget( uint32_t w, uint32_t h, uint32_t spp )  /* rendercor
 	sceneVersion++;
 	EnsureBuffers();
 	CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)w * h, stream ) );
+	CHK_HIP( hipMemsetAsync( delta.ptr, 0, sizeof( float4 ) * (size_t)w * h, stream ) );
 	samplesTaken = 0;
 }
 
@@ -190,6 +193,7 @@ void RenderCore::EnsureBuffers()
 {
 	accumulator.resize( (size_t)scrwidth * scrheight );
 	frame.resize( (size_t)scrwidth * scrheight );
+	delta.resize( (size_t)scrwidth * scrheight );
 }
 
 /* path buffers for `paths` paths (a bit extra, as the reference reserves, and room for LH2_SEGS segments
@@ -203,8 +207,10 @@ void RenderCore::EnsurePaths( uint32_t paths )
 		ps.hits.resize( ps.cap );
 		ps.rayOP.resize( ps.cap ), ps.rayDP.resize( ps.cap ), ps.T4P.resize( ps.cap ), ps.Q4P.resize( ps.cap ), ps.hitsP.resize( ps.cap );
 		ps.relaid = true;
-		ps.shO.resize( 2 * ps.cap ), ps.shD.resize( 2 * ps.cap ), ps.shP.resize( 2 * ps.cap );
-		ps.shMask.resize( (2 * ps.cap + 63) / 32 + 2 );
+		/* shadow rays: 2 per path, per frame parity */
+		ps.shCap = 2 * ps.cap, ps.shMaskWords = (ps.shCap + 63) / 32 + 2;
+		ps.shO.resize( 2 * ps.shCap ), ps.shD.resize( 2 * ps.shCap ), ps.shP.resize( 2 * ps.shCap );
+		ps.shMask.resize( 2 * ps.shMaskWords );
 	}
 	EnsureStack();
 }
@@ -250,6 +256,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "shadowOverlap" )) shadowOverlap = value != 0;
 	else if (!strcmp( name, "cameraFused" )) cameraFused = value != 0;
 	else if (!strcmp( name, "frameOverlap" )) frameOverlap = (int)value;
+	else if (!strcmp( name, "earlyShade" )) earlyShade = value != 0;
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
@@ -274,7 +281,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -568,6 +575,11 @@ void RenderCore::ConcatenateBlas( int ni )
 		FatalError( "BVH4 of %zu nodes exceeds the 2 GiB the traversal addresses", (size_t)node4Total + tlasCapacity );
 	if (bvh4) dNodes4.resize( ((size_t)node4Total + tlasCapacity) * 8 ), dNodes4q.resize( ((size_t)node4Total + tlasCapacity) * 4 );
 	dTris.resize( (size_t)std::max( triTotal, 1 ) * 3 );
+	/* the TLAS region starts as NaN boxes: a TLAS of fewer nodes than the capacity leaves no uninitialised (possibly huge,
+	   finite) boxes behind it for the quantizer's range check (k_quantize4) */
+	CHK_HIP( hipMemsetAsync( dNodes.ptr + (size_t)nodeTotal * 4, 0xff, sizeof( float4 ) * 4 * (size_t)tlasCapacity, stream ) );
+	dBlasQError.resize( 1 );
+	CHK_HIP( hipMemsetAsync( dBlasQError.ptr, 0, sizeof( int ), stream ) );
 	for (size_t mi = 0; mi < meshes.size(); mi++)
 	{
 		const CoreMeshHost& m = *meshes[mi];
@@ -575,7 +587,7 @@ void RenderCore::ConcatenateBlas( int ni )
 		if (bvh4) GpuBvhBuilder::Relocate4( m.bvh4Nodes.ptr, m.node4Count, meshNode4Base[mi], (uint32_t)meshTriBase[mi], dNodes4.ptr, stream );
 		if (m.leafTris) CHK_HIP( hipMemcpyAsync( dTris.ptr + (size_t)meshTriBase[mi] * 3, m.bvhTris.ptr, sizeof( float4 ) * 3 * (size_t)m.leafTris, hipMemcpyDeviceToDevice, stream ) );
 	}
-	if (bvh4) GpuBvhBuilder::Quantize4( dNodes4.ptr, 0, node4Total, dNodes4q.ptr, dSceneError.ptr, stream );
+	if (bvh4) GpuBvhBuilder::Quantize4( dNodes4.ptr, 0, node4Total, dNodes4q.ptr, dBlasQError.ptr, stream );
 	dMeshBounds.upload( bounds.data(), bounds.size(), stream );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	blasNodeCount = nodeTotal, blasTriCount = triTotal, blasNode4Count = node4Total, blasMeshTris = meshTris;
@@ -654,7 +666,8 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 	dSceneError.resize( 1 ), dTlasDepth.resize( 1 );
 	CHK_HIP( hipMemcpyAsync( dInst.ptr, di, nRec * sizeof( DevInstance ), hipMemcpyHostToDevice, stream ) );
 	CHK_HIP( hipMemcpyAsync( dInstDesc.ptr, desc, nRec * sizeof( lh2_CoreInstanceDesc ), hipMemcpyHostToDevice, stream ) );
-	CHK_HIP( hipMemsetAsync( dSceneError.ptr, 0, sizeof( int ), stream ) );
+	/* the scene error starts as the BLAS quantizer's (ConcatenateBlas), the TLAS checks add to it */
+	CHK_HIP( hipMemcpyAsync( dSceneError.ptr, dBlasQError.ptr, sizeof( int ), hipMemcpyDeviceToDevice, stream ) );
 	if (ni >= 2 && gpuTlas)
 	{
 		/* TLAS built on the device from the instance transforms (bvh_gpu.h) */
@@ -806,9 +819,18 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	   segments of shadowStride */
 	ps.count = pathCount;
 	ps.segStride = (pathCount + LH2_SEGS - 1) / LH2_SEGS;
-	ps.shadowStride = (uint32_t)(ps.shO.count / LH2_SEGS);
-	ps.in = 0, ps.pl = 0, ps.tailL = 0;
-	Counters* const c = ps.counters.ptr;
+	ps.shadowStride = (uint32_t)(ps.shCap / LH2_SEGS);
+	ps.pl = 0, ps.tailL = 0;
+	/* this frame's parity: its counters, work-queue heads, shadow stream and ray-count log (PathStreams) */
+	ps.fp ^= 1;
+	Counters* const c = FrameCounters();
+	uint32_t* const cursors = FrameCursors();
+	uint32_t* const rayLog = FrameRayLog();
+	float4* const shO = ps.shO.ptr + (size_t)ps.fp * ps.shCap;
+	float4* const shD = ps.shD.ptr + (size_t)ps.fp * ps.shCap;
+	float4* const shP = ps.shP.ptr + (size_t)ps.fp * ps.shCap;
+	uint32_t* const shMask = ps.shMask.ptr + (size_t)ps.fp * ps.shMaskWords;
+	uint32_t* const shSnap = ps.shSnap.ptr + (size_t)ps.fp * LH2_SEGS * LH2_SEGCOUNT_STRIDE;
 	/* primary rays (camera.h) for every sample of the tile; the camera launch also resets the frame's
 	   counters and work-queue heads (k_init_counters) */
 	CameraParams cp{};
@@ -822,7 +844,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	cp.band = tileBand > 0 ? tileBand : std::max( 1, tileRows ), cp.bandStride = tileBand > 0 ? tileStride : std::max( 1, tileRows );
 	cp.tiled = tiledRays;
 	cp.primeRef = primeRef;
-	cp.initC = c, cp.cursors = ps.cursors.ptr, cp.cursorWords = LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS;
+	cp.initC = c, cp.cursors = cursors, cp.cursorWords = LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS;
 	cp.pathCount = pathCount, cp.segStride = ps.segStride;
 	cp.clearAcc = restart && !tileChanged ? accumulator.ptr : nullptr;
 	/* heavy-first primary packets: this frame reads the block the previous one recorded, and records into the
@@ -841,29 +863,32 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		cp.hvZero = ps.hv.ptr + (size_t)(1 - ps.hvParity) * ps.hvBlock, cp.hvZeroWords = LH2_HV_MASK + ps.hvMaskWords;
 	}
 	const int grid = TraceGrid();
-	/* the camera fused into the primary packet launch: this frame's heads are slot 1 or LH2_PRIMARY_ALT_SLOT; the
-	   heavy-packet block it records into must be zero (the previous fused frame's first shade launch zeroed it) */
+	/* the camera fused into the primary packet launch: the heavy-packet block it records into must be zero (the previous
+	   fused frame's first shade launch zeroed it) */
 	const bool fusedCam = cameraFused && tiledRays && UsePackets() && !primeRef;
 	/* the fused primary launch beside the previous frame (frame overlap), or behind it on the core stream: on a restart
 	   (the launch zeroes accumulator pixels), after a change of scene data, buffers or tile, or when the previous frame
 	   had no fused primary launch */
 	const bool serialize = !frameOverlap || restart || !ps.lastFused || ps.relaid || tileChanged || sceneVersion != ps.lastSceneVersion;
 	hipStream_t primStream = stream;
-	const uint32_t primSlot = fusedCam && ps.primParity ? LH2_PRIMARY_ALT_SLOT : 1u;
+	/* the primary launch's work-queue heads: slot 1 of the frame parity's block, zeroed by the finalize of the frame before
+	   the previous one (FrameStatsDev::zeroHeads) */
+	const uint32_t primSlot = 1u;
 	if (fusedCam)
 	{
 		/* beside the previous frame (on the ahead stream, after the previous frame's shade launch before its path tail, or
 		   its first without one: the last reader of the primary buffers and of the heavy-packet block this frame records
-		   into), the frame's resets are a k_init_counters launch on the core stream (behind the previous frame); behind
-		   it, on the core stream, the primary launch does them itself.  Its own work-queue heads are left alone: they
-		   alternate between two slots, and the resets zero the other */
+		   into), the frame's resets are a k_init_counters launch before it on the ahead stream (this frame's parity: the
+		   frame before the previous one, the last user of these counters and heads, is done); behind it, on the core
+		   stream, the primary launch does them itself.  Its own work-queue heads are left alone: they alternate between
+		   two slots, and the resets zero the other */
 		primStream = serialize ? stream : aheadStream;
 		cp.keepCursor = (int)(primSlot * LH2_CURSOR_WORDS);
 		if (serialize) cp.initC = c;
 		else
 		{
-			lh2_launch_init_counters( c, pathCount, ps.segStride, ps.cursors.ptr, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, {}, stream, cp.keepCursor );
 			CHK_HIP( hipStreamWaitEvent( aheadStream, ps.overlapEv, 0 ) );
+			lh2_launch_init_counters( c, pathCount, ps.segStride, cursors, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, {}, aheadStream, -LH2_CURSOR_WORDS );
 			cp.initC = nullptr;
 		}
 		if (ps.hvOn && !ps.hvNextZeroed) CHK_HIP( hipMemsetAsync( cp.hvZero, 0, sizeof( uint32_t ) * cp.hvZeroWords, primStream ) );
@@ -871,6 +896,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ps.relaid = false;
 	}
 	ps.hvNextZeroed = false;
+	/* early shade: the first shade launch follows the primary launch on the ahead stream and writes the ping-pong buffer
+	   the previous frame's launches after its overlap event do not use (PathStreams::busy / earlyOk) */
+	const bool early = fusedCam && !serialize && earlyShade && frameOverlap == 1 && ps.earlyOk;
+	ps.early = early;
+	ps.in = early ? ps.busy : 0;
+	ps.earlyOk = false;
 	uint32_t* hvReadBlock = nullptr;
 	int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
 	/* no specular event and no alpha cut-out in any material: every path ends at its second vertex,
@@ -910,7 +941,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		TraceArgs ta{};
 		ta.version = TraceVersion();
 		ta.rayO = ps.rayO[ps.in].ptr, ta.rayD = ps.rayD[ps.in].ptr, ta.segCounts = segIn, ta.segStride = ps.segStride, ta.segBack = segInBack;
-		ta.cursor = ps.cursors.ptr + (size_t)(pathLength == 1 ? primSlot : (uint32_t)pathLength) * LH2_CURSOR_WORDS;
+		ta.cursor = cursors + (size_t)(pathLength == 1 ? primSlot : (uint32_t)pathLength) * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)(primary ? refillPrimary : refillOther);
 		ta.packet = primary && UsePackets() ? 1 : 0;
 		ta.leafBatch = (uint32_t)(primary ? leafBatchPrimary : leafBatch);
@@ -932,7 +963,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		}
 		ShadeParams sp{};
 		sp.shadowStride = ps.shadowStride;
-		sp.shO = ps.shO.ptr, sp.shD = ps.shD.ptr, sp.shP = ps.shP.ptr;
+		sp.shO = shO, sp.shD = shD, sp.shP = shP;
 		sp.acc = accumulator.ptr, sp.counters = c;
 		sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
 		sp.probePixel = probeX + scrwidth * probeY;
@@ -943,7 +974,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			   updated in place, its shadow rays queued for the shadow launch, and rayLog counted */
 			sp.rayO = ps.rayO[ps.in].ptr, sp.rayD = ps.rayD[ps.in].ptr, sp.T4 = ps.T4[ps.in].ptr, sp.Q4 = ps.Q4[ps.in].ptr;
 			sp.rayOut = ps.rayO[ps.in].ptr, sp.rayDOut = ps.rayD[ps.in].ptr, sp.T4Out = ps.T4[ps.in].ptr, sp.Q4Out = ps.Q4[ps.in].ptr;
-			sp.adv.rayCountLog = ps.rayLog.ptr;
+			sp.adv.rayCountLog = rayLog;
 			ta.shadeBatch = (uint32_t)pathTailBatch;
 			/* with the overlap the path tail runs fewer blocks per CU (pathTailBlocks, default 2) and leaves
 			   registers for the side launch's waves */
@@ -957,10 +988,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				CHK_HIP( hipStreamWaitEvent( sideStream, ps.prevStop, 0 ) );
 				TraceArgs ts{};
 				ts.version = TraceVersion();
-				ts.rayO = ps.shO.ptr, ts.rayD = ps.shD.ptr, ts.segCounts = ps.shSnap.ptr, ts.segStride = ps.shadowStride;
-				ts.cursor = ps.cursors.ptr + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS;
+				ts.rayO = shO, ts.rayD = shD, ts.segCounts = shSnap, ts.segStride = ps.shadowStride;
+				ts.cursor = cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS;
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
-				ts.mask = ps.shMask.ptr, ts.potentials = ps.shP.ptr, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
+				ts.mask = shMask, ts.potentials = shP, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
 				lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, ps.evSide }, sideStream );
 				ps.fromSide = ps.prevStop;
 				ps.sideOn = true;
@@ -974,8 +1005,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			/* the paths are dense (camera order): fixed counts, no segment counters; the core stream waits for it */
 			ta.segCounts = nullptr, ta.segBack = nullptr, ta.countFixed = pathCount;
 			lh2_launch_trace_primary( &sd, &ta, &cp, ps.T4P.ptr, ps.Q4P.ptr, PacketGrid(), { nullptr, ps.evTrace[pathLength] }, primStream );
-			if (primStream != stream) CHK_HIP( hipStreamWaitEvent( stream, ps.evTrace[pathLength], 0 ) );
-			ps.primParity ^= 1;
+			if (primStream != stream && !early) CHK_HIP( hipStreamWaitEvent( stream, ps.evTrace[pathLength], 0 ) );
 		}
 		else
 		{
@@ -999,8 +1029,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		/* the hand-off to the next bounce: the shade launch's last block (no launch of its own), except
 		   in PrimeRef mode, where the bounce's shadow rays are traced (and their counts reset) first */
 		const bool snap = overlap && pathLength + 1 == tailL;
-		const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, ps.rayLog.ptr, ps.activeLog, pathLength + 1 == tailL,
-			snap ? ps.shSnap.ptr : nullptr, snap ? ps.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr };
+		const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, rayLog, ps.activeLog, pathLength + 1 == tailL,
+			snap ? shSnap : nullptr, snap ? cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr };
 		snapped = snapped || snap;
 		sp.advance = pathLength < maxPL && !primeRef;
 		sp.adv = adv;
@@ -1016,12 +1046,22 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			sp.hvZero = hvReadBlock, sp.hvZeroWords = LH2_HV_MASK + ps.hvMaskWords;
 			ps.hvNextZeroed = true;
 		}
-		lh2_launch_shade( &sd, &sp, grid, { nullptr, ps.evShade[pathLength] }, stream );
+		const bool earlyHere = early && pathLength == 1;
+		if (earlyHere) sp.acc = delta.ptr;   /* the previous frame's finalize may not have read the accumulator yet */
+		lh2_launch_shade( &sd, &sp, grid, { nullptr, ps.evShade[pathLength] }, earlyHere ? aheadStream : stream );
+		if (earlyHere) CHK_HIP( hipStreamWaitEvent( stream, ps.evShade[pathLength], 0 ) );
 		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];
 		/* the next frame's primary launch starts after this frame's first shade launch (the last reader of the primary
 		   buffers), or (frameOverlap 1) after the shade launch before the path tail: beside the latency-bound tail */
-		if (pathLength == 1 || (frameOverlap == 1 && tailL && pathLength == tailL - 1)) ps.overlapEv = ps.evShade[pathLength],
+		if (pathLength == 1 || (frameOverlap == 1 && tailL && pathLength == tailL - 1))
+		{
+			ps.overlapEv = ps.evShade[pathLength];
 			besideNext = !serialize && fusedCam && !(frameOverlap == 1 && tailL && pathLength + 1 < tailL);   /* the final overlapEv */
+			/* after this launch only the path tail (in place) or the last bounce (no extension rays) runs: both use the
+			   buffer this launch writes, 1 - ps.in */
+			ps.busy = 1 - ps.in;
+			ps.earlyOk = (tailL && pathLength == tailL - 1) || (!tailL && pathLength == 1 && maxPL == 2);
+		}
 
 		if (pathLength == maxPL) break;
 		if (primeRef && shadows)
@@ -1030,10 +1070,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			   connect step), fused with finalizeConnections */
 			TraceArgs ts{};
 			ts.version = TraceVersion();
-			ts.rayO = ps.shO.ptr, ts.rayD = ps.shD.ptr, ts.segCounts = c->segShadow, ts.segStride = ps.shadowStride;
-			ts.cursor = ps.cursors.ptr + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
+			ts.rayO = shO, ts.rayD = shD, ts.segCounts = c->segShadow, ts.segStride = ps.shadowStride;
+			ts.cursor = cursors + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
 			ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
-			ts.mask = ps.shMask.ptr, ts.potentials = ps.shP.ptr, ts.acc = accumulator.ptr, ts.gstack = ps.gstack.ptr;
+			ts.mask = shMask, ts.potentials = shP, ts.acc = accumulator.ptr, ts.gstack = ps.gstack.ptr;
 			lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, ps.evShadowB[pathLength] }, stream );
 			ps.fromShadowB[pathLength] = ps.prevStop, ps.prevStop = ps.evShadowB[pathLength];
 		}
@@ -1056,15 +1096,15 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	/* a snapshot whose side launch did not happen (the frame ended before its path tail): the final launch
 	   traces every shadow ray, from the first */
 	if (snapped && !ps.sideOn)
-		CHK_HIP( hipMemsetAsync( ps.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
+		CHK_HIP( hipMemsetAsync( cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
 	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
 	if (!primeRef && shadows)
 	{
 		TraceArgs ta{};
 		ta.version = TraceVersion();
-		ta.rayO = ps.shO.ptr, ta.rayD = ps.shD.ptr, ta.segCounts = c->segShadow, ta.segStride = ps.shadowStride;
-		ta.cursor = ps.cursors.ptr + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
-		ta.mask = ps.shMask.ptr, ta.potentials = ps.shP.ptr, ta.acc = accumulator.ptr, ta.gstack = ps.gstack.ptr;
+		ta.rayO = shO, ta.rayD = shD, ta.segCounts = c->segShadow, ta.segStride = ps.shadowStride;
+		ta.cursor = cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
+		ta.mask = shMask, ta.potentials = shP, ta.acc = accumulator.ptr, ta.gstack = ps.gstack.ptr;
 		lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, ps.evShadow }, stream );
 		ps.fromShadow = ps.prevStop;
 	}
@@ -1072,7 +1112,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	if (ps.sideOn) CHK_HIP( hipStreamWaitEvent( stream, ps.evSide, 0 ) );
 	samplesTaken += scrspp;
 	/* finalize also delivers the frame's counters and ray-count log, and the scene error, to hostStats */
-	const FrameStatsDev fs{ c, ps.rayLog.ptr + 1, &hostStats->counters, hostStats->rayCount + 1, dSceneError.ptr, &hostStats->sceneError };
+	const FrameStatsDev fs{ c, rayLog + 1, &hostStats->counters, hostStats->rayCount + 1, dSceneError.ptr, &hostStats->sceneError,
+		cursors + (size_t)primSlot * LH2_CURSOR_WORDS, early ? delta.ptr : nullptr };
 	/* a tile finalizes its own rows only (a rank of the band partition: the gathered frame is finalized
 	   where it is assembled, MultiDevice / FinalizeFrame) */
 	RowMap rm{};
@@ -1159,7 +1200,18 @@ void RenderCore::Synchronize()
 	const uint32_t* rc = hostStats->rayCount;   /* rc[0] = primary; rc[L] = rays traced at pathLength L+1 */
 	auto ms = [&]( hipEvent_t a, hipEvent_t b ) { float t = 0; (void)hipEventElapsedTime( &t, a, b ); return t * 1e-3f; };
 	/* each interval: the previous launch's stop event -> this launch's stop event (kernel + launch gap) */
-	auto trace = [&]( int L ) { return L <= ps.pl ? ms( ps.fromTrace[L], ps.evTrace[L] ) : 0.0f; };
+	auto trace = [&]( int L ) {
+		if (L > ps.pl) return 0.0f;
+		float t = ms( ps.fromTrace[L], ps.evTrace[L] );
+		/* early shade: the second bounce's interval starts at the first shade launch's stop (ahead stream); the part
+		   before the previous frame's end is the previous frame's */
+		if (L == 2 && ps.early && prevFrameEndValid)
+		{
+			const float shared = ms( ps.fromTrace[L], evFrame[2] );
+			if (shared > 0) t = std::max( 0.0f, t - shared );
+		}
+		return t;
+	};
 	coreStats.primaryRayCount = rc[0];
 	coreStats.traceTime0 = trace( 1 );
 	coreStats.bounce1RayCount = framePathLengths >= 2 ? rc[1] : 0;
@@ -1215,7 +1267,7 @@ int RenderCore::DebugShadowRays( float* o4, float* d4, float* p4, int cap )
 		const uint32_t cnt = std::min( hostStats->counters.segShadow[k * LH2_SEGCOUNT_STRIDE], ps.shadowStride );
 		const int m = std::min( (int)cnt, cap - n );
 		if (m <= 0) break;
-		const size_t at = (size_t)k * ps.shadowStride;
+		const size_t at = (size_t)ps.fp * ps.shCap + (size_t)k * ps.shadowStride;   /* the last frame's parity */
 		CHK_HIP( hipMemcpy( o4 + 4 * (size_t)n, ps.shO.ptr + at, 16 * (size_t)m, hipMemcpyDeviceToHost ) );
 		CHK_HIP( hipMemcpy( d4 + 4 * (size_t)n, ps.shD.ptr + at, 16 * (size_t)m, hipMemcpyDeviceToHost ) );
 		CHK_HIP( hipMemcpy( p4 + 4 * (size_t)n, ps.shP.ptr + at, 16 * (size_t)m, hipMemcpyDeviceToHost ) );

@@ -72,14 +72,17 @@ struct PathStreams
 	   frame's later bounces */
 	DevBuf<float4> rayOP, rayDP, T4P, Q4P;
 	DevBuf<uint4> hitsP;
-	DevBuf<float4> shO, shD, shP;
-	DevBuf<uint32_t> shMask;
+	DevBuf<float4> shO, shD, shP;        /* 2 x shCap (frame parity) */
+	DevBuf<uint32_t> shMask;             /* 2 x shMaskWords */
+	size_t shCap = 0, shMaskWords = 0;
 	DevBuf<int> gstack;
 	DevBuf<int> sideStack;               /* the side shadow launch's global stack (shadowOverlap) */
-	DevBuf<uint32_t> shSnap;             /* the shadow rays queued before the path tail, per segment (advance_bounce) */
-	DevBuf<Counters> counters;
-	DevBuf<uint32_t> cursors;            /* LH2_CURSOR_SLOTS x LH2_CURSOR_WORDS work-queue heads */
-	DevBuf<uint32_t> rayLog;
+	DevBuf<uint32_t> shSnap;             /* the shadow rays queued before the path tail, per segment (advance_bounce); 2 (parity) */
+	/* per frame parity (fp): two consecutive frames' counters, work-queue heads, shadow streams and ray-count logs are
+	   apart, so the next frame's first launches can run beside this frame's last ones (frame overlap, early shade) */
+	DevBuf<Counters> counters;           /* 2 */
+	DevBuf<uint32_t> cursors;            /* 2 x LH2_CURSOR_SLOTS x LH2_CURSOR_WORDS work-queue heads */
+	DevBuf<uint32_t> rayLog;             /* 2 x LH2_RAYLOG */
 	DevBuf<uint32_t> hv;                 /* heavy-first packets: two blocks (TraceArgs::hvRead / hvWrite), the frame parity picks */
 	uint32_t hvCap = 0, hvMaskWords = 0, hvBlock = 0, hvParity = 0;
 	uint32_t* activeLog = nullptr;       /* pinned: extension rays after each bounce (advance_bounce) */
@@ -96,10 +99,8 @@ struct PathStreams
 	int in = 0, pl = 0;
 	int tailL = 0;                       /* this frame's path-tail launch (pathLength), 0: none */
 	bool hvOn = false;                   /* this frame's primary packets run heavy-first (TraceArgs::hvRead) */
-	/* the camera fused into the primary packet launch (setting "cameraFused"): the launch's work-queue heads alternate
-	   between slot 1 and LH2_PRIMARY_ALT_SLOT (each launch zeroes the other), and the heavy-packet block the next frame
+	/* the camera fused into the primary packet launch (setting "cameraFused"): the heavy-packet block the next frame
 	   records into is zeroed by the frame's first shade launch (hvNextZeroed: it was) */
-	int primParity = 0;
 	bool hvNextZeroed = false;
 	/* frame overlap (setting "frameOverlap"): the primary launch of a fused frame runs on the ahead stream after the
 	   previous frame's first shade launch, unless something since then needs it to wait for the whole previous frame */
@@ -107,6 +108,12 @@ struct PathStreams
 	uint64_t lastSceneVersion = 0;
 	hipEvent_t overlapEv = nullptr;      /* the last frame's shade launch the next primary launch waits for (not owned) */
 	hipEvent_t prevStop = nullptr;
+	int fp = 0;                          /* this (the last) frame's parity */
+	/* early shade (setting "earlyShade"): the next frame's first shade launch also runs beside this frame's launches
+	   after overlapEv.  Those use one ping-pong buffer (busy: the path tail's, or the last bounce's rays) and write
+	   neither (earlyOk), so the next frame's first shade writes the other one */
+	int busy = 0;
+	bool earlyOk = false, early = false;
 };
 
 struct FrameStats   /* per-frame values delivered by k_finalize into pinned host memory */
@@ -187,6 +194,9 @@ private:
 	void CheckSceneError();
 	bool UsePackets() const;
 	SceneDev MakeSceneDev() const;
+	Counters* FrameCounters() const { return ps.counters.ptr + ps.fp; }
+	uint32_t* FrameCursors() const { return ps.cursors.ptr + (size_t)ps.fp * LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS; }
+	uint32_t* FrameRayLog() const { return ps.rayLog.ptr + (size_t)ps.fp * LH2_RAYLOG; }
 	TraceArgs StreamArgs( const float4* o, const float4* d, const uint32_t* segCounts, uint32_t segStride, uint32_t* cursor, bool coherent ) const;
 	int TraceGrid() const { return smCount * blocksPerCU; }
 	int PacketGrid() const { return smCount * packetBlocksPerCU; }   /* packet kernel: its own occupancy */
@@ -215,6 +225,7 @@ private:
 	DevBuf<float> dInstT;                /* 16 per instance */
 	DevBuf<int> dInstMesh;
 	DevBuf<int> dSceneError, dTlasDepth;
+	DevBuf<int> dBlasQError;             /* the BLAS quantizer's range flag (LH2_SCENE_ERR_QRANGE), copied into dSceneError per TLAS update */
 	uint8_t* stage[2] = {};              /* pinned staging of UpdateToplevel (double-buffered) */
 	size_t stageBytes[2] = {};
 	hipEvent_t evStage[2] = {};
@@ -240,6 +251,7 @@ private:
 	int scrwidth = 0, scrheight = 0, scrspp = 1;
 	int tileY0 = 0, tileY1 = -1, tileBand = 0, tileStride = 0;
 	DevBuf<float4> accumulator, frame;
+	DevBuf<float4> delta;                /* early shade: the first shade launch's accumulator additions (FrameStatsDev::delta) */
 	PathStreams ps;                      /* on `stream`; also serves the unit-level trace calls */
 	bool tileChanged = false;            /* the next restart clears the whole accumulator, not only the tile's pixels */
 	bool frameShadows = true;            /* the last frame queued shadow-ray launches (the scene has lights) */
@@ -254,6 +266,11 @@ private:
 	/* a fused frame's primary launch beside the previous frame's later bounces (aheadStream): 1, after its shade launch
 	   before the path tail (its first without one); 2, after its first shade launch; 0: off */
 	int frameOverlap = 1;
+	/* with frameOverlap 1: the next frame's first shade launch follows its primary launch on the ahead stream, beside this
+	   frame's path tail and shadow launches, instead of after them on the core stream (frames whose later launches use one
+	   ping-pong buffer: PathStreams::earlyOk).  Accumulator additions of the two frames then interleave: the sum matches
+	   the sequential one within float rounding, not bit for bit (the first-vertex depths, w, stay exact) */
+	int earlyShade = 1;
 	uint64_t sceneVersion = 0;           /* incremented by every change of device-resident scene data or buffers */
 	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle; BLAS leaves parked until this many
 	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,

@@ -64,9 +64,12 @@ def xorshift_uints(seed: int, n: int, log2b: int = 14) -> np.ndarray:
     out = np.empty(n, np.uint32)
     s = seed & _MASK
     first = min(n, B)
-    for i in range(first):
-        s = _step(s)
-        out[i] = s
+    if log2b > 6 and first > 64:
+        out[:first] = xorshift_uints(seed, first, 6)   # the first block by jumps of 64 (a Python loop of 64 steps)
+    else:
+        for i in range(first):
+            s = _step(s)
+            out[i] = s
     if n <= B:
         return out
     tab = _jump_tables(log2b)

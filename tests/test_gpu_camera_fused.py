@@ -1,10 +1,12 @@
 """GPU parity of the camera fused into the primary packet launch (setting cameraFused, k_trace_primary_packet) and
 of the frame overlap (setting frameOverlap).  The packet launch makes each path's primary ray itself (camera.h:39-111,
 the code of k_camera) into primary buffers of its own, and runs on the core's ahead stream: beside the previous
-frame's later bounces once that frame's first shade launch is done, or behind the whole previous frame after a
-restart or a scene change.  Its work-queue heads alternate between two slots from frame to frame; the frame's resets
-are a k_init_counters launch on the core stream; the heavy-packet block the next frame records into is zeroed by the
-first shade launch.
+frame's later bounces once that frame's shade launch before its path tail (or its first) is done, or behind the whole
+previous frame after a restart or a scene change.  Consecutive frames use counters, work-queue heads and shadow streams of
+their own parity; the frame's resets are a k_init_counters launch before the primary launch on the ahead stream; the
+heavy-packet block the next frame records into is zeroed by the first shade launch.  With earlyShade (default) the
+frame's first shade launch follows its primary launch on the ahead stream too, beside the previous frame's path tail
+and shadow launches.
 
 Against the CPU oracle (pathtracer.h:54-245 after generateEyeRays): identical per-bounce ray counts every frame,
 accumulator rel-L2 <= 1e-4; and frames queued back to back (no host synchronisation between them, so the primary
@@ -59,6 +61,7 @@ def test_camera_fused_frames(fresh_core, kind):
     for tgt in (fresh_core, o):
         tgt.setting("maxPathLength", depth)
     assert fresh_core.get_setting("cameraFused") == 1 and fresh_core.get_setting("frameOverlap") == 1
+    assert fresh_core.get_setting("earlyShade") == 1
     # per-frame ray counts against the oracle (synchronised after every frame)
     for f, conv in enumerate(SEQUENCE):
         if anim:
@@ -68,17 +71,19 @@ def test_camera_fused_frames(fresh_core, kind):
         assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (f, fresh_core.ray_counts()[:6], o.ray_counts()[:6])
     ref = o.accumulator()
     res = {}
-    for fused, overlap in ((1, 1), (1, 0), (0, 0)):
+    for fused, overlap, early in ((1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 0, 0)):
         fresh_core.setting("cameraFused", fused)
         fresh_core.setting("frameOverlap", overlap)
+        fresh_core.setting("earlyShade", early)
         for f, conv in enumerate(SEQUENCE):   # queued back to back: no synchronisation between frames
             if anim:
                 _animate(sc, fresh_core, f)
             sc.render_frame(fresh_core, converge=conv)
-        res[(fused, overlap)] = fresh_core.accumulator()
-    a = res[(1, 1)]
+        res[(fused, overlap, early)] = fresh_core.accumulator()
+        assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (fused, overlap, early)
+    a = res[(1, 1, 1)]
     assert rel_l2(a[..., :3], ref[..., :3]) <= REL_L2_TOL
-    for k in ((1, 0), (0, 0)):
+    for k in ((1, 1, 0), (1, 0, 0), (0, 0, 0)):
         assert rel_l2(a[..., :3], res[k][..., :3]) <= 1e-6, k
         # the first-vertex distances (w): one addition per pixel per frame, in frame order: bit-identical
         assert np.array_equal(a[..., 3], res[k][..., 3]), k

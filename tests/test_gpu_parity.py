@@ -562,3 +562,20 @@ def test_quantized_nodes_hold_the_f32_boxes(fresh_core):
     assert np.all(refq[~valid] == np.iinfo(np.int32).min)
     # the grid is fine where the boxes are: a valid child's quantized box is at most 2 grid steps wider per side
     assert np.all((lo - dlo)[v3] <= 2 * np.broadcast_to(step[:, :, None], lo.shape)[v3])
+
+
+def test_quantized_grid_range_is_checked(fresh_core):
+    """A BVH4 node wider than the quantized grid reaches (255 * 2^27 per axis: box4q scales the ray's clamped
+    reciprocal +-1e30 by 2^e, which must stay finite, lh2_box4.inc / k_quantize4) is refused with a scene error,
+    not traversed with inf / NaN slabs."""
+    from lighthouse2_amd.core import CoreError
+    big = abi.tris_from_vertices(np.array([[-1e11, 0, 0], [0, 0, 5]], np.float32), np.array([[1e11, 0, 0], [1, 0, 5]], np.float32),
+                                 np.array([[0, 1e11, 0], [0, 1, 5]], np.float32), 0)
+    sc = scene.config2_scene(n=2000, width=64, height=36)
+    sc.meshes.append(big)
+    sc.instances.append((1, np.eye(4, dtype=np.float32)))
+    sc.load_into(fresh_core)
+    fresh_core.set_target(64, 36, 1)
+    with pytest.raises(CoreError, match="quantized"):
+        sc.render_frame(fresh_core)
+        fresh_core.sync()

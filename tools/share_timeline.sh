@@ -10,5 +10,5 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT" -o run --output-format csv -- \
   python3 "$ROOT/tools/config4_shares.py" --ranks "$N" --frames 10 "$@" > "$OUT/shares.jsonl" 2> "$OUT/shares.err"
-python3 "$ROOT/tools/frame_timeline.py" "$(find "$OUT" -name '*kernel_trace.csv' | head -1)" > "$OUT/timeline.txt"
+python3 "$ROOT/tools/overlap_timeline.py" "$(find "$OUT" -name "*kernel_trace.csv" | head -1)" 3 > "$OUT/timeline.txt"
 cat "$OUT/shares.jsonl" "$OUT/timeline.txt"
