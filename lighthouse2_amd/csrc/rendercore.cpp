@@ -156,7 +156,7 @@ void RenderCore::SetTarget( uint32_t w, uint32_t h, uint32_t spp )  /* rendercor
 	sceneVersion++;
 	EnsureBuffers();
 	CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)w * h, stream ) );
-	CHK_HIP( hipMemsetAsync( delta.ptr, 0, sizeof( float4 ) * (size_t)w * h, stream ) );
+	CHK_HIP( hipMemsetAsync( delta.ptr, 0, sizeof( float4 ) * 2 * (size_t)w * h, stream ) );
 	samplesTaken = 0;
 }
 
@@ -193,7 +193,7 @@ void RenderCore::EnsureBuffers()
 {
 	accumulator.resize( (size_t)scrwidth * scrheight );
 	frame.resize( (size_t)scrwidth * scrheight );
-	delta.resize( (size_t)scrwidth * scrheight );
+	delta.resize( 2 * (size_t)scrwidth * scrheight );   /* per frame parity: the next frame's first shade may run beside this finalize */
 }
 
 /* path buffers for `paths` paths (a bit extra, as the reference reserves, and room for LH2_SEGS segments
@@ -831,6 +831,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	float4* const shP = ps.shP.ptr + (size_t)ps.fp * ps.shCap;
 	uint32_t* const shMask = ps.shMask.ptr + (size_t)ps.fp * ps.shMaskWords;
 	uint32_t* const shSnap = ps.shSnap.ptr + (size_t)ps.fp * LH2_SEGS * LH2_SEGCOUNT_STRIDE;
+	float4* const frameDelta = delta.ptr + (size_t)ps.fp * scrwidth * scrheight;
 	/* primary rays (camera.h) for every sample of the tile; the camera launch also resets the frame's
 	   counters and work-queue heads (k_init_counters) */
 	CameraParams cp{};
@@ -1047,7 +1048,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ps.hvNextZeroed = true;
 		}
 		const bool earlyHere = early && pathLength == 1;
-		if (earlyHere) sp.acc = delta.ptr;   /* the previous frame's finalize may not have read the accumulator yet */
+		if (earlyHere) sp.acc = frameDelta;   /* the previous frame's finalize may not have read the accumulator yet */
 		lh2_launch_shade( &sd, &sp, grid, { nullptr, ps.evShade[pathLength] }, earlyHere ? aheadStream : stream );
 		if (earlyHere) CHK_HIP( hipStreamWaitEvent( stream, ps.evShade[pathLength], 0 ) );
 		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];
@@ -1113,7 +1114,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	samplesTaken += scrspp;
 	/* finalize also delivers the frame's counters and ray-count log, and the scene error, to hostStats */
 	const FrameStatsDev fs{ c, rayLog + 1, &hostStats->counters, hostStats->rayCount + 1, dSceneError.ptr, &hostStats->sceneError,
-		cursors + (size_t)primSlot * LH2_CURSOR_WORDS, early ? delta.ptr : nullptr };
+		cursors + (size_t)primSlot * LH2_CURSOR_WORDS, early ? frameDelta : nullptr };
 	/* a tile finalizes its own rows only (a rank of the band partition: the gathered frame is finalized
 	   where it is assembled, MultiDevice / FinalizeFrame) */
 	RowMap rm{};

@@ -251,7 +251,7 @@ private:
 	int scrwidth = 0, scrheight = 0, scrspp = 1;
 	int tileY0 = 0, tileY1 = -1, tileBand = 0, tileStride = 0;
 	DevBuf<float4> accumulator, frame;
-	DevBuf<float4> delta;                /* early shade: the first shade launch's accumulator additions (FrameStatsDev::delta) */
+	DevBuf<float4> delta;                /* early shade: the first shade launch's accumulator additions (FrameStatsDev::delta), per frame parity */
 	PathStreams ps;                      /* on `stream`; also serves the unit-level trace calls */
 	bool tileChanged = false;            /* the next restart clears the whole accumulator, not only the tile's pixels */
 	bool frameShadows = true;            /* the last frame queued shadow-ray launches (the scene has lights) */
