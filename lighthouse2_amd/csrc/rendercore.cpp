@@ -205,7 +205,7 @@ void RenderCore::EnsurePaths( uint32_t paths )
 		ps.cap = (size_t)paths + (paths >> 4) + 64;
 		for (int i = 0; i < 2; i++) ps.rayO[i].resize( ps.cap ), ps.rayD[i].resize( ps.cap ), ps.T4[i].resize( ps.cap ), ps.Q4[i].resize( ps.cap );
 		ps.hits.resize( ps.cap );
-		ps.rayOP.resize( ps.cap ), ps.rayDP.resize( ps.cap ), ps.T4P.resize( ps.cap ), ps.Q4P.resize( ps.cap ), ps.hitsP.resize( ps.cap );
+		for (int i = 0; i < 2; i++) ps.rayOP[i].resize( ps.cap ), ps.rayDP[i].resize( ps.cap ), ps.T4P[i].resize( ps.cap ), ps.Q4P[i].resize( ps.cap ), ps.hitsP[i].resize( ps.cap );
 		ps.relaid = true;
 		/* shadow rays: 2 per path, per frame parity */
 		ps.shCap = 2 * ps.cap, ps.shMaskWords = (ps.shCap + 63) / 32 + 2;
@@ -257,6 +257,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "cameraFused" )) cameraFused = value != 0;
 	else if (!strcmp( name, "frameOverlap" )) frameOverlap = (int)value;
 	else if (!strcmp( name, "earlyShade" )) earlyShade = value != 0;
+	else if (!strcmp( name, "primaryAhead" )) primaryAhead = value != 0;
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
@@ -281,7 +282,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -871,6 +872,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	   (the launch zeroes accumulator pixels), after a change of scene data, buffers or tile, or when the previous frame
 	   had no fused primary launch */
 	const bool serialize = !frameOverlap || restart || !ps.lastFused || ps.relaid || tileChanged || sceneVersion != ps.lastSceneVersion;
+	/* primary ahead: the previous frame had no path tail, and there is a frame before it whose finalize the wait can use */
+	const bool ahead = fusedCam && !serialize && primaryAhead && ps.lastNoTail && prevFrameEndValid;
 	hipStream_t primStream = stream;
 	/* the primary launch's work-queue heads: slot 1 of the frame parity's block, zeroed by the finalize of the frame before
 	   the previous one (FrameStatsDev::zeroHeads) */
@@ -888,7 +891,15 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		if (serialize) cp.initC = c;
 		else
 		{
-			CHK_HIP( hipStreamWaitEvent( aheadStream, ps.overlapEv, 0 ) );
+			/* primary ahead: after the previous frame's primary launch (its stop event: that launch may have run on the core
+			   stream) and the finalize of the frame before it (the last user of this parity's buffers); else after the
+			   previous frame's overlap event */
+			if (ahead)
+			{
+				CHK_HIP( hipStreamWaitEvent( aheadStream, ps.evTrace[1], 0 ) );
+				CHK_HIP( hipStreamWaitEvent( aheadStream, evFrame[2], 0 ) );
+			}
+			else CHK_HIP( hipStreamWaitEvent( aheadStream, ps.overlapEv, 0 ) );
 			lh2_launch_init_counters( c, pathCount, ps.segStride, cursors, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, {}, aheadStream, -LH2_CURSOR_WORDS );
 			cp.initC = nullptr;
 		}
@@ -948,7 +959,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.leafBatch = (uint32_t)(primary ? leafBatchPrimary : leafBatch);
 		ta.hits = ps.hits.ptr, ta.gstack = ps.gstack.ptr;
 		const bool fusedPrimary = pathLength == 1 && fusedCam;   /* the primary buffers (PathStreams::rayOP ..) */
-		if (fusedPrimary) ta.rayO = ps.rayOP.ptr, ta.rayD = ps.rayDP.ptr, ta.hits = ps.hitsP.ptr;
+		if (fusedPrimary) ta.rayO = ps.rayOP[ps.fp].ptr, ta.rayD = ps.rayDP[ps.fp].ptr, ta.hits = ps.hitsP[ps.fp].ptr;
 		if (pathLength == 1 && ta.packet && ps.hvOn)
 		{
 			ta.hvRead = ps.hv.ptr + (size_t)ps.hvParity * ps.hvBlock, ta.hvWrite = ps.hv.ptr + (size_t)(1 - ps.hvParity) * ps.hvBlock;
@@ -1005,7 +1016,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		{
 			/* the paths are dense (camera order): fixed counts, no segment counters; the core stream waits for it */
 			ta.segCounts = nullptr, ta.segBack = nullptr, ta.countFixed = pathCount;
-			lh2_launch_trace_primary( &sd, &ta, &cp, ps.T4P.ptr, ps.Q4P.ptr, PacketGrid(), { nullptr, ps.evTrace[pathLength] }, primStream );
+			lh2_launch_trace_primary( &sd, &ta, &cp, ps.T4P[ps.fp].ptr, ps.Q4P[ps.fp].ptr, PacketGrid(), { nullptr, ps.evTrace[pathLength] }, primStream );
 			if (primStream != stream && !early) CHK_HIP( hipStreamWaitEvent( stream, ps.evTrace[pathLength], 0 ) );
 		}
 		else
@@ -1036,12 +1047,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		sp.advance = pathLength < maxPL && !primeRef;
 		sp.adv = adv;
 		sp.rayO = ps.rayO[ps.in].ptr, sp.rayD = ps.rayD[ps.in].ptr, sp.T4 = ps.T4[ps.in].ptr, sp.Q4 = ps.Q4[ps.in].ptr, sp.hits = ps.hits.ptr;
-		if (fusedPrimary) sp.rayO = ps.rayOP.ptr, sp.rayD = ps.rayDP.ptr, sp.T4 = ps.T4P.ptr, sp.Q4 = ps.Q4P.ptr, sp.hits = ps.hitsP.ptr;
+		if (fusedPrimary) sp.rayO = ps.rayOP[ps.fp].ptr, sp.rayD = ps.rayDP[ps.fp].ptr, sp.T4 = ps.T4P[ps.fp].ptr, sp.Q4 = ps.Q4P[ps.fp].ptr, sp.hits = ps.hitsP[ps.fp].ptr;
 		sp.rayOut = ps.rayO[1 - ps.in].ptr, sp.rayDOut = ps.rayD[1 - ps.in].ptr, sp.T4Out = ps.T4[1 - ps.in].ptr, sp.Q4Out = ps.Q4[1 - ps.in].ptr;
 		sp.primeRef = primeRef;
 		sp.terminal = !primeRef && !shadows && !canEmit && pathLength > 1 && terminalShade;
 		sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
-		if (pathLength == 1 && fusedCam && hvReadBlock)
+		if (pathLength == 1 && fusedCam && hvReadBlock && tailL)
 		{
 			/* the block this frame's packets read is the one the next frame records into */
 			sp.hvZero = hvReadBlock, sp.hvZeroWords = LH2_HV_MASK + ps.hvMaskWords;
@@ -1061,7 +1072,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			/* after this launch only the path tail (in place) or the last bounce (no extension rays) runs: both use the
 			   buffer this launch writes, 1 - ps.in */
 			ps.busy = 1 - ps.in;
-			ps.earlyOk = (tailL && pathLength == tailL - 1) || (!tailL && pathLength == 1 && maxPL == 2);
+			ps.earlyOk = tailL && pathLength == tailL - 1;   /* config 2 (no tail): no gain, and the fold costs (r04b) */
 		}
 
 		if (pathLength == maxPL) break;
@@ -1135,6 +1146,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	}
 	hostStats->rayCount[0] = ps.count;
 	ps.lastFused = fusedCam, ps.lastSceneVersion = sceneVersion;
+	ps.lastNoTail = !ps.tailL;
 	framePathLengths = ps.tailL ? maxPL : ps.pl;
 	framePrimeRef = primeRef;
 	statsPending = true;

@@ -70,8 +70,8 @@ struct PathStreams
 	/* the primary rays, path state and hits of a fused frame (k_trace_primary_packet writes them, its first shade
 	   launch reads them): apart from the bounce ping-pong, so the next frame's primary launch can run beside this
 	   frame's later bounces */
-	DevBuf<float4> rayOP, rayDP, T4P, Q4P;
-	DevBuf<uint4> hitsP;
+	DevBuf<float4> rayOP[2], rayDP[2], T4P[2], Q4P[2];   /* per frame parity */
+	DevBuf<uint4> hitsP[2];
 	DevBuf<float4> shO, shD, shP;        /* 2 x shCap (frame parity) */
 	DevBuf<uint32_t> shMask;             /* 2 x shMaskWords */
 	size_t shCap = 0, shMaskWords = 0;
@@ -114,6 +114,9 @@ struct PathStreams
 	   neither (earlyOk), so the next frame's first shade writes the other one */
 	int busy = 0;
 	bool earlyOk = false, early = false;
+	/* primary ahead (setting "primaryAhead"): a frame without a path tail lets the next frame's primary launch start as soon
+	   as its own primary launch is done (the primary buffers are per parity), not after its first shade launch */
+	bool lastNoTail = false;
 };
 
 struct FrameStats   /* per-frame values delivered by k_finalize into pinned host memory */
@@ -271,6 +274,10 @@ private:
 	   ping-pong buffer: PathStreams::earlyOk).  Accumulator additions of the two frames then interleave: the sum matches
 	   the sequential one within float rounding, not bit for bit (the first-vertex depths, w, stay exact) */
 	int earlyShade = 1;
+	/* frames without a path tail (config 2: every path ends at its second vertex): the next frame's primary launch waits
+	   only for this frame's primary launch and the finalize of the frame before (its parity's last user), so it runs
+	   beside this frame's first shade launch and bounce, not only beside the bounce */
+	int primaryAhead = 1;
 	uint64_t sceneVersion = 0;           /* incremented by every change of device-resident scene data or buffers */
 	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle; BLAS leaves parked until this many
 	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,

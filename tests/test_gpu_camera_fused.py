@@ -4,9 +4,11 @@ the code of k_camera) into primary buffers of its own, and runs on the core's ah
 frame's later bounces once that frame's shade launch before its path tail (or its first) is done, or behind the whole
 previous frame after a restart or a scene change.  Consecutive frames use counters, work-queue heads and shadow streams of
 their own parity; the frame's resets are a k_init_counters launch before the primary launch on the ahead stream; the
-heavy-packet block the next frame records into is zeroed by the first shade launch.  With earlyShade (default) the
-frame's first shade launch follows its primary launch on the ahead stream too, beside the previous frame's path tail
-and shadow launches.
+heavy-packet block the next frame records into is zeroed by the first shade launch (or, before a frame whose primary
+launch may run ahead, by a memset on the ahead stream).  With earlyShade (default) the first shade launch of a frame after
+one with a path tail follows its primary launch on the ahead stream too, beside the previous frame's path tail and shadow
+launches; with primaryAhead (default) the primary launch of a frame after one without a path tail starts once that
+frame's primary launch is done (primary buffers per frame parity).
 
 Against the CPU oracle (pathtracer.h:54-245 after generateEyeRays): identical per-bounce ray counts every frame,
 accumulator rel-L2 <= 1e-4; and frames queued back to back (no host synchronisation between them, so the primary
@@ -71,19 +73,21 @@ def test_camera_fused_frames(fresh_core, kind):
         assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (f, fresh_core.ray_counts()[:6], o.ray_counts()[:6])
     ref = o.accumulator()
     res = {}
-    for fused, overlap, early in ((1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 0, 0)):
+    variants = ((1, 1, 1, 1), (1, 1, 1, 0), (1, 1, 0, 0), (1, 0, 0, 0), (0, 0, 0, 0))
+    for fused, overlap, early, ahead in variants:
         fresh_core.setting("cameraFused", fused)
         fresh_core.setting("frameOverlap", overlap)
         fresh_core.setting("earlyShade", early)
+        fresh_core.setting("primaryAhead", ahead)
         for f, conv in enumerate(SEQUENCE):   # queued back to back: no synchronisation between frames
             if anim:
                 _animate(sc, fresh_core, f)
             sc.render_frame(fresh_core, converge=conv)
-        res[(fused, overlap, early)] = fresh_core.accumulator()
-        assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (fused, overlap, early)
-    a = res[(1, 1, 1)]
+        res[(fused, overlap, early, ahead)] = fresh_core.accumulator()
+        assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (fused, overlap, early, ahead)
+    a = res[variants[0]]
     assert rel_l2(a[..., :3], ref[..., :3]) <= REL_L2_TOL
-    for k in ((1, 1, 0), (1, 0, 0), (0, 0, 0)):
+    for k in variants[1:]:
         assert rel_l2(a[..., :3], res[k][..., :3]) <= 1e-6, k
         # the first-vertex distances (w): one addition per pixel per frame, in frame order: bit-identical
         assert np.array_equal(a[..., 3], res[k][..., 3]), k
