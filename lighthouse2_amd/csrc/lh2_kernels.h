@@ -123,6 +123,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	int packet;                                       /* nonzero: wave-uniform packet traversal (coherent rays, lh2_trace_packet.inc) */
 	unsigned long long* stats;                        /* LH2_TRACE_STATS / LH2_TRACE_TIMES builds: per-launch counters */
 	uint32_t shadeBatch;                              /* path tail (k_trace_path4d): shade once >= shadeBatch lanes finished a query */
+	uint32_t prio;                                    /* the launch's waves' issue priority (s_setprio 0..3) against launches beside it */
 	/* heavy-first packets (packet kernel, hvWrite non-null): the previous frame's packets that took more
 	   than hvFactor x its mean node steps (hvRead: per-segment counts, step sums, a bit per packet and the
 	   lists of packet bits) are taken first, the rest in order; this frame's are recorded into hvWrite.

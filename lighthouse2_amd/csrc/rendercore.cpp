@@ -258,6 +258,11 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "frameOverlap" )) frameOverlap = (int)value;
 	else if (!strcmp( name, "earlyShade" )) earlyShade = value != 0;
 	else if (!strcmp( name, "primaryAhead" )) primaryAhead = value != 0;
+	else if (!strcmp( name, "prioTail" )) prioTail = std::min( 3, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "prioShadow" )) prioShadow = std::min( 3, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "prioSide" )) prioSide = std::min( 3, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "prioPrimary" )) prioPrimary = std::min( 3, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "prioTrace" )) prioTrace = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
@@ -282,7 +287,8 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
+		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -988,6 +994,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			sp.rayOut = ps.rayO[ps.in].ptr, sp.rayDOut = ps.rayD[ps.in].ptr, sp.T4Out = ps.T4[ps.in].ptr, sp.Q4Out = ps.Q4[ps.in].ptr;
 			sp.adv.rayCountLog = rayLog;
 			ta.shadeBatch = (uint32_t)pathTailBatch;
+			ta.prio = (uint32_t)prioTail;
 			/* with the overlap the path tail runs fewer blocks per CU (pathTailBlocks, default 2) and leaves
 			   registers for the side launch's waves */
 			const bool side = overlap && snapped;
@@ -1004,6 +1011,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				ts.cursor = cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS;
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
 				ts.mask = shMask, ts.potentials = shP, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
+				ts.prio = (uint32_t)prioSide;
 				lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, ps.evSide }, sideStream );
 				ps.fromSide = ps.prevStop;
 				ps.sideOn = true;
@@ -1016,6 +1024,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		{
 			/* the paths are dense (camera order): fixed counts, no segment counters; the core stream waits for it */
 			ta.segCounts = nullptr, ta.segBack = nullptr, ta.countFixed = pathCount;
+			ta.prio = (uint32_t)prioPrimary;
 			lh2_launch_trace_primary( &sd, &ta, &cp, ps.T4P[ps.fp].ptr, ps.Q4P[ps.fp].ptr, PacketGrid(), { nullptr, ps.evTrace[pathLength] }, primStream );
 			if (primStream != stream && !early) CHK_HIP( hipStreamWaitEvent( stream, ps.evTrace[pathLength], 0 ) );
 		}
@@ -1026,6 +1035,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			   of the bounce launch's tail (config 2: 4262-4296 -> 4437-4442 Mrays/s at 5, r03q_ab_trace_blocks.txt) */
 			const bool beside = besideNext && !ta.packet && overlapTraceBlocks > 0;
 			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, overlapTraceBlocks ) : grid;
+			ta.prio = (uint32_t)prioTrace;
 			lh2_launch_trace_closest( &sd, &ta, g, { nullptr, ps.evTrace[pathLength] }, stream );
 		}
 		ps.fromTrace[pathLength] = ps.prevStop, ps.prevStop = ps.evTrace[pathLength];
@@ -1117,6 +1127,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.rayO = shO, ta.rayD = shD, ta.segCounts = c->segShadow, ta.segStride = ps.shadowStride;
 		ta.cursor = cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.mask = shMask, ta.potentials = shP, ta.acc = accumulator.ptr, ta.gstack = ps.gstack.ptr;
+		ta.prio = (uint32_t)prioShadow;
 		lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, ps.evShadow }, stream );
 		ps.fromShadow = ps.prevStop;
 	}

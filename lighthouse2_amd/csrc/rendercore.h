@@ -278,6 +278,9 @@ private:
 	   only for this frame's primary launch and the finalize of the frame before (its parity's last user), so it runs
 	   beside this frame's first shade launch and bounce, not only beside the bounce */
 	int primaryAhead = 1;
+	/* issue priorities (s_setprio, TraceArgs::prio) of the frame's traversal launches: the path tail, the final shadow
+	   launch, the side shadow launch, the primary launch, the bounce launches */
+	int prioTail = 0, prioShadow = 0, prioSide = 0, prioPrimary = 0, prioTrace = 0;
 	uint64_t sceneVersion = 0;           /* incremented by every change of device-resident scene data or buffers */
 	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle; BLAS leaves parked until this many
 	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,
@@ -285,7 +288,10 @@ private:
 	   r03k_ab_leafbatch.txt) */
 	int refillPrimary = 48, refillOther = 48, leafBatch = 8, leafBatchPrimary = 8;
 	int bvhMaxLeaf = 1;
-	float bvhSpatial = 1e-5f;            /* spatial splits (SBVH): overlap threshold x root area; 0 = off */
+	/* spatial splits (SBVH): overlap threshold x root area; 0 = off.  1e-3 (round 4; 1e-5 before): the same node steps and
+	   triangle tests per ray (tools/bvh_quality.cpp: config 2 26.62 / 6.78 vs 26.64 / 6.68, the room 14.58 / 1.83 both)
+	   at a third of the build time (config 2 0.39 vs 1.44 s, the room 1.26 vs 2.88 s; profiles/r04d_sbvh_alpha.txt) */
+	float bvhSpatial = 1e-3f;
 	float bvhSpatialBudget = 1.0f;       /* ... adding at most this many references per triangle */
 	int bvh4Collapse = 1;                /* BVH4 collapse: 0 greedy (CollapseBvh4), 1 dynamic programming (CollapseBvh4Sah) */
 	float chordSplit = 0.35f;            /* extension rays with a chord through the scene box below this x its extent are traced last */

@@ -3,9 +3,9 @@ TLAS, 1080p 8 spp) per BLAS builder, on one MI355X: the core's scene setup time 
 builds, UpdateToplevel, SetTarget: what SynchronizeSceneData costs; the synthetic scene's generation in Python is
 timed apart) and the frame time with that tree, as bench.py's config5 times it.  One JSON line per builder.
 
-Builders (RenderCore settings, before SetGeometry): the default CPU binned SAH with spatial splits (SBVH) and the
-DP BVH4 collapse; the same without spatial splits (bvhSpatial 0); the GPU PLOC builder (gpuBuild 1,
-bvh_gpu.hip), whose BVH2 the host collapses to BVH4 the same way.
+Builders (RenderCore settings, before SetGeometry): the default CPU binned SAH with spatial splits (SBVH, overlap
+threshold bvhSpatial 1e-3) and the DP BVH4 collapse; the round-3 threshold 1e-5; no spatial splits (bvhSpatial 0); the
+GPU PLOC builder (gpuBuild 1, bvh_gpu.hip), whose BVH2 the host collapses to BVH4 the same way.
 """
 from __future__ import annotations
 
@@ -23,12 +23,13 @@ import torch  # noqa: E402,F401  (one HIP runtime in the process)
 from lighthouse2_amd import scene  # noqa: E402
 from lighthouse2_amd.core import RenderCore  # noqa: E402
 
-BUILDERS = {"cpu_sbvh": (), "cpu_sah": (("bvhSpatial", 0.0),), "gpu_ploc": (("gpuBuild", 1.0),)}
+BUILDERS = {"cpu_sbvh": (), "cpu_sbvh_1e-5": (("bvhSpatial", 1e-5),), "cpu_sah": (("bvhSpatial", 0.0),),
+            "gpu_ploc": (("gpuBuild", 1.0),)}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--builders", default="cpu_sbvh,cpu_sah,gpu_ploc")
+    ap.add_argument("--builders", default="cpu_sbvh,cpu_sbvh_1e-5,cpu_sah,gpu_ploc")
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--meshes", type=int, default=100)
