@@ -257,7 +257,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "cameraFused" )) cameraFused = value != 0;
 	else if (!strcmp( name, "frameOverlap" )) frameOverlap = (int)value;
 	else if (!strcmp( name, "earlyShade" )) earlyShade = value != 0;
-	else if (!strcmp( name, "primaryAhead" )) primaryAhead = value != 0;
+	else if (!strcmp( name, "primaryAhead" )) primaryAhead = std::min( 2, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "prioTail" )) prioTail = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "prioShadow" )) prioShadow = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "prioSide" )) prioSide = std::min( 3, std::max( 0, (int)value ) );
@@ -879,7 +879,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	   had no fused primary launch */
 	const bool serialize = !frameOverlap || restart || !ps.lastFused || ps.relaid || tileChanged || sceneVersion != ps.lastSceneVersion;
 	/* primary ahead: the previous frame had no path tail, and there is a frame before it whose finalize the wait can use */
-	const bool ahead = fusedCam && !serialize && primaryAhead && ps.lastNoTail && prevFrameEndValid;
+	const bool ahead = fusedCam && !serialize && (primaryAhead == 2 || (primaryAhead == 1 && ps.lastNoTail)) && prevFrameEndValid;
+	const hipEvent_t prevOverlapEv = ps.overlapEv;
 	hipStream_t primStream = stream;
 	/* the primary launch's work-queue heads: slot 1 of the frame parity's block, zeroed by the finalize of the frame before
 	   the previous one (FrameStatsDev::zeroHeads) */
@@ -1062,7 +1063,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		sp.primeRef = primeRef;
 		sp.terminal = !primeRef && !shadows && !canEmit && pathLength > 1 && terminalShade;
 		sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
-		if (pathLength == 1 && fusedCam && hvReadBlock && tailL)
+		/* (not when the next frame's primary launch may run ahead: it would record into the block while this launch zeroes it;
+		   that frame zeroes it on its own stream) */
+		const bool nextMayBeAhead = primaryAhead == 2 || (primaryAhead == 1 && !tailL);
+		if (pathLength == 1 && fusedCam && hvReadBlock && !nextMayBeAhead)
 		{
 			/* the block this frame's packets read is the one the next frame records into */
 			sp.hvZero = hvReadBlock, sp.hvZeroWords = LH2_HV_MASK + ps.hvMaskWords;
@@ -1070,6 +1074,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		}
 		const bool earlyHere = early && pathLength == 1;
 		if (earlyHere) sp.acc = frameDelta;   /* the previous frame's finalize may not have read the accumulator yet */
+		/* a primary launch run ahead has not waited for the previous frame's overlap event: the early shade does */
+		if (earlyHere && ahead) CHK_HIP( hipStreamWaitEvent( aheadStream, prevOverlapEv, 0 ) );
 		lh2_launch_shade( &sd, &sp, grid, { nullptr, ps.evShade[pathLength] }, earlyHere ? aheadStream : stream );
 		if (earlyHere) CHK_HIP( hipStreamWaitEvent( stream, ps.evShade[pathLength], 0 ) );
 		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];

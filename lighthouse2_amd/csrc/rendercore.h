@@ -274,9 +274,9 @@ private:
 	   ping-pong buffer: PathStreams::earlyOk).  Accumulator additions of the two frames then interleave: the sum matches
 	   the sequential one within float rounding, not bit for bit (the first-vertex depths, w, stay exact) */
 	int earlyShade = 1;
-	/* frames without a path tail (config 2: every path ends at its second vertex): the next frame's primary launch waits
-	   only for this frame's primary launch and the finalize of the frame before (its parity's last user), so it runs
-	   beside this frame's first shade launch and bounce, not only beside the bounce */
+	/* 1: after a frame without a path tail (config 2: every path ends at its second vertex), 2: after every frame: the
+	   next frame's primary launch waits only for this frame's primary launch and the finalize of the frame before (its
+	   parity's last user), so it runs beside this frame's first shade launch and bounce, not only beside the bounce */
 	int primaryAhead = 1;
 	/* issue priorities (s_setprio, TraceArgs::prio) of the frame's traversal launches: the path tail, the final shadow
 	   launch, the side shadow launch, the primary launch, the bounce launches */

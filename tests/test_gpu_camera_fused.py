@@ -73,7 +73,7 @@ def test_camera_fused_frames(fresh_core, kind):
         assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (f, fresh_core.ray_counts()[:6], o.ray_counts()[:6])
     ref = o.accumulator()
     res = {}
-    variants = ((1, 1, 1, 1), (1, 1, 1, 0), (1, 1, 0, 0), (1, 0, 0, 0), (0, 0, 0, 0))
+    variants = ((1, 1, 1, 1), (1, 1, 1, 2), (1, 1, 0, 2), (1, 1, 1, 0), (1, 1, 0, 0), (1, 0, 0, 0), (0, 0, 0, 0))
     for fused, overlap, early, ahead in variants:
         fresh_core.setting("cameraFused", fused)
         fresh_core.setting("frameOverlap", overlap)
