@@ -17,6 +17,19 @@ namespace {
 #define LH2_SAH_BINS 32   /* A/B 8/16/32/64 bins: 32 best by 1-3 % (profiles/r01b_ab_sah_bins.jsonl) */
 #endif
 constexpr int BINS = LH2_SAH_BINS;
+/* build-time A/B knobs of the spatial splits (profiles/r04d_sbvh_build.txt): fewer spatial bins, the object split's axis
+   only, or no spatial split below a node size each cut the build time by a third to a half but cost config-2 traversal
+   3-6 % more node steps per ray (0.3 % at a minimum of 64 references); the defaults keep the full search */
+#ifndef LH2_SBVH_BINS
+#define LH2_SBVH_BINS 32
+#endif
+#ifndef LH2_SBVH_AXES
+#define LH2_SBVH_AXES 0
+#endif
+#ifndef LH2_SBVH_MINCOUNT
+#define LH2_SBVH_MINCOUNT 0
+#endif
+constexpr int SBINS = LH2_SBVH_BINS;
 constexpr float C_ISECT = 1.0f;   /* node-visit cost C_TRAV is a build parameter (relative to one triangle test) */
 constexpr uint32_t PAR_THRESHOLD = 16384;
 
@@ -279,7 +292,7 @@ struct SpatialBuilder
 		/* spatial split, where the object split's children overlap */
 		int spAxis = -1;
 		float spPos = 0, spCost = std::numeric_limits<float>::max();
-		if (bestAxis >= 0 && refBudget.load( std::memory_order_relaxed ) > 0)
+		if (bestAxis >= 0 && count >= (uint32_t)LH2_SBVH_MINCOUNT && refBudget.load( std::memory_order_relaxed ) > 0)
 		{
 			Aabb ov;
 			for (int k = 0; k < 3; k++) ov.lo[k] = std::max( bestL.lo[k], bestR.lo[k] ), ov.hi[k] = std::min( bestL.hi[k], bestR.hi[k] );
@@ -287,12 +300,13 @@ struct SpatialBuilder
 			{
 				for (int a = 0; a < 3; a++)
 				{
+					if (LH2_SBVH_AXES == 1 && a != bestAxis) continue;
 					const float lo = box.lo[a], ext = box.hi[a] - lo;
 					if (!(ext > 0)) continue;
-					const float w = ext / (float)BINS;
-					Aabb bb[BINS]; uint32_t entry[BINS], exitc[BINS];
-					for (int b = 0; b < BINS; b++) bb[b] = empty_box(), entry[b] = exitc[b] = 0;
-					auto bin_of = [&]( float x ) { int b = (int)((x - lo) / w); return std::min( std::max( b, 0 ), BINS - 1 ); };
+					const float w = ext / (float)SBINS;
+					Aabb bb[SBINS]; uint32_t entry[SBINS], exitc[SBINS];
+					for (int b = 0; b < SBINS; b++) bb[b] = empty_box(), entry[b] = exitc[b] = 0;
+					auto bin_of = [&]( float x ) { int b = (int)((x - lo) / w); return std::min( std::max( b, 0 ), SBINS - 1 ); };
 					for (const Ref& r : refs)
 					{
 						const int b0 = bin_of( r.box.lo[a] ), b1 = std::max( b0, bin_of( r.box.hi[a] ) );
@@ -308,11 +322,11 @@ struct SpatialBuilder
 						}
 						if (valid( cur.box )) grow( bb[b1], cur.box );
 					}
-					Aabb rightBox[BINS]; uint32_t rightCount[BINS];
+					Aabb rightBox[SBINS]; uint32_t rightCount[SBINS];
 					Aabb acc = empty_box(); uint32_t n = 0;
-					for (int b = BINS - 1; b > 0; b--) { grow( acc, bb[b] ); n += exitc[b]; rightBox[b] = acc, rightCount[b] = n; }
+					for (int b = SBINS - 1; b > 0; b--) { grow( acc, bb[b] ); n += exitc[b]; rightBox[b] = acc, rightCount[b] = n; }
 					acc = empty_box(); n = 0;
-					for (int b = 0; b < BINS - 1; b++)
+					for (int b = 0; b < SBINS - 1; b++)
 					{
 						grow( acc, bb[b] ); n += entry[b];
 						if (n == 0 || rightCount[b + 1] == 0) continue;
