@@ -133,7 +133,8 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipEventCreate( &ps.evCamera ) );
 	CHK_HIP( hipEventCreate( &ps.evShadow ) );
 	CHK_HIP( hipEventCreate( &ps.evSide ) );
-	ps.shSnap.resize( 2 * LH2_SEGS * LH2_SEGCOUNT_STRIDE );
+	CHK_HIP( hipEventCreate( &ps.evSideA ) );
+	ps.shSnap.resize( 4 * LH2_SEGS * LH2_SEGCOUNT_STRIDE );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
@@ -263,6 +264,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "prioSide" )) prioSide = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "prioPrimary" )) prioPrimary = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "prioTrace" )) prioTrace = std::min( 3, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "sideSplit" )) sideSplit = value != 0;
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
@@ -288,7 +290,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
-		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -837,7 +839,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	float4* const shD = ps.shD.ptr + (size_t)ps.fp * ps.shCap;
 	float4* const shP = ps.shP.ptr + (size_t)ps.fp * ps.shCap;
 	uint32_t* const shMask = ps.shMask.ptr + (size_t)ps.fp * ps.shMaskWords;
-	uint32_t* const shSnap = ps.shSnap.ptr + (size_t)ps.fp * LH2_SEGS * LH2_SEGCOUNT_STRIDE;
+	uint32_t* const shSnap = ps.shSnap.ptr + (size_t)(2 * ps.fp) * LH2_SEGS * LH2_SEGCOUNT_STRIDE;   /* B: before the tail */
+	uint32_t* const shSnapA = shSnap + (size_t)LH2_SEGS * LH2_SEGCOUNT_STRIDE;                         /* A (sideSplit) */
 	float4* const frameDelta = delta.ptr + (size_t)ps.fp * scrwidth * scrheight;
 	/* primary rays (camera.h) for every sample of the tile; the camera launch also resets the frame's
 	   counters and work-queue heads (k_init_counters) */
@@ -946,7 +949,9 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const bool overlap = shadows && tailL && shadowOverlap;
 	bool snapped = false;
 	bool besideNext = false;   /* the next frame's primary launch may run beside the launches from here on */
-	ps.sideOn = false;
+	ps.sideOn = false, ps.sideAOn = false;
+	/* sideSplit: the shadow rays of the shade launch before the bounce before the tail on the side stream beside that bounce */
+	const bool splitSide = overlap && sideSplit && tailL >= 3;
 	/* the bounce loop */
 	for (int pathLength = 1; pathLength <= maxPL; pathLength++)
 	{
@@ -1052,8 +1057,11 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		/* the hand-off to the next bounce: the shade launch's last block (no launch of its own), except
 		   in PrimeRef mode, where the bounce's shadow rays are traced (and their counts reset) first */
 		const bool snap = overlap && pathLength + 1 == tailL;
+		/* snapshot A (sideSplit): the first side launch's counts, and the start of the second one's work-queue heads */
+		const bool snapA = splitSide && pathLength + 2 == tailL;
 		const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, rayLog, ps.activeLog, pathLength + 1 == tailL,
-			snap ? shSnap : nullptr, snap ? cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr };
+			snap ? shSnap : snapA ? shSnapA : nullptr,
+			snap ? cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : snapA ? cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS : nullptr };
 		snapped = snapped || snap;
 		sp.advance = pathLength < maxPL && !primeRef;
 		sp.adv = adv;
@@ -1079,6 +1087,21 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		lh2_launch_shade( &sd, &sp, grid, { nullptr, ps.evShade[pathLength] }, earlyHere ? aheadStream : stream );
 		if (earlyHere) CHK_HIP( hipStreamWaitEvent( stream, ps.evShade[pathLength], 0 ) );
 		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];
+		if (snapA)
+		{
+			/* the first side launch: the shadow rays queued so far (snapshot A), beside this frame's next bounce */
+			CHK_HIP( hipStreamWaitEvent( sideStream, ps.evShade[pathLength], 0 ) );
+			TraceArgs ts{};
+			ts.version = TraceVersion();
+			ts.rayO = shO, ts.rayD = shD, ts.segCounts = shSnapA, ts.segStride = ps.shadowStride;
+			ts.cursor = cursors + (size_t)(LH2_SHADOW_SLOT + 2) * LH2_CURSOR_WORDS;
+			ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
+			ts.mask = shMask, ts.potentials = shP, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
+			ts.prio = (uint32_t)prioSide;
+			lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, ps.evSideA }, sideStream );
+			ps.fromSideA = ps.evShade[pathLength];
+			ps.sideAOn = true;
+		}
 		/* the next frame's primary launch starts after this frame's first shade launch (the last reader of the primary
 		   buffers), or (frameOverlap 1) after the shade launch before the path tail: beside the latency-bound tail */
 		if (pathLength == 1 || (frameOverlap == 1 && tailL && pathLength == tailL - 1))
@@ -1123,7 +1146,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	}
 	/* a snapshot whose side launch did not happen (the frame ended before its path tail): the final launch
 	   traces every shadow ray, from the first */
-	if (snapped && !ps.sideOn)
+	if (!ps.sideOn && ps.sideAOn)   /* ... except those the first side launch traced (sideSplit): from snapshot A */
+		CHK_HIP( hipMemcpyAsync( cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS,
+			sizeof( uint32_t ) * LH2_CURSOR_WORDS, hipMemcpyDeviceToDevice, stream ) );
+	else if (snapped && !ps.sideOn)
 		CHK_HIP( hipMemsetAsync( cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
 	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
 	if (!primeRef && shadows)
@@ -1139,6 +1165,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	}
 	/* the side launch's contributions are in the accumulator before the frame is finalized */
 	if (ps.sideOn) CHK_HIP( hipStreamWaitEvent( stream, ps.evSide, 0 ) );
+	if (ps.sideAOn) CHK_HIP( hipStreamWaitEvent( stream, ps.evSideA, 0 ) );
 	samplesTaken += scrspp;
 	/* finalize also delivers the frame's counters and ray-count log, and the scene error, to hostStats */
 	const FrameStatsDev fs{ c, rayLog + 1, &hostStats->counters, hostStats->rayCount + 1, dSceneError.ptr, &hostStats->sceneError,
@@ -1254,7 +1281,8 @@ void RenderCore::Synchronize()
 		if (L <= ps.pl) coreStats.traceTimeX = trace( L );
 	}
 	float shadow = 0, shade = 0;
-	if (frameShadows && !framePrimeRef) shadow = ms( ps.fromShadow, ps.evShadow ) + (ps.sideOn ? ms( ps.fromSide, ps.evSide ) : 0.0f);
+	if (frameShadows && !framePrimeRef)
+		shadow = ms( ps.fromShadow, ps.evShadow ) + (ps.sideOn ? ms( ps.fromSide, ps.evSide ) : 0.0f) + (ps.sideAOn ? ms( ps.fromSideA, ps.evSideA ) : 0.0f);
 	else if (frameShadows) for (int L = 1; L < ps.pl; L++) shadow += ms( ps.fromShadowB[L], ps.evShadowB[L] );
 	for (int L = 1; L <= ps.pl; L++) if (L != ps.tailL) shade += ms( ps.fromShade[L], ps.evShade[L] );
 	coreStats.shadowTraceTime = shadow;
@@ -1516,7 +1544,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto& e : ps.evShade) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evShadowB) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evCount) (void)hipEventDestroy( e ), e = nullptr;
-	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow, &ps.evSide }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
+	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow, &ps.evSide, &ps.evSideA }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
 	if (ps.activeLog) (void)hipHostFree( ps.activeLog );
 	ps.activeLog = nullptr;
 	for (hipEvent_t* e : { &evConsumer, &evPacked }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
