@@ -265,6 +265,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "prioPrimary" )) prioPrimary = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "prioTrace" )) prioTrace = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "sideSplit" )) sideSplit = value != 0;
+	else if (!strcmp( name, "earlyShadeMaxPaths" )) earlyShadeMaxPaths = std::max( 0.0f, value );
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
@@ -290,7 +291,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
-		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -920,7 +921,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	ps.hvNextZeroed = false;
 	/* early shade: the first shade launch follows the primary launch on the ahead stream and writes the ping-pong buffer
 	   the previous frame's launches after its overlap event do not use (PathStreams::busy / earlyOk) */
-	const bool early = fusedCam && !serialize && earlyShade && frameOverlap == 1 && ps.earlyOk;
+	const bool early = fusedCam && !serialize && earlyShade && frameOverlap == 1 && ps.earlyOk && (float)pathCount <= earlyShadeMaxPaths;
 	ps.early = early;
 	ps.in = early ? ps.busy : 0;
 	ps.earlyOk = false;

@@ -277,10 +277,13 @@ private:
 	   ping-pong buffer: PathStreams::earlyOk).  Accumulator additions of the two frames then interleave: the sum matches
 	   the sequential one within float rounding, not bit for bit (the first-vertex depths, w, stay exact) */
 	int earlyShade = 1;
+	/* ... for frames of at most this many paths: beside a large frame's tail the early shade gains nothing and its fold
+	   (FrameStatsDev::delta) costs (config-4 N = 1 frames 1 % slower, the N = 8 share 1.5 % faster: profiles/r04e_ab.txt) */
+	float earlyShadeMaxPaths = 4.2e6f;
 	/* 1: after a frame without a path tail (config 2: every path ends at its second vertex), 2: after every frame: the
 	   next frame's primary launch waits only for this frame's primary launch and the finalize of the frame before (its
 	   parity's last user), so it runs beside this frame's first shade launch and bounce, not only beside the bounce */
-	int primaryAhead = 1;
+	int primaryAhead = 0;   /* config 2 5 % slower with 1 (profiles/r04e_ab.txt): off */
 	/* issue priorities (s_setprio, TraceArgs::prio) of the frame's traversal launches: the path tail, the final shadow
 	   launch, the side shadow launch, the primary launch, the bounce launches */
 	int prioTail = 0, prioShadow = 0, prioSide = 0, prioPrimary = 0, prioTrace = 0;
