@@ -26,9 +26,6 @@ constexpr int BINS = LH2_SAH_BINS;
 #ifndef LH2_SBVH_AXES
 #define LH2_SBVH_AXES 0
 #endif
-#ifndef LH2_SBVH_MINCOUNT
-#define LH2_SBVH_MINCOUNT 0
-#endif
 constexpr int SBINS = LH2_SBVH_BINS;
 constexpr float C_ISECT = 1.0f;   /* node-visit cost C_TRAV is a build parameter (relative to one triangle test) */
 constexpr uint32_t PAR_THRESHOLD = 16384;
@@ -203,6 +200,7 @@ struct SpatialBuilder
 	std::atomic<int> threadsLeft{ 0 };
 	int maxLeaf = 1;
 	float C_TRAV = 1.0f, alpha = 1e-5f, rootArea = 1.0f;
+	uint32_t minRefs = 0;         /* nodes of fewer references take the object split only */
 
 	void make_leaf( int ni, const std::vector<Ref>& refs, const Aabb& box )
 	{
@@ -243,6 +241,47 @@ struct SpatialBuilder
 			R.box.lo[k] = std::max( R.box.lo[k], r.box.lo[k] ), R.box.hi[k] = std::min( R.box.hi[k], r.box.hi[k] );
 		}
 		L.box.hi[a] = std::min( L.box.hi[a], p ), R.box.lo[a] = std::max( R.box.lo[a], p );
+	}
+
+	/* the spatial binning: grows bb[b0..b1] by the box of reference r's part in each slab [lo + w b, lo + w (b + 1)]
+	   of axis a (the first and last slab open towards the reference's box).  The triangle's cross-section at a
+	   plane is the segment between its long edge (lowest to highest vertex on a) and the short edge on the
+	   plane's side of the middle vertex; each plane's section is shared by the two slabs it bounds.  These boxes
+	   only price the candidate planes (the chosen split clips with split_ref), so they are not widened. */
+	void bin_slabs( const Ref& r, const int a, const float lo, const float w, const int b0, const int b1, Aabb* bb ) const
+	{
+		const float* v = tv + (size_t)r.prim * 9;
+		const float* A = v; const float* B = v + 3; const float* C = v + 6;
+		if (B[a] < A[a]) std::swap( A, B );
+		if (C[a] < B[a]) std::swap( B, C );
+		if (B[a] < A[a]) std::swap( A, B );
+		auto lerp = []( const float* p, const float* q, const float t, float* x ) { for (int k = 0; k < 3; k++) x[k] = p[k] + t * (q[k] - p[k]); };
+		auto add = []( Aabb& b, const float* x ) { for (int k = 0; k < 3; k++) b.lo[k] = std::min( b.lo[k], x[k] ), b.hi[k] = std::max( b.hi[k], x[k] ); };
+		float sec[2][3];   /* the section at the slab's lower plane */
+		bool haveSec = false;
+		for (int b = b0; b <= b1; b++)
+		{
+			Aabb box = empty_box();
+			const float pl = lo + w * (float)b, pu = lo + w * (float)(b + 1);
+			if (haveSec) add( box, sec[0] ), add( box, sec[1] );
+			for (const float* V : { A, B, C })
+				if ((b == b0 || V[a] >= pl) && (b == b1 || V[a] <= pu)) add( box, V );
+			haveSec = false;
+			if (b < b1 && C[a] > A[a] && pu > A[a] && pu < C[a])
+			{
+				lerp( A, C, (pu - A[a]) / (C[a] - A[a]), sec[0] );
+				if (pu < B[a]) lerp( A, B, (pu - A[a]) / (B[a] - A[a]), sec[1] );
+				else if (C[a] > B[a]) lerp( B, C, (pu - B[a]) / (C[a] - B[a]), sec[1] );
+				else for (int k = 0; k < 3; k++) sec[1][k] = B[k];
+				sec[0][a] = sec[1][a] = pu;
+				add( box, sec[0] ), add( box, sec[1] );
+				haveSec = true;
+			}
+			for (int k = 0; k < 3; k++) box.lo[k] = std::max( box.lo[k], r.box.lo[k] ), box.hi[k] = std::min( box.hi[k], r.box.hi[k] );
+			if (b > b0) box.lo[a] = std::max( box.lo[a], pl );
+			if (b < b1) box.hi[a] = std::min( box.hi[a], pu );
+			if (valid( box )) grow( bb[b], box );
+		}
 	}
 
 	void build( int ni, std::vector<Ref>& refs )
@@ -292,7 +331,7 @@ struct SpatialBuilder
 		/* spatial split, where the object split's children overlap */
 		int spAxis = -1;
 		float spPos = 0, spCost = std::numeric_limits<float>::max();
-		if (bestAxis >= 0 && count >= (uint32_t)LH2_SBVH_MINCOUNT && refBudget.load( std::memory_order_relaxed ) > 0)
+		if (bestAxis >= 0 && count >= minRefs && refBudget.load( std::memory_order_relaxed ) > 0)
 		{
 			Aabb ov;
 			for (int k = 0; k < 3; k++) ov.lo[k] = std::max( bestL.lo[k], bestR.lo[k] ), ov.hi[k] = std::min( bestL.hi[k], bestR.hi[k] );
@@ -311,16 +350,8 @@ struct SpatialBuilder
 					{
 						const int b0 = bin_of( r.box.lo[a] ), b1 = std::max( b0, bin_of( r.box.hi[a] ) );
 						entry[b0]++, exitc[b1]++;
-						Ref cur = r;
-						for (int b = b0; b < b1; b++)
-						{
-							Ref L, R;
-							split_ref( cur, a, lo + w * (float)(b + 1), L, R );
-							if (valid( L.box )) grow( bb[b], L.box );
-							cur = R;
-							if (!valid( cur.box )) break;
-						}
-						if (valid( cur.box )) grow( bb[b1], cur.box );
+						if (b0 == b1) grow( bb[b0], r.box );
+						else bin_slabs( r, a, lo, w, b0, b1, bb );
 					}
 					Aabb rightBox[SBINS]; uint32_t rightCount[SBINS];
 					Aabb acc = empty_box(); uint32_t n = 0;
@@ -504,11 +535,12 @@ static void Flatten( const std::vector<TNode>& tn, const float C_TRAV, BvhOutput
 }
 
 static void BuildSbvh( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost,
-	const float* triVerts, float alpha, float budget )
+	const float* triVerts, float alpha, float budget, int minRefs )
 {
 	const uint32_t N = (uint32_t)prims.size();
 	SpatialBuilder b;
 	b.tv = triVerts, b.maxLeaf = maxLeaf, b.C_TRAV = traversalCost > 0 ? traversalCost : 1.0f, b.alpha = alpha;
+	b.minRefs = (uint32_t)std::max( 0, minRefs );
 	const int64_t extra = (int64_t)((double)N * std::min( budget, 4.0f ));
 	b.refBudget = extra;
 	const size_t maxRefs = (size_t)N + (size_t)extra;   /* splits reserve their added references first */
@@ -531,14 +563,14 @@ static void BuildSbvh( const std::vector<Aabb>& prims, int maxLeaf, int threads,
 }  // namespace
 
 void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost, int sweepMax,
-	const float* triVerts, float spatialAlpha, float spatialBudget )
+	const float* triVerts, float spatialAlpha, float spatialBudget, int spatialMinRefs )
 {
 	const uint32_t N = (uint32_t)prims.size();
 	if (maxLeaf < 1) maxLeaf = 1;
 	if (maxLeaf > 16) maxLeaf = 16;
 	if (triVerts && spatialAlpha > 0 && spatialBudget > 0 && N >= 2)
 	{
-		BuildSbvh( prims, maxLeaf, threads, out, traversalCost, triVerts, spatialAlpha, spatialBudget );
+		BuildSbvh( prims, maxLeaf, threads, out, traversalCost, triVerts, spatialAlpha, spatialBudget, spatialMinRefs );
 		return;
 	}
 	Builder b( prims );

@@ -30,9 +30,10 @@ struct BvhOutput
    this many primitives split by an exact SAH sweep over the sorted centroids (0: binned only);
    triVerts (9 floats per primitive: the triangle's vertices), spatialAlpha > 0 and spatialBudget > 0:
    spatial splits (SBVH) where the object split's children overlap by more than spatialAlpha x the
-   root's surface area, adding at most spatialBudget x N references (out.perm then repeats primitives) */
+   root's surface area, adding at most spatialBudget x N references (out.perm then repeats primitives);
+   spatialMinRefs: nodes of fewer references try the object split only */
 void BuildBvh2( const std::vector<Aabb>& prims, int maxLeaf, int threads, BvhOutput& out, float traversalCost = 1.0f, int sweepMax = 0,
-	const float* triVerts = nullptr, float spatialAlpha = 0.0f, float spatialBudget = 0.0f );
+	const float* triVerts = nullptr, float spatialAlpha = 0.0f, float spatialBudget = 0.0f, int spatialMinRefs = 0 );
 
 /* BVH2 (16 floats per node, root 0) -> BVH4 (32 floats per node, root 0; layout: lh2_device.h) by
    greedy surface-area collapse; returns the BVH4 depth (interior levels) */

@@ -244,6 +244,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
 	else if (!strcmp( name, "bvhSpatial" )) bvhSpatial = std::max( 0.0f, value );   /* SBVH overlap threshold (x root area); 0: off */
 	else if (!strcmp( name, "bvhSpatialBudget" )) bvhSpatialBudget = std::min( 4.0f, std::max( 0.0f, value ) );
+	else if (!strcmp( name, "bvhSpatialMinRefs" )) bvhSpatialMinRefs = std::max( 0, (int)value );
 	else if (!strcmp( name, "bvh4Collapse" )) bvh4Collapse = value != 0;
 	else if (!strcmp( name, "bvh4" )) { bvh4 = value != 0; }   /* before SetGeometry */
 	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
@@ -289,7 +290,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "epsilon", geometryEpsilon }, { "clampValue", clampValue }, { "maxPathLength", (float)maxPathLength },
 		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
-		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvh4Collapse", (float)bvh4Collapse },
+		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvhSpatialMinRefs", (float)bvhSpatialMinRefs }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
 		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
@@ -453,10 +454,11 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 		}
 		const int maxLeaf = bvhMaxLeaf, collapse = bvh4Collapse, wide = bvh4;
 		const float cost = bvhTraversalCost, spatial = bvhSpatial, budget = bvhSpatialBudget;
+		const int minRefs = bvhSpatialMinRefs;
 		CoreMeshHost* mp = &m;
-		m.build = [mp, prims = std::move( prims ), verts = std::move( verts ), maxLeaf, collapse, wide, cost, spatial, budget]( int threads ) {
+		m.build = [mp, prims = std::move( prims ), verts = std::move( verts ), maxLeaf, collapse, wide, cost, spatial, budget, minRefs]( int threads ) {
 			BvhOutput bvh;
-			BuildBvh2( prims, maxLeaf, threads, bvh, cost, 0, spatial > 0 ? verts.data() : nullptr, spatial, budget );
+			BuildBvh2( prims, maxLeaf, threads, bvh, cost, 0, spatial > 0 ? verts.data() : nullptr, spatial, budget, minRefs );
 			/* one triangle record per leaf slot (a spatial split can reference a triangle from several leaves):
 			   v0, e1 = v1 - v0, e2 = v2 - v0 in fp32, exactly as the oracle's intersect_tri */
 			std::vector<float>& t48 = mp->hostTris48;

@@ -129,7 +129,9 @@ int main( int argc, char** argv )
 	const auto t0 = std::chrono::steady_clock::now();
 	BvhOutput out;
 	const float ctrav = getenv( "CTRAV" ) ? (float)atof( getenv( "CTRAV" ) ) : 1.0f;
-	BuildBvh2( prims, maxLeaf, 0, out, ctrav, 0, alpha > 0 ? sc.tv.data() : nullptr, alpha, budget );
+	const int minRefs = std::getenv( "LH2_MINREFS" ) ? atoi( std::getenv( "LH2_MINREFS" ) ) : 0;   /* bvhSpatialMinRefs */
+	const int threads = std::getenv( "LH2_THREADS" ) ? atoi( std::getenv( "LH2_THREADS" ) ) : 0;
+	BuildBvh2( prims, maxLeaf, threads, out, ctrav, 0, alpha > 0 ? sc.tv.data() : nullptr, alpha, budget, minRefs );
 	const double buildS = std::chrono::duration<double>( std::chrono::steady_clock::now() - t0 ).count();
 	const float cLeaf = argc > 5 ? (float)atof( argv[5] ) : -1.0f, cTri = argc > 6 ? (float)atof( argv[6] ) : 0.5f;
 	const int mlt = argc > 7 ? atoi( argv[7] ) : 1;

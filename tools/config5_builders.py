@@ -4,7 +4,8 @@ builds, UpdateToplevel, SetTarget: what SynchronizeSceneData costs; the syntheti
 timed apart) and the frame time with that tree, as bench.py's config5 times it.  One JSON line per builder.
 
 Builders (RenderCore settings, before SetGeometry): the default CPU binned SAH with spatial splits (SBVH, overlap
-threshold bvhSpatial 1e-3) and the DP BVH4 collapse; the round-3 threshold 1e-5; no spatial splits (bvhSpatial 0); the
+threshold bvhSpatial 1e-3, spatial splits tried in nodes of >= 64 references) and the DP BVH4 collapse; spatial splits
+tried in every node (bvhSpatialMinRefs 0); the round-3 threshold 1e-5; no spatial splits (bvhSpatial 0); the
 GPU PLOC builder (gpuBuild 1, bvh_gpu.hip), whose BVH2 the host collapses to BVH4 the same way.
 """
 from __future__ import annotations
@@ -23,7 +24,7 @@ import torch  # noqa: E402,F401  (one HIP runtime in the process)
 from lighthouse2_amd import scene  # noqa: E402
 from lighthouse2_amd.core import RenderCore  # noqa: E402
 
-BUILDERS = {"cpu_sbvh": (), "cpu_sbvh_1e-5": (("bvhSpatial", 1e-5),), "cpu_sah": (("bvhSpatial", 0.0),),
+BUILDERS = {"cpu_sbvh": (), "cpu_sbvh_min0": (("bvhSpatialMinRefs", 0.0),), "cpu_sbvh_1e-5": (("bvhSpatial", 1e-5),), "cpu_sah": (("bvhSpatial", 0.0),),
             "gpu_ploc": (("gpuBuild", 1.0),)}
 
 

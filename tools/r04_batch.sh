@@ -28,7 +28,7 @@ if [[ "$STEPS" == *l* ]]; then
   tail -14 "$OUT/share8.txt"
 fi
 if [[ "$STEPS" == *c* ]]; then
-  timeout -k 10 500 python3 tools/config5_builders.py > "$OUT/config5_builders.jsonl" 2> "$OUT/config5_builders.err"
+  timeout -k 10 500 python3 tools/config5_builders.py --builders "${BUILDERS:-cpu_sbvh,cpu_sbvh_1e-5,cpu_sah,gpu_ploc}" > "$OUT/config5_builders.jsonl" 2> "$OUT/config5_builders.err"
   cat "$OUT/config5_builders.jsonl"
 fi
 echo "batch done"
