@@ -226,9 +226,9 @@ def single_gpu_frames(core, sc, steps, warmup, per_frame=None):
 def config2_restart(args, local):
     """The config-2 frame as tinyapp's animated main loop renders it (apps/tinyapp/main.cpp:98-118): every frame a
     SetNodeTransform of one node (here the scene's one instance: a small rotation, SetInstance + UpdateToplevel,
-    rendersystem.cpp:143-174) and Render(Restart) (camMoved is set every frame).  A restart zeroes the accumulator
-    and a changed scene must not be traversed by the previous frame's rays, so the frame cannot start beside the
-    previous one the way a converging frame does."""
+    rendersystem.cpp:143-174) and Render(Restart) (camMoved is set every frame).  The instance-only UpdateToplevel writes
+    the TLAS slot no frame in flight reads and the restart zeroes the accumulator on the core stream, so these frames
+    overlap like converging ones (DESIGN §4 "Animated frames")."""
     t0 = time.perf_counter()
     sc = scene.config2_scene(n=args.tris, width=args.width, height=args.height)
     core = RenderCore(device=local)

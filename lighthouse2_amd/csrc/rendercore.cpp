@@ -139,12 +139,17 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
 	for (auto& e : evStage) CHK_HIP( hipEventCreateWithFlags( &e, hipEventDisableTiming ) );
-	dSceneError.resize( 1 ), dTlasDepth.resize( 1 ), dBlasQError.resize( 1 );
-	CHK_HIP( hipMemsetAsync( dSceneError.ptr, 0, sizeof( int ), stream ) );
+	dSceneError.resize( 2 ), dTlasDepth.resize( 1 ), dBlasQError.resize( 1 );
+	CHK_HIP( hipMemsetAsync( dSceneError.ptr, 0, sizeof( int ) * 2, stream ) );
+	CHK_HIP( hipEventCreateWithFlags( &evTlasReady, hipEventDisableTiming ) );
+	for (auto& e : evTlasFree) CHK_HIP( hipEventCreateWithFlags( &e, hipEventDisableTiming ) );
 	CHK_HIP( hipMemsetAsync( dTlasDepth.ptr, 0, sizeof( int ), stream ) );
 	CHK_HIP( hipMemsetAsync( dBlasQError.ptr, 0, sizeof( int ), stream ) );
-	dInstDesc.resize( 1 );   /* shading reads record 0 for a miss (HitInstance): it always exists */
-	CHK_HIP( hipMemsetAsync( dInstDesc.ptr, 0, sizeof( lh2_CoreInstanceDesc ), stream ) );
+	for (auto& d : dInstDesc)   /* shading reads record 0 for a miss (HitInstance): it always exists */
+	{
+		d.resize( 1 );
+		CHK_HIP( hipMemsetAsync( d.ptr, 0, sizeof( lh2_CoreInstanceDesc ), stream ) );
+	}
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	initialized = true;
 }
@@ -552,7 +557,7 @@ void RenderCore::BuildBlas4( CoreMeshHost& m, const float* nodes2 )
 
 void RenderCore::SetInstance( int instanceIdx, int meshIdx, const float* M )   /* rendercore.cpp:229-243 */
 {
-	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
+	/* host state only: UpdateToplevel writes it into the TLAS slot no frame in flight reads */
 	if (meshIdx == -1) { if ((int)instances.size() > instanceIdx) instances.resize( instanceIdx ); instancesDirty = true; return; }
 	if (meshIdx < 0 || meshIdx >= (int)meshes.size()) FatalError( "SetInstance: unknown mesh %d", meshIdx );
 	if (instanceIdx >= (int)instances.size()) instances.resize( instanceIdx + 1 );
@@ -579,17 +584,20 @@ void RenderCore::ConcatenateBlas( int ni )
 		if (m.triCount == 0) bounds[mi * 6] = 1.0f, bounds[mi * 6 + 3] = 0.0f;   /* empty-mesh marker */
 	}
 	tlasCapacity = std::max( 64, 2 * ni + 16 );
-	CHK_HIP( hipStreamSynchronize( stream ) );   /* frames in flight may still read the old arrays */
+	/* frames in flight may still read the old arrays, and a TLAS update may be queued on the ahead stream */
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	CHK_HIP( hipStreamSynchronize( aheadStream ) );
 	dNodes.free(), dTris.free(), dNodes4.free(), dNodes4q.free();
-	dNodes.resize( ((size_t)nodeTotal + tlasCapacity) * 4 );
+	/* after the BLAS: two TLAS slots of tlasCapacity nodes each (UpdateToplevel) */
+	dNodes.resize( ((size_t)nodeTotal + 2 * tlasCapacity) * 4 );
 	/* the BVH4 loops address nodes with 32-bit buffer offsets (lh2_trace4d.inc): the array stays below 2 GiB */
-	if (bvh4 && ((size_t)node4Total + tlasCapacity) * 128 > 0x7fffffffull)
-		FatalError( "BVH4 of %zu nodes exceeds the 2 GiB the traversal addresses", (size_t)node4Total + tlasCapacity );
-	if (bvh4) dNodes4.resize( ((size_t)node4Total + tlasCapacity) * 8 ), dNodes4q.resize( ((size_t)node4Total + tlasCapacity) * 4 );
+	if (bvh4 && ((size_t)node4Total + 2 * tlasCapacity) * 128 > 0x7fffffffull)
+		FatalError( "BVH4 of %zu nodes exceeds the 2 GiB the traversal addresses", (size_t)node4Total + 2 * tlasCapacity );
+	if (bvh4) dNodes4.resize( ((size_t)node4Total + 2 * tlasCapacity) * 8 ), dNodes4q.resize( ((size_t)node4Total + 2 * tlasCapacity) * 4 );
 	dTris.resize( (size_t)std::max( triTotal, 1 ) * 3 );
 	/* the TLAS region starts as NaN boxes: a TLAS of fewer nodes than the capacity leaves no uninitialised (possibly huge,
 	   finite) boxes behind it for the quantizer's range check (k_quantize4) */
-	CHK_HIP( hipMemsetAsync( dNodes.ptr + (size_t)nodeTotal * 4, 0xff, sizeof( float4 ) * 4 * (size_t)tlasCapacity, stream ) );
+	CHK_HIP( hipMemsetAsync( dNodes.ptr + (size_t)nodeTotal * 4, 0xff, sizeof( float4 ) * 4 * 2 * (size_t)tlasCapacity, stream ) );
 	dBlasQError.resize( 1 );
 	CHK_HIP( hipMemsetAsync( dBlasQError.ptr, 0, sizeof( int ), stream ) );
 	for (size_t mi = 0; mi < meshes.size(); mi++)
@@ -608,10 +616,18 @@ void RenderCore::ConcatenateBlas( int ni )
 
 void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 (instance descriptors) */
 {
-	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	const int ni = (int)instances.size();
-	if (geometryDirty || ni + 1 > tlasCapacity) ConcatenateBlas( ni );
-	tlasRoot = blasNodeCount;
+	if (geometryDirty || ni + 1 > tlasCapacity)
+	{
+		sceneVersion++;   /* new BLAS arrays: the next fused frame's primary launch waits for the previous frame */
+		ConcatenateBlas( ni );
+	}
+	/* the TLAS slot no frame in flight reads (the other one is the last frame's), written on the ahead stream behind the
+	   last frame that read it; instance-only updates leave sceneVersion alone, so the next frame may still overlap */
+	const int ts = tlasSlot ^ 1;
+	hipStream_t us = aheadStream;
+	if (tlasFreeValid[ts]) CHK_HIP( hipStreamWaitEvent( us, evTlasFree[ts], 0 ) );
+	tlasRoot = TlasBase2( ts );
 	/* host part: inverse transforms and instance records, written to pinned staging (double-buffered)
 	   and copied asynchronously; no host-device round trip per frame */
 	const int slot = stageSlot;
@@ -674,22 +690,27 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 	for (const auto& m : meshes)
 		if (m->triCount) for (int k = 0; k < 3; k++) qBound = std::max( qBound, std::max( fabsf( m->aabbLo[k] ), fabsf( m->aabbHi[k] ) ) );
 	qBound = qBound * 1.01f + 1e-30f;
-	dInst.resize( nRec * sizeof( DevInstance ) ), dInstDesc.resize( nRec ), dInstT.resize( nRec * 16 ), dInstMesh.resize( nRec );
-	dSceneError.resize( 1 ), dTlasDepth.resize( 1 );
-	CHK_HIP( hipMemcpyAsync( dInst.ptr, di, nRec * sizeof( DevInstance ), hipMemcpyHostToDevice, stream ) );
-	CHK_HIP( hipMemcpyAsync( dInstDesc.ptr, desc, nRec * sizeof( lh2_CoreInstanceDesc ), hipMemcpyHostToDevice, stream ) );
+	/* a slot's tables grow only with the work that may read them drained (DevBuf::resize frees the old buffer) */
+	if (dInst[ts].count < nRec * sizeof( DevInstance ) || dInstDesc[ts].count < nRec || dInstT.count < nRec * 16 || dInstMesh.count < nRec)
+	{
+		CHK_HIP( hipStreamSynchronize( stream ) );
+		CHK_HIP( hipStreamSynchronize( us ) );
+		dInst[ts].resize( nRec * sizeof( DevInstance ) ), dInstDesc[ts].resize( nRec ), dInstT.resize( nRec * 16 ), dInstMesh.resize( nRec );
+	}
+	CHK_HIP( hipMemcpyAsync( dInst[ts].ptr, di, nRec * sizeof( DevInstance ), hipMemcpyHostToDevice, us ) );
+	CHK_HIP( hipMemcpyAsync( dInstDesc[ts].ptr, desc, nRec * sizeof( lh2_CoreInstanceDesc ), hipMemcpyHostToDevice, us ) );
 	/* the scene error starts as the BLAS quantizer's (ConcatenateBlas), the TLAS checks add to it */
-	CHK_HIP( hipMemcpyAsync( dSceneError.ptr, dBlasQError.ptr, sizeof( int ), hipMemcpyDeviceToDevice, stream ) );
+	CHK_HIP( hipMemcpyAsync( SceneErr( ts ), dBlasQError.ptr, sizeof( int ), hipMemcpyDeviceToDevice, us ) );
 	if (ni >= 2 && gpuTlas)
 	{
 		/* TLAS built on the device from the instance transforms (bvh_gpu.h) */
-		CHK_HIP( hipMemcpyAsync( dInstT.ptr, Ts, nRec * 64, hipMemcpyHostToDevice, stream ) );
-		CHK_HIP( hipMemcpyAsync( dInstMesh.ptr, meshIds, nRec * 4, hipMemcpyHostToDevice, stream ) );
+		CHK_HIP( hipMemcpyAsync( dInstT.ptr, Ts, nRec * 64, hipMemcpyHostToDevice, us ) );
+		CHK_HIP( hipMemcpyAsync( dInstMesh.ptr, meshIds, nRec * 4, hipMemcpyHostToDevice, us ) );
 		GpuTlasArgs ta;
 		ta.T = dInstT.ptr, ta.instMesh = dInstMesh.ptr, ta.meshBounds = dMeshBounds.ptr, ta.count = ni;
-		ta.nodeBase = blasNodeCount, ta.nodes = dNodes.ptr, ta.maxBlasDepth = StackDepthBound();
-		ta.sceneError = dSceneError.ptr, ta.tlasDepth = dTlasDepth.ptr;
-		gpuBvh.BuildTlas( ta, stream );
+		ta.nodeBase = TlasBase2( ts ), ta.nodes = dNodes.ptr, ta.maxBlasDepth = StackDepthBound();
+		ta.sceneError = SceneErr( ts ), ta.tlasDepth = dTlasDepth.ptr;
+		gpuBvh.BuildTlas( ta, us );
 		tlasOnDevice = true;
 		sceneMaxDepth = -1;   /* known on the device; SceneInfo reads it */
 	}
@@ -732,7 +753,7 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 			int* refs = (int*)&tlas.nodes[k * 16 + 12];
 			for (int c = 0; c < 2; c++)
 			{
-				if (refs[c] >= 0) refs[c] += blasNodeCount;
+				if (refs[c] >= 0) refs[c] += TlasBase2( ts );
 				else if (!prims.empty())
 				{
 					if (LEAF_COUNT( refs[c] ) != 1) FatalError( "TLAS leaf with %d instances", LEAF_COUNT( refs[c] ) );
@@ -742,7 +763,7 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		}
 		if (tlas.nodes.size() * sizeof( float ) > need - offNodes) FatalError( "TLAS staging overflow" );
 		memcpy( sb + offNodes, tlas.nodes.data(), tlas.nodes.size() * sizeof( float ) );
-		CHK_HIP( hipMemcpyAsync( dNodes.ptr + (size_t)blasNodeCount * 4, sb + offNodes, tlas.nodes.size() * sizeof( float ), hipMemcpyHostToDevice, stream ) );
+		CHK_HIP( hipMemcpyAsync( dNodes.ptr + (size_t)TlasBase2( ts ) * 4, sb + offNodes, tlas.nodes.size() * sizeof( float ), hipMemcpyHostToDevice, us ) );
 		sceneMaxDepth = tlas.maxDepth + StackDepthBound();
 		tlasOnDevice = false;
 		if (sceneMaxDepth >= LH2_STACK_TOTAL - 1) FatalError( "BVH depth %d exceeds the traversal stack (%d)", sceneMaxDepth, LH2_STACK_TOTAL );
@@ -750,10 +771,12 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 	/* the TLAS in the BVH4 array: its BVH2 nodes as two-child BVH4 nodes (one short launch) */
 	if (bvh4)
 	{
-		GpuBvhBuilder::TlasToBvh4( dNodes.ptr, blasNodeCount, tlasCapacity, blasNode4Count, dNodes4.ptr, stream );
-		GpuBvhBuilder::Quantize4( dNodes4.ptr, blasNode4Count, tlasCapacity, dNodes4q.ptr, dSceneError.ptr, stream );
+		GpuBvhBuilder::TlasToBvh4( dNodes.ptr, TlasBase2( ts ), tlasCapacity, TlasBase4( ts ), dNodes4.ptr, us );
+		GpuBvhBuilder::Quantize4( dNodes4.ptr, TlasBase4( ts ), tlasCapacity, dNodes4q.ptr, SceneErr( ts ), us );
 	}
-	CHK_HIP( hipEventRecord( evStage[slot], stream ) );
+	CHK_HIP( hipEventRecord( evStage[slot], us ) );
+	CHK_HIP( hipEventRecord( evTlasReady, us ) );
+	tlasSlot = ts, tlasPending = true;
 	instancesDirty = false;
 }
 
@@ -771,28 +794,38 @@ void RenderCore::CheckSceneError()
 {
 	if (!dSceneError.ptr) return;
 	int e = 0;
-	CHK_HIP( hipMemcpyAsync( &hostStats->sceneError, dSceneError.ptr, sizeof( int ), hipMemcpyDeviceToHost, stream ) );
+	SyncTlas();
+	CHK_HIP( hipMemcpyAsync( &hostStats->sceneError, SceneErr( tlasSlot ), sizeof( int ), hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	e = hostStats->sceneError;
 	if (e) FatalError( "%s", SceneErrorText( e ) );
 }
 
-SceneDev RenderCore::MakeSceneDev() const
+/* the core stream's next launch reads the TLAS slot the last UpdateToplevel wrote on the ahead stream */
+void RenderCore::SyncTlas()
 {
+	if (!tlasPending) return;
+	CHK_HIP( hipStreamWaitEvent( stream, evTlasReady, 0 ) );
+	tlasPending = false;
+}
+
+SceneDev RenderCore::MakeSceneDev()
+{
+	SyncTlas();
 	SceneDev s;
-	s.nodes = dNodes.ptr, s.tris = dTris.ptr, s.inst = (const DevInstance*)dInst.ptr;
-	s.sceneError = dSceneError.ptr;
+	s.nodes = dNodes.ptr, s.tris = dTris.ptr, s.inst = (const DevInstance*)dInst[tlasSlot].ptr;
+	s.sceneError = SceneErr( tlasSlot );
 	s.argb32 = dArgb32.ptr, s.nrm32 = dNrm32.ptr;
 	s.argb32Count = (uint32_t)dArgb32.count, s.nrm32Count = (uint32_t)dNrm32.count;
 	s.tlasRoot = tlasRoot, s.instCount = (int)instances.size();
-	s.nodes4 = dNodes4.ptr, s.nodes4q = dNodes4q.ptr, s.qBound = qBound, s.tlasRoot4 = blasNode4Count;
+	s.nodes4 = dNodes4.ptr, s.nodes4q = dNodes4q.ptr, s.qBound = qBound, s.tlasRoot4 = TlasBase4( tlasSlot );
 	/* one instance of a non-empty mesh: rays start at its TLAS leaf (MAKE_LEAF( 0, 1 ) = ~0) and skip
 	   the TLAS root's box test, which can only cull (TopLevelBVH::Traverse bvh.cpp:594-649); the
 	   instance transform runs as at the leaf, so the hits are unchanged: one loop iteration less per ray */
 	if (singleInstanceStart && instances.size() == 1 && instances[0].mesh >= 0 && instances[0].mesh < (int)meshes.size() &&
 		meshes[instances[0].mesh]->triCount > 0)
 		s.tlasRoot = s.tlasRoot4 = ~0;
-	s.instDesc = dInstDesc.ptr, s.materials = dMaterials.ptr;
+	s.instDesc = dInstDesc[tlasSlot].ptr, s.materials = dMaterials.ptr;
 	s.areaLights = dArea.ptr, s.pointLights = dPoint.ptr, s.spotLights = dSpot.ptr, s.dirLights = dDir.ptr;
 	s.nArea = nArea, s.nPoint = nPoint, s.nSpot = nSpot, s.nDir = nDir;
 	s.sky = dSky.ptr, s.skyW = skyW, s.skyH = skyH;
@@ -823,6 +856,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const int tileRows = TileRows();
 	const uint32_t pathCount = (uint32_t)tileRows * (uint32_t)scrwidth * (uint32_t)scrspp;
 	const SceneDev sd = MakeSceneDev();
+	const int frameTlas = tlasSlot;   /* the TLAS slot this frame reads (evTlasFree after its finalize) */
 	/* the accumulator reset of a restart is folded into the camera launch (each pixel's first sample zeroes
 	   it; rows outside this rank's tile stay zero from SetTarget); a changed tile clears the whole frame */
 	if (restart && tileChanged) CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
@@ -883,7 +917,14 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	/* the fused primary launch beside the previous frame (frame overlap), or behind it on the core stream: on a restart
 	   (the launch zeroes accumulator pixels), after a change of scene data, buffers or tile, or when the previous frame
 	   had no fused primary launch */
-	const bool serialize = !frameOverlap || restart || !ps.lastFused || ps.relaid || tileChanged || sceneVersion != ps.lastSceneVersion;
+	const bool serialize = !frameOverlap || !ps.lastFused || ps.relaid || tileChanged || sceneVersion != ps.lastSceneVersion;
+	/* a restart beside the previous frame: the accumulator is zeroed on the core stream, behind the previous frame's finalize
+	   and before this frame's first addition there (the early shade adds into the delta), not by the primary launch */
+	if (fusedCam && !serialize && cp.clearAcc)
+	{
+		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
+		cp.clearAcc = nullptr;
+	}
 	/* primary ahead: the previous frame had no path tail, and there is a frame before it whose finalize the wait can use */
 	const bool ahead = fusedCam && !serialize && (primaryAhead == 2 || (primaryAhead == 1 && ps.lastNoTail)) && prevFrameEndValid;
 	const hipEvent_t prevOverlapEv = ps.overlapEv;
@@ -921,17 +962,24 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ps.relaid = false;
 	}
 	ps.hvNextZeroed = false;
-	/* early shade: the first shade launch follows the primary launch on the ahead stream and writes the ping-pong buffer
-	   the previous frame's launches after its overlap event do not use (PathStreams::busy / earlyOk) */
-	const bool early = fusedCam && !serialize && earlyShade && frameOverlap == 1 && ps.earlyOk && (float)pathCount <= earlyShadeMaxPaths;
-	ps.early = early;
-	ps.in = early ? ps.busy : 0;
-	ps.earlyOk = false;
 	uint32_t* hvReadBlock = nullptr;
 	int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
 	/* no specular event and no alpha cut-out in any material: every path ends at its second vertex,
 	   so the bounce after it would be empty; not launching it saves three launches (~25 us) */
 	if (!primeRef && diffuseOnly) maxPL = std::min( maxPL, 2 );
+	/* the path tail (setting "pathTail"): bounces pathTail .. maxPL in one launch of k_trace_path4d */
+	const int tailL = (!primeRef && pathTail >= 2 && pathTail <= maxPL && TraceVersion() == 7) ? pathTail : 0;
+	/* early shade: the first shade launch follows the primary launch on the ahead stream and writes the ping-pong buffer
+	   the previous frame's launches after its overlap event do not use (PathStreams::busy / earlyOk).  Only when this
+	   frame has a path tail from bounce 3 on: else its first shade launch is its overlap event (and, with the tail from
+	   bounce 2, its shadow snapshot), and on the ahead stream neither would follow the previous frame's finalize (the
+	   side shadow launch and the next frames' early shades would add into the accumulator and the delta before the
+	   previous frame is finalized) */
+	const bool early = fusedCam && !serialize && earlyShade && frameOverlap == 1 && ps.earlyOk && (float)pathCount <= earlyShadeMaxPaths &&
+		tailL >= 3;
+	ps.early = early;
+	ps.in = early ? ps.busy : 0;
+	ps.earlyOk = false;
 	/* the frame's start: a marker before the camera launch (~4 us of idle GPU), not the launch's own start
 	   event (hipExtLaunchKernelGGL start events cost ~8 us: tools/launch_gap.hip, profiles/r02q_launch_gap.txt) */
 	CHK_HIP( hipEventRecord( evFrame[0], fusedCam ? primStream : stream ) );
@@ -946,8 +994,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	   rays and their launches are not queued */
 	const bool shadows = nArea + nPoint + nSpot + nDir > 0;
 	frameShadows = shadows;
-	/* the path tail (setting "pathTail"): bounces pathTail .. maxPL in one launch of k_trace_path4d */
-	const int tailL = (!primeRef && pathTail >= 2 && pathTail <= maxPL && TraceVersion() == 7) ? pathTail : 0;
 	/* shadow overlap: the shade launch before the tail snapshots the queued shadow rays (advance_bounce) */
 	const bool overlap = shadows && tailL && shadowOverlap;
 	bool snapped = false;
@@ -1171,7 +1217,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	if (ps.sideAOn) CHK_HIP( hipStreamWaitEvent( stream, ps.evSideA, 0 ) );
 	samplesTaken += scrspp;
 	/* finalize also delivers the frame's counters and ray-count log, and the scene error, to hostStats */
-	const FrameStatsDev fs{ c, rayLog + 1, &hostStats->counters, hostStats->rayCount + 1, dSceneError.ptr, &hostStats->sceneError,
+	const FrameStatsDev fs{ c, rayLog + 1, &hostStats->counters, hostStats->rayCount + 1, SceneErr( frameTlas ), &hostStats->sceneError,
 		cursors + (size_t)primSlot * LH2_CURSOR_WORDS, early ? frameDelta : nullptr };
 	/* a tile finalizes its own rows only (a rank of the band partition: the gathered frame is finalized
 	   where it is assembled, MultiDevice / FinalizeFrame) */
@@ -1183,6 +1229,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	prevFrameEndValid = frameEndRecorded, frameWasOverlapped = fusedCam && !serialize;
 	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, &fs, { nullptr, evFrame[1] }, stream, &rm );
 	frameEndRecorded = true;
+	CHK_HIP( hipEventRecord( evTlasFree[frameTlas], stream ) );   /* the next update of this TLAS slot waits for it */
+	tlasFreeValid[frameTlas] = true;
 	if (glResource && !displayAtFinalize)
 	{
 		hipArray_t arr = nullptr;
@@ -1341,11 +1389,19 @@ int RenderCore::DebugBvh4( float* f32Nodes, uint32_t* qNodes, int cap )
 {
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	Synchronize();
+	SyncTlas();
+	CHK_HIP( hipStreamSynchronize( stream ) );
 	if (!dNodes4.ptr || !dNodes4q.ptr) return 0;
 	if (cap <= 0 || !f32Nodes || !qNodes) return blasNode4Count + tlasCapacity;   /* a count-only call */
-	const int n = std::min( cap, blasNode4Count + tlasCapacity );
-	CHK_HIP( hipMemcpy( f32Nodes, dNodes4.ptr, 128 * (size_t)n, hipMemcpyDeviceToHost ) );
-	CHK_HIP( hipMemcpy( qNodes, dNodes4q.ptr, 64 * (size_t)n, hipMemcpyDeviceToHost ) );
+	/* the BLAS nodes, then the current TLAS slot's */
+	const int n = std::min( cap, blasNode4Count + tlasCapacity ), nb = std::min( n, blasNode4Count ), nt = n - nb;
+	CHK_HIP( hipMemcpy( f32Nodes, dNodes4.ptr, 128 * (size_t)nb, hipMemcpyDeviceToHost ) );
+	CHK_HIP( hipMemcpy( qNodes, dNodes4q.ptr, 64 * (size_t)nb, hipMemcpyDeviceToHost ) );
+	if (nt > 0)
+	{
+		CHK_HIP( hipMemcpy( f32Nodes + 32 * (size_t)nb, dNodes4.ptr + 8 * (size_t)TlasBase4( tlasSlot ), 128 * (size_t)nt, hipMemcpyDeviceToHost ) );
+		CHK_HIP( hipMemcpy( qNodes + 16 * (size_t)nb, dNodes4q.ptr + 4 * (size_t)TlasBase4( tlasSlot ), 64 * (size_t)nt, hipMemcpyDeviceToHost ) );
+	}
 	return n;
 }
 
@@ -1528,6 +1584,7 @@ void RenderCore::SceneInfo( int* nodeCount, int* triCount, int* maxDepth, int* i
 	if (tlasOnDevice)
 	{
 		int d = 0;
+		SyncTlas();
 		CHK_HIP( hipMemcpyAsync( &d, dTlasDepth.ptr, sizeof( int ), hipMemcpyDeviceToHost, stream ) );
 		CHK_HIP( hipStreamSynchronize( stream ) );
 		sceneMaxDepth = d + maxBlasDepth;
@@ -1540,6 +1597,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 {
 	if (!initialized) return;
 	(void)hipStreamSynchronize( stream );
+	if (aheadStream) (void)hipStreamSynchronize( aheadStream );   /* a TLAS update nothing waited for */
 	for (auto* m : meshes) delete m;
 	meshes.clear();
 	instances.clear();
@@ -1553,6 +1611,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (hipEvent_t* e : { &evConsumer, &evPacked }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
 	for (auto& e : evFrame) (void)hipEventDestroy( e );
 	for (auto& e : evStage) (void)hipEventDestroy( e );
+	for (hipEvent_t* e : { &evTlasReady, &evTlasFree[0], &evTlasFree[1] }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
 	for (int i = 0; i < 2; i++) { if (stage[i]) (void)hipHostFree( stage[i] ); stage[i] = nullptr, stageBytes[i] = 0; }
 	if (glResource) (void)hipGraphicsUnregisterResource( glResource );
 	glResource = nullptr, glTexture = 0;

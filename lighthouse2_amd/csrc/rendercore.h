@@ -199,7 +199,8 @@ private:
 	void EnsureStack();
 	void CheckSceneError();
 	bool UsePackets() const;
-	SceneDev MakeSceneDev() const;
+	SceneDev MakeSceneDev();             /* the latest TLAS slot's scene; the core stream waits for its update (SyncTlas) */
+	void SyncTlas();
 	Counters* FrameCounters() const { return ps.counters.ptr + ps.fp; }
 	uint32_t* FrameCursors() const { return ps.cursors.ptr + (size_t)ps.fp * LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS; }
 	uint32_t* FrameRayLog() const { return ps.rayLog.ptr + (size_t)ps.fp * LH2_RAYLOG; }
@@ -217,8 +218,8 @@ private:
 	DevBuf<float4> dNodes, dTris;
 	DevBuf<float4> dNodes4;              /* BVH4: all BLAS (relocated), then the TLAS as two-child nodes */
 	DevBuf<uint4> dNodes4q;              /* the same nodes with quantized child boxes (GpuBvhBuilder::Quantize4) */
-	DevBuf<uint8_t> dInst;               /* DevInstance[] */
-	DevBuf<lh2_CoreInstanceDesc> dInstDesc;
+	DevBuf<uint8_t> dInst[2];            /* DevInstance[], per TLAS slot */
+	DevBuf<lh2_CoreInstanceDesc> dInstDesc[2];
 	int tlasRoot = 0, blasNodeCount = 0, blasTriCount = 0, blasMeshTris = 0, sceneMaxDepth = 0;   /* blasTriCount: leaf triangle records; blasMeshTris: triangles */
 	std::vector<int> meshNodeBase, meshTriBase, meshNode4Base;
 	int tlasCapacity = 0, maxBlasDepth = 0;
@@ -230,12 +231,22 @@ private:
 	DevBuf<float> dMeshBounds;           /* 6 per mesh */
 	DevBuf<float> dInstT;                /* 16 per instance */
 	DevBuf<int> dInstMesh;
-	DevBuf<int> dSceneError, dTlasDepth;
+	DevBuf<int> dSceneError, dTlasDepth; /* dSceneError: one flag per TLAS slot */
 	DevBuf<int> dBlasQError;             /* the BLAS quantizer's range flag (LH2_SCENE_ERR_QRANGE), copied into dSceneError per TLAS update */
 	uint8_t* stage[2] = {};              /* pinned staging of UpdateToplevel (double-buffered) */
 	size_t stageBytes[2] = {};
 	hipEvent_t evStage[2] = {};
 	int stageSlot = 0;
+	/* TLAS slots (round 4): an instance-only UpdateToplevel writes the instance tables, the TLAS (the BVH2 and BVH4 regions
+	   after the BLAS, tlasCapacity nodes per slot) and the scene-error flag of the slot no frame in flight reads, on the ahead
+	   stream behind the last frame that read that slot (evTlasFree), so an animated frame's primary launch can still run
+	   beside the previous frame; the core stream waits for the update (evTlasReady) before its next launch */
+	int tlasSlot = 0;
+	bool tlasPending = false, tlasFreeValid[2] = {};
+	hipEvent_t evTlasReady = nullptr, evTlasFree[2] = {};
+	int TlasBase2( int s ) const { return blasNodeCount + s * tlasCapacity; }
+	int TlasBase4( int s ) const { return blasNode4Count + s * tlasCapacity; }
+	int* SceneErr( int s ) const { return dSceneError.ptr + s; }
 	hipGraphicsResource_t glResource = nullptr;   /* registered GL_RGBA32F target texture */
 	uint32_t glTexture = 0;
 	DevBuf<uint4> dMaterials;

@@ -91,3 +91,48 @@ def test_camera_fused_frames(fresh_core, kind):
         assert rel_l2(a[..., :3], res[k][..., :3]) <= 1e-6, k
         # the first-vertex distances (w): one addition per pixel per frame, in frame order: bit-identical
         assert np.array_equal(a[..., 3], res[k][..., 3]), k
+
+
+@pytest.mark.parametrize("kind", ["room", "config2", "instanced"])
+def test_animated_restart_frames(fresh_core, kind):
+    """tinyapp's animated loop (apps/tinyapp/main.cpp:98-118): SetInstance + UpdateToplevel and Render(Restart) every
+    frame.  An instance-only UpdateToplevel writes the TLAS slot no frame in flight reads, on the ahead stream behind
+    the last frame that read it, and a restart beside the previous frame zeroes the accumulator on the core stream, so
+    these frames overlap too.  Every prefix of the sequence, queued back to back, equals the same frames serialised
+    (frameOverlap 0): the same per-bounce ray counts, the accumulator to float summation order (w bit for bit).  A
+    second UpdateToplevel before a frame (the slot the frame in flight reads) must wait for that frame."""
+    w, h = 96, 64
+    sc, depth = _scene(kind, w, h)
+    if kind == "config2":
+        sc.sky = scene.gradient_sky(64, 32)   # something to accumulate (config 2 has no lights)
+    base = list(sc.instances)
+    sc.load_into(fresh_core)
+    fresh_core.set_target(w, h, 1)
+    fresh_core.setting("maxPathLength", depth)
+
+    def turn(f):
+        for k, (mesh, T) in enumerate(base):
+            M = (scene.rotation_y(0.02 * (f + 1) * (1 + k % 3)) @ T).astype(np.float32) if kind != "instanced" else None
+            if M is None:
+                M = scene.rotation_y(0.3 * (f + 1) * (1 + k % 3))
+                M[:3, 3] = T[:3, 3]
+            fresh_core.set_instance(k, mesh, M)
+        fresh_core.update_toplevel()
+
+    def run(n, overlap, double):
+        fresh_core.setting("frameOverlap", overlap)
+        for f in range(n):
+            turn(f)
+            if double and f % 2:
+                turn(f)   # the same instances again: the update of the slot the previous frame still reads
+            sc.render_frame(fresh_core, converge=1)
+        return fresh_core.accumulator(), fresh_core.ray_counts()
+
+    for n in (1, 2, 3, 5):
+        for double in (False, True):
+            a, ca = run(n, 0, double)
+            b, cb = run(n, 1, double)
+            assert np.array_equal(ca, cb), (n, double, ca[:6], cb[:6])
+            assert np.any(a[..., :3] != 0)
+            assert rel_l2(b[..., :3], a[..., :3]) <= 1e-6, (n, double)
+            assert np.array_equal(a[..., 3], b[..., 3]), (n, double)
