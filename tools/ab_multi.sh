@@ -1,5 +1,6 @@
 #!/bin/bash
-# A/B of setting combinations (through gpurun): per variant (comma-separated name=value list, "base" = defaults) the
+# A/B of setting combinations (through gpurun): per variant (comma-separated name=value list, "base" = defaults;
+# lib=<name> loads the variant build gpuab/<name>/libRenderCore_MI355X.so, tools/build_variant.sh) the
 # config-4 rank shares at N = 1 and 8, config 3 (tools/bench_configs.py) and config 2 (bench.py, no other configs),
 # the variants interleaved, REPS rounds.  usage: VARIANTS="base prioTail=2 prioTail=2,prioShadow=2" REPS=2
 set -euo pipefail
@@ -10,7 +11,10 @@ cd "$ROOT"
 for rep in $(seq 1 "${REPS:-2}"); do
   for v in ${VARIANTS:-base}; do
     args=()
-    if [ "$v" != "base" ]; then IFS=',' read -ra kvs <<< "$v"; for kv in "${kvs[@]}"; do args+=(--setting "$kv"); done; fi
+    unset LH2_CORE_LIB
+    if [ "$v" != "base" ]; then IFS=',' read -ra kvs <<< "$v"; for kv in "${kvs[@]}"; do
+      if [[ "$kv" == lib=* ]]; then export LH2_CORE_LIB="$ROOT/gpuab/${kv#lib=}/libRenderCore_MI355X.so"; else args+=(--setting "$kv"); fi
+    done; fi
     n="${v//[=,]/_}_$rep"
     timeout -k 10 200 python3 tools/config4_shares.py --ranks 1,8 "${args[@]}" > "$OUT/sh_$n.jsonl" 2> "$OUT/sh_$n.err"
     timeout -k 10 200 python3 tools/bench_configs.py --configs 3 --frames 10 "${args[@]}" > "$OUT/c3_$n.jsonl" 2> "$OUT/c3_$n.err"
@@ -25,4 +29,5 @@ print(f"{v:40s} N1 {sh[0]['ms_per_frame']:.4f} N8 {sh[-1]['ms_per_frame']:.4f} r
 PY
   done
 done
+unset LH2_CORE_LIB
 echo "ab_multi done"

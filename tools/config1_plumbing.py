@@ -118,7 +118,7 @@ def main():
     args = ap.parse_args()
     sc = scene.tinyapp_scene(args.width, args.height)
     out = {"config": "config1", "workload": f"tinyapp default scene, {sc.tri_count} tris (pica glTF 76,274 in 170 "
-           f"instances + legocar.obj 10,992 at scale 10 + 2-tri light quad; untextured), {args.width}x{args.height}",
+           f"instances + legocar.obj 10,992 at scale 10 + 2-tri light quad; the six glTF textures), {args.width}x{args.height}",
            "soft_rasterizer_reference": soft_rasterizer(sc, args.width, args.height, args.cpu_seconds)}
     if not args.no_gpu:
         out["mi355x_core"] = mi355x_core(sc, args.width, args.height, args.frames, args.setting)
