@@ -272,6 +272,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "prioTrace" )) prioTrace = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "sideSplit" )) sideSplit = value != 0;
 	else if (!strcmp( name, "earlyShadeMaxPaths" )) earlyShadeMaxPaths = std::max( 0.0f, value );
+	else if (!strcmp( name, "sideBlocks" )) sideBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
@@ -297,7 +298,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvhSpatialMinRefs", (float)bvhSpatialMinRefs }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
-		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "sideBlocks", (float)sideBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -1067,7 +1068,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
 				ts.mask = shMask, ts.potentials = shP, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
 				ts.prio = (uint32_t)prioSide;
-				lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, ps.evSide }, sideStream );
+				lh2_launch_trace_any( &sd, &ts, sideBlocks > 0 ? smCount * sideBlocks : grid, 1, { nullptr, ps.evSide }, sideStream );
 				ps.fromSide = ps.prevStop;
 				ps.sideOn = true;
 			}

@@ -331,6 +331,7 @@ private:
 	   shade launch slows the bounces it overlaps (2.344 / 1.426 ms) */
 	bool shadowOverlap = true;
 	int pathTailBlocks = 0;              /* the path tail's blocks per CU; 0: 2 with the overlap, else its occupancy limit */
+	int sideBlocks = 0;                  /* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's) */
 	int overlapTraceBlocks = 5;          /* blocks per CU of a closest-hit launch that the next frame's primary launch runs
 	                                        beside (an overlapped frame's later bounces, no path tail); 0: the trace grid's */
 	/* heavy-first primary packets (TraceArgs::hvRead): the packets of the previous frame that took more than
