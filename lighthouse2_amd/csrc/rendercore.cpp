@@ -226,7 +226,6 @@ void RenderCore::EnsureStack()
 	const size_t need = (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256;
 	if (ps.gstack.count < need) ps.gstack.resize( need );
 	if (shadowOverlap && ps.sideStack.count < need) ps.sideStack.resize( need );
-	if (earlyBounce && ps.aheadStack.count < need) ps.aheadStack.resize( need );
 }
 
 void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439-457 */
@@ -273,7 +272,6 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "prioTrace" )) prioTrace = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "sideSplit" )) sideSplit = value != 0;
 	else if (!strcmp( name, "earlyShadeMaxPaths" )) earlyShadeMaxPaths = std::max( 0.0f, value );
-	else if (!strcmp( name, "earlyBounce" )) earlyBounce = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "sideBlocks" )) sideBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
@@ -300,7 +298,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvhSpatialMinRefs", (float)bvhSpatialMinRefs }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
-		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "sideBlocks", (float)sideBlocks }, { "earlyBounce", (float)earlyBounce }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "sideBlocks", (float)sideBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -1094,17 +1092,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			const bool beside = besideNext && !ta.packet && overlapTraceBlocks > 0;
 			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, overlapTraceBlocks ) : grid;
 			ta.prio = (uint32_t)prioTrace;
-			/* early bounce: after the early first shade on the ahead stream, beside the previous frame's tail phase (its own
-			   global stack: the tail's spills use ps.gstack; ps.hits: no launch of the previous frame after its overlap
-			   event reads it); the core stream waits for it before the next shade launch */
-			const bool earlyB = early && earlyBounce > 0 && pathLength == 2 && !ta.packet;
-			if (earlyB)
-			{
-				ta.gstack = ps.aheadStack.ptr;
-				lh2_launch_trace_closest( &sd, &ta, smCount * std::min( blocksPerCU, earlyBounce ), { nullptr, ps.evTrace[pathLength] }, aheadStream );
-				CHK_HIP( hipStreamWaitEvent( stream, ps.evTrace[pathLength], 0 ) );
-			}
-			else lh2_launch_trace_closest( &sd, &ta, g, { nullptr, ps.evTrace[pathLength] }, stream );
+			lh2_launch_trace_closest( &sd, &ta, g, { nullptr, ps.evTrace[pathLength] }, stream );
 		}
 		ps.fromTrace[pathLength] = ps.prevStop, ps.prevStop = ps.evTrace[pathLength];
 		sp.segCounts = segIn, sp.segOut = segNext, sp.segStride = ps.segStride;

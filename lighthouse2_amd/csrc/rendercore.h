@@ -77,7 +77,6 @@ struct PathStreams
 	size_t shCap = 0, shMaskWords = 0;
 	DevBuf<int> gstack;
 	DevBuf<int> sideStack;               /* the side shadow launch's global stack (shadowOverlap) */
-	DevBuf<int> aheadStack;              /* the early bounce launch's global stack (earlyBounce: beside the previous frame's tail) */
 	DevBuf<uint32_t> shSnap;             /* the shadow rays queued before the path tail (B) and, with sideSplit, before the bounce
 	                                        before it (A), per segment (advance_bounce); 2 (parity) x 2 */
 	/* per frame parity (fp): two consecutive frames' counters, work-queue heads, shadow streams and ray-count logs are
@@ -332,10 +331,6 @@ private:
 	   shade launch slows the bounces it overlaps (2.344 / 1.426 ms) */
 	bool shadowOverlap = true;
 	int pathTailBlocks = 0;              /* the path tail's blocks per CU; 0: 2 with the overlap, else its occupancy limit */
-	/* early bounce: in a frame whose first shade launch runs early (earlyShade), its bounce launch follows on the ahead stream
-	   with this many blocks per CU (0: off), beside the previous frame's path tail and shadow launches; the second shade
-	   launch waits for it on the core stream (it writes the ping-pong half the previous frame's tail uses) */
-	int earlyBounce = 0;
 	int sideBlocks = 0;                  /* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's) */
 	int overlapTraceBlocks = 5;          /* blocks per CU of a closest-hit launch that the next frame's primary launch runs
 	                                        beside (an overlapped frame's later bounces, no path tail); 0: the trace grid's */

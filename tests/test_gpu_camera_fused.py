@@ -8,8 +8,7 @@ heavy-packet block the next frame records into is zeroed by the first shade laun
 launch may run ahead, by a memset on the ahead stream).  With earlyShade (default) the first shade launch of a frame after
 one with a path tail follows its primary launch on the ahead stream too, beside the previous frame's path tail and shadow
 launches; with primaryAhead the primary launch of a frame after one without a path tail starts once that frame's
-primary launch is done (primary buffers per frame parity); with earlyBounce the early frame's bounce launch follows its
-first shade launch on the ahead stream too.
+primary launch is done (primary buffers per frame parity).
 
 Against the CPU oracle (pathtracer.h:54-245 after generateEyeRays): identical per-bounce ray counts every frame,
 accumulator rel-L2 <= 1e-4; and frames queued back to back (no host synchronisation between them, so the primary
@@ -74,21 +73,19 @@ def test_camera_fused_frames(fresh_core, kind):
         assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (f, fresh_core.ray_counts()[:6], o.ray_counts()[:6])
     ref = o.accumulator()
     res = {}
-    # (cameraFused, frameOverlap, earlyShade, primaryAhead, earlyBounce)
-    variants = ((1, 1, 1, 1, 0), (1, 1, 1, 2, 0), (1, 1, 0, 2, 0), (1, 1, 1, 0, 0), (1, 1, 1, 0, 7), (1, 1, 1, 2, 4),
-                (1, 1, 0, 0, 0), (1, 0, 0, 0, 0), (0, 0, 0, 0, 0))
-    for fused, overlap, early, ahead, ebounce in variants:
+    # (cameraFused, frameOverlap, earlyShade, primaryAhead)
+    variants = ((1, 1, 1, 1), (1, 1, 1, 2), (1, 1, 0, 2), (1, 1, 1, 0), (1, 1, 0, 0), (1, 0, 0, 0), (0, 0, 0, 0))
+    for fused, overlap, early, ahead in variants:
         fresh_core.setting("cameraFused", fused)
         fresh_core.setting("frameOverlap", overlap)
         fresh_core.setting("earlyShade", early)
         fresh_core.setting("primaryAhead", ahead)
-        fresh_core.setting("earlyBounce", ebounce)
         for f, conv in enumerate(SEQUENCE):   # queued back to back: no synchronisation between frames
             if anim:
                 _animate(sc, fresh_core, f)
             sc.render_frame(fresh_core, converge=conv)
-        res[(fused, overlap, early, ahead, ebounce)] = fresh_core.accumulator()
-        assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (fused, overlap, early, ahead, ebounce)
+        res[(fused, overlap, early, ahead)] = fresh_core.accumulator()
+        assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (fused, overlap, early, ahead)
     a = res[variants[0]]
     assert rel_l2(a[..., :3], ref[..., :3]) <= REL_L2_TOL
     for k in variants[1:]:
@@ -123,9 +120,8 @@ def test_animated_restart_frames(fresh_core, kind):
             fresh_core.set_instance(k, mesh, M)
         fresh_core.update_toplevel()
 
-    def run(n, overlap, double, ebounce=0):
+    def run(n, overlap, double):
         fresh_core.setting("frameOverlap", overlap)
-        fresh_core.setting("earlyBounce", ebounce)
         for f in range(n):
             turn(f)
             if double and f % 2:
@@ -136,9 +132,8 @@ def test_animated_restart_frames(fresh_core, kind):
     for n in (1, 2, 3, 5):
         for double in (False, True):
             a, ca = run(n, 0, double)
+            b, cb = run(n, 1, double)
+            assert np.array_equal(ca, cb), (n, double, ca[:6], cb[:6])
             assert np.any(a[..., :3] != 0)
-            for eb in (0, 7):
-                b, cb = run(n, 1, double, eb)
-                assert np.array_equal(ca, cb), (n, double, eb, ca[:6], cb[:6])
-                assert rel_l2(b[..., :3], a[..., :3]) <= 1e-6, (n, double, eb)
-                assert np.array_equal(a[..., 3], b[..., 3]), (n, double, eb)
+            assert rel_l2(b[..., :3], a[..., :3]) <= 1e-6, (n, double)
+            assert np.array_equal(a[..., 3], b[..., 3]), (n, double)
