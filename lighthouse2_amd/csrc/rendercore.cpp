@@ -95,15 +95,13 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	const char* name = props.gcnArchName[0] ? props.gcnArchName : props.name;
 	coreStats.deviceName = new char[strlen( name ) + 1];   /* owned (and leaked) by the core: core_api_base.h:33 */
 	memcpy( coreStats.deviceName, name, strlen( name ) + 1 );
-	CHK_HIP( hipStreamCreateWithFlags( &stream, hipStreamNonBlocking ) );
+	MakeCoreStream();
 	{
 		int least = 0, greatest = 0;
 		CHK_HIP( hipDeviceGetStreamPriorityRange( &least, &greatest ) );
 		CHK_HIP( hipStreamCreateWithPriority( &sideStream, hipStreamNonBlocking, least ) );
-		/* frameOverlap: the next frame's primary launch yields to the current frame's launches (lowest priority): config 3
-		   1.98 -> 1.96 ms, config-4 N = 8 share 1.19 -> 1.17 ms (profiles/r03m_ab_overlap_policy.txt) */
-		CHK_HIP( hipStreamCreateWithPriority( &aheadStream, hipStreamNonBlocking, least ) );
 	}
+	MakeAheadStream();
 	/* blue noise sampler tables (rendercore.cpp:125-134), shipped as data/bluenoise.bin */
 	std::string path = getenv( "LH2_BLUENOISE" ) ? getenv( "LH2_BLUENOISE" ) : LibraryDir() + "/data/bluenoise.bin";
 	FILE* f = fopen( path.c_str(), "rb" );
@@ -228,6 +226,39 @@ void RenderCore::EnsureStack()
 	if (shadowOverlap && ps.sideStack.count < need) ps.sideStack.resize( need );
 }
 
+/* frameOverlap: the ahead stream at the device's least priority (aheadPriority 0), which on MI355X (range 0 .. -1) is the
+   default level, the core stream's; the high level (aheadPriority 2) and the core stream at the high level (corePriority 1)
+   measured no faster (profiles/r04k_ab.txt, r04l_ab.txt, r04m_ab.txt) */
+void RenderCore::MakeAheadStream()
+{
+	if (aheadStream)
+	{
+		CHK_HIP( hipStreamSynchronize( stream ) );
+		CHK_HIP( hipStreamSynchronize( aheadStream ) );
+		CHK_HIP( hipStreamDestroy( aheadStream ) );
+		aheadStream = nullptr;
+	}
+	int least = 0, greatest = 0;
+	CHK_HIP( hipDeviceGetStreamPriorityRange( &least, &greatest ) );
+	const int prio = aheadPriority >= 2 ? greatest : aheadPriority == 1 ? (least + greatest) / 2 : least;
+	CHK_HIP( hipStreamCreateWithPriority( &aheadStream, hipStreamNonBlocking, prio ) );
+}
+
+void RenderCore::MakeCoreStream()
+{
+	if (stream)
+	{
+		CHK_HIP( hipStreamSynchronize( stream ) );
+		if (aheadStream) CHK_HIP( hipStreamSynchronize( aheadStream ) );
+		if (sideStream) CHK_HIP( hipStreamSynchronize( sideStream ) );
+		CHK_HIP( hipStreamDestroy( stream ) );
+		stream = nullptr;
+	}
+	int least = 0, greatest = 0;
+	CHK_HIP( hipDeviceGetStreamPriorityRange( &least, &greatest ) );
+	CHK_HIP( hipStreamCreateWithPriority( &stream, hipStreamNonBlocking, corePriority ? greatest : least ) );
+}
+
 void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439-457 */
 {
 	if (!strcmp( name, "epsilon" )) geometryEpsilon = value;
@@ -272,6 +303,16 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "prioTrace" )) prioTrace = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "sideSplit" )) sideSplit = value != 0;
 	else if (!strcmp( name, "earlyShadeMaxPaths" )) earlyShadeMaxPaths = std::max( 0.0f, value );
+	else if (!strcmp( name, "corePriority" ))
+	{
+		const int v = value != 0 ? 1 : 0;
+		if (v != corePriority) { corePriority = v; if (initialized) MakeCoreStream(); }
+	}
+	else if (!strcmp( name, "aheadPriority" ))
+	{
+		const int v = std::min( 2, std::max( 0, (int)value ) );
+		if (v != aheadPriority) { aheadPriority = v; if (initialized) MakeAheadStream(); }
+	}
 	else if (!strcmp( name, "sideBlocks" )) sideBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
@@ -298,7 +339,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvhSpatialMinRefs", (float)bvhSpatialMinRefs }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
-		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "sideBlocks", (float)sideBlocks }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },

@@ -184,8 +184,14 @@ public:
 
 	lh2_CoreStats coreStats{};
 	hipStream_t stream = nullptr;
-	hipStream_t sideStream = nullptr;    /* shadowOverlap: lowest priority */
+	hipStream_t sideStream = nullptr;    /* shadowOverlap: the device's least priority (the default level on MI355X) */
 	hipStream_t aheadStream = nullptr;   /* frameOverlap: the fused primary launch */
+	/* stream priorities (HIP's range on MI355X is 0 = the default .. -1 = high): the ahead stream's, 0 the default (the
+	   device's least: the same level as the core stream), 2 high; the core stream's, 0 the default, 1 high (the current
+	   frame's launches dispatch before the next frame's primary launch and the side shadow launch) */
+	int aheadPriority = 0, corePriority = 0;
+	void MakeAheadStream();
+	void MakeCoreStream();
 
 private:
 	void EnsureBuffers();
@@ -324,14 +330,16 @@ private:
 	   a wave shading its finished queries once pathTailBatch lanes hold one (or none walks); 0: a launch
 	   pair per bounce.  Config 3 (profiles/r02zb_ab_path_tail.txt): 2.542 -> 2.389 ms per frame at 3 / 56 */
 	int pathTail = 3, pathTailBatch = 56;
-	/* shadow overlap: the shadow rays queued before the path tail are traced on a low-priority side stream
+	/* shadow overlap: the shadow rays queued before the path tail are traced on a side stream
 	   while the path tail runs (latency bound, it leaves much of the chip idle); the final shadow launch
 	   traces only the path tail's.  Config 3 2.29 -> 2.235 ms, config-4 rank share at N = 8 1.431 -> 1.363
 	   ms with the tail at 2 blocks per CU (profiles/r03g_overlap_sweep.txt); a side launch after every
 	   shade launch slows the bounces it overlaps (2.344 / 1.426 ms) */
 	bool shadowOverlap = true;
 	int pathTailBlocks = 0;              /* the path tail's blocks per CU; 0: 2 with the overlap, else its occupancy limit */
-	int sideBlocks = 0;                  /* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's) */
+	/* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's): 4 leaves the next frame's primary
+	   and early shade launches room: config 3 -0.5 %, the N = 8 share -0.8 to -1.5 % (profiles/r04m_ab.txt, r04n_ab.txt) */
+	int sideBlocks = 4;
 	int overlapTraceBlocks = 5;          /* blocks per CU of a closest-hit launch that the next frame's primary launch runs
 	                                        beside (an overlapped frame's later bounces, no path tail); 0: the trace grid's */
 	/* heavy-first primary packets (TraceArgs::hvRead): the packets of the previous frame that took more than
