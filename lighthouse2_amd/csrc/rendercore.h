@@ -336,7 +336,11 @@ private:
 	   ms with the tail at 2 blocks per CU (profiles/r03g_overlap_sweep.txt); a side launch after every
 	   shade launch slows the bounces it overlaps (2.344 / 1.426 ms) */
 	bool shadowOverlap = true;
-	int pathTailBlocks = 0;              /* the path tail's blocks per CU; 0: 2 with the overlap, else its occupancy limit */
+	int pathTailBlocks = 0;              /* the path tail's blocks per CU; 0: with the overlap 3 for frames of at most
+	                                        pathTailSmallPaths paths, else 2 (without: its occupancy limit) */
+	/* 3 blocks per CU: the N = 8 share 1.133 -> 1.112-1.125 ms, config 3 unchanged, the 4K frame 6.54 -> 6.64-6.69 ms
+	   (profiles/r04o_ab.txt, r04p_ab.txt) */
+	float pathTailSmallPaths = 4.2e6f;
 	/* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's): 4 leaves the next frame's primary
 	   and early shade launches room: config 3 -0.5 %, the N = 8 share -0.8 to -1.5 % (profiles/r04m_ab.txt, r04n_ab.txt) */
 	int sideBlocks = 4;
