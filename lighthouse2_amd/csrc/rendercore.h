@@ -295,8 +295,9 @@ private:
 	   the sequential one within float rounding, not bit for bit (the first-vertex depths, w, stay exact) */
 	int earlyShade = 1;
 	/* ... for frames of at most this many paths: beside a large frame's tail the early shade gains nothing and its fold
-	   (FrameStatsDev::delta) costs (config-4 N = 1 frames 1 % slower, the N = 8 share 1.5 % faster: profiles/r04e_ab.txt) */
-	float earlyShadeMaxPaths = 4.2e6f;
+	   (FrameStatsDev::delta) costs (config-4 N = 1 frames 1 % slower, the N = 8 share 1.5 % faster: profiles/r04e_ab.txt;
+	   the N = 2 share, 4.1 M paths, 0.3 % faster without: r04r_ab.txt) */
+	float earlyShadeMaxPaths = 2.5e6f;
 	/* 1: after a frame without a path tail (config 2: every path ends at its second vertex), 2: after every frame: the
 	   next frame's primary launch waits only for this frame's primary launch and the finalize of the frame before (its
 	   parity's last user), so it runs beside this frame's first shade launch and bounce, not only beside the bounce */
@@ -338,9 +339,9 @@ private:
 	bool shadowOverlap = true;
 	int pathTailBlocks = 0;              /* the path tail's blocks per CU; 0: with the overlap 3 for frames of at most
 	                                        pathTailSmallPaths paths, else 2 (without: its occupancy limit) */
-	/* 3 blocks per CU: the N = 8 share 1.133 -> 1.112-1.125 ms, config 3 unchanged, the 4K frame 6.54 -> 6.64-6.69 ms
-	   (profiles/r04o_ab.txt, r04p_ab.txt) */
-	float pathTailSmallPaths = 4.2e6f;
+	/* 3 blocks per CU: the N = 8 share 1.133 -> 1.112-1.125 ms, config 3 unchanged, the 4K frame 6.54 -> 6.64-6.69 ms and
+	   the N = 2 share (4.1 M paths) 3.48 -> 3.53 ms (profiles/r04p_ab.txt, r04r_ab.txt) */
+	float pathTailSmallPaths = 2.5e6f;
 	/* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's): 4 leaves the next frame's primary
 	   and early shade launches room: config 3 -0.5 %, the N = 8 share -0.8 to -1.5 % (profiles/r04m_ab.txt, r04n_ab.txt) */
 	int sideBlocks = 4;

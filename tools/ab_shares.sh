@@ -11,11 +11,11 @@ for rep in $(seq 1 "${REPS:-3}"); do
     args=()
     if [ "$v" != "base" ]; then IFS=',' read -ra kvs <<< "$v"; for kv in "${kvs[@]}"; do args+=(--setting "$kv"); done; fi
     n="${v//[=,]/_}_$rep"
-    timeout -k 10 200 python3 tools/config4_shares.py --ranks 1,8 "${args[@]}" > "$OUT/sh_$n.jsonl" 2> "$OUT/sh_$n.err"
+    timeout -k 10 200 python3 tools/config4_shares.py --ranks "${RANKS:-1,8}" "${args[@]}" > "$OUT/sh_$n.jsonl" 2> "$OUT/sh_$n.err"
     python3 - "$OUT/sh_$n.jsonl" "$v" <<'PY'
 import json, sys
 sh = [json.loads(l) for l in open(sys.argv[1]) if l.strip()]
-print(f"{sys.argv[2]:40s} N1 {sh[0]['ms_per_frame']:.4f} N8 {sh[-1]['ms_per_frame']:.4f} ratio {sh[0]['ms_per_frame'] / sh[-1]['ms_per_frame']:.3f}", flush=True)
+print(f"{sys.argv[2]:40s} " + " ".join(f"N{s['ranks']} {s['ms_per_frame']:.4f}" for s in sh) + f" ratio {sh[0]['ms_per_frame'] / sh[-1]['ms_per_frame']:.3f}", flush=True)
 PY
   done
 done
