@@ -315,6 +315,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	}
 	else if (!strcmp( name, "sideBlocks" )) sideBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "finalShadowBlocks" )) finalShadowBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailSmallPaths" )) pathTailSmallPaths = std::max( 0.0f, value );
 	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
@@ -340,7 +341,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvhSpatialMinRefs", (float)bvhSpatialMinRefs }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
-		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "pathTailSmallPaths", pathTailSmallPaths }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "pathTailSmallPaths", pathTailSmallPaths }, { "finalShadowBlocks", (float)finalShadowBlocks }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -1252,7 +1253,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.cursor = cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.mask = shMask, ta.potentials = shP, ta.acc = accumulator.ptr, ta.gstack = ps.gstack.ptr;
 		ta.prio = (uint32_t)prioShadow;
-		lh2_launch_trace_any( &sd, &ta, grid, 1, { nullptr, ps.evShadow }, stream );
+		lh2_launch_trace_any( &sd, &ta, finalShadowBlocks > 0 ? smCount * finalShadowBlocks : grid, 1, { nullptr, ps.evShadow }, stream );
 		ps.fromShadow = ps.prevStop;
 	}
 	/* the side launch's contributions are in the accumulator before the frame is finalized */
