@@ -566,8 +566,16 @@ void RenderCore::FlushBuilds()
 	const int perJob = std::max( 1, workers / std::max( 1, (int)jobs.size() ) );
 	std::atomic<int> next{ 0 };
 	std::vector<std::string> errors( nthreads );
+	/* the last jobs, fewer than the workers, get the idle workers' share as threads of their own build (SBVH subtrees) */
 	auto work = [&]( int w ) {
-		try { for (int j; (j = next.fetch_add( 1 )) < (int)jobs.size();) jobs[j]->build( perJob ); }
+		try
+		{
+			for (int j; (j = next.fetch_add( 1 )) < (int)jobs.size();)
+			{
+				const int remaining = (int)jobs.size() - j;
+				jobs[j]->build( std::max( perJob, std::min( 8, workers / std::max( 1, remaining ) ) ) );
+			}
+		}
 		catch (const std::exception& e) { errors[w] = e.what(); }
 	};
 	std::vector<std::thread> pool;

@@ -320,9 +320,10 @@ private:
 	   at a third of the build time (config 2 0.39 vs 1.44 s, the room 1.26 vs 2.88 s; profiles/r04d_sbvh_alpha.txt) */
 	float bvhSpatial = 1e-3f;
 	float bvhSpatialBudget = 1.0f;       /* ... adding at most this many references per triangle */
-	/* ... in nodes of at least this many references (64: 0.3 % more node steps on config 2, config-5 setup within noise
-	   on the GPU box once the spatial binning was direct, profiles/r04g_sbvh_build.txt; 0: every node) */
-	int bvhSpatialMinRefs = 0;
+	/* ... in nodes of at least this many references (0: every node): 64 builds config 5's 100 meshes 17-20 % faster
+	   (setup 4.55 -> 3.64-3.76 s on one box) for 0.3 % more node steps (config-5 frame +0.4 %; config 2 and 3 within the
+	   noise), profiles/r04g_sbvh_build.txt, r04u_config5_setup.jsonl */
+	int bvhSpatialMinRefs = 64;
 	int bvh4Collapse = 1;                /* BVH4 collapse: 0 greedy (CollapseBvh4), 1 dynamic programming (CollapseBvh4Sah) */
 	float chordSplit = 0.35f;            /* extension rays with a chord through the scene box below this x its extent are traced last */
 	float sceneLo[3] = { 0, 0, 0 }, sceneHi[3] = { 0, 0, 0 };   /* world box of the instanced meshes (UpdateToplevel) */

@@ -24,7 +24,7 @@ import torch  # noqa: E402,F401  (one HIP runtime in the process)
 from lighthouse2_amd import scene  # noqa: E402
 from lighthouse2_amd.core import RenderCore  # noqa: E402
 
-BUILDERS = {"cpu_sbvh": (), "cpu_sbvh_min0": (("bvhSpatialMinRefs", 0.0),), "cpu_sbvh_1e-5": (("bvhSpatial", 1e-5),), "cpu_sah": (("bvhSpatial", 0.0),),
+BUILDERS = {"cpu_sbvh": (), "cpu_sbvh_min0": (("bvhSpatialMinRefs", 0.0),), "cpu_sbvh_min64": (("bvhSpatialMinRefs", 64.0),), "cpu_sbvh_1e-5": (("bvhSpatial", 1e-5),), "cpu_sah": (("bvhSpatial", 0.0),),
             "gpu_ploc": (("gpuBuild", 1.0),)}
 
 
