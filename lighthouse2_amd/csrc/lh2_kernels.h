@@ -200,7 +200,7 @@ void lh2_launch_finalize( float4* acc, float4* out, int n, float scale, const Fr
 #define LH2_CURSOR_WORDS (2 * LH2_CHUNKS * LH2_CURSOR_STRIDE)
 #define LH2_HEAVY_CURSOR (LH2_CHUNKS * LH2_CURSOR_STRIDE)
 #define LH2_MAX_BOUNCES 64                                   /* RenderCore_PrimeRef MAXPATHLENGTH (core_settings.h:25) */
-#define LH2_CURSOR_SLOTS (2 * LH2_MAX_BOUNCES + 5)           /* launches per frame: [L] bounce L, [64 + L] shadow after bounce L, [130] shadow, [131] side shadow, [132] first side shadow (sideSplit) */
+#define LH2_CURSOR_SLOTS (2 * LH2_MAX_BOUNCES + 5)           /* launches per frame: [L] bounce L, [64 + L] shadow after bounce L, [130] shadow, [131] side shadow */
 #define LH2_SHADOW_SLOT (2 * LH2_MAX_BOUNCES + 2)
 /* traversal stacks: LH2_STACK_LDS entries per lane in LDS (16 x 256 x 4 B = 16 KiB per block), the rest in global memory */
 #ifndef LH2_STACK_LDS

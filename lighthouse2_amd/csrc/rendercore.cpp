@@ -131,8 +131,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipEventCreate( &ps.evCamera ) );
 	CHK_HIP( hipEventCreate( &ps.evShadow ) );
 	CHK_HIP( hipEventCreate( &ps.evSide ) );
-	CHK_HIP( hipEventCreate( &ps.evSideA ) );
-	ps.shSnap.resize( 4 * LH2_SEGS * LH2_SEGCOUNT_STRIDE );
+	ps.shSnap.resize( 2 * LH2_SEGS * LH2_SEGCOUNT_STRIDE );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
@@ -301,7 +300,6 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "prioSide" )) prioSide = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "prioPrimary" )) prioPrimary = std::min( 3, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "prioTrace" )) prioTrace = std::min( 3, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "sideSplit" )) sideSplit = value != 0;
 	else if (!strcmp( name, "earlyShadeMaxPaths" )) earlyShadeMaxPaths = std::max( 0.0f, value );
 	else if (!strcmp( name, "corePriority" ))
 	{
@@ -341,7 +339,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvhSpatialMinRefs", (float)bvhSpatialMinRefs }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
-		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "sideSplit", (float)sideSplit }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "pathTailSmallPaths", pathTailSmallPaths }, { "finalShadowBlocks", (float)finalShadowBlocks }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "pathTailSmallPaths", pathTailSmallPaths }, { "finalShadowBlocks", (float)finalShadowBlocks }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -928,8 +926,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	float4* const shD = ps.shD.ptr + (size_t)ps.fp * ps.shCap;
 	float4* const shP = ps.shP.ptr + (size_t)ps.fp * ps.shCap;
 	uint32_t* const shMask = ps.shMask.ptr + (size_t)ps.fp * ps.shMaskWords;
-	uint32_t* const shSnap = ps.shSnap.ptr + (size_t)(2 * ps.fp) * LH2_SEGS * LH2_SEGCOUNT_STRIDE;   /* B: before the tail */
-	uint32_t* const shSnapA = shSnap + (size_t)LH2_SEGS * LH2_SEGCOUNT_STRIDE;                         /* A (sideSplit) */
+	uint32_t* const shSnap = ps.shSnap.ptr + (size_t)ps.fp * LH2_SEGS * LH2_SEGCOUNT_STRIDE;   /* the rays queued before the tail */
 	float4* const frameDelta = delta.ptr + (size_t)ps.fp * scrwidth * scrheight;
 	/* primary rays (camera.h) for every sample of the tile; the camera launch also resets the frame's
 	   counters and work-queue heads (k_init_counters) */
@@ -1050,9 +1047,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const bool overlap = shadows && tailL && shadowOverlap;
 	bool snapped = false;
 	bool besideNext = false;   /* the next frame's primary launch may run beside the launches from here on */
-	ps.sideOn = false, ps.sideAOn = false;
-	/* sideSplit: the shadow rays of the shade launch before the bounce before the tail on the side stream beside that bounce */
-	const bool splitSide = overlap && sideSplit && tailL >= 3;
+	ps.sideOn = false;
 	/* the bounce loop */
 	for (int pathLength = 1; pathLength <= maxPL; pathLength++)
 	{
@@ -1158,11 +1153,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		/* the hand-off to the next bounce: the shade launch's last block (no launch of its own), except
 		   in PrimeRef mode, where the bounce's shadow rays are traced (and their counts reset) first */
 		const bool snap = overlap && pathLength + 1 == tailL;
-		/* snapshot A (sideSplit): the first side launch's counts, and the start of the second one's work-queue heads */
-		const bool snapA = splitSide && pathLength + 2 == tailL;
 		const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, rayLog, ps.activeLog, pathLength + 1 == tailL,
-			snap ? shSnap : snapA ? shSnapA : nullptr,
-			snap ? cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : snapA ? cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS : nullptr };
+			snap ? shSnap : nullptr, snap ? cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr };
 		snapped = snapped || snap;
 		sp.advance = pathLength < maxPL && !primeRef;
 		sp.adv = adv;
@@ -1188,21 +1180,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		lh2_launch_shade( &sd, &sp, grid, { nullptr, ps.evShade[pathLength] }, earlyHere ? aheadStream : stream );
 		if (earlyHere) CHK_HIP( hipStreamWaitEvent( stream, ps.evShade[pathLength], 0 ) );
 		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];
-		if (snapA)
-		{
-			/* the first side launch: the shadow rays queued so far (snapshot A), beside this frame's next bounce */
-			CHK_HIP( hipStreamWaitEvent( sideStream, ps.evShade[pathLength], 0 ) );
-			TraceArgs ts{};
-			ts.version = TraceVersion();
-			ts.rayO = shO, ts.rayD = shD, ts.segCounts = shSnapA, ts.segStride = ps.shadowStride;
-			ts.cursor = cursors + (size_t)(LH2_SHADOW_SLOT + 2) * LH2_CURSOR_WORDS;
-			ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
-			ts.mask = shMask, ts.potentials = shP, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
-			ts.prio = (uint32_t)prioSide;
-			lh2_launch_trace_any( &sd, &ts, grid, 1, { nullptr, ps.evSideA }, sideStream );
-			ps.fromSideA = ps.evShade[pathLength];
-			ps.sideAOn = true;
-		}
 		/* the next frame's primary launch starts after this frame's first shade launch (the last reader of the primary
 		   buffers), or (frameOverlap 1) after the shade launch before the path tail: beside the latency-bound tail */
 		if (pathLength == 1 || (frameOverlap == 1 && tailL && pathLength == tailL - 1))
@@ -1247,10 +1224,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	}
 	/* a snapshot whose side launch did not happen (the frame ended before its path tail): the final launch
 	   traces every shadow ray, from the first */
-	if (!ps.sideOn && ps.sideAOn)   /* ... except those the first side launch traced (sideSplit): from snapshot A */
-		CHK_HIP( hipMemcpyAsync( cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS,
-			sizeof( uint32_t ) * LH2_CURSOR_WORDS, hipMemcpyDeviceToDevice, stream ) );
-	else if (snapped && !ps.sideOn)
+	if (snapped && !ps.sideOn)
 		CHK_HIP( hipMemsetAsync( cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
 	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
 	if (!primeRef && shadows)
@@ -1266,7 +1240,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	}
 	/* the side launch's contributions are in the accumulator before the frame is finalized */
 	if (ps.sideOn) CHK_HIP( hipStreamWaitEvent( stream, ps.evSide, 0 ) );
-	if (ps.sideAOn) CHK_HIP( hipStreamWaitEvent( stream, ps.evSideA, 0 ) );
 	samplesTaken += scrspp;
 	/* finalize also delivers the frame's counters and ray-count log, and the scene error, to hostStats */
 	const FrameStatsDev fs{ c, rayLog + 1, &hostStats->counters, hostStats->rayCount + 1, SceneErr( frameTlas ), &hostStats->sceneError,
@@ -1385,7 +1358,7 @@ void RenderCore::Synchronize()
 	}
 	float shadow = 0, shade = 0;
 	if (frameShadows && !framePrimeRef)
-		shadow = ms( ps.fromShadow, ps.evShadow ) + (ps.sideOn ? ms( ps.fromSide, ps.evSide ) : 0.0f) + (ps.sideAOn ? ms( ps.fromSideA, ps.evSideA ) : 0.0f);
+		shadow = ms( ps.fromShadow, ps.evShadow ) + (ps.sideOn ? ms( ps.fromSide, ps.evSide ) : 0.0f);
 	else if (frameShadows) for (int L = 1; L < ps.pl; L++) shadow += ms( ps.fromShadowB[L], ps.evShadowB[L] );
 	for (int L = 1; L <= ps.pl; L++) if (L != ps.tailL) shade += ms( ps.fromShade[L], ps.evShade[L] );
 	coreStats.shadowTraceTime = shadow;
@@ -1657,7 +1630,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto& e : ps.evShade) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evShadowB) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evCount) (void)hipEventDestroy( e ), e = nullptr;
-	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow, &ps.evSide, &ps.evSideA }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
+	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow, &ps.evSide }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
 	if (ps.activeLog) (void)hipHostFree( ps.activeLog );
 	ps.activeLog = nullptr;
 	for (hipEvent_t* e : { &evConsumer, &evPacked }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }

@@ -77,8 +77,7 @@ struct PathStreams
 	size_t shCap = 0, shMaskWords = 0;
 	DevBuf<int> gstack;
 	DevBuf<int> sideStack;               /* the side shadow launch's global stack (shadowOverlap) */
-	DevBuf<uint32_t> shSnap;             /* the shadow rays queued before the path tail (B) and, with sideSplit, before the bounce
-	                                        before it (A), per segment (advance_bounce); 2 (parity) x 2 */
+	DevBuf<uint32_t> shSnap;             /* the shadow rays queued before the path tail, per segment (advance_bounce), per frame parity */
 	/* per frame parity (fp): two consecutive frames' counters, work-queue heads, shadow streams and ray-count logs are
 	   apart, so the next frame's first launches can run beside this frame's last ones (frame overlap, early shade) */
 	DevBuf<Counters> counters;           /* 2 */
@@ -93,8 +92,6 @@ struct PathStreams
 	hipEvent_t evCount[LH2_MAX_BOUNCES + 2] = {}, evCamera = nullptr, evShadow = nullptr;
 	hipEvent_t evSide = nullptr, fromSide = nullptr;   /* shadowOverlap: the side launch */
 	bool sideOn = false;                 /* this frame traced its early shadow rays on the side stream */
-	hipEvent_t evSideA = nullptr, fromSideA = nullptr; /* sideSplit: the first side launch (the bounce before the tail) */
-	bool sideAOn = false;
 	hipEvent_t countReady[LH2_MAX_BOUNCES + 2] = {};   /* [L]: the event after which bounce L's hand-off is done (evShade or evCount, not owned) */
 	hipEvent_t fromTrace[LH2_MAX_BOUNCES + 1] = {}, fromShade[LH2_MAX_BOUNCES + 1] = {}, fromShadowB[LH2_MAX_BOUNCES + 1] = {}, fromShadow = nullptr;
 	/* this frame */
@@ -305,9 +302,6 @@ private:
 	/* issue priorities (s_setprio, TraceArgs::prio) of the frame's traversal launches: the path tail, the final shadow
 	   launch, the side shadow launch, the primary launch, the bounce launches */
 	int prioTail = 0, prioShadow = 0, prioSide = 0, prioPrimary = 0, prioTrace = 0;
-	/* shadow overlap in two side launches: the shadow rays queued by the shade launch before the bounce before the path
-	   tail are traced beside that bounce, the rest beside the tail */
-	int sideSplit = 0;
 	uint64_t sceneVersion = 0;           /* incremented by every change of device-resident scene data or buffers */
 	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle; BLAS leaves parked until this many
 	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,
