@@ -124,6 +124,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	unsigned long long* stats;                        /* LH2_TRACE_STATS / LH2_TRACE_TIMES builds: per-launch counters */
 	uint32_t shadeBatch;                              /* path tail (k_trace_path4d): shade once >= shadeBatch lanes finished a query */
 	uint32_t prio;                                    /* the launch's waves' issue priority (s_setprio 0..3) against launches beside it */
+	uint32_t tailWaves;                               /* path tail (lh2_launch_trace_path): the kernel variant for 4 waves per SIMD (4) or 3 */
 	/* heavy-first packets (packet kernel, hvWrite non-null): the previous frame's packets that took more
 	   than hvFactor x its mean node steps (hvRead: per-segment counts, step sums, a bit per packet and the
 	   lists of packet bits) are taken first, the rest in order; this frame's are recorded into hvWrite.
@@ -173,7 +174,7 @@ int lh2_trace_blocks_per_cu( void );
 int lh2_packet_blocks_per_cu( void );
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
-int lh2_path_blocks_per_cu( void );
+int lh2_path_blocks_per_cu( int waves );
 void lh2_launch_spin( unsigned long long ticks, hipStream_t st );
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
 void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );

@@ -1618,11 +1618,11 @@ __global__ __launch_bounds__( 256 ) void k_shade_last( const SceneDev s, const S
    on with the extension ray in place, so a path's later bounces do not wait for every other path's
    (the few rays of the deep bounces run latency-bound: config 3's bounces 3 and 4 took 292 + 200 us for
    ~0.6 M rays as launches of their own).  The shade code's registers set the occupancy */
-#ifndef LH2_PATH_MINWAVES
-#define LH2_PATH_MINWAVES 3   /* 4: 128 VGPRs + 176 B of spills (lit); config 3 tail 0.655 ms at 4, 0.558 ms at 3 */
-#endif
-template <bool NL, bool SINGLE>
-__global__ __launch_bounds__( 256, LH2_PATH_MINWAVES ) void k_trace_path4d( const SceneDev s, const TraceArgs a, const ShadeParams p )
+/* W: the waves per SIMD the kernel is compiled for.  3: the lit variant's 168 VGPRs, no spills; 4: 128 VGPRs and ~190 B
+   of spills.  Beside the side shadow launch a large frame's tail phase is 3 % faster with 4 (the 4K frame 6.58 -> 6.39 ms),
+   a small frame's 3.5 % slower (the N = 8 share 1.125 -> 1.165 ms, profiles/r04w_ab.txt): TraceArgs::tailWaves picks */
+template <bool NL, bool SINGLE, int W>
+__global__ __launch_bounds__( 256, W ) void k_trace_path4d( const SceneDev s, const TraceArgs a, const ShadeParams p )
 {
 	__shared__ int lstack[LH2_STACK_LDS * 256];
 	__shared__ __attribute__( (aligned( 4096 )) ) int lrefs[4 * 256];
@@ -2053,16 +2053,31 @@ void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadePa
 {
 	if (!s->nodes4) return;   /* the host selects the path tail only over a BVH4 */
 	const bool nl = s->nArea + s->nPoint + s->nSpot + s->nDir == 0, single = s->tlasRoot4 < 0;
-	if (nl && single) LH2_LAUNCH( (k_trace_path4d<true, true>), grid, 256, st, ev, *s, *a, *p );
-	else if (nl) LH2_LAUNCH( (k_trace_path4d<true, false>), grid, 256, st, ev, *s, *a, *p );
-	else if (single) LH2_LAUNCH( (k_trace_path4d<false, true>), grid, 256, st, ev, *s, *a, *p );
-	else LH2_LAUNCH( (k_trace_path4d<false, false>), grid, 256, st, ev, *s, *a, *p );
+	if (a->tailWaves == 4)
+	{
+		if (nl && single) LH2_LAUNCH( (k_trace_path4d<true, true, 4>), grid, 256, st, ev, *s, *a, *p );
+		else if (nl) LH2_LAUNCH( (k_trace_path4d<true, false, 4>), grid, 256, st, ev, *s, *a, *p );
+		else if (single) LH2_LAUNCH( (k_trace_path4d<false, true, 4>), grid, 256, st, ev, *s, *a, *p );
+		else LH2_LAUNCH( (k_trace_path4d<false, false, 4>), grid, 256, st, ev, *s, *a, *p );
+	}
+	else if (nl && single) LH2_LAUNCH( (k_trace_path4d<true, true, 3>), grid, 256, st, ev, *s, *a, *p );
+	else if (nl) LH2_LAUNCH( (k_trace_path4d<true, false, 3>), grid, 256, st, ev, *s, *a, *p );
+	else if (single) LH2_LAUNCH( (k_trace_path4d<false, true, 3>), grid, 256, st, ev, *s, *a, *p );
+	else LH2_LAUNCH( (k_trace_path4d<false, false, 3>), grid, 256, st, ev, *s, *a, *p );
 }
-int lh2_path_blocks_per_cu( void )
+int lh2_path_blocks_per_cu( int waves )
 {
 	int n = 0, n2 = 0;
-	(void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_path4d<false, false>, 256, 0 );
-	(void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_path4d<false, true>, 256, 0 );
+	if (waves == 4)
+	{
+		(void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_path4d<false, false, 4>, 256, 0 );
+		(void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_path4d<false, true, 4>, 256, 0 );
+	}
+	else
+	{
+		(void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_path4d<false, false, 3>, 256, 0 );
+		(void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_path4d<false, true, 3>, 256, 0 );
+	}
 	return n < n2 ? n : n2;
 }
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st )

@@ -115,7 +115,8 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	dBlueNoise.upload( bn.data(), bn.size(), stream );
 	blocksPerCU = maxBlocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
 	packetBlocksPerCU = std::max( 1, std::min( 8, lh2_packet_blocks_per_cu() ) );
-	pathBlocksPerCU = std::max( 1, std::min( 8, lh2_path_blocks_per_cu() ) );
+	pathBlocksPerCU = std::max( 1, std::min( 8, lh2_path_blocks_per_cu( 3 ) ) );
+	pathBlocksPerCU4 = std::max( 1, std::min( 8, lh2_path_blocks_per_cu( 4 ) ) );
 	ps.counters.resize( 2 );
 	CHK_HIP( hipMemsetAsync( ps.counters.ptr, 0, sizeof( Counters ) * 2, stream ) );
 	ps.cursors.resize( 2 * (size_t)LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS );
@@ -314,6 +315,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "sideBlocks" )) sideBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "finalShadowBlocks" )) finalShadowBlocks = std::min( 8, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "pathTailWaves" )) pathTailWaves = std::min( 4, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailSmallPaths" )) pathTailSmallPaths = std::max( 0.0f, value );
 	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
@@ -339,7 +341,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvhSpatialMinRefs", (float)bvhSpatialMinRefs }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
-		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "pathTailSmallPaths", pathTailSmallPaths }, { "finalShadowBlocks", (float)finalShadowBlocks }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "pathTailSmallPaths", pathTailSmallPaths }, { "pathTailWaves", (float)pathTailWaves }, { "finalShadowBlocks", (float)finalShadowBlocks }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
@@ -1100,8 +1102,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			/* with the overlap the path tail runs fewer blocks per CU and leaves registers for the side launch's waves
 			   (pathTailBlocks; 0: 3 for small frames, whose tail phase is the frame's longest, else 2) */
 			const bool side = overlap && snapped;
-			const int ptBlocks = pathTailBlocks > 0 ? pathTailBlocks : side ? ((float)pathCount <= pathTailSmallPaths ? 3 : 2) : pathBlocksPerCU;
-			lh2_launch_trace_path( &sd, &ta, &sp, smCount * std::min( std::min( blocksPerCU, pathBlocksPerCU ), ptBlocks ), { nullptr, ps.evTrace[pathLength] }, stream );
+			const bool small = (float)pathCount <= pathTailSmallPaths;
+			/* the kernel variant: 3 waves per SIMD (no spills) for small frames, 4 (128 VGPRs) for large ones (pathTailWaves) */
+			ta.tailWaves = pathTailWaves == 3 || pathTailWaves == 4 ? (uint32_t)pathTailWaves : small ? 3u : 4u;
+			const int occ = ta.tailWaves == 4 ? pathBlocksPerCU4 : pathBlocksPerCU;
+			const int ptBlocks = pathTailBlocks > 0 ? pathTailBlocks : side ? (small ? 3 : 2) : occ;
+			lh2_launch_trace_path( &sd, &ta, &sp, smCount * std::min( std::min( blocksPerCU, occ ), ptBlocks ), { nullptr, ps.evTrace[pathLength] }, stream );
 			if (side)
 			{
 				/* the shadow rays of the bounces before the tail, beside it on the side stream (segment counts:

@@ -212,7 +212,7 @@ private:
 	int PacketGrid() const { return smCount * packetBlocksPerCU; }   /* packet kernel: its own occupancy */
 	int PathGrid() const { return smCount * std::min( blocksPerCU, pathBlocksPerCU ); }   /* path tail: its occupancy, within the stack's */
 
-	int device = 0, smCount = 256, blocksPerCU = 7, maxBlocksPerCU = 7, packetBlocksPerCU = 8, pathBlocksPerCU = 3;
+	int device = 0, smCount = 256, blocksPerCU = 7, maxBlocksPerCU = 7, packetBlocksPerCU = 8, pathBlocksPerCU = 3, pathBlocksPerCU4 = 4;
 	bool initialized = false;
 	/* scene */
 	std::vector<CoreMeshHost*> meshes;
@@ -337,6 +337,8 @@ private:
 	/* 3 blocks per CU: the N = 8 share 1.133 -> 1.112-1.125 ms, config 3 unchanged, the 4K frame 6.54 -> 6.64-6.69 ms and
 	   the N = 2 share (4.1 M paths) 3.48 -> 3.53 ms (profiles/r04p_ab.txt, r04r_ab.txt) */
 	float pathTailSmallPaths = 2.5e6f;
+	/* the path tail kernel's variant: 0, by frame size (3 waves per SIMD for small frames, 4 for larger ones); 3 or 4 */
+	int pathTailWaves = 0;
 	int finalShadowBlocks = 0;           /* blocks per CU of the frame's last shadow launch (0: the trace grid's) */
 	/* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's): 4 leaves the next frame's primary
 	   and early shade launches room: config 3 -0.5 %, the N = 8 share -0.8 to -1.5 % (profiles/r04m_ab.txt, r04n_ab.txt) */

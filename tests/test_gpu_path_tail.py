@@ -45,13 +45,17 @@ def _scene(kind, w, h):
 
 @pytest.mark.parametrize("kind,depth", [("room", 4), ("room", 6), ("specular", 5), ("instanced", 4)])
 @pytest.mark.parametrize("tail", [2, 3])
-def test_path_tail_frame_parity(fresh_core, kind, depth, tail):
+@pytest.mark.parametrize("waves", [0, 4])
+def test_path_tail_frame_parity(fresh_core, kind, depth, tail, waves):
+    """The path tail against the oracle and against a launch pair per bounce; waves 4: the kernel variant compiled for
+    4 waves per SIMD (128 VGPRs, spills), which large frames use (pathTailWaves; 0: by frame size, 3 here)."""
     w, h = 128, 72
     sc = _scene(kind, w, h)
     o = _load_both(fresh_core, sc, w, h)
     for tgt in (fresh_core, o):
         tgt.setting("maxPathLength", depth)
     fresh_core.setting("pathTail", tail)
+    fresh_core.setting("pathTailWaves", waves)
     for f in range(2):
         sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
         sc.render_frame(o, converge=1 if f == 0 else 0)
