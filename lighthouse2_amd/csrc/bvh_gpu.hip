@@ -661,6 +661,9 @@ void GpuBvhBuilder::Reserve( int n )
 		CHK( hipHostMalloc( (void**)&hred, 16 * sizeof( uint32_t ), hipHostMallocDefault ) );
 	}
 	if (n <= cap) return;
+	/* the TLAS builds run on the core's ahead stream and the BLAS builds on its core stream, both with this scratch: the
+	   old buffers are freed only once no launch on any stream can still use them */
+	if (cap) CHK( hipDeviceSynchronize() );
 	cap = std::max( n, 64 );
 	const size_t c = (size_t)cap, c2 = 2 * c;
 	grow_buf( (Box8*&)boxes, c2 ); grow_buf( (Box8*&)prim, c ); grow_buf( (Box8*&)cl[0], c ); grow_buf( (Box8*&)cl[1], c );
@@ -674,7 +677,7 @@ void* GpuBvhBuilder::Scratch( size_t bytes )
 {
 	if (bytes > tmpBytes)
 	{
-		if (tmp) CHK( hipFree( tmp ) );
+		if (tmp) { CHK( hipDeviceSynchronize() ); CHK( hipFree( tmp ) ); }
 		tmpBytes = std::max<size_t>( bytes, 1 << 20 );
 		CHK( hipMalloc( &tmp, tmpBytes ) );
 	}

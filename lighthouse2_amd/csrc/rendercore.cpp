@@ -471,6 +471,7 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 		/* GPU PLOC build straight from the uploaded CoreTri records (bvh_gpu.h) */
 		float4 *nodes = nullptr, *tris48 = nullptr;
 		GpuBuildResult r;
+		SyncTlas();   /* a TLAS build queued on the ahead stream uses the same builder scratch: this build follows it */
 		gpuBvh.BuildBlas( m.shadeTris.ptr, triangleCount, bvhMaxLeaf, bvhTraversalCost, &nodes, &tris48, r, stream );
 		m.bvhNodes.adopt( nodes, (size_t)r.nodeCount * 4 );
 		m.bvhTris.adopt( tris48, (size_t)triangleCount * 3 );
