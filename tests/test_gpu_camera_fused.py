@@ -18,6 +18,7 @@ import numpy as np
 import pytest
 
 from lighthouse2_amd import scene
+from lighthouse2_amd.core import RenderCore
 from oracle.oracle import Oracle
 
 pytestmark = pytest.mark.gpu
@@ -137,3 +138,46 @@ def test_animated_restart_frames(fresh_core, kind):
             assert np.any(a[..., :3] != 0)
             assert rel_l2(b[..., :3], a[..., :3]) <= 1e-6, (n, double)
             assert np.array_equal(a[..., 3], b[..., 3]), (n, double)
+
+
+@pytest.mark.parametrize("gpu_build", [0, 1])
+def test_animated_frames_with_new_geometry(gpu_build):
+    """Instances moved every frame (instance-only UpdateToplevel: the TLAS slot no frame in flight reads, on the ahead
+    stream) and, midway, a new mesh and instance (SetGeometry: new BLAS arrays, the frame waits for everything queued;
+    gpuBuild 1: the GPU builder, whose scratch the queued TLAS builds share).  Frames queued back to back equal the
+    same frames serialised (frameOverlap 0): the same ray counts, the accumulator to float summation order."""
+    w, h = 96, 64
+    sc = scene.instanced_scene(meshes=4, tris_per_mesh=4000, width=w, height=h, grid=2, spacing=10.0)
+    sc.sky = scene.gradient_sky(64, 32)
+    extra = scene.random_triangles(3000, seed=99)
+
+    def run(overlap):
+        core = RenderCore(device=0)   # each run from a fresh core (the first one leaves its extra mesh behind)
+        core.setting("gpuBuild", gpu_build)
+        core.setting("frameOverlap", overlap)
+        sc2 = scene.instanced_scene(meshes=4, tris_per_mesh=4000, width=w, height=h, grid=2, spacing=10.0)
+        sc2.sky = sc.sky
+        sc2.load_into(core)
+        core.set_target(w, h, 1)
+        core.setting("maxPathLength", 3)
+        n = len(sc2.instances)
+        for f in range(6):
+            scene.animate_instances(sc2, f)
+            for k, (mesh, T) in enumerate(sc2.instances):
+                core.set_instance(k, mesh, T)
+            if f == 3:
+                core.set_geometry(len(sc2.meshes), extra)
+                T = np.eye(4, dtype=np.float32)
+                T[1, 3] = 3.0
+                core.set_instance(n, len(sc2.meshes), T)
+            core.update_toplevel()
+            sc2.render_frame(core, converge=1 if f == 0 else 0)
+        out = core.accumulator(), core.ray_counts()
+        core.close()
+        return out
+
+    a, ca = run(0)
+    b, cb = run(1)
+    assert np.array_equal(ca, cb), (ca[:6], cb[:6])
+    assert np.any(a[..., :3] != 0)
+    assert rel_l2(b[..., :3], a[..., :3]) <= 1e-6
