@@ -125,6 +125,7 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	uint32_t shadeBatch;                              /* path tail (k_trace_path4d): shade once >= shadeBatch lanes finished a query */
 	uint32_t prio;                                    /* the launch's waves' issue priority (s_setprio 0..3) against launches beside it */
 	uint32_t tailWaves;                               /* path tail (lh2_launch_trace_path): the kernel variant for 4 waves per SIMD (4) or 3 */
+	uint32_t traceWaves;                              /* BVH4 closest hit: the kernel variant for 8 waves per SIMD (8) or 7 */
 	/* heavy-first packets (packet kernel, hvWrite non-null): the previous frame's packets that took more
 	   than hvFactor x its mean node steps (hvRead: per-segment counts, step sums, a bit per packet and the
 	   lists of packet bits) are taken first, the rest in order; this frame's are recorded into hvWrite.
@@ -170,7 +171,7 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
    reset by k_init_counters on the core stream (the launch itself may run beside the previous frame's tail) */
 void lh2_launch_trace_primary( const SceneDev* s, const TraceArgs* a, const CameraParams* cp, float4* T4, float4* Q4, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st );
-int lh2_trace_blocks_per_cu( void );
+int lh2_trace_blocks_per_cu( int waves );
 int lh2_packet_blocks_per_cu( void );
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );

@@ -2003,8 +2003,13 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
 	else if (a->version == 7 && s->nodes4)
 	{
 		/* a single-instance scene (tlasRoot4 < 0): the loop without instance state (lh2_trace4d.inc SINGLE) */
-		if (s->tlasRoot4 < 0) LH2_LAUNCH( k_trace_closest4d<true>, grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( k_trace_closest4d<false>, grid, 256, st, ev, *s, *a );
+		if (a->traceWaves == 8)
+		{
+			if (s->tlasRoot4 < 0) LH2_LAUNCH( (k_trace_closest4d<true, 8>), grid, 256, st, ev, *s, *a );
+			else LH2_LAUNCH( (k_trace_closest4d<false, 8>), grid, 256, st, ev, *s, *a );
+		}
+		else if (s->tlasRoot4 < 0) LH2_LAUNCH( (k_trace_closest4d<true, LH2_TRACE_MINWAVES>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_closest4d<false, LH2_TRACE_MINWAVES>), grid, 256, st, ev, *s, *a );
 	}
 	else if (a->leafBatch) LH2_LAUNCH( k_trace_closest<true>, grid, 256, st, ev, *s, *a );
 	else LH2_LAUNCH( k_trace_closest<false>, grid, 256, st, ev, *s, *a );
@@ -2029,12 +2034,20 @@ int lh2_packet_blocks_per_cu( void )
 	return n;
 }
 /* the per-ray traversal kernels' occupancy (persistent grid: CUs x blocks per CU) */
-int lh2_trace_blocks_per_cu( void )
+int lh2_trace_blocks_per_cu( int waves )
 {
 	/* the smaller of the variants' (the global stack is sized for this grid) */
 	int n1 = 0, n2 = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest4d<false>, 256, 0 ) != hipSuccess) n1 = 4;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_closest4d<true>, 256, 0 ) != hipSuccess) n2 = 4;
+	if (waves == 8)
+	{
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest4d<false, 8>, 256, 0 ) != hipSuccess) n1 = 4;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_closest4d<true, 8>, 256, 0 ) != hipSuccess) n2 = 4;
+	}
+	else
+	{
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n1, k_trace_closest4d<false, LH2_TRACE_MINWAVES>, 256, 0 ) != hipSuccess) n1 = 4;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n2, k_trace_closest4d<true, LH2_TRACE_MINWAVES>, 256, 0 ) != hipSuccess) n2 = 4;
+	}
 	return n1 < n2 ? n1 : n2;
 }
 static int lh2_shade_last_grid( void )   /* k_shade_last: every CU full (occupancy x CUs), at least a block per segment */

@@ -113,7 +113,10 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	fclose( f );
 	if (got != 65536 * 5) FatalError( "blue noise table truncated: %s", path.c_str() );
 	dBlueNoise.upload( bn.data(), bn.size(), stream );
-	blocksPerCU = maxBlocksPerCU = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu() ) );
+	traceBlocksPerCU7 = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu( 7 ) ) );
+	traceBlocksPerCU8 = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu( 8 ) ) );
+	maxBlocksPerCU = std::max( traceBlocksPerCU7, traceBlocksPerCU8 );
+	blocksPerCU = traceWaves == 8 ? traceBlocksPerCU8 : traceBlocksPerCU7;
 	packetBlocksPerCU = std::max( 1, std::min( 8, lh2_packet_blocks_per_cu() ) );
 	pathBlocksPerCU = std::max( 1, std::min( 8, lh2_path_blocks_per_cu( 3 ) ) );
 	pathBlocksPerCU4 = std::max( 1, std::min( 8, lh2_path_blocks_per_cu( 4 ) ) );
@@ -221,7 +224,8 @@ void RenderCore::EnsurePaths( uint32_t paths )
 
 void RenderCore::EnsureStack()
 {
-	const size_t need = (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * TraceGrid() * 256;
+	/* sized for the largest grid traceBlocksPerCU / traceWaves may select later */
+	const size_t need = (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * smCount * maxBlocksPerCU * 256;
 	if (ps.gstack.count < need) ps.gstack.resize( need );
 	if (shadowOverlap && ps.sideStack.count < need) ps.sideStack.resize( need );
 }
@@ -325,7 +329,12 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "terminalShade" )) terminalShade = value != 0;   /* drop hits that cannot contribute before shading them (ShadeParams::terminal) */
 	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (default: occupancy limit) */
 	{
-		blocksPerCU = value > 0 ? std::min( maxBlocksPerCU, std::max( 1, (int)value ) ) : maxBlocksPerCU;
+		blocksPerCU = value > 0 ? std::min( maxBlocksPerCU, std::max( 1, (int)value ) ) : traceWaves == 8 ? traceBlocksPerCU8 : traceBlocksPerCU7;
+	}
+	else if (!strcmp( name, "traceWaves" ))   /* closest-hit kernel variant (7 or 8 waves per SIMD); resets traceBlocksPerCU */
+	{
+		traceWaves = (int)value == 7 ? 7 : 8;
+		blocksPerCU = traceWaves == 8 ? traceBlocksPerCU8 : traceBlocksPerCU7;
 	}
 	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice traces as the frame traces primary rays */
 	else if (!strcmp( name, "traceVersion" )) traceVersion = (int)value == 1 ? 1 : 0;   /* 1: the reference BVH2 loop; else the BVH4 loop */
@@ -344,7 +353,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "pathTailSmallPaths", pathTailSmallPaths }, { "pathTailWaves", (float)pathTailWaves }, { "finalShadowBlocks", (float)finalShadowBlocks }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
-		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU },
+		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU }, { "traceWaves", (float)traceWaves },
 		{ "usePackets", (float)UsePackets() } };
 	for (const auto& e : t) if (!strcmp( name, e.n )) { value = e.v; return true; }
 	return false;
@@ -1145,6 +1154,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			const bool beside = besideNext && !ta.packet && overlapTraceBlocks > 0;
 			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, overlapTraceBlocks ) : grid;
 			ta.prio = (uint32_t)prioTrace;
+			ta.traceWaves = beside ? 7u : (uint32_t)traceWaves;   /* 8 waves slow the packets beside the launch (r04ad) */
 			lh2_launch_trace_closest( &sd, &ta, g, { nullptr, ps.evTrace[pathLength] }, stream );
 		}
 		ps.fromTrace[pathLength] = ps.prevStop, ps.prevStop = ps.evTrace[pathLength];
@@ -1494,6 +1504,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
 	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
 	ta.packet = unitCoherent && UsePackets() ? 1 : 0;
+	ta.traceWaves = (uint32_t)traceWaves;
 	lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : TraceGrid(), {}, stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
@@ -1558,6 +1569,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 #ifdef LH2_TRACE_TIMES
 		ta.stats = ttimes.ptr;
 #endif
+			ta.traceWaves = (uint32_t)traceWaves;
 			lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : TraceGrid(), { ev[2 * i], ev[2 * i + 1] }, stream );
 	}
 	CHK_HIP( hipStreamSynchronize( stream ) );

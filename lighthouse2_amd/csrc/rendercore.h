@@ -212,7 +212,9 @@ private:
 	int PacketGrid() const { return smCount * packetBlocksPerCU; }   /* packet kernel: its own occupancy */
 	int PathGrid() const { return smCount * std::min( blocksPerCU, pathBlocksPerCU ); }   /* path tail: its occupancy, within the stack's */
 
-	int device = 0, smCount = 256, blocksPerCU = 7, maxBlocksPerCU = 7, packetBlocksPerCU = 8, pathBlocksPerCU = 3, pathBlocksPerCU4 = 4;
+	int device = 0, smCount = 256, blocksPerCU = 8, maxBlocksPerCU = 8, packetBlocksPerCU = 8, pathBlocksPerCU = 3, pathBlocksPerCU4 = 4;
+	int traceBlocksPerCU7 = 7, traceBlocksPerCU8 = 8;   /* occupancy of the closest-hit kernel's 7- and 8-wave variants */
+	int traceWaves = 8;                  /* closest-hit launches with the chip alone: the 8-wave variant (W7 beside the packets) */
 	bool initialized = false;
 	/* scene */
 	std::vector<CoreMeshHost*> meshes;
