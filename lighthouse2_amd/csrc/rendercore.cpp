@@ -331,6 +331,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	{
 		blocksPerCU = value > 0 ? std::min( maxBlocksPerCU, std::max( 1, (int)value ) ) : traceWaves == 8 ? traceBlocksPerCU8 : traceBlocksPerCU7;
 	}
+	else if (!strcmp( name, "unitTraceWaves" )) unitTraceWaves = (int)value == 8 ? 8 : 7;   /* the same for the unit queries (TraceClosest*) */
 	else if (!strcmp( name, "traceWaves" ))   /* closest-hit kernel variant (7 or 8 waves per SIMD); resets traceBlocksPerCU */
 	{
 		traceWaves = (int)value == 7 ? 7 : 8;
@@ -353,7 +354,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "pathTailSmallPaths", pathTailSmallPaths }, { "pathTailWaves", (float)pathTailWaves }, { "finalShadowBlocks", (float)finalShadowBlocks }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
-		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU }, { "traceWaves", (float)traceWaves },
+		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU }, { "traceWaves", (float)traceWaves }, { "unitTraceWaves", (float)unitTraceWaves },
 		{ "usePackets", (float)UsePackets() } };
 	for (const auto& e : t) if (!strcmp( name, e.n )) { value = e.v; return true; }
 	return false;
@@ -1504,8 +1505,8 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
 	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
 	ta.packet = unitCoherent && UsePackets() ? 1 : 0;
-	ta.traceWaves = (uint32_t)traceWaves;
-	lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : TraceGrid(), {}, stream );
+	ta.traceWaves = (uint32_t)unitTraceWaves;
+	lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : UnitGrid(), {}, stream );
 	CHK_HIP( hipMemcpyAsync( hits4, h.ptr, sizeof( uint4 ) * (size_t)n, hipMemcpyDeviceToHost, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	CheckSceneError();
@@ -1569,8 +1570,8 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 #ifdef LH2_TRACE_TIMES
 		ta.stats = ttimes.ptr;
 #endif
-			ta.traceWaves = (uint32_t)traceWaves;
-			lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : TraceGrid(), { ev[2 * i], ev[2 * i + 1] }, stream );
+		ta.traceWaves = (uint32_t)unitTraceWaves;
+		lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : UnitGrid(), { ev[2 * i], ev[2 * i + 1] }, stream );
 	}
 	CHK_HIP( hipStreamSynchronize( stream ) );
 #ifdef LH2_TRACE_TIMES

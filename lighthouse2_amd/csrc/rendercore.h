@@ -209,12 +209,14 @@ private:
 	uint32_t* FrameRayLog() const { return ps.rayLog.ptr + (size_t)ps.fp * LH2_RAYLOG; }
 	TraceArgs StreamArgs( const float4* o, const float4* d, const uint32_t* segCounts, uint32_t segStride, uint32_t* cursor, bool coherent ) const;
 	int TraceGrid() const { return smCount * blocksPerCU; }
+	int UnitGrid() const { return smCount * std::min( blocksPerCU, unitTraceWaves == 8 ? traceBlocksPerCU8 : traceBlocksPerCU7 ); }
 	int PacketGrid() const { return smCount * packetBlocksPerCU; }   /* packet kernel: its own occupancy */
 	int PathGrid() const { return smCount * std::min( blocksPerCU, pathBlocksPerCU ); }   /* path tail: its occupancy, within the stack's */
 
 	int device = 0, smCount = 256, blocksPerCU = 8, maxBlocksPerCU = 8, packetBlocksPerCU = 8, pathBlocksPerCU = 3, pathBlocksPerCU4 = 4;
 	int traceBlocksPerCU7 = 7, traceBlocksPerCU8 = 8;   /* occupancy of the closest-hit kernel's 7- and 8-wave variants */
 	int traceWaves = 8;                  /* closest-hit launches with the chip alone: the 8-wave variant (W7 beside the packets) */
+	int unitTraceWaves = 7;              /* the unit queries' variant: 7 (the config-2 bounce rays alone: 0.481 vs 0.515 ms, r04ag) */
 	bool initialized = false;
 	/* scene */
 	std::vector<CoreMeshHost*> meshes;

@@ -341,7 +341,7 @@ def test_bvh4_deep_stack(fresh_core, version, waves):
     """A deep BLAS (triangles shrinking geometrically along a line: a chain-like SAH tree) next to the
     random cloud: BVH4 nodes push up to three children per level, the LDS part of the traversal
     stack spills into the global part, and hits stay exact; with the closest-hit kernel's 8-wave
-    variant (64 VGPRs, the default: 8 blocks per CU) and its 7-wave one (traceWaves)."""
+    variant (64 VGPRs, 8 blocks per CU) and its 7-wave one (traceWaves / unitTraceWaves)."""
     k = np.arange(120, dtype=np.float32)
     x = (6.0 * 0.93 ** k).astype(np.float32)
     s_ = (0.02 * 0.93 ** k).astype(np.float32)
@@ -355,6 +355,7 @@ def test_bvh4_deep_stack(fresh_core, version, waves):
     sc.instances.append((1, np.eye(4, dtype=np.float32)))
     fresh_core.setting("traceVersion", version)
     fresh_core.setting("traceWaves", waves)
+    fresh_core.setting("unitTraceWaves", waves)      # the unit queries below launch this variant
     assert fresh_core.get_setting("traceBlocksPerCU") == waves
     o = _load_both(fresh_core, sc, 64, 36)
     info = fresh_core.scene_info()
