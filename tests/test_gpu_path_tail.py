@@ -137,12 +137,13 @@ def test_heavy_first_packets_frames(fresh_core, factor):
     assert rel_l2(fresh_core.accumulator()[..., :3], o2.accumulator()[..., :3]) <= REL_L2_TOL
 
 
-@pytest.mark.parametrize("blocks,tail,side", [(0, 2, 0), (3, 2, 0), (0, 3, 0), (3, 3, 0), (0, 3, 7), (0, 4, 2)])
-def test_shadow_overlap(fresh_core, blocks, tail, side):
+@pytest.mark.parametrize("blocks,tail,side,final", [(0, 2, 0, 6), (3, 2, 0, 6), (0, 3, 0, 6), (3, 3, 0, 0), (0, 3, 7, 6),
+                                                    (0, 4, 2, 3)])
+def test_shadow_overlap(fresh_core, blocks, tail, side, final):
     """shadowOverlap: the shadow rays queued before the path tail are traced on the side stream beside it
     (their segment counts snapshotted by the shade launch before the tail; the path tail at 2 or 3 blocks per CU
     by frame size, or pathTailBlocks; the side launch at sideBlocks per CU, 0: the trace grid's), and the final shadow
-    launch starts behind them.
+    launch (finalShadowBlocks per CU, 6 by default, 0: the trace grid's) starts behind them.
     Every shadow ray is traced once: the same ray counts and occlusion as the oracle, three converging frames within
     rel-L2 1e-4 of it, and within float summation order of the frames traced with the overlap off."""
     w, h = 128, 72
@@ -153,6 +154,7 @@ def test_shadow_overlap(fresh_core, blocks, tail, side):
     fresh_core.setting("pathTail", tail)
     fresh_core.setting("pathTailBlocks", blocks)
     fresh_core.setting("sideBlocks", side)
+    fresh_core.setting("finalShadowBlocks", final)
     res = {}
     for ov in (1, 0):
         fresh_core.setting("shadowOverlap", ov)
