@@ -318,6 +318,9 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	}
 	else if (!strcmp( name, "sideBlocks" )) sideBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "shadeBlocks" )) shadeBlocks = std::min( 64, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "shadeMaxBlocks" )) shadeMaxBlocks = std::min( 64, std::max( 1, (int)value ) );
+	else if (!strcmp( name, "shadePathsPerThread" )) shadePathsPerThread = std::max( 0.25f, value );
 	else if (!strcmp( name, "finalShadowBlocks" )) finalShadowBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailWaves" )) pathTailWaves = std::min( 4, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailSmallPaths" )) pathTailSmallPaths = std::max( 0.0f, value );
@@ -351,7 +354,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
 		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvhSpatialMinRefs", (float)bvhSpatialMinRefs }, { "bvh4Collapse", (float)bvh4Collapse },
 		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
-		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "pathTailSmallPaths", pathTailSmallPaths }, { "pathTailWaves", (float)pathTailWaves }, { "finalShadowBlocks", (float)finalShadowBlocks }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
+		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "pathTailSmallPaths", pathTailSmallPaths }, { "pathTailWaves", (float)pathTailWaves }, { "finalShadowBlocks", (float)finalShadowBlocks }, { "shadeBlocks", (float)shadeBlocks }, { "shadeMaxBlocks", (float)shadeMaxBlocks }, { "shadePathsPerThread", shadePathsPerThread }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
 		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
 		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU }, { "traceWaves", (float)traceWaves }, { "unitTraceWaves", (float)unitTraceWaves },
@@ -973,6 +976,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		cp.hvZero = ps.hv.ptr + (size_t)(1 - ps.hvParity) * ps.hvBlock, cp.hvZeroWords = LH2_HV_MASK + ps.hvMaskWords;
 	}
 	const int grid = TraceGrid();
+	/* the shade launches walk their segment with a static block stride: blocks beyond the resident ones start as others
+	   end, so more, smaller block shares balance the launch's end.  shadeBlocks 0: about shadePathsPerThread paths per
+	   thread, between the trace grid and shadeMaxBlocks per CU (the N = 8 share 12 per CU, config 3 24: -1.5 / -1.5 %,
+	   profiles/r04al_ab.txt, r04am_ab.txt) */
+	const int shadeGrid = shadeBlocks > 0 ? smCount * shadeBlocks : std::max( grid, std::min( smCount * shadeMaxBlocks,
+		(int)((double)pathCount / (256.0 * std::max( 0.25f, shadePathsPerThread ))) ) );
 	/* the camera fused into the primary packet launch: the heavy-packet block it records into must be zero (the previous
 	   fused frame's first shade launch zeroed it) */
 	const bool fusedCam = cameraFused && tiledRays && UsePackets() && !primeRef;
@@ -1195,7 +1204,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		if (earlyHere) sp.acc = frameDelta;   /* the previous frame's finalize may not have read the accumulator yet */
 		/* a primary launch run ahead has not waited for the previous frame's overlap event: the early shade does */
 		if (earlyHere && ahead) CHK_HIP( hipStreamWaitEvent( aheadStream, prevOverlapEv, 0 ) );
-		lh2_launch_shade( &sd, &sp, grid, { nullptr, ps.evShade[pathLength] }, earlyHere ? aheadStream : stream );
+		lh2_launch_shade( &sd, &sp, shadeGrid, { nullptr, ps.evShade[pathLength] }, earlyHere ? aheadStream : stream );
 		if (earlyHere) CHK_HIP( hipStreamWaitEvent( stream, ps.evShade[pathLength], 0 ) );
 		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];
 		/* the next frame's primary launch starts after this frame's first shade launch (the last reader of the primary

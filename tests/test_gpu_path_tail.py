@@ -169,3 +169,27 @@ def test_shadow_overlap(fresh_core, blocks, tail, side, final):
     assert co[16] > 0 and st.totalShadowRays == co[16], (st.totalShadowRays, co[16])
     assert rel_l2(ag[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
     assert rel_l2(ag[..., :3], res[0][0][..., :3]) <= 1e-6
+
+
+@pytest.mark.parametrize("blocks,ppt", [(0, 1.3), (0, 0.25), (1, 1.3), (8, 1.3), (40, 1.3)])
+def test_shade_grid(fresh_core, blocks, ppt):
+    """The shade launches' grid (shadeBlocks per CU; 0: about shadePathsPerThread paths per thread, between the trace
+    grid and shadeMaxBlocks per CU): each block walks its segment with a static stride, so every grid must shade every
+    path once; the same ray counts as the oracle and the frame within float summation order of the default grid's."""
+    w, h = 128, 72
+    sc = _scene("room", w, h)
+    o = _load_both(fresh_core, sc, w, h)
+    for tgt in (fresh_core, o):
+        tgt.setting("maxPathLength", 4)
+    res = []
+    for b, p in ((0, 1.3), (blocks, ppt)):
+        fresh_core.setting("shadeBlocks", b)
+        fresh_core.setting("shadePathsPerThread", p)
+        for f in range(2):
+            sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
+            if not res:
+                sc.render_frame(o, converge=1 if f == 0 else 0)
+        res.append((fresh_core.accumulator(), fresh_core.ray_counts()))
+    assert np.array_equal(res[1][1], o.ray_counts())
+    assert rel_l2(res[1][0][..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
+    assert rel_l2(res[1][0][..., :3], res[0][0][..., :3]) <= 1e-6
