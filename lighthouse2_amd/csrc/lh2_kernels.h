@@ -103,6 +103,7 @@ struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path st
 	/* the camera fused into the primary packet launch (RenderCore::Render): the first shade launch zeroes the first
 	   hvZeroWords words of the heavy-packet block the frame read, the block the next frame records into */
 	uint32_t* hvZero; uint32_t hvZeroWords;
+	int lastGrid;                    /* k_shade_last's grid (0: its occupancy x CUs) */
 };
 
 struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (any) out */

@@ -348,6 +348,7 @@ private:
 	int finalShadowBlocks = 6;
 	int shadeBlocks = 0;                 /* blocks per CU of the frame's shade launches (0: by path count, Render) */
 	int shadeMaxBlocks = 24;
+	int shadeLastBlocks = 0;             /* blocks per CU of k_shade_last (config 2's last shade; 0: its occupancy) */
 	float shadePathsPerThread = 1.3f;
 	/* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's): 4 leaves the next frame's primary
 	   and early shade launches room: config 3 -0.5 %, the N = 8 share -0.8 to -1.5 % (profiles/r04m_ab.txt, r04n_ab.txt) */
