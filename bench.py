@@ -27,6 +27,7 @@ from __future__ import annotations
 import argparse
 import glob
 import json
+import re
 import os
 import pathlib
 import sys
@@ -58,8 +59,12 @@ def log(msg):
 
 
 def newest(pattern, pred=lambda d: True):
-    """(path, dict) of the newest committed profile summary matching pattern and pred."""
-    for f in sorted(glob.glob(str(ROOT / "profiles" / pattern)), reverse=True):
+    """(path, dict) of the newest committed profile summary matching pattern and pred (tags r<round><letters>_: by
+    round, then by the letters as a base-26 count, so r04ah follows r04z)."""
+    def tag(f):
+        m = re.match(r"r(\d+)([a-z]*)_", pathlib.Path(f).name)
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    for f in sorted(glob.glob(str(ROOT / "profiles" / pattern)), key=tag, reverse=True):
         try:
             d = json.load(open(f))
         except Exception:
