@@ -32,7 +32,7 @@
      lh2_core_set_tile, lh2_core_set_tile_bands, lh2_core_sync, lh2_core_get_accumulator, lh2_core_get_frame,
      lh2_core_copy_accumulator_rows, lh2_core_copy_frame_async, lh2_core_pack_tile, lh2_core_pack_tile_ordered, lh2_core_tile_rows, lh2_core_stream, lh2_core_ray_counts, lh2_core_trace_closest,
      lh2_core_trace_any, lh2_core_trace_closest_device, lh2_core_generate_eye_rays,
-     lh2_core_scene_info, lh2_core_debug_shadow_rays, lh2_core_debug_bvh4, lh2_core_get_setting, lh2_set_device, lh2_xorshift_floats, lh2_version.
+     lh2_core_scene_info, lh2_core_debug_shadow_rays, lh2_core_debug_bvh4, lh2_core_debug_poison_tlas, lh2_core_get_setting, lh2_set_device, lh2_xorshift_floats, lh2_version.
 */
 #ifndef LH2_RENDERCORE_H
 #define LH2_RENDERCORE_H
@@ -98,6 +98,8 @@ int lh2_core_debug_shadow_rays( lh2_core core, float* o4, float* d4, float* p4, 
    each, the layout of k_quantize4); *n = the nodes copied */
 /* cap 0 (or null arrays): *n = the node count, nothing copied */
 int lh2_core_debug_bvh4( lh2_core core, float* f32Nodes, uint32_t* qNodes, int cap, int* n );
+/* test hook: fill both TLAS slots' node regions with `value` (stale memory behind the nodes a TLAS update writes) */
+int lh2_core_debug_poison_tlas( lh2_core core, float value );
 
 /* host utility: n successive RandomFloat() values of Marsaglia xorshift32 (platform/system.cpp:44-46) */
 int lh2_xorshift_floats( uint32_t seed, float* out, uint64_t n );

@@ -82,6 +82,7 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
         "lh2_xorshift_floats": [C.c_uint32, _F, C.c_uint64],
         "lh2_core_debug_shadow_rays": [_P, _F, _F, _F, C.c_int, C.POINTER(C.c_int)],
         "lh2_core_debug_bvh4": [_P, _F, C.c_void_p, C.c_int, C.POINTER(C.c_int)],
+        "lh2_core_debug_poison_tlas": [_P, C.c_float],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -310,6 +311,10 @@ class RenderCore:
         q = np.zeros((max(cap, 1), 16), np.uint32)
         self._chk(self.lib.lh2_core_debug_bvh4(self.h, _fp(f), q.ctypes.data, int(cap), C.byref(n)))
         return f[:n.value], q[:n.value]
+
+    def debug_poison_tlas(self, value: float) -> None:
+        """Test hook: fill both TLAS slots' node regions with `value` (stale memory behind a TLAS update's nodes)."""
+        self._chk(self.lib.lh2_core_debug_poison_tlas(self.h, float(value)))
 
     def scene_info(self) -> dict:
         v = [C.c_int(0) for _ in range(4)]

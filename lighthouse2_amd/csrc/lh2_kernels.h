@@ -103,7 +103,6 @@ struct ShadeParams    /* shadeKernel arguments (pathtracer.h:54-59), SoA path st
 	/* the camera fused into the primary packet launch (RenderCore::Render): the first shade launch zeroes the first
 	   hvZeroWords words of the heavy-packet block the frame read, the block the next frame records into */
 	uint32_t* hvZero; uint32_t hvZeroWords;
-	int lastGrid;                    /* k_shade_last's grid (0: its occupancy x CUs) */
 };
 
 struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (any) out */
@@ -124,7 +123,6 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	int packet;                                       /* nonzero: wave-uniform packet traversal (coherent rays, lh2_trace_packet.inc) */
 	unsigned long long* stats;                        /* LH2_TRACE_STATS / LH2_TRACE_TIMES builds: per-launch counters */
 	uint32_t shadeBatch;                              /* path tail (k_trace_path4d): shade once >= shadeBatch lanes finished a query */
-	uint32_t prio;                                    /* the launch's waves' issue priority (s_setprio 0..3) against launches beside it */
 	uint32_t tailWaves;                               /* path tail (lh2_launch_trace_path): the kernel variant for 4 waves per SIMD (4) or 3 */
 	uint32_t traceWaves;                              /* BVH4 closest hit: the kernel variant for 8 waves per SIMD (8) or 7 */
 	/* heavy-first packets (packet kernel, hvWrite non-null): the previous frame's packets that took more

@@ -2097,7 +2097,7 @@ void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, Launch
 {
 	grid = grid < LH2_SEGS ? LH2_SEGS : grid;   /* every segment needs a block */
 	if (p->primeRef) LH2_LAUNCH( k_shade_ref, grid, 256, st, ev, *s, *p );
-	else if (p->terminal && p->pathLength == p->maxPathLength) LH2_LAUNCH( k_shade_last, p->lastGrid >= LH2_SEGS ? p->lastGrid : lh2_shade_last_grid(), 256, st, ev, *s, *p );
+	else if (p->terminal && p->pathLength == p->maxPathLength) LH2_LAUNCH( k_shade_last, lh2_shade_last_grid(), 256, st, ev, *s, *p );
 	else if (p->terminal) LH2_LAUNCH( (k_shade<true, true>), grid, 256, st, ev, *s, *p );
 	else if (s->nArea + s->nPoint + s->nSpot + s->nDir == 0) LH2_LAUNCH( (k_shade<false, true>), grid, 256, st, ev, *s, *p );
 	else LH2_LAUNCH( (k_shade<false, false>), grid, 256, st, ev, *s, *p );

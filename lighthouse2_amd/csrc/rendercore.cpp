@@ -95,13 +95,15 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	const char* name = props.gcnArchName[0] ? props.gcnArchName : props.name;
 	coreStats.deviceName = new char[strlen( name ) + 1];   /* owned (and leaked) by the core: core_api_base.h:33 */
 	memcpy( coreStats.deviceName, name, strlen( name ) + 1 );
-	MakeCoreStream();
+	/* the core, side and ahead streams at the device's least priority, which on MI355X (range 0 .. -1) is the default level:
+	   the high level for the ahead stream or the core stream measured no faster (profiles/r04k_ab.txt, r04l_ab.txt) */
 	{
 		int least = 0, greatest = 0;
 		CHK_HIP( hipDeviceGetStreamPriorityRange( &least, &greatest ) );
+		CHK_HIP( hipStreamCreateWithPriority( &stream, hipStreamNonBlocking, least ) );
 		CHK_HIP( hipStreamCreateWithPriority( &sideStream, hipStreamNonBlocking, least ) );
+		CHK_HIP( hipStreamCreateWithPriority( &aheadStream, hipStreamNonBlocking, least ) );
 	}
-	MakeAheadStream();
 	/* blue noise sampler tables (rendercore.cpp:125-134), shipped as data/bluenoise.bin */
 	std::string path = getenv( "LH2_BLUENOISE" ) ? getenv( "LH2_BLUENOISE" ) : LibraryDir() + "/data/bluenoise.bin";
 	FILE* f = fopen( path.c_str(), "rb" );
@@ -135,6 +137,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipEventCreate( &ps.evCamera ) );
 	CHK_HIP( hipEventCreate( &ps.evShadow ) );
 	CHK_HIP( hipEventCreate( &ps.evSide ) );
+	CHK_HIP( hipEventCreateWithFlags( &ps.evEarlyEnd, hipEventDisableTiming ) );
 	ps.shSnap.resize( 2 * LH2_SEGS * LH2_SEGCOUNT_STRIDE );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
@@ -189,7 +192,7 @@ bool RenderCore::UsePackets() const
 {
 	if (packetPrimary >= 0) return packetPrimary != 0;
 	const double bytes = ((double)blasNodeCount + tlasCapacity) * 64.0 + (double)blasTriCount * 48.0;
-	return bytes <= (double)packetMaxMB * 1048576.0;
+	return bytes <= kPacketMaxBytes;
 }
 
 /* traversal loop of the per-ray launches (setting "traceVersion"): 7, the BVH4 loop (lh2_trace4d.inc), unless
@@ -230,39 +233,6 @@ void RenderCore::EnsureStack()
 	if (shadowOverlap && ps.sideStack.count < need) ps.sideStack.resize( need );
 }
 
-/* frameOverlap: the ahead stream at the device's least priority (aheadPriority 0), which on MI355X (range 0 .. -1) is the
-   default level, the core stream's; the high level (aheadPriority 2) and the core stream at the high level (corePriority 1)
-   measured no faster (profiles/r04k_ab.txt, r04l_ab.txt, r04m_ab.txt) */
-void RenderCore::MakeAheadStream()
-{
-	if (aheadStream)
-	{
-		CHK_HIP( hipStreamSynchronize( stream ) );
-		CHK_HIP( hipStreamSynchronize( aheadStream ) );
-		CHK_HIP( hipStreamDestroy( aheadStream ) );
-		aheadStream = nullptr;
-	}
-	int least = 0, greatest = 0;
-	CHK_HIP( hipDeviceGetStreamPriorityRange( &least, &greatest ) );
-	const int prio = aheadPriority >= 2 ? greatest : aheadPriority == 1 ? (least + greatest) / 2 : least;
-	CHK_HIP( hipStreamCreateWithPriority( &aheadStream, hipStreamNonBlocking, prio ) );
-}
-
-void RenderCore::MakeCoreStream()
-{
-	if (stream)
-	{
-		CHK_HIP( hipStreamSynchronize( stream ) );
-		if (aheadStream) CHK_HIP( hipStreamSynchronize( aheadStream ) );
-		if (sideStream) CHK_HIP( hipStreamSynchronize( sideStream ) );
-		CHK_HIP( hipStreamDestroy( stream ) );
-		stream = nullptr;
-	}
-	int least = 0, greatest = 0;
-	CHK_HIP( hipDeviceGetStreamPriorityRange( &least, &greatest ) );
-	CHK_HIP( hipStreamCreateWithPriority( &stream, hipStreamNonBlocking, corePriority ? greatest : least ) );
-}
-
 void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439-457 */
 {
 	if (!strcmp( name, "epsilon" )) geometryEpsilon = value;
@@ -274,14 +244,11 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "tiledRays" )) tiledRays = value != 0;
 	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle (64 = whole batches);
 	   coherent 8x8-tiled primary rays trace best in batches, incoherent bounce rays with refills */
-	else if (!strcmp( name, "refillPrimary" )) refillPrimary = std::min( 64, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "refill" )) refillOther = std::min( 64, std::max( 1, (int)value ) );
 	/* traversal: test parked BLAS leaves once this many lanes of a wave hold one (0 = every step) */
 	else if (!strcmp( name, "leafBatch" )) leafBatch = std::min( 64, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "leafBatchPrimary" )) leafBatchPrimary = std::min( 64, std::max( 0, (int)value ) );
 	/* BLAS build parameters, used by later SetGeometry calls */
 	else if (!strcmp( name, "bvhMaxLeaf" )) bvhMaxLeaf = std::min( 16, std::max( 1, (int)value ) );
-	else if (!strcmp( name, "bvhTraversalCost" )) bvhTraversalCost = std::max( 0.01f, value );
 	else if (!strcmp( name, "bvhSpatial" )) bvhSpatial = std::max( 0.0f, value );   /* SBVH overlap threshold (x root area); 0: off */
 	else if (!strcmp( name, "bvhSpatialBudget" )) bvhSpatialBudget = std::min( 4.0f, std::max( 0.0f, value ) );
 	else if (!strcmp( name, "bvhSpatialMinRefs" )) bvhSpatialMinRefs = std::max( 0, (int)value );
@@ -290,7 +257,6 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "gpuBuild" )) gpuBuild = value != 0;          /* BLAS builder of later SetGeometry calls */
 	else if (!strcmp( name, "buildThreads" )) buildThreads = std::max( 0, (int)value );   /* host threads of the deferred CPU builds */
 	else if (!strcmp( name, "gpuTlas" )) { gpuTlas = value != 0; instancesDirty = true; }
-	else if (!strcmp( name, "plocRadius" )) gpuBvh.radius = std::min( 32, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "chordSplit" )) chordSplit = std::max( 0.0f, value );   /* two-ended path segments (longest first); 0: off */
 	else if (!strcmp( name, "packetHeavy" )) packetHeavy = std::max( 0.0f, value );   /* heavy-first primary packets; 0: off */
 	else if (!strcmp( name, "pathTail" )) pathTail = std::max( 0, (int)value );   /* bounces from this one in one trace-and-shade launch; 0: off */
@@ -299,36 +265,13 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "cameraFused" )) cameraFused = value != 0;
 	else if (!strcmp( name, "frameOverlap" )) frameOverlap = (int)value;
 	else if (!strcmp( name, "earlyShade" )) earlyShade = value != 0;
-	else if (!strcmp( name, "primaryAhead" )) primaryAhead = std::min( 2, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "prioTail" )) prioTail = std::min( 3, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "prioShadow" )) prioShadow = std::min( 3, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "prioSide" )) prioSide = std::min( 3, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "prioPrimary" )) prioPrimary = std::min( 3, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "prioTrace" )) prioTrace = std::min( 3, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "earlyShadeMaxPaths" )) earlyShadeMaxPaths = std::max( 0.0f, value );
-	else if (!strcmp( name, "corePriority" ))
-	{
-		const int v = value != 0 ? 1 : 0;
-		if (v != corePriority) { corePriority = v; if (initialized) MakeCoreStream(); }
-	}
-	else if (!strcmp( name, "aheadPriority" ))
-	{
-		const int v = std::min( 2, std::max( 0, (int)value ) );
-		if (v != aheadPriority) { aheadPriority = v; if (initialized) MakeAheadStream(); }
-	}
 	else if (!strcmp( name, "sideBlocks" )) sideBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "shadeBlocks" )) shadeBlocks = std::min( 64, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "shadeLastBlocks" )) shadeLastBlocks = std::min( 64, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "shadeMaxBlocks" )) shadeMaxBlocks = std::min( 64, std::max( 1, (int)value ) );
-	else if (!strcmp( name, "shadePathsPerThread" )) shadePathsPerThread = std::max( 0.25f, value );
 	else if (!strcmp( name, "finalShadowBlocks" )) finalShadowBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "pathTailWaves" )) pathTailWaves = std::min( 4, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "pathTailSmallPaths" )) pathTailSmallPaths = std::max( 0.0f, value );
-	else if (!strcmp( name, "overlapTraceBlocks" )) overlapTraceBlocks = std::min( 8, std::max( 0, (int)value ) );
 	/* packet traversal of tiled primary rays: 1 on, 0 off, -1 when the BVH + triangles fit in packetMaxMB */
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
-	else if (!strcmp( name, "packetMaxMB" )) packetMaxMB = std::max( 0.0f, value );
 	else if (!strcmp( name, "singleInstanceStart" )) singleInstanceStart = value != 0;   /* one instance: rays start at its TLAS leaf */
 	else if (!strcmp( name, "terminalShade" )) terminalShade = value != 0;   /* drop hits that cannot contribute before shading them (ShadeParams::terminal) */
 	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (default: occupancy limit) */
@@ -351,14 +294,15 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 {
 	struct { const char* n; float v; } t[] = {
 		{ "epsilon", geometryEpsilon }, { "clampValue", clampValue }, { "maxPathLength", (float)maxPathLength },
-		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refillPrimary", (float)refillPrimary },
-		{ "refill", (float)refillOther }, { "leafBatch", (float)leafBatch }, { "leafBatchPrimary", (float)leafBatchPrimary },
-		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvhSpatialMinRefs", (float)bvhSpatialMinRefs }, { "bvh4Collapse", (float)bvh4Collapse },
-		{ "chordSplit", chordSplit }, { "pathTail", (float)pathTail }, { "packetHeavy", packetHeavy }, { "pathTailBatch", (float)pathTailBatch }, { "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade }, { "primaryAhead", (float)primaryAhead }, { "prioTail", (float)prioTail }, { "prioShadow", (float)prioShadow },
-		{ "prioSide", (float)prioSide }, { "prioPrimary", (float)prioPrimary }, { "prioTrace", (float)prioTrace }, { "earlyShadeMaxPaths", earlyShadeMaxPaths }, { "pathTailBlocks", (float)pathTailBlocks }, { "pathTailSmallPaths", pathTailSmallPaths }, { "pathTailWaves", (float)pathTailWaves }, { "finalShadowBlocks", (float)finalShadowBlocks }, { "shadeBlocks", (float)shadeBlocks }, { "shadeMaxBlocks", (float)shadeMaxBlocks }, { "shadeLastBlocks", (float)shadeLastBlocks }, { "shadePathsPerThread", shadePathsPerThread }, { "sideBlocks", (float)sideBlocks }, { "aheadPriority", (float)aheadPriority }, { "corePriority", (float)corePriority }, { "overlapTraceBlocks", (float)overlapTraceBlocks },
-		{ "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
-		{ "terminalShade", (float)terminalShade }, { "traceVersion", (float)TraceVersion() }, { "bvh4", (float)bvh4 },
-		{ "gpuBuild", (float)gpuBuild }, { "gpuTlas", (float)gpuTlas }, { "traceBlocksPerCU", (float)blocksPerCU }, { "traceWaves", (float)traceWaves }, { "unitTraceWaves", (float)unitTraceWaves },
+		{ "primeRef", (float)primeRef }, { "tiledRays", (float)tiledRays }, { "refill", (float)refillOther }, { "leafBatch", (float)leafBatch },
+		{ "bvhMaxLeaf", (float)bvhMaxLeaf }, { "bvhSpatial", bvhSpatial }, { "bvhSpatialBudget", bvhSpatialBudget }, { "bvhSpatialMinRefs", (float)bvhSpatialMinRefs },
+		{ "bvh4Collapse", (float)bvh4Collapse }, { "bvh4", (float)bvh4 }, { "gpuBuild", (float)gpuBuild }, { "buildThreads", (float)buildThreads }, { "gpuTlas", (float)gpuTlas },
+		{ "chordSplit", chordSplit }, { "packetHeavy", packetHeavy }, { "pathTail", (float)pathTail }, { "pathTailBatch", (float)pathTailBatch },
+		{ "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade },
+		{ "sideBlocks", (float)sideBlocks }, { "pathTailBlocks", (float)pathTailBlocks }, { "shadeBlocks", (float)shadeBlocks }, { "finalShadowBlocks", (float)finalShadowBlocks },
+		{ "pathTailWaves", (float)pathTailWaves }, { "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
+		{ "terminalShade", (float)terminalShade }, { "traceBlocksPerCU", (float)blocksPerCU }, { "unitTraceWaves", (float)unitTraceWaves }, { "traceWaves", (float)traceWaves },
+		{ "unitCoherent", (float)unitCoherent }, { "traceVersion", (float)TraceVersion() },
 		{ "usePackets", (float)UsePackets() } };
 	for (const auto& e : t) if (!strcmp( name, e.n )) { value = e.v; return true; }
 	return false;
@@ -486,7 +430,7 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 		float4 *nodes = nullptr, *tris48 = nullptr;
 		GpuBuildResult r;
 		SyncTlas();   /* a TLAS build queued on the ahead stream uses the same builder scratch: this build follows it */
-		gpuBvh.BuildBlas( m.shadeTris.ptr, triangleCount, bvhMaxLeaf, bvhTraversalCost, &nodes, &tris48, r, stream );
+		gpuBvh.BuildBlas( m.shadeTris.ptr, triangleCount, bvhMaxLeaf, 1.0f, &nodes, &tris48, r, stream );
 		m.bvhNodes.adopt( nodes, (size_t)r.nodeCount * 4 );
 		m.bvhTris.adopt( tris48, (size_t)triangleCount * 3 );
 		m.leafTris = triangleCount;
@@ -517,7 +461,7 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 			}
 		}
 		const int maxLeaf = bvhMaxLeaf, collapse = bvh4Collapse, wide = bvh4;
-		const float cost = bvhTraversalCost, spatial = bvhSpatial, budget = bvhSpatialBudget;
+		const float cost = 1.0f, spatial = bvhSpatial, budget = bvhSpatialBudget;
 		const int minRefs = bvhSpatialMinRefs;
 		CoreMeshHost* mp = &m;
 		m.build = [mp, prims = std::move( prims ), verts = std::move( verts ), maxLeaf, collapse, wide, cost, spatial, budget, minRefs]( int threads ) {
@@ -579,16 +523,21 @@ void RenderCore::FlushBuilds()
 	}
 	const int nthreads = std::max( 1, std::min( workers, (int)jobs.size() ) );
 	const int perJob = std::max( 1, workers / std::max( 1, (int)jobs.size() ) );
-	std::atomic<int> next{ 0 };
+	std::atomic<int> next{ 0 }, inUse{ 0 };
 	std::vector<std::string> errors( nthreads );
-	/* the last jobs, fewer than the workers, get the idle workers' share as threads of their own build (SBVH subtrees) */
+	/* the last jobs, fewer than the workers, get the idle workers' share as threads of their own build (SBVH subtrees):
+	   a job is granted threads only out of those no running build holds, so the total stays near `workers` */
 	auto work = [&]( int w ) {
 		try
 		{
 			for (int j; (j = next.fetch_add( 1 )) < (int)jobs.size();)
 			{
 				const int remaining = (int)jobs.size() - j;
-				jobs[j]->build( std::max( perJob, std::min( 8, workers / std::max( 1, remaining ) ) ) );
+				const int want = std::max( perJob, std::min( 8, workers / std::max( 1, remaining ) ) );
+				const int grant = std::max( 1, std::min( want, workers - inUse.load() ) );
+				inUse += grant;
+				jobs[j]->build( grant );
+				inUse -= grant;
 			}
 		}
 		catch (const std::exception& e) { errors[w] = e.what(); }
@@ -768,6 +717,7 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 	CHK_HIP( hipMemcpyAsync( dInstDesc[ts].ptr, desc, nRec * sizeof( lh2_CoreInstanceDesc ), hipMemcpyHostToDevice, us ) );
 	/* the scene error starts as the BLAS quantizer's (ConcatenateBlas), the TLAS checks add to it */
 	CHK_HIP( hipMemcpyAsync( SceneErr( ts ), dBlasQError.ptr, sizeof( int ), hipMemcpyDeviceToDevice, us ) );
+	int tlasNodes = 1;   /* the nodes this TLAS has (the slot holds tlasCapacity): the BVH4 copy and the quantizer touch no others */
 	if (ni >= 2 && gpuTlas)
 	{
 		/* TLAS built on the device from the instance transforms (bvh_gpu.h) */
@@ -778,6 +728,7 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		ta.nodeBase = TlasBase2( ts ), ta.nodes = dNodes.ptr, ta.maxBlasDepth = StackDepthBound();
 		ta.sceneError = SceneErr( ts ), ta.tlasDepth = dTlasDepth.ptr;
 		gpuBvh.BuildTlas( ta, us );
+		tlasNodes = ni - 1;   /* one instance per leaf: ni - 1 child-pair nodes, dense in preorder (bvh_gpu.hip emit_node) */
 		tlasOnDevice = true;
 		sceneMaxDepth = -1;   /* known on the device; SceneInfo reads it */
 	}
@@ -815,6 +766,7 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		BuildBvh2( prims, 1, 1, tlas );
 		const size_t tn = tlas.nodes.size() / 16;
 		if (tn > (size_t)tlasCapacity) FatalError( "TLAS of %zu nodes exceeds its capacity %d", tn, tlasCapacity );
+		tlasNodes = std::max( 1, (int)tn );
 		for (size_t k = 0; k < tn; k++)
 		{
 			int* refs = (int*)&tlas.nodes[k * 16 + 12];
@@ -835,11 +787,14 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		tlasOnDevice = false;
 		if (sceneMaxDepth >= LH2_STACK_TOTAL - 1) FatalError( "BVH depth %d exceeds the traversal stack (%d)", sceneMaxDepth, LH2_STACK_TOTAL );
 	}
-	/* the TLAS in the BVH4 array: its BVH2 nodes as two-child BVH4 nodes (one short launch) */
+	/* the TLAS in the BVH4 array: its BVH2 nodes as two-child BVH4 nodes (one short launch), quantized.  Only the nodes this
+	   TLAS has: the slot's nodes beyond them hold an earlier, larger TLAS or memory never written, whose boxes (possibly huge,
+	   finite) would set the quantizer's range error (round 4 fixed that by NaN-filling the region, 651cce0; no traversal ever
+	   reaches such a node, so it is not read at all now; test_gpu_parity.py::test_stale_tlas_region_is_not_quantized) */
 	if (bvh4)
 	{
-		GpuBvhBuilder::TlasToBvh4( dNodes.ptr, TlasBase2( ts ), tlasCapacity, TlasBase4( ts ), dNodes4.ptr, us );
-		GpuBvhBuilder::Quantize4( dNodes4.ptr, TlasBase4( ts ), tlasCapacity, dNodes4q.ptr, SceneErr( ts ), us );
+		GpuBvhBuilder::TlasToBvh4( dNodes.ptr, TlasBase2( ts ), tlasNodes, TlasBase4( ts ), dNodes4.ptr, us );
+		GpuBvhBuilder::Quantize4( dNodes4.ptr, TlasBase4( ts ), tlasNodes, dNodes4q.ptr, SceneErr( ts ), us );
 	}
 	CHK_HIP( hipEventRecord( evStage[slot], us ) );
 	CHK_HIP( hipEventRecord( evTlasReady, us ) );
@@ -981,8 +936,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	   end, so more, smaller block shares balance the launch's end.  shadeBlocks 0: about shadePathsPerThread paths per
 	   thread, between the trace grid and shadeMaxBlocks per CU (the N = 8 share 12 per CU, config 3 24: -1.5 / -1.5 %,
 	   profiles/r04al_ab.txt, r04am_ab.txt) */
-	const int shadeGrid = shadeBlocks > 0 ? smCount * shadeBlocks : std::max( grid, std::min( smCount * shadeMaxBlocks,
-		(int)((double)pathCount / (256.0 * std::max( 0.25f, shadePathsPerThread ))) ) );
+	const int shadeGrid = shadeBlocks > 0 ? smCount * shadeBlocks : std::max( grid, std::min( smCount * kShadeMaxBlocks,
+		(int)((double)pathCount / (256.0 * kShadePathsPerThread)) ) );
 	/* the camera fused into the primary packet launch: the heavy-packet block it records into must be zero (the previous
 	   fused frame's first shade launch zeroed it) */
 	const bool fusedCam = cameraFused && tiledRays && UsePackets() && !primeRef;
@@ -997,9 +952,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
 		cp.clearAcc = nullptr;
 	}
-	/* primary ahead: the previous frame had no path tail, and there is a frame before it whose finalize the wait can use */
-	const bool ahead = fusedCam && !serialize && (primaryAhead == 2 || (primaryAhead == 1 && ps.lastNoTail)) && prevFrameEndValid;
-	const hipEvent_t prevOverlapEv = ps.overlapEv;
 	hipStream_t primStream = stream;
 	/* the primary launch's work-queue heads: slot 1 of the frame parity's block, zeroed by the finalize of the frame before
 	   the previous one (FrameStatsDev::zeroHeads) */
@@ -1017,15 +969,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		if (serialize) cp.initC = c;
 		else
 		{
-			/* primary ahead: after the previous frame's primary launch (its stop event: that launch may have run on the core
-			   stream) and the finalize of the frame before it (the last user of this parity's buffers); else after the
-			   previous frame's overlap event */
-			if (ahead)
-			{
-				CHK_HIP( hipStreamWaitEvent( aheadStream, ps.evTrace[1], 0 ) );
-				CHK_HIP( hipStreamWaitEvent( aheadStream, evFrame[2], 0 ) );
-			}
-			else CHK_HIP( hipStreamWaitEvent( aheadStream, ps.overlapEv, 0 ) );
+			CHK_HIP( hipStreamWaitEvent( aheadStream, ps.overlapEv, 0 ) );
 			lh2_launch_init_counters( c, pathCount, ps.segStride, cursors, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, {}, aheadStream, -LH2_CURSOR_WORDS );
 			cp.initC = nullptr;
 		}
@@ -1047,7 +991,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	   bounce 2, its shadow snapshot), and on the ahead stream neither would follow the previous frame's finalize (the
 	   side shadow launch and the next frames' early shades would add into the accumulator and the delta before the
 	   previous frame is finalized) */
-	const bool early = fusedCam && !serialize && earlyShade && frameOverlap == 1 && ps.earlyOk && (float)pathCount <= earlyShadeMaxPaths &&
+	const bool early = fusedCam && !serialize && earlyShade && frameOverlap == 1 && ps.earlyOk && (float)pathCount <= kSmallFramePaths &&
 		tailL >= 3;
 	ps.early = early;
 	ps.in = early ? ps.busy : 0;
@@ -1085,9 +1029,9 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.version = TraceVersion();
 		ta.rayO = ps.rayO[ps.in].ptr, ta.rayD = ps.rayD[ps.in].ptr, ta.segCounts = segIn, ta.segStride = ps.segStride, ta.segBack = segInBack;
 		ta.cursor = cursors + (size_t)(pathLength == 1 ? primSlot : (uint32_t)pathLength) * LH2_CURSOR_WORDS;
-		ta.refill = (uint32_t)(primary ? refillPrimary : refillOther);
+		ta.refill = (uint32_t)refillOther;
 		ta.packet = primary && UsePackets() ? 1 : 0;
-		ta.leafBatch = (uint32_t)(primary ? leafBatchPrimary : leafBatch);
+		ta.leafBatch = (uint32_t)leafBatch;
 		ta.hits = ps.hits.ptr, ta.gstack = ps.gstack.ptr;
 		const bool fusedPrimary = pathLength == 1 && fusedCam;   /* the primary buffers (PathStreams::rayOP ..) */
 		if (fusedPrimary) ta.rayO = ps.rayOP[ps.fp].ptr, ta.rayD = ps.rayDP[ps.fp].ptr, ta.hits = ps.hitsP[ps.fp].ptr;
@@ -1111,7 +1055,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
 		sp.probePixel = probeX + scrwidth * probeY;
 		sp.spreadAngle = view.spreadAngle;
-		sp.lastGrid = shadeLastBlocks > 0 ? smCount * shadeLastBlocks : 0;
 		if (pathLength == tailL)
 		{
 			/* the path tail: trace and shade every remaining bounce in one launch; each path's records are
@@ -1120,11 +1063,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			sp.rayOut = ps.rayO[ps.in].ptr, sp.rayDOut = ps.rayD[ps.in].ptr, sp.T4Out = ps.T4[ps.in].ptr, sp.Q4Out = ps.Q4[ps.in].ptr;
 			sp.adv.rayCountLog = rayLog;
 			ta.shadeBatch = (uint32_t)pathTailBatch;
-			ta.prio = (uint32_t)prioTail;
 			/* with the overlap the path tail runs fewer blocks per CU and leaves registers for the side launch's waves
 			   (pathTailBlocks; 0: 3 for small frames, whose tail phase is the frame's longest, else 2) */
 			const bool side = overlap && snapped;
-			const bool small = (float)pathCount <= pathTailSmallPaths;
+			const bool small = (float)pathCount <= kSmallFramePaths;
 			/* the kernel variant: 3 waves per SIMD (no spills) for small frames, 4 (128 VGPRs) for large ones (pathTailWaves) */
 			ta.tailWaves = pathTailWaves == 3 || pathTailWaves == 4 ? (uint32_t)pathTailWaves : small ? 3u : 4u;
 			const int occ = ta.tailWaves == 4 ? pathBlocksPerCU4 : pathBlocksPerCU;
@@ -1141,8 +1083,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				ts.cursor = cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS;
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
 				ts.mask = shMask, ts.potentials = shP, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
-				ts.prio = (uint32_t)prioSide;
-				lh2_launch_trace_any( &sd, &ts, sideBlocks > 0 ? smCount * sideBlocks : grid, 1, { nullptr, ps.evSide }, sideStream );
+				/* the global stack (sideStack) is sized for maxBlocksPerCU blocks per CU: the grid stays within it */
+				lh2_launch_trace_any( &sd, &ts, sideBlocks > 0 ? smCount * std::min( sideBlocks, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evSide }, sideStream );
 				ps.fromSide = ps.prevStop;
 				ps.sideOn = true;
 			}
@@ -1154,7 +1096,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		{
 			/* the paths are dense (camera order): fixed counts, no segment counters; the core stream waits for it */
 			ta.segCounts = nullptr, ta.segBack = nullptr, ta.countFixed = pathCount;
-			ta.prio = (uint32_t)prioPrimary;
 			lh2_launch_trace_primary( &sd, &ta, &cp, ps.T4P[ps.fp].ptr, ps.Q4P[ps.fp].ptr, PacketGrid(), { nullptr, ps.evTrace[pathLength] }, primStream );
 			if (primStream != stream && !early) CHK_HIP( hipStreamWaitEvent( stream, ps.evTrace[pathLength], 0 ) );
 		}
@@ -1163,9 +1104,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			/* a bounce launch the next frame's primary launch will likely run beside (this frame overlapped: the next one
 			   probably does too): fewer blocks per CU, so the packets' latency-bound waves get slots from the start instead
 			   of the bounce launch's tail (config 2: 4262-4296 -> 4437-4442 Mrays/s at 5, r03q_ab_trace_blocks.txt) */
-			const bool beside = besideNext && !ta.packet && overlapTraceBlocks > 0;
-			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, overlapTraceBlocks ) : grid;
-			ta.prio = (uint32_t)prioTrace;
+			const bool beside = besideNext && !ta.packet;
+			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, kOverlapTraceBlocks ) : grid;
 			ta.traceWaves = beside ? 7u : (uint32_t)traceWaves;   /* 8 waves slow the packets beside the launch (r04ad) */
 			lh2_launch_trace_closest( &sd, &ta, g, { nullptr, ps.evTrace[pathLength] }, stream );
 		}
@@ -1193,10 +1133,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		sp.primeRef = primeRef;
 		sp.terminal = !primeRef && !shadows && !canEmit && pathLength > 1 && terminalShade;
 		sp.R0 = (uint32_t)samplesTaken * 7907u + (uint32_t)pathLength * 91771u;
-		/* (not when the next frame's primary launch may run ahead: it would record into the block while this launch zeroes it;
-		   that frame zeroes it on its own stream) */
-		const bool nextMayBeAhead = primaryAhead == 2 || (primaryAhead == 1 && !tailL);
-		if (pathLength == 1 && fusedCam && hvReadBlock && !nextMayBeAhead)
+		if (pathLength == 1 && fusedCam && hvReadBlock)
 		{
 			/* the block this frame's packets read is the one the next frame records into */
 			sp.hvZero = hvReadBlock, sp.hvZeroWords = LH2_HV_MASK + ps.hvMaskWords;
@@ -1204,8 +1141,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		}
 		const bool earlyHere = early && pathLength == 1;
 		if (earlyHere) sp.acc = frameDelta;   /* the previous frame's finalize may not have read the accumulator yet */
-		/* a primary launch run ahead has not waited for the previous frame's overlap event: the early shade does */
-		if (earlyHere && ahead) CHK_HIP( hipStreamWaitEvent( aheadStream, prevOverlapEv, 0 ) );
 		lh2_launch_shade( &sd, &sp, shadeGrid, { nullptr, ps.evShade[pathLength] }, earlyHere ? aheadStream : stream );
 		if (earlyHere) CHK_HIP( hipStreamWaitEvent( stream, ps.evShade[pathLength], 0 ) );
 		ps.fromShade[pathLength] = ps.prevStop, ps.prevStop = ps.evShade[pathLength];
@@ -1251,6 +1186,15 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		}
 		ps.in = 1 - ps.in;
 	}
+	/* an early frame whose paths all ended before the shade launch before its path tail (pathTail >= 4, e.g. every primary
+	   ray misses): its overlap event is still its first shade launch, on the ahead stream, which never waited for the
+	   previous frame's finalize; the next frame's counter resets on this parity's block two frames on order themselves after
+	   overlapEv only.  So it moves to the core stream, behind the previous frame's finalize */
+	if (early && ps.overlapEv == ps.evShade[1])
+	{
+		CHK_HIP( hipEventRecord( ps.evEarlyEnd, stream ) );
+		ps.overlapEv = ps.evEarlyEnd;
+	}
 	/* a snapshot whose side launch did not happen (the frame ended before its path tail): the final launch
 	   traces every shadow ray, from the first */
 	if (snapped && !ps.sideOn)
@@ -1263,8 +1207,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.rayO = shO, ta.rayD = shD, ta.segCounts = c->segShadow, ta.segStride = ps.shadowStride;
 		ta.cursor = cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.mask = shMask, ta.potentials = shP, ta.acc = accumulator.ptr, ta.gstack = ps.gstack.ptr;
-		ta.prio = (uint32_t)prioShadow;
-		lh2_launch_trace_any( &sd, &ta, finalShadowBlocks > 0 ? smCount * finalShadowBlocks : grid, 1, { nullptr, ps.evShadow }, stream );
+		/* the global stack (gstack) is sized for maxBlocksPerCU blocks per CU: the grid stays within it */
+		lh2_launch_trace_any( &sd, &ta, finalShadowBlocks > 0 ? smCount * std::min( finalShadowBlocks, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evShadow }, stream );
 		ps.fromShadow = ps.prevStop;
 	}
 	/* the side launch's contributions are in the accumulator before the frame is finalized */
@@ -1295,7 +1239,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	}
 	hostStats->rayCount[0] = ps.count;
 	ps.lastFused = fusedCam, ps.lastSceneVersion = sceneVersion;
-	ps.lastNoTail = !ps.tailL;
 	framePathLengths = ps.tailL ? maxPL : ps.pl;
 	framePrimeRef = primeRef;
 	statsPending = true;
@@ -1459,6 +1402,24 @@ int RenderCore::DebugBvh4( float* f32Nodes, uint32_t* qNodes, int cap )
 	return n;
 }
 
+/* diagnostics (test hook): fill both TLAS slots' node regions (BVH2 and BVH4, f32 and quantized) with `value`, as memory an
+   earlier, larger TLAS or an uninitialised allocation leaves behind the nodes a TLAS update writes */
+void RenderCore::DebugPoisonTlas( float value )
+{
+	if (geometryDirty || instancesDirty) UpdateToplevel();
+	Synchronize();
+	SyncTlas();
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	CHK_HIP( hipStreamSynchronize( aheadStream ) );
+	std::vector<float> fill( (size_t)2 * tlasCapacity * 32, value );
+	CHK_HIP( hipMemcpy( dNodes.ptr + (size_t)blasNodeCount * 4, fill.data(), sizeof( float4 ) * 4 * 2 * (size_t)tlasCapacity, hipMemcpyHostToDevice ) );
+	if (bvh4)
+	{
+		CHK_HIP( hipMemcpy( dNodes4.ptr + (size_t)blasNode4Count * 8, fill.data(), sizeof( float4 ) * 8 * 2 * (size_t)tlasCapacity, hipMemcpyHostToDevice ) );
+		CHK_HIP( hipMemcpy( dNodes4q.ptr + (size_t)blasNode4Count * 4, fill.data(), sizeof( uint4 ) * 4 * 2 * (size_t)tlasCapacity, hipMemcpyHostToDevice ) );
+	}
+}
+
 void RenderCore::GetAccumulator( float* hostOut4 )
 {
 	Synchronize();
@@ -1514,7 +1475,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	TraceArgs ta{};
 	ta.version = TraceVersion();
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
-	ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
+	ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 	ta.packet = unitCoherent && UsePackets() ? 1 : 0;
 	ta.traceWaves = (uint32_t)unitTraceWaves;
 	lh2_launch_trace_closest( &sd, &ta, ta.packet ? PacketGrid() : UnitGrid(), {}, stream );
@@ -1573,7 +1534,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = cursors.ptr + (size_t)i * LH2_CURSOR_WORDS;
 		ta.hits = (uint4*)hitsOut, ta.gstack = ps.gstack.ptr;
 		/* unitCoherent: trace as the frame traces its (tiled) primary rays */
-		ta.refill = (uint32_t)(unitCoherent ? refillPrimary : refillOther), ta.leafBatch = (uint32_t)(unitCoherent ? leafBatchPrimary : leafBatch);
+		ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.packet = unitCoherent && UsePackets() ? 1 : 0;
 #ifdef LH2_TRACE_STATS
 		ta.stats = tstats.ptr;
@@ -1661,7 +1622,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto& e : ps.evShade) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evShadowB) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evCount) (void)hipEventDestroy( e ), e = nullptr;
-	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow, &ps.evSide }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
+	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow, &ps.evSide, &ps.evEarlyEnd }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
 	if (ps.activeLog) (void)hipHostFree( ps.activeLog );
 	ps.activeLog = nullptr;
 	for (hipEvent_t* e : { &evConsumer, &evPacked }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }

@@ -107,6 +107,7 @@ struct PathStreams
 	bool lastFused = false, relaid = true;
 	uint64_t lastSceneVersion = 0;
 	hipEvent_t overlapEv = nullptr;      /* the last frame's shade launch the next primary launch waits for (not owned) */
+	hipEvent_t evEarlyEnd = nullptr;     /* an early frame that ended before its path tail: overlapEv on the core stream (owned) */
 	hipEvent_t prevStop = nullptr;
 	int fp = 0;                          /* this (the last) frame's parity */
 	/* early shade (setting "earlyShade"): the next frame's first shade launch also runs beside this frame's launches
@@ -114,9 +115,6 @@ struct PathStreams
 	   neither (earlyOk), so the next frame's first shade writes the other one */
 	int busy = 0;
 	bool earlyOk = false, early = false;
-	/* primary ahead (setting "primaryAhead"): a frame without a path tail lets the next frame's primary launch start as soon
-	   as its own primary launch is done (the primary buffers are per parity), not after its first shade launch */
-	bool lastNoTail = false;
 };
 
 struct FrameStats   /* per-frame values delivered by k_finalize into pinned host memory */
@@ -172,6 +170,7 @@ public:
 	/* diagnostics: the last frame's queued shadow rays {O, tmin} {D, tmax} {potential rgb, pixel bits}, segment by segment */
 	int DebugShadowRays( float* o4, float* d4, float* p4, int cap );
 	int DebugBvh4( float* f32Nodes, uint32_t* qNodes, int cap );   /* the BVH4 nodes, f32 (32 floats) and quantized (16 words) */
+	void DebugPoisonTlas( float value );   /* test hook: both TLAS slots' node regions filled with value */
 	void TraceClosest( const float* orgTmin4, const float* dirTmax4, int n, uint32_t* hits4 );   /* host in/out */
 	void TraceAny( const float* orgTmin4, const float* dirTmax4, int n, uint32_t* occluded );
 	void TraceClosestDevice( const void* rayO, const void* rayD, int n, void* hits, int iterations, float* msOut );
@@ -183,12 +182,6 @@ public:
 	hipStream_t stream = nullptr;
 	hipStream_t sideStream = nullptr;    /* shadowOverlap: the device's least priority (the default level on MI355X) */
 	hipStream_t aheadStream = nullptr;   /* frameOverlap: the fused primary launch */
-	/* stream priorities (HIP's range on MI355X is 0 = the default .. -1 = high): the ahead stream's, 0 the default (the
-	   device's least: the same level as the core stream), 2 high; the core stream's, 0 the default, 1 high (the current
-	   frame's launches dispatch before the next frame's primary launch and the side shadow launch) */
-	int aheadPriority = 0, corePriority = 0;
-	void MakeAheadStream();
-	void MakeCoreStream();
 
 private:
 	void EnsureBuffers();
@@ -295,23 +288,28 @@ private:
 	   ping-pong buffer: PathStreams::earlyOk).  Accumulator additions of the two frames then interleave: the sum matches
 	   the sequential one within float rounding, not bit for bit (the first-vertex depths, w, stay exact) */
 	int earlyShade = 1;
-	/* ... for frames of at most this many paths: beside a large frame's tail the early shade gains nothing and its fold
-	   (FrameStatsDev::delta) costs (config-4 N = 1 frames 1 % slower, the N = 8 share 1.5 % faster: profiles/r04e_ab.txt;
-	   the N = 2 share, 4.1 M paths, 0.3 % faster without: r04r_ab.txt) */
-	float earlyShadeMaxPaths = 2.5e6f;
-	/* 1: after a frame without a path tail (config 2: every path ends at its second vertex), 2: after every frame: the
-	   next frame's primary launch waits only for this frame's primary launch and the finalize of the frame before (its
-	   parity's last user), so it runs beside this frame's first shade launch and bounce, not only beside the bounce */
-	int primaryAhead = 0;   /* config 2 5 % slower with 1 (profiles/r04e_ab.txt): off */
-	/* issue priorities (s_setprio, TraceArgs::prio) of the frame's traversal launches: the path tail, the final shadow
-	   launch, the side shadow launch, the primary launch, the bounce launches */
-	int prioTail = 0, prioShadow = 0, prioSide = 0, prioPrimary = 0, prioTrace = 0;
+	/* fixed policy constants (round 5: the knobs behind them were pruned; the values are the measured winners).
+	   Small frames (at most kSmallFramePaths paths: the N = 8 rank share, config 3) take the early shade (beside a large frame's
+	   tail it gains nothing and its fold costs: config-4 N = 1 1 % slower, r04e_ab.txt) and the path tail at 3 blocks per CU
+	   beside the side shadow launch (large frames 2: the 4K frame 6.54 vs 6.64-6.69 ms, r04p_ab.txt, r04r_ab.txt) */
+	static constexpr float kSmallFramePaths = 2.5e6f;
+	/* the shade launches' grid: about kShadePathsPerThread paths per thread, between the trace grid and kShadeMaxBlocks per CU
+	   (the N = 8 share 12 blocks per CU, config 3 24: -1.5 / -1.5 %, r04al_ab.txt, r04am_ab.txt, r04av_ab.txt) */
+	static constexpr float kShadePathsPerThread = 1.3f;
+	static constexpr int kShadeMaxBlocks = 24;
+	/* blocks per CU of a closest-hit launch that the next frame's primary launch runs beside (an overlapped frame's later
+	   bounces, no path tail): the packets' latency-bound waves get slots from the start (config 2 +4 %, r03q_ab_trace_blocks.txt) */
+	static constexpr int kOverlapTraceBlocks = 5;
+	/* packets while the BVH + triangles fit the 256 MB Infinity Cache (a packet's node and triangle records come through
+	   the scalar cache, one at a time: beyond the cache each is a DRAM round trip).  Config 3 (134 MB): primary 0.29 ->
+	   0.24 ms with packets; config 5 (1.4 GB): 5.3 -> 7.8 ms (profiles/r02zc_ab_packets_configs.txt) */
+	static constexpr double kPacketMaxBytes = 256.0 * 1048576.0;
 	uint64_t sceneVersion = 0;           /* incremented by every change of device-resident scene data or buffers */
 	/* dynamic ray fetch: refill a wave's idle lanes once this many are idle; BLAS leaves parked until this many
 	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,
 	   r02y_ab_v7.txt); leafBatch 8 with the quantized nodes (bounce 0.492 -> 0.488 ms, N = 8 share 1.35 -> 1.32 ms,
 	   r03k_ab_leafbatch.txt) */
-	int refillPrimary = 48, refillOther = 48, leafBatch = 8, leafBatchPrimary = 8;
+	int refillOther = 48, leafBatch = 8;   /* primary rays traced per ray (no packets) take the same (profiles/r04ag_refill_sweep.txt) */
 	int bvhMaxLeaf = 1;
 	/* spatial splits (SBVH): overlap threshold x root area; 0 = off.  1e-3 (round 4; 1e-5 before): the same node steps and
 	   triangle tests per ray (tools/bvh_quality.cpp: config 2 26.62 / 6.78 vs 26.64 / 6.68, the room 14.58 / 1.83 both)
@@ -337,24 +335,16 @@ private:
 	   shade launch slows the bounces it overlaps (2.344 / 1.426 ms) */
 	bool shadowOverlap = true;
 	int pathTailBlocks = 0;              /* the path tail's blocks per CU; 0: with the overlap 3 for frames of at most
-	                                        pathTailSmallPaths paths, else 2 (without: its occupancy limit) */
-	/* 3 blocks per CU: the N = 8 share 1.133 -> 1.112-1.125 ms, config 3 unchanged, the 4K frame 6.54 -> 6.64-6.69 ms and
-	   the N = 2 share (4.1 M paths) 3.48 -> 3.53 ms (profiles/r04p_ab.txt, r04r_ab.txt) */
-	float pathTailSmallPaths = 2.5e6f;
+	                                        kSmallFramePaths paths, else 2 (without: its occupancy limit) */
 	/* the path tail kernel's variant: 0, by frame size (3 waves per SIMD for small frames, 4 for larger ones); 3 or 4 */
 	int pathTailWaves = 0;
 	/* blocks per CU of the frame's last shadow launch (0: the trace grid's): 6 leaves the next frame's primary and early
 	   shade launches room beside it: config 3 and the N = 8 share -0.5 % (profiles/r04aj_ab.txt, r04ak_ab.txt) */
 	int finalShadowBlocks = 6;
 	int shadeBlocks = 0;                 /* blocks per CU of the frame's shade launches (0: by path count, Render) */
-	int shadeMaxBlocks = 24;
-	int shadeLastBlocks = 0;             /* blocks per CU of k_shade_last (config 2's last shade; 0: its occupancy) */
-	float shadePathsPerThread = 1.3f;
 	/* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's): 4 leaves the next frame's primary
 	   and early shade launches room: config 3 -0.5 %, the N = 8 share -0.8 to -1.5 % (profiles/r04m_ab.txt, r04n_ab.txt) */
 	int sideBlocks = 4;
-	int overlapTraceBlocks = 5;          /* blocks per CU of a closest-hit launch that the next frame's primary launch runs
-	                                        beside (an overlapped frame's later bounces, no path tail); 0: the trace grid's */
 	/* heavy-first primary packets (TraceArgs::hvRead): the packets of the previous frame that took more than
 	   packetHeavy x its mean node steps are taken first; 0: off */
 	float packetHeavy = 2.0f;
@@ -362,13 +352,7 @@ private:
 	int TraceVersion() const;
 	int unitCoherent = 0;
 	int packetPrimary = -1;              /* wave-uniform packet traversal for 8x8-tiled primary rays (-1: by scene size) */
-	/* auto: packets while the BVH + triangles fit the 256 MB Infinity Cache (a packet's node and triangle
-	   records come through the scalar cache, one at a time: beyond the cache each is a DRAM round trip).
-	   Config 3 (134 MB): primary 0.29 -> 0.24 ms with packets; config 5 (1.4 GB): 5.3 -> 7.8 ms
-	   (profiles/r02zc_ab_packets_configs.txt) */
-	float packetMaxMB = 256.0f;
 	int gpuBuild = 0, gpuTlas = 1;       /* BLAS builder (1: GPU PLOC, 0: CPU binned SAH); TLAS on the GPU */
-	float bvhTraversalCost = 1.0f;
 	int framePathLengths = 0, framePrimeRef = 0;
 	double frameHostMs = 0;
 	int samplesTaken = 0;

@@ -277,6 +277,40 @@ def light_from_tri(tri: np.ndarray, tri_idx: int, inst_idx: int, radiance) -> ab
     return L
 
 
+def point_light(pos, radiance, energy: float | None = None) -> abi.CorePointLight:
+    """HostScene::AddPointLight + HostPointLight::ConvertToCorePointLight (host_scene.cpp:568-577, host_light.cpp:68-75).
+    RenderSystem never sets HostPointLight::energy (default 0, host_light.h:61), so a point light reaching the core through
+    an unchanged RenderSystem has energy 0: its NEE potential (lights_shared.h:64-72) is 0 and it is never picked.
+    energy=None keeps that; a number is what a direct user of the core ABI may store."""
+    L = abi.CorePointLight()
+    L.position = abi.float3(*map(float, pos))
+    L.radiance = abi.float3(*map(float, radiance))
+    L.energy = 0.0 if energy is None else float(energy)
+    return L
+
+
+def spot_light(pos, direction, cos_inner: float, cos_outer: float, radiance) -> abi.CoreSpotLight:
+    """HostScene::AddSpotLight + ConvertToCoreSpotLight (host_scene.cpp:583-595, host_light.cpp:81-90): the direction as
+    given (RenderSystem does not normalise it), the cone as cosines; the potential uses the radiance sum
+    (lights_shared.h:78-95), so spot lights are sampled through an unchanged RenderSystem."""
+    L = abi.CoreSpotLight()
+    L.position = abi.float3(*map(float, pos))
+    L.direction = abi.float3(*map(float, direction))
+    L.radiance = abi.float3(*map(float, radiance))
+    L.cosInner, L.cosOuter = float(cos_inner), float(cos_outer)
+    return L
+
+
+def directional_light(direction, radiance, energy: float | None = None) -> abi.CoreDirectionalLight:
+    """HostScene::AddDirectionalLight + ConvertToCoreDirectionalLight (host_scene.cpp:601-610, host_light.cpp:96-102):
+    the direction as given; energy, as for point lights, stays 0 through RenderSystem (None) unless set."""
+    L = abi.CoreDirectionalLight()
+    L.direction = abi.float3(*map(float, direction))
+    L.radiance = abi.float3(*map(float, radiance))
+    L.energy = 0.0 if energy is None else float(energy)
+    return L
+
+
 def quad_tris(N, pos, width: float, height: float, material: int) -> np.ndarray:
     """HostScene::AddQuad (host_scene.cpp:346-393): two triangles, explicit normal N."""
     N = _norm(_f3(*N))

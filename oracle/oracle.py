@@ -75,6 +75,14 @@ def lib() -> C.CDLL:
         L.orc_bluenoise.restype = C.c_float
         L.orc_pack_normal.argtypes = [C.c_float] * 3
         L.orc_pack_normal.restype = C.c_uint32
+        L.orc_light_potential.argtypes = [_P, C.c_int, _F, _F, _F, _F]
+        L.orc_light_potential.restype = C.c_float
+        L.orc_light_pick_prob.argtypes = [_P, C.c_int, _F, _F, _F]
+        L.orc_light_pick_prob.restype = C.c_float
+        L.orc_random_barycentrics.argtypes = [C.c_float, _F]
+        L.orc_random_barycentrics.restype = None
+        L.orc_random_point_on_light.argtypes = [_P, C.c_float, C.c_float, _F, _F, _F]
+        L.orc_random_point_on_light.restype = None
         _lib = L
     return _lib
 

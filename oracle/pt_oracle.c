@@ -1108,6 +1108,31 @@ static f3 RandomPointOnLight( const Oracle* o, float r0, float r1, f3 I, f3 N, f
 	}
 }
 
+/* unit-level light entry points (the light KATs, tests/test_oracle_kats.py): the functions above, on the lights set by
+   orc_set_lights.  Vectors are float[3]. */
+float orc_light_potential( const Oracle* o, int i, const float* I, const float* N, const float* bary, const float* areaI )
+{
+	return potential_i( o, i, mk3( I[0], I[1], I[2] ), mk3( N[0], N[1], N[2] ), mk3( bary[0], bary[1], bary[2] ), mk3( areaI[0], areaI[1], areaI[2] ) );
+}
+float orc_light_pick_prob( const Oracle* o, int idx, const float* O, const float* N, const float* I )
+{
+	return LightPickProb( o, idx, mk3( O[0], O[1], O[2] ), mk3( N[0], N[1], N[2] ), mk3( I[0], I[1], I[2] ) );
+}
+void orc_random_barycentrics( float r0, float* out3 )
+{
+	const f3 b = RandomBarycentrics( r0 );
+	out3[0] = b.x, out3[1] = b.y, out3[2] = b.z;
+}
+/* out8: the point on the light (x, y, z), pickProb, lightPdf, lightColor (r, g, b); pickProb and lightColor are 0 when
+   no light has potential (lightPdf 0: the shade code queues no shadow ray) */
+void orc_random_point_on_light( const Oracle* o, float r0, float r1, const float* I, const float* N, float* out8 )
+{
+	float pickProb = 0, lightPdf = 0;
+	f3 color = s3( 0 );
+	const f3 P = RandomPointOnLight( o, r0, r1, mk3( I[0], I[1], I[2] ), mk3( N[0], N[1], N[2] ), &pickProb, &lightPdf, &color );
+	out8[0] = P.x, out8[1] = P.y, out8[2] = P.z, out8[3] = pickProb, out8[4] = lightPdf, out8[5] = color.x, out8[6] = color.y, out8[7] = color.z;
+}
+
 /* ------------------------------------------------------------------------------------- */
 /* Disney BSDF: sharedBSDFs/disney.h:33-333, ggxmdf.h:23-243                               */
 /* ------------------------------------------------------------------------------------- */

@@ -67,6 +67,14 @@ void orc_trace_closest( const Oracle* o, const float* orgTmin4, const float* dir
 /* any hit: bit i of occluded[i>>5] set when ray i hits anything in (tmin, tmax) */
 void orc_trace_any( const Oracle* o, const float* orgTmin4, const float* dirTmax4, int n, uint32_t* occluded );
 
+/* lights (lights_shared.h:36-261) on the lights of orc_set_lights: light i's potential (area, point, spot, directional
+   order; bary / areaI as RandomPointOnLight / LightPickProb pass them), LightPickProb, RandomBarycentrics, and
+   RandomPointOnLight (out8: point xyz, pickProb, lightPdf, lightColor rgb) */
+float orc_light_potential( const Oracle* o, int i, const float* I3, const float* N3, const float* bary3, const float* areaI3 );
+float orc_light_pick_prob( const Oracle* o, int idx, const float* O3, const float* N3, const float* I3 );
+void orc_random_barycentrics( float r0, float* out3 );
+void orc_random_point_on_light( const Oracle* o, float r0, float r1, const float* I3, const float* N3, float* out8 );
+
 /* numerics KATs */
 uint32_t orc_wanghash( uint32_t s );
 uint32_t orc_xorshift( uint32_t s );

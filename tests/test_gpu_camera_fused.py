@@ -7,8 +7,7 @@ their own parity; the frame's resets are a k_init_counters launch before the pri
 heavy-packet block the next frame records into is zeroed by the first shade launch (or, before a frame whose primary
 launch may run ahead, by a memset on the ahead stream).  With earlyShade (default) the first shade launch of a frame after
 one with a path tail follows its primary launch on the ahead stream too, beside the previous frame's path tail and shadow
-launches; with primaryAhead the primary launch of a frame after one without a path tail starts once that frame's
-primary launch is done (primary buffers per frame parity).
+launches.
 
 Against the CPU oracle (pathtracer.h:54-245 after generateEyeRays): identical per-bounce ray counts every frame,
 accumulator rel-L2 <= 1e-4; and frames queued back to back (no host synchronisation between them, so the primary
@@ -74,19 +73,18 @@ def test_camera_fused_frames(fresh_core, kind):
         assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (f, fresh_core.ray_counts()[:6], o.ray_counts()[:6])
     ref = o.accumulator()
     res = {}
-    # (cameraFused, frameOverlap, earlyShade, primaryAhead)
-    variants = ((1, 1, 1, 1), (1, 1, 1, 2), (1, 1, 0, 2), (1, 1, 1, 0), (1, 1, 0, 0), (1, 0, 0, 0), (0, 0, 0, 0))
-    for fused, overlap, early, ahead in variants:
+    # (cameraFused, frameOverlap, earlyShade)
+    variants = ((1, 1, 1), (1, 1, 0), (1, 2, 0), (1, 0, 0), (0, 0, 0))
+    for fused, overlap, early in variants:
         fresh_core.setting("cameraFused", fused)
         fresh_core.setting("frameOverlap", overlap)
         fresh_core.setting("earlyShade", early)
-        fresh_core.setting("primaryAhead", ahead)
         for f, conv in enumerate(SEQUENCE):   # queued back to back: no synchronisation between frames
             if anim:
                 _animate(sc, fresh_core, f)
             sc.render_frame(fresh_core, converge=conv)
-        res[(fused, overlap, early, ahead)] = fresh_core.accumulator()
-        assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (fused, overlap, early, ahead)
+        res[(fused, overlap, early)] = fresh_core.accumulator()
+        assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (fused, overlap, early)
     a = res[variants[0]]
     assert rel_l2(a[..., :3], ref[..., :3]) <= REL_L2_TOL
     for k in variants[1:]:
@@ -181,3 +179,34 @@ def test_animated_frames_with_new_geometry(gpu_build):
     assert np.array_equal(ca, cb), (ca[:6], cb[:6])
     assert np.any(a[..., :3] != 0)
     assert rel_l2(b[..., :3], a[..., :3]) <= 1e-6
+
+
+def test_early_frame_ending_before_its_tail(fresh_core):
+    """with the path tail from bounce 4, an early frame (its first shade launch on the ahead stream, beside the
+    previous frame's tail) whose paths all end at their first vertex (every primary ray misses: the camera looks away from
+    the room) leaves the bounce loop before the shade launch before its tail.  Its overlap event, which the next frames'
+    counter resets and primary launches order themselves after, must then be a core-stream event behind the previous
+    frame's finalize (RenderCore::Render, PathStreams::evEarlyEnd), not the early shade.  Frames that alternate between the
+    room and the empty view, queued back to back, equal the same frames serialised (frameOverlap 0)."""
+    w, h = 96, 64
+    sc = scene.room_scene(40000, w, h)
+    room_view = sc.view
+    away = scene.camera_view((0, 6, 200), (0, 0, 1), fov_deg=60, aspect=w / h, focal=5, pixel_height=h)
+    sc.load_into(fresh_core)
+    fresh_core.set_target(w, h, 1)
+    fresh_core.setting("maxPathLength", 6)
+    fresh_core.setting("pathTail", 4)
+    views = [room_view, away, away, room_view, away, room_view, room_view, away]
+
+    def run(overlap):
+        fresh_core.setting("frameOverlap", overlap)
+        for f, v in enumerate(views):
+            sc.render_frame(fresh_core, converge=1 if f == 0 else 0, view=v)
+        return fresh_core.accumulator(), fresh_core.ray_counts()
+
+    a, ca = run(0)
+    b, cb = run(1)
+    assert np.array_equal(ca, cb)
+    assert np.any(a[..., :3] != 0)
+    assert rel_l2(b[..., :3], a[..., :3]) <= 1e-6
+    assert np.array_equal(a[..., 3], b[..., 3])

@@ -588,3 +588,43 @@ def test_quantized_grid_range_is_checked(fresh_core):
     with pytest.raises(CoreError, match="quantized"):
         sc.render_frame(fresh_core)
         fresh_core.sync()
+
+
+@pytest.mark.parametrize("gpu_tlas", [1, 0])
+def test_stale_tlas_region_is_not_quantized(gpu_tlas):
+    """The TLAS slots hold tlasCapacity nodes; a TLAS update writes only the nodes its tree has.  The rest is an earlier,
+    larger TLAS or memory never written, which may hold huge finite boxes.  Round 4's range check (k_quantize4) fired on
+    such memory (`test_traversal_variants_bitexact[7-1-2]`, fixed by NaN-filling the region at allocation, 651cce0);
+    since round 5 the BVH4 copy and the quantizer touch only the TLAS's own nodes (rendercore.cpp UpdateToplevel).  Here
+    both slots are filled with 3e38 (finite: it passes k_quantize4's validity test and needs a grid exponent far past
+    LH2_QEXP_MAX) before an instance update: the frame must render, equal to the same frames without the fill."""
+    from lighthouse2_amd.core import RenderCore
+
+    def run(poison):
+        c = RenderCore(device=0)
+        try:
+            c.setting("gpuTlas", gpu_tlas)
+            sc = scene.instanced_scene(meshes=6, tris_per_mesh=2000, width=64, height=36, grid=3, spacing=12.0)
+            sc.load_into(c)
+            c.set_target(64, 36, 1)
+            sc.render_frame(c, converge=1)
+            c.sync()
+            if poison:
+                c.debug_poison_tlas(3e38)
+            scene.animate_instances(sc, 1)
+            for k, (mesh, T) in enumerate(sc.instances[:4]):   # fewer instances: a smaller TLAS than the slot held
+                c.set_instance(k, mesh, T)
+            c.set_instance(4, -1, None)
+            c.update_toplevel()
+            sc.render_frame(c, converge=0)
+            c.sync()
+            return c.accumulator(), c.ray_counts()
+        finally:
+            c.close()
+
+    a, ca = run(False)
+    b, cb = run(True)
+    assert np.array_equal(ca, cb)
+    assert np.any(a[..., :3] != 0)
+    assert rel_l2(b[..., :3], a[..., :3]) <= 1e-6
+    assert np.array_equal(a[..., 3], b[..., 3])

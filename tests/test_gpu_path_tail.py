@@ -171,20 +171,20 @@ def test_shadow_overlap(fresh_core, blocks, tail, side, final):
     assert rel_l2(ag[..., :3], res[0][0][..., :3]) <= 1e-6
 
 
-@pytest.mark.parametrize("blocks,ppt", [(0, 1.3), (0, 0.25), (1, 1.3), (8, 1.3), (40, 1.3)])
-def test_shade_grid(fresh_core, blocks, ppt):
-    """The shade launches' grid (shadeBlocks per CU; 0: about shadePathsPerThread paths per thread, between the trace
-    grid and shadeMaxBlocks per CU): each block walks its segment with a static stride, so every grid must shade every
-    path once; the same ray counts as the oracle and the frame within float summation order of the default grid's."""
+@pytest.mark.parametrize("blocks", [1, 8, 40, 64])
+def test_shade_grid(fresh_core, blocks):
+    """The shade launches' grid (shadeBlocks per CU; 0, the default: about 1.3 paths per thread, between the trace grid
+    and 24 blocks per CU, RenderCore::kShadePathsPerThread / kShadeMaxBlocks): each block walks its segment with a static
+    stride, so every grid must shade every path once; the same ray counts as the oracle and the frame within float
+    summation order of the default grid's."""
     w, h = 128, 72
     sc = _scene("room", w, h)
     o = _load_both(fresh_core, sc, w, h)
     for tgt in (fresh_core, o):
         tgt.setting("maxPathLength", 4)
     res = []
-    for b, p in ((0, 1.3), (blocks, ppt)):
+    for b in (0, blocks):
         fresh_core.setting("shadeBlocks", b)
-        fresh_core.setting("shadePathsPerThread", p)
         for f in range(2):
             sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
             if not res:

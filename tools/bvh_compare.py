@@ -50,7 +50,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scenes", default="config2,room,instanced")
     ap.add_argument("--frames", type=int, default=5)
-    ap.add_argument("--radius", type=int, default=16)
     ap.add_argument("--builders", default="0,1")
     a = ap.parse_args()
     for name in a.scenes.split(","):
@@ -64,7 +63,6 @@ def main():
         else:
             sc = scene.instanced_scene(meshes=20, tris_per_mesh=100_000, width=1920, height=1080, grid=5)
             spp, st = 2, {}
-        st["plocRadius"] = a.radius
         for b in a.builders.split(","):
             run(name, sc, int(b), spp, a.frames, st)
 

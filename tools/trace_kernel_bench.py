@@ -37,11 +37,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tris", type=int, default=100_000)
     ap.add_argument("--set", default="both")
-    # defaults = the core's (RenderCore refillOther / refillPrimary / leafBatch / leafBatchPrimary)
+    # defaults = the core's (RenderCore refillOther / leafBatch: primary rays traced per ray take the same)
     ap.add_argument("--refill", type=int, default=None, help="default: the core's setting")
-    ap.add_argument("--refill-primary", type=int, default=None)
     ap.add_argument("--leaf-batch", type=int, default=None)
-    ap.add_argument("--leaf-batch-primary", type=int, default=None)
     ap.add_argument("--no-frame-launch", action="store_true",
                     help="do not set unitCoherent=1 for the primary set (the frame's launch: packets when auto-selected)")
     ap.add_argument("--pre-setting", action="append", default=[], help="name=value set before loading (BVH build)")
@@ -176,12 +174,10 @@ def main():
             continue
         n = len(o)
         prim = name.startswith("primary")
-        rf = args.refill_primary if prim else args.refill
-        lb = args.leaf_batch_primary if prim else args.leaf_batch
-        if rf is not None:
-            core.setting("refillPrimary" if prim else "refill", rf)
-        if lb is not None:
-            core.setting("leafBatchPrimary" if prim else "leafBatch", lb)
+        if args.refill is not None:
+            core.setting("refill", args.refill)
+        if args.leaf_batch is not None:
+            core.setting("leafBatch", args.leaf_batch)
         if not args.no_frame_launch:
             core.setting("unitCoherent", 1 if prim else 0)
         ro, rd = torch.from_numpy(o).to(dev), torch.from_numpy(d).to(dev)
