@@ -436,6 +436,33 @@ def roofline_of(core, sc, W, H, dev, kernel_iters):
     return roof, prim, detail, model_gbs
 
 
+def roofline_config5(c5):
+    """The HBM view of the DRAM-real workload (config 5: 1 GB of BVH + triangles, beyond the 256 MB Infinity Cache): the
+    per-ray closest-hit launch's measured bytes (2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes over config-5
+    frames, the committed *_pmc_config5_traffic.json) / its launch time in the same passes / 8 TB/s.  An UPPER bound of
+    DRAM traffic: FETCH_SIZE also counts Infinity-Cache (MALL) hits (MI355X_MICROARCH.md, the HBM / rocprofv3 section).
+    The live launch times of this run's config-5 frames (CoreStats traceTime0 / traceTime1: the primary and the bounce
+    launch, each with its launch gap) sit beside it."""
+    src, d = newest("*_pmc_config5_traffic.json")
+    if not d:
+        return None
+    ks = [k for k in d["kernels"] if k["kernel"].startswith("void k_trace_closest4d")]
+    if not ks:
+        return None
+    k = max(ks, key=lambda r: r["launch_ms_median"] * r["launches"])
+    gbs = k["bytes_per_launch"] / (k["launch_ms_median"] * 1e-3) / 1e9
+    out = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+           "traffic": k["bytes_per_launch"], "upper_bound": True,
+           "kernel": k["kernel"].split("(")[0] + " (config 5: per-ray closest hit, primary and bounce launches of 1080p 8 spp frames)",
+           "kernel_ms": k["launch_ms_median"], "launches": k["launches"], "evidence": src,
+           "note": "bytes = 2 x FETCH_SIZE + WRITE_SIZE per launch (gfx950 calibration), medians over the passes' launches; "
+                   "FETCH_SIZE counts Infinity-Cache hits too, so frac is an upper bound of the DRAM fraction"}
+    if c5:
+        cs = c5["coreStats_ms"]
+        out["live_launch_ms"] = {"primary": cs["trace0"], "bounce": cs["trace1"]}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -552,6 +579,7 @@ def main():
         out["config4_incore"] = c4in
         out["config3"] = c3
         out["config5"] = c5
+        out["roofline_config5"] = roofline_config5(c5) if world == 1 else None
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(sc, args.width, args.height, args.cpu_seconds)
         else:

@@ -1,5 +1,6 @@
 /* bvh_build.cpp - parallel binned-SAH BVH2 builder (see bvh_build.h). */
 #include "bvh_build.h"
+#include "lh2_w8.h"
 
 #include <algorithm>
 #include <atomic>
@@ -682,22 +683,26 @@ int CollapseBvh4( const float* nodes2, size_t nodeCount2, std::vector<float>& no
 }
 
 
-/* ---- BVH2 -> BVH4 by dynamic programming over the BVH2 (surface-area cost) ----------------------
+/* ---- BVH2 -> W-wide by dynamic programming over the BVH2 (surface-area cost) ---------------------
    The collapse of Ylitie, Karras and Laine ("Efficient Incoherent Ray Traversal on GPUs Through
-   Compressed Wide BVHs", HPG 2017, section 4) for four-wide nodes: for every BVH2 subtree and every
-   slot count j <= 4, the cheapest way to hand it to a BVH4 parent as at most j entries - one BVH4
-   node, one leaf (a subtree of at most maxLeafTris triangles, its leaves contiguous in the DFS perm
+   Compressed Wide BVHs", HPG 2017, section 4) for W-wide nodes (4: the BVH4, 8: the W8 of lh2_w8.h): for every
+   BVH2 subtree and every slot count j <= W, the cheapest way to hand it to a wide parent as at most j entries -
+   one wide node, one leaf (a subtree of at most maxLeafTris triangles, its leaves contiguous in the DFS perm
    order that Flatten emits), or its two children's entries side by side - under the expected cost
    area x (cNode per node step, cLeaf + cTri x triangles per leaf visit).  Costs are in units of a
-   node step of the traversal loop. */
-int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>& nodes4, float cLeaf, float cTri, int maxLeafTris )
+   node step of the traversal loop.  Output: the wide nodes in breadth-first order (node 0 the root), each a list of
+   its children (ref >= 0: a wide node's index, < 0: a leaf reference as the BVH2's). */
+namespace {
+struct WEnt { float lo[3], hi[3]; int ref; };
+int CollapseWideSah( const float* nodes2, size_t nodeCount2, const int W, float cLeaf, float cTri, int maxLeafTris,
+	std::vector<std::vector<WEnt>>& wide )
 {
-	const float nanv = std::numeric_limits<float>::quiet_NaN();
-	nodes4.assign( 32, 0.0f );
-	if (nodeCount2 == 0) { for (int i = 0; i < 24; i++) nodes4[i] = nanv; return 1; }
+	wide.clear();
+	if (nodeCount2 == 0) { wide.emplace_back(); return 1; }
 	maxLeafTris = std::min( 16, std::max( 1, maxLeafTris ) );
+	const int J = W + 1;
 	const float INF = std::numeric_limits<float>::infinity();
-	struct Ent { float lo[3], hi[3]; int ref; };                 /* a BVH2 child: box + reference */
+	typedef WEnt Ent;                                           /* a BVH2 child: box + reference */
 	auto child = [&]( size_t k, int c, Ent& e ) {
 		const float* n = nodes2 + k * 16;
 		e.lo[0] = n[c * 4 + 0], e.hi[0] = n[c * 4 + 1], e.lo[1] = n[c * 4 + 2], e.hi[1] = n[c * 4 + 3];
@@ -711,20 +716,20 @@ int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>&
 		const float dx = std::max( 0.0f, e.hi[0] - e.lo[0] ), dy = std::max( 0.0f, e.hi[1] - e.lo[1] ), dz = std::max( 0.0f, e.hi[2] - e.lo[2] );
 		return dx * dy + dy * dz + dz * dx;
 	};
-	/* per BVH2 node: its children, triangle count, first perm slot, and d[j] (j = 1..4) with choices */
+	/* per BVH2 node: its children, triangle count, first perm slot, and d[j] (j = 1..W) with choices */
 	const size_t N2 = nodeCount2;
 	std::vector<Ent> ch( N2 * 2 );
 	std::vector<uint8_t> nch( N2 );
 	std::vector<uint32_t> tris( N2 ), first( N2 );
-	std::vector<float> d( N2 * 5, INF ), asNode( N2, INF );
-	std::vector<int8_t> choice( N2 * 5, 0 );     /* d[j]: 0 = one entry (node or leaf), -1 = as d[j-1], i > 0: i entries to child 0 */
+	std::vector<float> d( N2 * J, INF ), asNode( N2, INF );
+	std::vector<int8_t> choice( N2 * J, 0 );     /* d[j]: 0 = one entry (node or leaf), -1 = as d[j-1], i > 0: i entries to child 0 */
 	std::vector<int8_t> nodeSplit( N2, 0 );      /* asNode: entries to child 0 (0: single child takes all) */
 	std::vector<uint8_t> nodeCnt( N2, 0 );
 	auto ent_tris = [&]( const Ent& e ) { return e.ref < 0 ? (uint32_t)(((uint32_t)(~e.ref) & 15u) + 1) : tris[e.ref]; };
 	auto ent_first = [&]( const Ent& e ) { return e.ref < 0 ? (uint32_t)(~e.ref) >> 4 : first[e.ref]; };
 	auto dist = [&]( const Ent& e, int j ) {
 		if (e.ref < 0) return harea( e ) * (cLeaf + cTri * (float)ent_tris( e ));
-		return d[(size_t)e.ref * 5 + j];
+		return d[(size_t)e.ref * J + j];
 	};
 	for (size_t kk = N2; kk-- > 0;)
 	{
@@ -759,24 +764,24 @@ int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>&
 	for (size_t kk = N2; kk-- > 0;)
 	{
 		const float A = area2[kk];
-		/* as a BVH4 node: the best 2..4 entries of its children */
+		/* as a wide node: the best 2..W entries of its children */
 		float bestN = INF;
-		for (int m = 2; m <= 4; m++)
+		for (int m = 2; m <= W; m++)
 		{
 			int at;
 			const float c = split( kk, m, at );
 			if (c < bestN) bestN = c, nodeSplit[kk] = (int8_t)at, nodeCnt[kk] = (uint8_t)m;
 		}
-		if (nch[kk] < 2) { int at; bestN = split( kk, 4, at ); nodeSplit[kk] = 0, nodeCnt[kk] = 4; }
+		if (nch[kk] < 2) { int at; bestN = split( kk, W, at ); nodeSplit[kk] = 0, nodeCnt[kk] = (uint8_t)W; }
 		asNode[kk] = A * 1.0f + bestN;
 		const float asLeaf = tris[kk] <= (uint32_t)maxLeafTris && tris[kk] > 0 ? A * (cLeaf + cTri * (float)tris[kk]) : INF;
-		d[kk * 5 + 1] = std::min( asNode[kk], asLeaf ), choice[kk * 5 + 1] = 0;
-		for (int j = 2; j <= 4; j++)
+		d[kk * J + 1] = std::min( asNode[kk], asLeaf ), choice[kk * J + 1] = 0;
+		for (int j = 2; j <= W; j++)
 		{
 			int at;
 			const float c = split( kk, j, at );
-			if (c < d[kk * 5 + j - 1]) d[kk * 5 + j] = c, choice[kk * 5 + j] = (int8_t)(nch[kk] == 1 ? 100 : at);
-			else d[kk * 5 + j] = d[kk * 5 + j - 1], choice[kk * 5 + j] = -1;
+			if (c < d[kk * J + j - 1]) d[kk * J + j] = c, choice[kk * J + j] = (int8_t)(nch[kk] == 1 ? 100 : at);
+			else d[kk * J + j] = d[kk * J + j - 1], choice[kk * J + j] = -1;
 		}
 	}
 	auto is_leaf_choice = [&]( size_t k ) {
@@ -787,21 +792,22 @@ int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>&
 	std::function<void( const Ent&, int, std::vector<Ent>& )> expand = [&]( const Ent& e, int j, std::vector<Ent>& out ) {
 		if (e.ref < 0) { out.push_back( e ); return; }
 		const size_t k = (size_t)e.ref;
-		while (j > 1 && choice[k * 5 + j] == -1) j--;
-		if (j == 1 || choice[k * 5 + j] == 0)
+		while (j > 1 && choice[k * J + j] == -1) j--;
+		if (j == 1 || choice[k * J + j] == 0)
 		{
 			Ent x = e;
 			if (is_leaf_choice( k )) x.ref = (int)~((first[k] << 4) | (tris[k] - 1));
 			out.push_back( x );
 			return;
 		}
-		if (choice[k * 5 + j] == 100) { expand( ch[k * 2], j, out ); return; }
-		const int i = choice[k * 5 + j];
+		if (choice[k * J + j] == 100) { expand( ch[k * 2], j, out ); return; }
+		const int i = choice[k * J + j];
 		expand( ch[k * 2], i, out );
 		expand( ch[k * 2 + 1], j - i, out );
 	};
-	struct Item { size_t node2; int node4, depth; };
-	std::vector<Item> queue{ { 0, 0, 1 } };
+	struct Item { size_t node2; int depth; };
+	std::vector<Item> queue{ { 0, 1 } };
+	wide.emplace_back();
 	int depth = 1;
 	for (size_t qi = 0; qi < queue.size(); qi++)
 	{
@@ -816,20 +822,34 @@ int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>&
 			expand( ch[k * 2], i, list );
 			expand( ch[k * 2 + 1], nodeCnt[k] - i, list );
 		}
-		int refs[4] = { 0, 0, 0, 0 };
-		const int n = (int)list.size();
-		for (int i = 0; i < n; i++)
-		{
-			if (list[i].ref >= 0)
+		for (auto& e : list)
+			if (e.ref >= 0)
 			{
-				const int child4 = (int)(nodes4.size() / 32);
-				nodes4.resize( nodes4.size() + 32, 0.0f );
-				queue.push_back( { (size_t)list[i].ref, child4, it.depth + 1 } );
-				refs[i] = child4;
+				queue.push_back( { (size_t)e.ref, it.depth + 1 } );
+				e.ref = (int)wide.size();
+				wide.emplace_back();
 			}
-			else refs[i] = list[i].ref;
-		}
-		float* q = &nodes4[(size_t)it.node4 * 32];
+		wide[qi] = std::move( list );
+	}
+	return depth;
+}
+}  // namespace
+
+int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>& nodes4, float cLeaf, float cTri, int maxLeafTris )
+{
+	const float nanv = std::numeric_limits<float>::quiet_NaN();
+	nodes4.assign( 32, 0.0f );
+	if (nodeCount2 == 0) { for (int i = 0; i < 24; i++) nodes4[i] = nanv; return 1; }
+	std::vector<std::vector<WEnt>> wide;
+	const int depth = CollapseWideSah( nodes2, nodeCount2, 4, cLeaf, cTri, maxLeafTris, wide );
+	nodes4.assign( wide.size() * 32, 0.0f );
+	for (size_t w = 0; w < wide.size(); w++)
+	{
+		const auto& list = wide[w];
+		const int n = (int)list.size();
+		int refs[4] = { 0, 0, 0, 0 };
+		for (int i = 0; i < n; i++) refs[i] = list[i].ref;
+		float* q = &nodes4[w * 32];
 		for (int i = 0; i < 4; i++)
 		{
 			/* the six planes of four (lh2_device.h): lo.x, hi.x, lo.y, hi.y, lo.z, hi.z of children 0..3 */
@@ -840,6 +860,61 @@ int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>&
 		memcpy( q + 24, refs, 16 );
 	}
 	return depth;
+}
+
+/* ---- BVH2 -> W8 (lh2_w8.h) ---------------------------------------------------------------------
+   The 8-wide DP collapse, laid out breadth-first in blocks of 8 records: block 0 holds the root's record in slot 0;
+   each node's children get the next free block, in the slots of their centroids' directions (lh2_w8_assign), a node
+   child as its quantized record, a leaf child (one triangle: the BLAS is built with one triangle per leaf) as the
+   48-B triangle record of its perm slot (tris48, 12 floats per slot).  Returns false when a leaf holds more than one
+   triangle (bvhMaxLeaf > 1: no W8 for this mesh); child blocks are relative to the mesh's first block. */
+bool BuildW8( const float* nodes2, size_t nodeCount2, const float* tris48, size_t triRecords, float cLeaf, float cTri,
+	std::vector<uint32_t>& records, int& blocks, int& depth, int& qerr )
+{
+	std::vector<std::vector<WEnt>> wide;
+	depth = CollapseWideSah( nodes2, nodeCount2, 8, cLeaf, cTri, 1, wide );
+	for (const auto& l : wide) for (const auto& e : l) if (e.ref < 0 && (((uint32_t)~e.ref) & 15u) != 0) return false;
+	/* blocks: the root block, then one per wide node */
+	blocks = (int)wide.size() + 1;
+	records.assign( (size_t)blocks * 8 * LH2_W8_WORDS, 0u );
+	qerr = 0;
+	struct Item { size_t w; size_t slot; };
+	std::vector<Item> queue{ { 0, 0 } };
+	uint32_t nextBlock = 1;
+	for (size_t qi = 0; qi < queue.size(); qi++)
+	{
+		const Item it = queue[qi];
+		const auto& list = wide[it.w];
+		const int n = std::min( 8, (int)list.size() );
+		const uint32_t blk = nextBlock++;
+		float d[8][3] = {}, lo[8][3], hi[8][3];
+		float plo[3] = { INFINITY, INFINITY, INFINITY }, phi[3] = { -INFINITY, -INFINITY, -INFINITY };
+		for (int i = 0; i < n; i++) for (int a = 0; a < 3; a++) plo[a] = std::min( plo[a], list[i].lo[a] ), phi[a] = std::max( phi[a], list[i].hi[a] );
+		for (int i = 0; i < n; i++) for (int a = 0; a < 3; a++) d[i][a] = 0.5f * (list[i].lo[a] + list[i].hi[a]) - 0.5f * (plo[a] + phi[a]);
+		int slotOf[8];
+		lh2_w8_assign( n, d, slotOf );
+		bool valid[8] = {};
+		uint32_t imask = 0;
+		for (int s = 0; s < 8; s++) for (int a = 0; a < 3; a++) lo[s][a] = hi[s][a] = 0.0f;
+		for (int i = 0; i < n; i++)
+		{
+			const int sl = slotOf[i];
+			valid[sl] = lh2_w8_box_valid( list[i].lo, list[i].hi );
+			for (int a = 0; a < 3; a++) lo[sl][a] = list[i].lo[a], hi[sl][a] = list[i].hi[a];
+			const size_t at = (size_t)blk * 8 + (size_t)sl;
+			if (list[i].ref >= 0) { imask |= 1u << sl; queue.push_back( { (size_t)list[i].ref, at } ); }
+			else
+			{
+				const uint32_t tf = (uint32_t)(~list[i].ref) >> 4;
+				if (tf >= triRecords) return false;
+				memcpy( &records[at * LH2_W8_WORDS], tris48 + (size_t)tf * 12, 48 );
+			}
+		}
+		uint32_t* rec = &records[it.slot * LH2_W8_WORDS];
+		qerr |= lh2_w8_quantize( valid, lo, hi, imask, rec );
+		rec[18] = blk;
+	}
+	return true;
 }
 
 }  // namespace lh2

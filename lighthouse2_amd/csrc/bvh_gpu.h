@@ -42,7 +42,8 @@ struct GpuTlasArgs
 	int count;                   /* instances (>= 2) */
 	int nodeBase;                /* index of the TLAS root in the node array */
 	float4* nodes;               /* node array; the TLAS is written at nodeBase (<= count - 1 nodes) */
-	int maxBlasDepth;            /* stack check: TLAS depth + this must stay below LH2_STACK_TOTAL - 1 */
+	int maxBlasDepth;            /* stack check: tlasFactor x TLAS depth + this must stay below LH2_STACK_TOTAL - 1 */
+	int tlasFactor = 1;          /* stack entries per TLAS level (the W8 loop: 2) */
 	int* sceneError;             /* device flag: set when the stack check fails (traversal then exits) */
 	int* tlasDepth;              /* device: TLAS depth out */
 };
@@ -76,6 +77,11 @@ public:
 	   8-bit child planes on a per-node, per-axis power-of-two grid, rounded outward; a node beyond the grid's range
 	   sets LH2_SCENE_ERR_QRANGE in *sceneError */
 	static void Quantize4( const float4* nodes4, int first, int count, uint4* q, int* sceneError, hipStream_t stream );
+	/* the TLAS BVH2 nodes [base2, base2 + count) as W8 records (lh2_w8.h) in blocks rootBlock .. rootBlock + count: the
+	   root's record in slot 0 of rootBlock, node k's children in block rootBlock + 1 + k (a node child as its quantized
+	   record, an instance leaf as its instance record: inverse rows, index, its mesh's first block meshBlock[mesh]) */
+	static void TlasToW8( const float4* nodes2, int base2, int count, const void* instances, const int* meshBlock, uint32_t rootBlock,
+		uint32_t* w8, int* sceneError, hipStream_t stream );
 
 private:
 	void Reserve( int n );

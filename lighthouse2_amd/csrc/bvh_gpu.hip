@@ -12,6 +12,7 @@
 #include "bvh_gpu.h"
 #include "lh2_device.h"
 #include "lh2_kernels.h"
+#include "lh2_w8.h"
 
 namespace lh2 {
 void FatalError( const char* fmt, ... );
@@ -347,11 +348,11 @@ __global__ __launch_bounds__( 256 ) void k_emit( int N, int tlas, int nodeBase, 
 	emit_node( x, N, tlas, nodeBase, triBase, boxes, child, parent, P, I, leafOrig, coreTris, nodes, tris, red + 14 );
 }
 
-__global__ void k_tlas_check( const uint32_t* red, int maxBlasDepth, int* sceneError, int* tlasDepth )
+__global__ void k_tlas_check( const uint32_t* red, int maxBlasDepth, int tlasFactor, int* sceneError, int* tlasDepth )
 {
 	const int d = (int)red[14];
 	*tlasDepth = d;
-	if (d + maxBlasDepth >= LH2_STACK_TOTAL - 1) atomicOr( sceneError, LH2_SCENE_ERR_DEPTH );
+	if (tlasFactor * d + maxBlasDepth >= LH2_STACK_TOTAL - 1) atomicOr( sceneError, LH2_SCENE_ERR_DEPTH );
 }
 
 /* ---- single-workgroup TLAS build (count <= LH2_TLAS_WG_MAX): no host round trip ---------- */
@@ -497,7 +498,7 @@ __global__ __launch_bounds__( 1024 ) void k_tlas_build_wg( const GpuTlasArgs a, 
 	if (t == 0)
 	{
 		*a.tlasDepth = (int)depthMax;
-		if ((int)depthMax + a.maxBlasDepth >= LH2_STACK_TOTAL - 1) atomicOr( a.sceneError, LH2_SCENE_ERR_DEPTH );
+		if (a.tlasFactor * (int)depthMax + a.maxBlasDepth >= LH2_STACK_TOTAL - 1) atomicOr( a.sceneError, LH2_SCENE_ERR_DEPTH );
 	}
 }
 
@@ -566,7 +567,6 @@ __global__ __launch_bounds__( 256 ) void k_tlas_to_bvh4( const float4* __restric
    +-1e30 (fast_inv), so 1e30 * 2^27 = 1.3e38 stays finite (a larger e makes it inf, and a zero byte plane times
    inf a NaN slab).  A node that would need more (extent > 255 * 2^27 = 3.4e10, or coordinates beyond 2^55) sets
    bit LH2_SCENE_ERR_QRANGE of the scene error flag, and the traversal kernels refuse the scene. */
-#define LH2_QEXP_MAX 27
 __global__ __launch_bounds__( 256 ) void k_quantize4( const float4* __restrict__ nodes4, int first, int count, uint4* __restrict__ q, int* __restrict__ err )
 {
 	const int i = blockIdx.x * 256 + threadIdx.x;
@@ -632,6 +632,77 @@ __global__ __launch_bounds__( 256 ) void k_quantize4( const float4* __restrict__
 	if (!valid[2]) r.z = INT_MIN;
 	if (!valid[3]) r.w = INT_MIN;
 	d[3] = make_uint4( (uint32_t)r.x, (uint32_t)r.y, (uint32_t)r.z, (uint32_t)r.w );
+}
+
+/* the W8 record of TLAS BVH2 node j (its two children in block rootBlock + 1 + j, slots by lh2_w8_tlas_slots) */
+__device__ void w8_tlas_slots( const float4* n, bool valid[2], int slot[2], float lo[2][3], float hi[2][3] )
+{
+	const float4 a = n[0], b = n[1], z = n[2];
+	lo[0][0] = a.x, hi[0][0] = a.y, lo[0][1] = a.z, hi[0][1] = a.w, lo[0][2] = z.x, hi[0][2] = z.y;
+	lo[1][0] = b.x, hi[1][0] = b.y, lo[1][1] = b.z, hi[1][1] = b.w, lo[1][2] = z.z, hi[1][2] = z.w;
+	float d[8][3] = {}, plo[3], phi[3];
+	int idx[2], m = 0;
+	for (int c = 0; c < 2; c++) { valid[c] = lh2_w8_box_valid( lo[c], hi[c] ); slot[c] = -1; if (valid[c]) idx[m++] = c; }
+	for (int a2 = 0; a2 < 3; a2++)
+	{
+		plo[a2] = INFINITY, phi[a2] = -INFINITY;
+		for (int i = 0; i < m; i++) plo[a2] = fminf( plo[a2], lo[idx[i]][a2] ), phi[a2] = fmaxf( phi[a2], hi[idx[i]][a2] );
+		for (int i = 0; i < m; i++) d[i][a2] = 0.5f * (lo[idx[i]][a2] + hi[idx[i]][a2]) - 0.5f * (plo[a2] + phi[a2]);
+	}
+	int so[8];
+	lh2_w8_assign( m, d, so );
+	for (int i = 0; i < m; i++) slot[idx[i]] = so[i];
+}
+__device__ void w8_tlas_record( const float4* __restrict__ nodes2, int base2, int j, uint32_t rootBlock, uint32_t* rec, int* err )
+{
+	const float4* n = nodes2 + (size_t)(base2 + j) * 4;
+	bool v2[2];
+	int sl[2];
+	float lo2[2][3], hi2[2][3];
+	w8_tlas_slots( n, v2, sl, lo2, hi2 );
+	const float4 r = n[3];
+	const int ref[2] = { __float_as_int( r.x ), __float_as_int( r.y ) };
+	bool valid[8] = {};
+	float lo[8][3] = {}, hi[8][3] = {};
+	uint32_t imask = 0;
+	for (int c = 0; c < 2; c++)
+		if (v2[c])
+		{
+			valid[sl[c]] = true;
+			for (int a = 0; a < 3; a++) lo[sl[c]][a] = lo2[c][a], hi[sl[c]][a] = hi2[c][a];
+			if (ref[c] >= 0) imask |= 1u << sl[c];
+		}
+	uint32_t w[LH2_W8_WORDS];
+	if (lh2_w8_quantize( valid, lo, hi, imask, w )) atomicOr( err, LH2_SCENE_ERR_QRANGE );
+	w[18] = rootBlock + 1u + (uint32_t)j, w[19] = 0;
+	for (int k = 0; k < LH2_W8_WORDS; k += 4) *(uint4*)(rec + k) = make_uint4( w[k], w[k + 1], w[k + 2], w[k + 3] );
+}
+__global__ __launch_bounds__( 256 ) void k_tlas_to_w8( const float4* __restrict__ nodes2, int base2, int count, const DevInstance* __restrict__ inst,
+	const int* __restrict__ meshBlock, uint32_t rootBlock, uint32_t* __restrict__ w8, int* __restrict__ err )
+{
+	const int t = blockIdx.x * 256 + threadIdx.x;
+	if (t > count) return;
+	if (t == count) { w8_tlas_record( nodes2, base2, 0, rootBlock, w8 + (size_t)rootBlock * 8 * LH2_W8_WORDS, err ); return; }
+	const float4* n = nodes2 + (size_t)(base2 + t) * 4;
+	bool v2[2];
+	int sl[2];
+	float lo2[2][3], hi2[2][3];
+	w8_tlas_slots( n, v2, sl, lo2, hi2 );
+	const float4 r = n[3];
+	const int ref[2] = { __float_as_int( r.x ), __float_as_int( r.y ) };
+	for (int c = 0; c < 2; c++)
+	{
+		if (!v2[c]) continue;
+		uint32_t* rec = w8 + ((size_t)(rootBlock + 1u + (uint32_t)t) * 8 + (size_t)sl[c]) * LH2_W8_WORDS;
+		if (ref[c] >= 0) w8_tlas_record( nodes2, base2, ref[c] - base2, rootBlock, rec, err );
+		else
+		{
+			const uint32_t i = LEAF_FIRST( ref[c] );
+			const DevInstance in = inst[i];
+			*(float4*)(rec + 0) = in.inv0, *(float4*)(rec + 4) = in.inv1, *(float4*)(rec + 8) = in.inv2;
+			*(uint4*)(rec + 12) = make_uint4( i, (uint32_t)meshBlock[in.mesh], 0u, 0u );
+		}
+	}
 }
 
 inline int blocks( long n, int bs = 256 ) { return (int)std::max<long>( 1, (n + bs - 1) / bs ); }
@@ -756,7 +827,7 @@ void GpuBvhBuilder::BuildTlas( const GpuTlasArgs& a, hipStream_t st )
 	GpuBuildResult res;
 	Cluster( N, 1, 1.0f, 1, res, st );
 	k_emit<<<blocks( 2L * N - 1 ), 256, 0, st>>>( N, 1, a.nodeBase, 0, (const Box8*)boxes, child, parent, P, I, leafOrig, nullptr, a.nodes, nullptr, dred );
-	k_tlas_check<<<1, 1, 0, st>>>( dred, a.maxBlasDepth, a.sceneError, a.tlasDepth );
+	k_tlas_check<<<1, 1, 0, st>>>( dred, a.maxBlasDepth, a.tlasFactor, a.sceneError, a.tlasDepth );
 }
 
 void GpuBvhBuilder::Relocate( const float4* src, int nodeCount, int nodeBase, uint32_t triBase, float4* dst, hipStream_t st )
@@ -773,6 +844,14 @@ void GpuBvhBuilder::Quantize4( const float4* nodes4, int first, int count, uint4
 {
 	if (count <= 0) return;
 	k_quantize4<<<blocks( count ), 256, 0, st>>>( nodes4, first, count, q, sceneError );
+	CHK( hipGetLastError() );
+}
+
+void GpuBvhBuilder::TlasToW8( const float4* nodes2, int base2, int count, const void* instances, const int* meshBlock, uint32_t rootBlock,
+	uint32_t* w8, int* sceneError, hipStream_t st )
+{
+	if (count <= 0) return;
+	k_tlas_to_w8<<<blocks( count + 1 ), 256, 0, st>>>( nodes2, base2, count, (const DevInstance*)instances, meshBlock, rootBlock, w8, sceneError );
 	CHK( hipGetLastError() );
 }
 

@@ -11,6 +11,7 @@
 #include "../../include/lh2_core_types.h"
 #include "bvh_build.h"
 #include "bvh_gpu.h"
+#include "lh2_w8.h"
 #include "lh2_kernels.h"
 #include "lh2_device.h"
 
@@ -53,9 +54,12 @@ struct CoreMeshHost   /* RenderCore always copies what it needs (rendercore.h:57
 	int nodeCount = 0, maxDepth = 0;
 	DevBuf<float4> bvh4Nodes;            /* the same BLAS collapsed to BVH4 (CollapseBvh4), mesh-local refs */
 	int node4Count = 0, depth4 = 0;
+	DevBuf<uint32_t> w8;                 /* the same BLAS as W8 records (lh2_w8.h, child blocks relative to the mesh's first); w8Blocks 0: none */
+	int w8Blocks = 0, w8Depth = 0, w8QErr = 0;
 	/* a deferred CPU build (RenderCore::FlushBuilds): the job (its argument: threads for the build) and its results */
 	std::function<void( int )> build;
 	std::vector<float> hostNodes2, hostTris48, hostNodes4;
+	std::vector<uint32_t> hostW8;
 };
 
 struct CoreInstanceHost { int mesh; float T[16]; float inv[16]; };
@@ -225,7 +229,24 @@ private:
 	int tlasCapacity = 0, maxBlasDepth = 0;
 	int blasNode4Count = 0, maxBlas4Depth = 0;
 	int bvh4 = 1;                        /* build BVH4 copies of the BLAS (the default traversal loop needs them) */
-	int StackDepthBound() const { return bvh4 ? std::max( maxBlasDepth, 3 * maxBlas4Depth ) : maxBlasDepth; }
+	/* the W8 (lh2_w8.h, round 5): every mesh's records, then two TLAS slots of tlasCapacity + 1 blocks; w8Avail: every mesh
+	   has one (CPU or GPU builds with one triangle per leaf) */
+	DevBuf<uint32_t> dW8;
+	DevBuf<int> dMeshBlock;              /* each mesh's first block */
+	std::vector<int> meshBlockBase;
+	int blasW8Blocks = 0, maxBlasW8Depth = 0;
+	bool w8Avail = false;
+	int W8TlasBlock( int s ) const { return blasW8Blocks + s * (tlasCapacity + 1); }
+	/* the loop over the W8 for the frame's per-ray launches (setting "traceWide"): 0 off (BVH4), 1 on, 2 for frames of at most
+	   kSmallFramePaths paths; the unit queries take it when nonzero */
+	int traceWide = 2;
+	/* the shadow (any-hit) launches of single-instance scenes test a lane's last occluder first and share each occluder found
+	   with the wave's other rays (setting "shadowOccluders"): parity-exact, any occluder ends a shadow ray */
+	int shadowOccluders = 1;
+	bool UseWide( uint32_t paths ) const { return w8Avail && (traceWide == 1 || (traceWide == 2 && (float)paths <= kSmallFramePaths)); }
+	/* stack entries a ray may need: the BVH2 loop's BLAS depth, the BVH4 loop's 3 per level, the W8 loop's 2 per level (a node
+	   group and a leaf group per node step) */
+	int StackDepthBound() const { return std::max( bvh4 ? std::max( maxBlasDepth, 3 * maxBlas4Depth ) : maxBlasDepth, w8Avail ? 2 * maxBlasW8Depth + 2 : 0 ); }
 	bool tlasOnDevice = false;           /* TLAS of the last UpdateToplevel built by the GPU (depth in dTlasDepth) */
 	GpuBvhBuilder gpuBvh;
 	DevBuf<float> dMeshBounds;           /* 6 per mesh */

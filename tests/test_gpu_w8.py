@@ -1,0 +1,159 @@
+"""GPU parity of the 8-wide compressed BVH loop (round 5, lh2_w8.h, lh2_trace4d.inc WIDE; setting traceWide): hit records
+{t, triid, instid, uv16} bit-exact against the CPU oracle and against the BVH4 loop on the same rays (random, primary,
+instanced with a TLAS of instance records, deep stacks, grazing), occlusion bits identical, and frames (the lit room with
+its path tail and shadow launches, config 2, instanced) with identical ray counts and the accumulator within float
+summation order of the BVH4 loop's.  The W8's boxes only cull (outward-rounded quantized planes): hits are Bart's
+BVH2::Traverse's (RenderCore_Bart/bvh.cpp:258-302) under the (t, instance, triangle) tie rule, whatever the tree."""
+import numpy as np
+import pytest
+
+from lighthouse2_amd import abi, scene
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+REL_L2_TOL = 1e-4
+
+
+def rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _random_rays(n, seed, center=(0, 0, 0), radius=14.0, tmin=1e-4):
+    rng = np.random.default_rng(seed)
+    o = rng.normal(size=(n, 3)).astype(np.float32)
+    o = o / np.linalg.norm(o, axis=1, keepdims=True) * np.float32(radius) + np.array(center, np.float32)
+    tgt = rng.uniform(-4, 4, size=(n, 3)).astype(np.float32)
+    d = tgt - o
+    d = (d * (np.float32(1) / np.sqrt((d * d).sum(1, dtype=np.float32)))[:, None]).astype(np.float32)
+    d[::11, 0] = 0.0                       # axis-parallel components
+    return np.concatenate([o, np.full((n, 1), tmin, np.float32)], 1), np.concatenate([d, np.full((n, 1), 1e34, np.float32)], 1)
+
+
+def _load(core, sc, w, h, wide=1, **settings):
+    core.setting("traceWide", wide)
+    for k, v in settings.items():
+        core.setting(k, v)
+    sc.load_into(core)
+    core.set_target(w, h, 1)
+
+
+@pytest.mark.parametrize("kind", ["soup", "room", "instanced"])
+def test_w8_closest_hits_bitexact(fresh_core, kind):
+    if kind == "soup":
+        sc, O4, D4 = scene.config2_scene(n=20000, width=64, height=36), *_random_rays(60000, 1)
+    elif kind == "room":
+        sc = scene.room_scene(30000, 64, 36)
+        O4, D4 = _random_rays(60000, 2, center=(0, 6, 0), radius=8.0)
+    else:
+        sc = scene.instanced_scene(meshes=6, tris_per_mesh=3000, width=64, height=36, grid=3, spacing=12.0)
+        scene.animate_instances(sc, 3)
+        T = sc.instances[2][1].copy()
+        T[0, 0] *= 1.7
+        T[1, 0] += 0.3
+        sc.instances[2] = (2, T)
+        O4, D4 = _random_rays(60000, 3, radius=40.0)
+    _load(fresh_core, sc, 64, 36, wide=1)
+    assert fresh_core.get_setting("w8Avail") == 1
+    o = Oracle()
+    sc.load_into(o)
+    o.set_target(64, 36, 1)
+    hw = fresh_core.trace_closest(O4, D4)
+    ho = o.trace_closest(O4, D4)
+    assert (ho[:, 1] != 0xFFFFFFFF).mean() > 0.05
+    assert np.array_equal(hw, ho), np.argwhere((hw != ho).any(1))[:10]
+    fresh_core.setting("traceWide", 0)
+    assert np.array_equal(fresh_core.trace_closest(O4, D4), ho)
+
+
+def test_w8_any_hit_bits(fresh_core):
+    sc = scene.instanced_scene(meshes=4, tris_per_mesh=4000, width=64, height=36, grid=2, spacing=10.0)
+    _load(fresh_core, sc, 64, 36, wide=1)
+    o = Oracle()
+    sc.load_into(o)
+    o.set_target(64, 36, 1)
+    O4, D4 = _random_rays(40001, 4, radius=30.0, tmin=0.0)
+    D4[:, 3] = np.random.default_rng(5).uniform(5.0, 60.0, len(D4)).astype(np.float32)
+    mo = o.trace_any(O4, D4)
+    assert 0.05 < np.unpackbits(mo.view(np.uint8)).mean() < 0.95
+    assert np.array_equal(fresh_core.trace_any(O4, D4), mo)
+
+
+@pytest.mark.parametrize("leaf_batch", [0, 1, 8, 32])
+def test_w8_leaf_batches_bitexact(fresh_core, leaf_batch):
+    sc = scene.config2_scene(n=20000, width=192, height=108)
+    _load(fresh_core, sc, 192, 108, wide=1, leafBatch=leaf_batch)
+    o = Oracle()
+    sc.load_into(o)
+    o.set_target(192, 108, 1)
+    O4, D4, _ = o.generate_eye_rays(sc.view, 0, 0)
+    hp = o.trace_closest(O4, D4)
+    assert np.array_equal(fresh_core.trace_closest(O4, D4), hp)
+    bo, bd = scene.bounce_rays(sc.meshes[0], O4, D4, hp)
+    assert np.array_equal(fresh_core.trace_closest(bo, bd), o.trace_closest(bo, bd))
+
+
+@pytest.mark.parametrize("gpu_build", [0, 1])
+def test_w8_deep_stack_and_builders(fresh_core, gpu_build):
+    """A deep, narrow tree (a long run of nested thin triangles) that spills the LDS stack into the global one; the BLAS
+    from the GPU builder (its W8 collapsed on the host from the downloaded BVH2)."""
+    k = np.arange(3000, dtype=np.float32)
+    x = (0.001 * k).astype(np.float32)
+    z0 = np.zeros_like(x)
+    chain = abi.tris_from_vertices(np.stack([x, -1 - x, z0], 1), np.stack([x + 0.0005, 1 + x, z0], 1), np.stack([x, 1 + x, 0.01 + x], 1), 0)
+    sc = scene.config2_scene(n=5000, width=64, height=36)
+    sc.meshes[0] = np.concatenate([sc.meshes[0], chain])
+    _load(fresh_core, sc, 64, 36, wide=1, gpuBuild=gpu_build)
+    assert fresh_core.get_setting("w8Avail") == 1
+    o = Oracle()
+    sc.load_into(o)
+    o.set_target(64, 36, 1)
+    O4, D4 = _random_rays(40000, 6)
+    rng = np.random.default_rng(7)
+    O4[::3, :3] = np.stack([rng.uniform(-1, 4, 13334), rng.uniform(-2, 2, 13334), np.full(13334, -6.0)], 1)[: len(O4[::3])]
+    D4[::3, :3] = np.array([0.0, 0.0, 1.0], np.float32)
+    assert np.array_equal(fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4))
+
+
+def test_w8_needs_one_triangle_leaves(fresh_core):
+    """bvhMaxLeaf > 1 (leaves of several triangles): no W8 is built, the BVH4 loop runs, the hits are unchanged."""
+    sc = scene.config2_scene(n=8000, width=64, height=36)
+    _load(fresh_core, sc, 64, 36, wide=1, bvhMaxLeaf=2)
+    assert fresh_core.get_setting("w8Avail") == 0
+    o = Oracle()
+    sc.load_into(o)
+    o.set_target(64, 36, 1)
+    O4, D4 = _random_rays(20000, 8)
+    assert np.array_equal(fresh_core.trace_closest(O4, D4), o.trace_closest(O4, D4))
+
+
+@pytest.mark.parametrize("kind", ["room", "config2", "instanced"])
+def test_w8_frames(fresh_core, kind):
+    """Whole frames with every per-ray launch on the W8 (traceWide 1: bounce closest hit, the path tail, the side and
+    final shadow launches) against the oracle, and against the same frames on the BVH4 (traceWide 0)."""
+    w, h = 128, 72
+    if kind == "room":
+        sc, depth = scene.room_scene(40000, w, h), 4
+    elif kind == "config2":
+        sc, depth = scene.config2_scene(n=20000, width=w, height=h, sky=True, light=True), 2
+    else:
+        sc = scene.instanced_scene(meshes=4, tris_per_mesh=4000, width=w, height=h, grid=2, spacing=10.0)
+        sc.sky = scene.gradient_sky(64, 32)
+        depth = 3
+    o = Oracle()
+    sc.load_into(o)
+    o.set_target(w, h, 1)
+    o.setting("maxPathLength", depth)
+    _load(fresh_core, sc, w, h, wide=1, maxPathLength=depth)
+    res = {}
+    for wide in (1, 0):
+        fresh_core.setting("traceWide", wide)
+        for f in range(3):
+            sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
+            if wide:
+                sc.render_frame(o, converge=1 if f == 0 else 0)
+                assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), (f, fresh_core.ray_counts()[:6], o.ray_counts()[:6])
+        res[wide] = fresh_core.accumulator()
+    assert rel_l2(res[1][..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
+    assert rel_l2(res[1][..., :3], res[0][..., :3]) <= 1e-6
+    assert np.array_equal(res[1][..., 3], res[0][..., 3])

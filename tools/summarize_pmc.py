@@ -59,8 +59,13 @@ def trace_sq(src, kernel, p1="sq1", p2="sq2", what="config-2 bounce rays from th
     ds2 = list(dispatches(src / p2 / "run_counter_collection.csv", kernel).values()) if p2 else []
     ns = med(ds, "ns")
     valu = med(ds, "SQ_INSTS_VALU")
-    clk = med(ds, "GRBM_GUI_ACTIVE") / 8 / ns           # GHz (sum over the 8 XCDs)
-    cycles = ns * clk
+    # GRBM_GUI_ACTIVE counts the GPU's busy clocks over the counter pass's sampling window of the dispatch, summed over the 8
+    # XCDs; for short launches (fills, k_finalize, k_shade: a few us) that window is longer than the kernel's own
+    # timestamps and the quotient exceeds the chip's 2.4 GHz.  Only a clock the chip can run is kept;
+    # otherwise the fields that divide by it are null (not evidence) and the issue fraction uses the nominal clock
+    clk_raw = med(ds, "GRBM_GUI_ACTIVE") / 8 / ns      # GHz
+    clk = clk_raw if 0.5 <= clk_raw <= 2.45 else None
+    cycles = ns * (clk or CLOCK_GHZ)
     rate = valu / ns                                   # G wave-instructions / s
     cyc = cycles_per_valu()
     peak = SIMDS * CLOCK_GHZ / cyc
@@ -71,12 +76,13 @@ def trace_sq(src, kernel, p1="sq1", p2="sq2", what="config-2 bounce rays from th
         "kernel": f"{kernel} ({what})",
         "launches": len(ds), "launch_ms_median": ns / 1e6,
         "counters_per_launch_median": counters,
-        "effective_clock_ghz": round(clk, 3),
+        "effective_clock_ghz": round(clk, 3) if clk else None,
+        "grbm_clock_quotient_ghz": round(clk_raw, 3),
         "valu_wave_insts_per_launch": valu,
         "valu_issue_rate_g_per_s": round(rate, 1),
         "valu_issue_peak_g_per_s": peak,
         "valu_issue_frac": round(rate / peak, 4),
-        "valu_issue_frac_at_effective_clock": round(valu * cyc / (SIMDS * cycles), 4),
+        "valu_issue_frac_at_effective_clock": round(valu * cyc / (SIMDS * cycles), 4) if clk else None,
         "cycles_per_valu_instruction": cyc,
         "valu_lane_utilisation": round(counters["SQ_THREAD_CYCLES_VALU"] / (64 * counters["SQ_ACTIVE_INST_VALU"]), 4),
         "valu_busy_frac_quad_cycles": round(counters["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cycles), 4),
