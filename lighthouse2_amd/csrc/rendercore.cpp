@@ -847,6 +847,7 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 	}
 	/* ... and as W8 records (lh2_w8.h) in the slot's blocks: the instance leaves carry their inverse rows */
 	if (w8Avail) GpuBvhBuilder::TlasToW8( dNodes.ptr, TlasBase2( ts ), tlasNodes, dInst[ts].ptr, dMeshBlock.ptr, (uint32_t)W8TlasBlock( ts ), dW8.ptr, SceneErr( ts ), us );
+	tlasNodeCount[ts] = tlasNodes;
 	CHK_HIP( hipEventRecord( evStage[slot], us ) );
 	CHK_HIP( hipEventRecord( evTlasReady, us ) );
 	tlasSlot = ts, tlasPending = true;
@@ -1449,9 +1450,10 @@ int RenderCore::DebugBvh4( float* f32Nodes, uint32_t* qNodes, int cap )
 	SyncTlas();
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	if (!dNodes4.ptr || !dNodes4q.ptr) return 0;
-	if (cap <= 0 || !f32Nodes || !qNodes) return blasNode4Count + tlasCapacity;   /* a count-only call */
+	const int tn = tlasNodeCount[tlasSlot];   /* the current TLAS's own nodes (the slot's others are never written, §3) */
+	if (cap <= 0 || !f32Nodes || !qNodes) return blasNode4Count + tn;   /* a count-only call */
 	/* the BLAS nodes, then the current TLAS slot's */
-	const int n = std::min( cap, blasNode4Count + tlasCapacity ), nb = std::min( n, blasNode4Count ), nt = n - nb;
+	const int n = std::min( cap, blasNode4Count + tn ), nb = std::min( n, blasNode4Count ), nt = n - nb;
 	CHK_HIP( hipMemcpy( f32Nodes, dNodes4.ptr, 128 * (size_t)nb, hipMemcpyDeviceToHost ) );
 	CHK_HIP( hipMemcpy( qNodes, dNodes4q.ptr, 64 * (size_t)nb, hipMemcpyDeviceToHost ) );
 	if (nt > 0)

@@ -263,6 +263,7 @@ private:
 	   stream behind the last frame that read that slot (evTlasFree), so an animated frame's primary launch can still run
 	   beside the previous frame; the core stream waits for the update (evTlasReady) before its next launch */
 	int tlasSlot = 0;
+	int tlasNodeCount[2] = { 1, 1 };     /* the nodes of each slot's TLAS (UpdateToplevel) */
 	bool tlasPending = false, tlasFreeValid[2] = {};
 	hipEvent_t evTlasReady = nullptr, evTlasFree[2] = {};
 	int TlasBase2( int s ) const { return blasNodeCount + s * tlasCapacity; }
