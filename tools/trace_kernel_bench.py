@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tris", type=int, default=100_000)
     ap.add_argument("--set", default="both")
+    ap.add_argument("--scene", default="config2", choices=["config2", "room"])
     # defaults = the core's (RenderCore refillOther / leafBatch: primary rays traced per ray take the same)
     ap.add_argument("--refill", type=int, default=None, help="default: the core's setting")
     ap.add_argument("--leaf-batch", type=int, default=None)
@@ -53,7 +54,8 @@ def main():
                     help="also time the bounce rays with the shortest-chord fraction F of each segment moved to its end")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    sc = scene.config2_scene(n=args.tris)
+    # --scene room: config 3's room (1M triangles, a closed room of tessellated walls and clutter) instead of config 2's soup
+    sc = scene.room_scene(args.tris, 1920, 1080) if args.scene == "room" else scene.config2_scene(n=args.tris)
     core = RenderCore(device=0)
     for s in args.pre_setting:               # build parameters: before the scene is loaded
         k, v = s.split("=")
