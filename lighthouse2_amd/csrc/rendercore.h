@@ -237,12 +237,15 @@ private:
 	int blasW8Blocks = 0, maxBlasW8Depth = 0;
 	bool w8Avail = false;
 	int W8TlasBlock( int s ) const { return blasW8Blocks + s * (tlasCapacity + 1); }
-	/* the loop over the W8 for the frame's per-ray launches (setting "traceWide"): 0 off (BVH4), 1 on, 2 for frames of at most
-	   kSmallFramePaths paths; the unit queries take it when nonzero */
-	int traceWide = 2;
+	/* the loop over the W8 for the frame's per-ray launches (setting "traceWide"): 0 off (BVH4, no W8 built), 1 on, 2 for
+	   frames of at most kSmallFramePaths paths; the unit queries take it when nonzero.  Off by default: the W8 loop's node
+	   step costs 1.8x the BVH4's issue slots for 0.72x the steps (room bounce 0.503 vs 0.432 ms, config 3 2.28 vs 1.94 ms,
+	   the N = 8 share 1.32 vs 1.15 ms: profiles/r05_ab_w8.txt) */
+	int traceWide = 0;
 	/* the shadow (any-hit) launches of single-instance scenes test a lane's last occluder first and share each occluder found
-	   with the wave's other rays (setting "shadowOccluders"): parity-exact, any occluder ends a shadow ray */
-	int shadowOccluders = 1;
+	   with the wave's other rays (setting "shadowOccluders"): parity-exact, any occluder ends a shadow ray.
+	   Off by default: config 3 1.94 (on) vs 1.88 ms (off), neither half alone wins (profiles/r05_ab_occluders.txt) */
+	int shadowOccluders = 0;
 	bool UseWide( uint32_t paths ) const { return w8Avail && (traceWide == 1 || (traceWide == 2 && (float)paths <= kSmallFramePaths)); }
 	/* stack entries a ray may need: the BVH2 loop's BLAS depth, the BVH4 loop's 3 per level, the W8 loop's 2 per level (a node
 	   group and a leaf group per node step) */
