@@ -17,3 +17,9 @@ print(f"tail per wave (end - exhausted): median {np.median(end - exh):.1f}  p90 
 print(f"iterations per wave: median {np.median(it):.0f}, after exhaustion median {np.median(dry):.0f}; share after exhaustion {dry.sum() / it.sum():.2f}")
 for q in (0.5, 0.9, 0.99, 1.0):
     print(f"  {q:4.2f} of the waves have ended by {np.quantile(end, q):.1f} us")
+# the launch's drain: live waves over time after the first wave found the queue dry
+ex0 = exh.min()
+span = end.max()
+print(f"drain (first queue-dry wave -> last wave end): {span - ex0:.1f} us = {(span - ex0) / span:.2f} of the span")
+for f in (0.75, 0.5, 0.25, 0.1, 0.02):
+    print(f"  {f:4.2f} of the waves still running at {np.quantile(end, 1 - f):.1f} us")
