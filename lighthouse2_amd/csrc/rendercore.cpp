@@ -289,7 +289,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* the W8 loop (lh2_w8.h): 0 off, 1 every per-ray launch, 2 frames of at most kSmallFramePaths paths; 0 before SetGeometry also
 	   skips building the W8 */
 	else if (!strcmp( name, "traceWide" )) traceWide = std::min( 2, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "shadowOccluders" )) shadowOccluders = value != 0;   /* the shadow launches share found occluders (TraceArgs::occShare) */
+	else if (!strcmp( name, "tailShadows" )) tailShadows = value != 0;   /* the path tail traces its paths' shadow rays (TraceArgs::tailShadows) */
 	/* other names ("clampDirect", "filter", "TAA", ...) are ignored, as in the reference */
 }
 
@@ -306,7 +306,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "sideBlocks", (float)sideBlocks }, { "pathTailBlocks", (float)pathTailBlocks }, { "shadeBlocks", (float)shadeBlocks }, { "finalShadowBlocks", (float)finalShadowBlocks },
 		{ "pathTailWaves", (float)pathTailWaves }, { "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceBlocksPerCU", (float)blocksPerCU }, { "unitTraceWaves", (float)unitTraceWaves }, { "traceWaves", (float)traceWaves },
-		{ "unitCoherent", (float)unitCoherent }, { "traceVersion", (float)TraceVersion() }, { "traceWide", (float)traceWide }, { "w8Avail", (float)w8Avail }, { "shadowOccluders", (float)shadowOccluders },
+		{ "unitCoherent", (float)unitCoherent }, { "traceVersion", (float)TraceVersion() }, { "traceWide", (float)traceWide }, { "w8Avail", (float)w8Avail }, { "tailShadows", (float)tailShadows },
 		{ "usePackets", (float)UsePackets() } };
 	for (const auto& e : t) if (!strcmp( name, e.n )) { value = e.v; return true; }
 	return false;
@@ -1121,6 +1121,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			sp.rayOut = ps.rayO[ps.in].ptr, sp.rayDOut = ps.rayD[ps.in].ptr, sp.T4Out = ps.T4[ps.in].ptr, sp.Q4Out = ps.Q4[ps.in].ptr;
 			sp.adv.rayCountLog = rayLog;
 			ta.shadeBatch = (uint32_t)pathTailBatch;
+			ta.tailShadows = tailShadows && shadows ? 1u : 0u;
 			/* with the overlap the path tail runs fewer blocks per CU and leaves registers for the side launch's waves
 			   (pathTailBlocks; 0: 3 for small frames, whose tail phase is the frame's longest, else 2) */
 			const bool side = overlap && snapped;
@@ -1137,7 +1138,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				CHK_HIP( hipStreamWaitEvent( sideStream, ps.prevStop, 0 ) );
 				TraceArgs ts{};
 				ts.version = TraceVersion();
-				ts.wide = frameWide ? 1u : 0u, ts.occShare = (uint32_t)shadowOccluders;
+				ts.wide = frameWide ? 1u : 0u;
 				ts.rayO = shO, ts.rayD = shD, ts.segCounts = shSnap, ts.segStride = ps.shadowStride;
 				ts.cursor = cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS;
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
@@ -1264,7 +1265,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	{
 		TraceArgs ta{};
 		ta.version = TraceVersion();
-		ta.wide = frameWide ? 1u : 0u, ta.occShare = (uint32_t)shadowOccluders;
+		ta.wide = frameWide ? 1u : 0u;
 		ta.rayO = shO, ta.rayD = shD, ta.segCounts = c->segShadow, ta.segStride = ps.shadowStride;
 		ta.cursor = cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.mask = shMask, ta.potentials = shP, ta.acc = accumulator.ptr, ta.gstack = ps.gstack.ptr;
@@ -1344,10 +1345,11 @@ int RenderCore::TileRows() const
 	return std::max( 0, y1 - y0 );
 }
 
-/* shadow rays queued in the segments of the shadow stream (the final shadow pass traces them all) */
+/* the frame's shadow rays: queued in the segments of the shadow stream (the shadow launches trace them), and traced by the
+   path tail itself (tailShadows: Counters::shadowRays) */
 static uint32_t QueuedShadowRays( const Counters& c )
 {
-	uint32_t n = 0;
+	uint32_t n = c.shadowRays;
 	for (int k = 0; k < LH2_SEGS; k++) n += c.segShadow[k * LH2_SEGCOUNT_STRIDE];
 	return n;
 }
@@ -1561,7 +1563,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	TraceArgs ta{};
 	ta.version = TraceVersion();
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
-	ta.wide = w8Avail && traceWide != 0 ? 1u : 0u, ta.occShare = (uint32_t)shadowOccluders;
+	ta.wide = w8Avail && traceWide != 0 ? 1u : 0u;
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, {}, stream );
 	std::vector<uint32_t> tmp( words );
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );

@@ -242,10 +242,9 @@ private:
 	   step costs 1.8x the BVH4's issue slots for 0.72x the steps (room bounce 0.503 vs 0.432 ms, config 3 2.28 vs 1.94 ms,
 	   the N = 8 share 1.32 vs 1.15 ms: profiles/r05_ab_w8.txt) */
 	int traceWide = 0;
-	/* the shadow (any-hit) launches of single-instance scenes test a lane's last occluder first and share each occluder found
-	   with the wave's other rays (setting "shadowOccluders"): parity-exact, any occluder ends a shadow ray.
-	   Off by default: config 3 1.94 (on) vs 1.88 ms (off), neither half alone wins (profiles/r05_ab_occluders.txt) */
-	int shadowOccluders = 0;
+	/* the path tail traces its own paths' shadow rays in its waves' idle lanes (setting "tailShadows", TraceArgs::tailShadows):
+	   the final shadow launch traces only those that found no free slot */
+	int tailShadows = 0;
 	bool UseWide( uint32_t paths ) const { return w8Avail && (traceWide == 1 || (traceWide == 2 && (float)paths <= kSmallFramePaths)); }
 	/* stack entries a ray may need: the BVH2 loop's BLAS depth, the BVH4 loop's 3 per level, the W8 loop's 2 per level (a node
 	   group and a leaf group per node step) */
@@ -306,7 +305,8 @@ private:
 	int tiledRays = 1;                   /* primary rays stored in 8x8 pixel blocks per wave (coherent packets) */
 	int cameraFused = 1;                 /* primary rays made by the packet launch itself (k_trace_primary_packet), no camera launch */
 	/* a fused frame's primary launch beside the previous frame's later bounces (aheadStream): 1, after its shade launch
-	   before the path tail (its first without one); 2, after its first shade launch; 0: off */
+	   before the path tail (its first without one); 2, after its first shade launch; 0: off.  Right after the previous
+	   frame's primary launch, beside its first shade launch too, measured slower (profiles/r05_ab_frame_overlap_chain.txt) */
 	int frameOverlap = 1;
 	/* with frameOverlap 1: the next frame's first shade launch follows its primary launch on the ahead stream, beside this
 	   frame's path tail and shadow launches, instead of after them on the core stream (frames whose later launches use one

@@ -157,44 +157,3 @@ def test_w8_frames(fresh_core, kind):
     assert rel_l2(res[1][..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
     assert rel_l2(res[1][..., :3], res[0][..., :3]) <= 1e-6
     assert np.array_equal(res[1][..., 3], res[0][..., 3])
-
-
-@pytest.mark.parametrize("wide", [0, 1])
-def test_shadow_occluder_sharing(fresh_core, wide):
-    """Occluder sharing (setting shadowOccluders, TraceArgs::occShare: a lane tests its previous occluder first, and an
-    occluder found in a leaf phase is tested by the wave's other rays): the occlusion bits of coherent shadow rays (from
-    the room's primary hits toward its lights, in frame order) equal the oracle's with and without it, and the lit room's
-    frames (side and final shadow launches) have identical ray counts and the accumulator within float summation order."""
-    w, h = 160, 90
-    sc = scene.room_scene(40000, w, h)
-    _load(fresh_core, sc, w, h, wide=wide, maxPathLength=4)
-    o = Oracle()
-    sc.load_into(o)
-    o.set_target(w, h, 1)
-    o.setting("maxPathLength", 4)
-    O4, D4, _ = o.generate_eye_rays(sc.view, 0, 0)
-    hp = o.trace_closest(O4, D4)
-    hit = hp[:, 1] != 0xFFFFFFFF
-    t = hp[hit, 0].view(np.float32)
-    P = O4[hit, :3] + t[:, None] * D4[hit, :3]
-    rng = np.random.default_rng(9)
-    L = np.array([[-8, 15.9, 0], [8, 15.9, 0]], np.float32)[rng.integers(0, 2, len(P))] + rng.uniform(-2, 2, (len(P), 3)).astype(np.float32) * [1, 0, 1]
-    d = (L - P).astype(np.float32)
-    dist = np.linalg.norm(d, axis=1).astype(np.float32)
-    SO = np.concatenate([P - 1e-3 * D4[hit, :3], np.zeros((len(P), 1), np.float32)], 1).astype(np.float32)
-    SD = np.concatenate([d / dist[:, None], (dist * 0.999)[:, None]], 1).astype(np.float32)
-    mo = o.trace_any(SO, SD)
-    occ = np.unpackbits(mo.view(np.uint8)).mean()
-    assert 0.02 < occ < 0.98, occ
-    res = {}
-    for share in (1, 0):
-        fresh_core.setting("shadowOccluders", share)
-        assert np.array_equal(fresh_core.trace_any(SO, SD), mo), share
-        for f in range(2):
-            sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
-            if share:
-                sc.render_frame(o, converge=1 if f == 0 else 0)
-        res[share] = (fresh_core.accumulator(), fresh_core.ray_counts())
-    assert np.array_equal(res[1][1], o.ray_counts()) and np.array_equal(res[0][1], res[1][1])
-    assert rel_l2(res[1][0][..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
-    assert rel_l2(res[1][0][..., :3], res[0][0][..., :3]) <= 1e-6
