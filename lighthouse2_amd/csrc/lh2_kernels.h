@@ -130,7 +130,6 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	uint32_t tailWaves;                               /* path tail (lh2_launch_trace_path): the kernel variant for 4 waves per SIMD (4) or 3 */
 	uint32_t traceWaves;                              /* BVH4 closest hit: the kernel variant for 8 waves per SIMD (8) or 7 */
 	uint32_t wide;                                    /* version 7: the loop over the W8 (SceneDev::w8, lh2_w8.h) instead of the BVH4 */
-	uint32_t tailShadows;                             /* path tail: the wave's idle lanes trace its paths' shadow rays (LH2_TS_SLOTS queued per wave) */
 	/* heavy-first packets (packet kernel, hvWrite non-null): the previous frame's packets that took more
 	   than hvFactor x its mean node steps (hvRead: per-segment counts, step sums, a bit per packet and the
 	   lists of packet bits) are taken first, the rest in order; this frame's are recorded into hvWrite.
@@ -210,8 +209,6 @@ void lh2_launch_finalize( float4* acc, float4* out, int n, float scale, const Fr
 #define LH2_CURSOR_SLOTS (2 * LH2_MAX_BOUNCES + 5)           /* launches per frame: [L] bounce L, [64 + L] shadow after bounce L, [130] shadow, [131] side shadow */
 #define LH2_SHADOW_SLOT (2 * LH2_MAX_BOUNCES + 2)
 /* traversal stacks: LH2_STACK_LDS entries per lane in LDS (16 x 256 x 4 B = 16 KiB per block), the rest in global memory */
-/* the path tail's shadow-ray slots per wave (TraceArgs::tailShadows; LDS: 48 B each) */
-#define LH2_TS_SLOTS 32
 #ifndef LH2_STACK_LDS
 #define LH2_STACK_LDS 16
 #endif

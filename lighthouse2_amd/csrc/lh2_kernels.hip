@@ -1627,9 +1627,7 @@ __global__ __launch_bounds__( 256, W ) void k_trace_path4d( const SceneDev s, co
 {
 	__shared__ int lstack[LH2_STACK_LDS * 256];
 	__shared__ __attribute__( (aligned( 4096 )) ) int lrefs[WIDE ? 64 : 4 * 256];
-	__shared__ float4 tsRing[4 * LH2_TS_SLOTS * 3];   /* TraceArgs::tailShadows: each wave's shadow-ray slots */
-	trace_stream4d<3, SINGLE, NL, WIDE>( s, a, lstack + threadIdx.x, lrefs + (WIDE ? 0 : threadIdx.x), blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &p,
-		tsRing + (threadIdx.x >> 6) * (LH2_TS_SLOTS * 3) );
+	trace_stream4d<3, SINGLE, NL, WIDE>( s, a, lstack + threadIdx.x, lrefs + (WIDE ? 0 : threadIdx.x), blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &p );
 }
 
 /* counters: .cuda.cu:64-84 */

@@ -289,7 +289,6 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	/* the W8 loop (lh2_w8.h): 0 off, 1 every per-ray launch, 2 frames of at most kSmallFramePaths paths; 0 before SetGeometry also
 	   skips building the W8 */
 	else if (!strcmp( name, "traceWide" )) traceWide = std::min( 2, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "tailShadows" )) tailShadows = value != 0;   /* the path tail traces its paths' shadow rays (TraceArgs::tailShadows) */
 	/* other names ("clampDirect", "filter", "TAA", ...) are ignored, as in the reference */
 }
 
@@ -306,7 +305,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "sideBlocks", (float)sideBlocks }, { "pathTailBlocks", (float)pathTailBlocks }, { "shadeBlocks", (float)shadeBlocks }, { "finalShadowBlocks", (float)finalShadowBlocks },
 		{ "pathTailWaves", (float)pathTailWaves }, { "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceBlocksPerCU", (float)blocksPerCU }, { "unitTraceWaves", (float)unitTraceWaves }, { "traceWaves", (float)traceWaves },
-		{ "unitCoherent", (float)unitCoherent }, { "traceVersion", (float)TraceVersion() }, { "traceWide", (float)traceWide }, { "w8Avail", (float)w8Avail }, { "tailShadows", (float)tailShadows },
+		{ "unitCoherent", (float)unitCoherent }, { "traceVersion", (float)TraceVersion() }, { "traceWide", (float)traceWide }, { "w8Avail", (float)w8Avail },
 		{ "usePackets", (float)UsePackets() } };
 	for (const auto& e : t) if (!strcmp( name, e.n )) { value = e.v; return true; }
 	return false;
@@ -1121,7 +1120,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			sp.rayOut = ps.rayO[ps.in].ptr, sp.rayDOut = ps.rayD[ps.in].ptr, sp.T4Out = ps.T4[ps.in].ptr, sp.Q4Out = ps.Q4[ps.in].ptr;
 			sp.adv.rayCountLog = rayLog;
 			ta.shadeBatch = (uint32_t)pathTailBatch;
-			ta.tailShadows = tailShadows && shadows ? 1u : 0u;
 			/* with the overlap the path tail runs fewer blocks per CU and leaves registers for the side launch's waves
 			   (pathTailBlocks; 0: 3 for small frames, whose tail phase is the frame's longest, else 2) */
 			const bool side = overlap && snapped;
@@ -1345,11 +1343,10 @@ int RenderCore::TileRows() const
 	return std::max( 0, y1 - y0 );
 }
 
-/* the frame's shadow rays: queued in the segments of the shadow stream (the shadow launches trace them), and traced by the
-   path tail itself (tailShadows: Counters::shadowRays) */
+/* shadow rays queued in the segments of the shadow stream (the final shadow pass traces them all) */
 static uint32_t QueuedShadowRays( const Counters& c )
 {
-	uint32_t n = c.shadowRays;
+	uint32_t n = 0;
 	for (int k = 0; k < LH2_SEGS; k++) n += c.segShadow[k * LH2_SEGCOUNT_STRIDE];
 	return n;
 }

@@ -242,9 +242,6 @@ private:
 	   step costs 1.8x the BVH4's issue slots for 0.72x the steps (room bounce 0.503 vs 0.432 ms, config 3 2.28 vs 1.94 ms,
 	   the N = 8 share 1.32 vs 1.15 ms: profiles/r05_ab_w8.txt) */
 	int traceWide = 0;
-	/* the path tail traces its own paths' shadow rays in its waves' idle lanes (setting "tailShadows", TraceArgs::tailShadows):
-	   the final shadow launch traces only those that found no free slot */
-	int tailShadows = 0;
 	bool UseWide( uint32_t paths ) const { return w8Avail && (traceWide == 1 || (traceWide == 2 && (float)paths <= kSmallFramePaths)); }
 	/* stack entries a ray may need: the BVH2 loop's BLAS depth, the BVH4 loop's 3 per level, the W8 loop's 2 per level (a node
 	   group and a leaf group per node step) */
