@@ -43,6 +43,8 @@ struct SceneDev       /* everything the traversal and shading kernels read, by v
 	const uint4* nodes4q;            /* the same BVH4 with quantized child boxes, 64 B per node (lh2_box4.inc, box4q) */
 	float qBound;                    /* >= |coordinate| of every node origin, world and mesh space (slab_offsets) */
 	int tlasRoot4;
+	int root40;                      /* tlasRoot4 ~0 (single-instance start): the instance's BVH4 root, a kernel argument so that a
+	                                    ray's first node needs no load */
 	const lh2_CoreInstanceDesc* instDesc;
 	const uint4* materials;          /* 128 B CUDAMaterial records (core_settings.h:94-104) */
 	const lh2_CoreLightTri* areaLights;

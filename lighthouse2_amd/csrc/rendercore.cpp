@@ -896,10 +896,12 @@ SceneDev RenderCore::MakeSceneDev()
 	   the TLAS root's box test, which can only cull (TopLevelBVH::Traverse bvh.cpp:594-649); the
 	   instance transform runs as at the leaf, so the hits are unchanged: one loop iteration less per ray */
 	s.w8 = w8Avail ? dW8.ptr : nullptr, s.w8Root = W8TlasBlock( tlasSlot ) * 8, s.w8Base0 = 0;
+	s.root40 = 0;
 	if (singleInstanceStart && instances.size() == 1 && instances[0].mesh >= 0 && instances[0].mesh < (int)meshes.size() &&
 		meshes[instances[0].mesh]->triCount > 0)
 	{
 		s.tlasRoot = s.tlasRoot4 = ~0;
+		s.root40 = bvh4 ? meshNode4Base[instances[0].mesh] : 0;   /* DevInstance::root4 of instance 0 (UpdateToplevel) */
 		if (w8Avail) s.w8Base0 = meshBlockBase[instances[0].mesh], s.w8Root = s.w8Base0 * 8;
 	}
 	s.instDesc = dInstDesc[tlasSlot].ptr, s.materials = dMaterials.ptr;
