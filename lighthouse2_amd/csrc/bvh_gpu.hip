@@ -733,9 +733,11 @@ void GpuBvhBuilder::Reserve( int n )
 	}
 	if (n <= cap) return;
 	/* the TLAS builds run on the core's ahead stream and the BLAS builds on its core stream, both with this scratch: the
-	   old buffers are freed only once no launch on any stream can still use them */
+	   old buffers are freed only once no launch on any stream can still use them.  That sync stalls frames in flight, so the
+	   capacity grows by half again at least (a scene that keeps adding instances syncs O(log n) times, not per
+	   instance) */
 	if (cap) CHK( hipDeviceSynchronize() );
-	cap = std::max( n, 64 );
+	cap = std::max( n, std::max( 64, cap + cap / 2 ) );
 	const size_t c = (size_t)cap, c2 = 2 * c;
 	grow_buf( (Box8*&)boxes, c2 ); grow_buf( (Box8*&)prim, c ); grow_buf( (Box8*&)cl[0], c ); grow_buf( (Box8*&)cl[1], c );
 	grow_buf( clNode[0], c ); grow_buf( clNode[1], c ); grow_buf( child, 2 * c2 ); grow_buf( parent, c2 );
@@ -749,7 +751,7 @@ void* GpuBvhBuilder::Scratch( size_t bytes )
 	if (bytes > tmpBytes)
 	{
 		if (tmp) { CHK( hipDeviceSynchronize() ); CHK( hipFree( tmp ) ); }
-		tmpBytes = std::max<size_t>( bytes, 1 << 20 );
+		tmpBytes = std::max<size_t>( bytes, std::max<size_t>( 1 << 20, tmpBytes + tmpBytes / 2 ) );
 		CHK( hipMalloc( &tmp, tmpBytes ) );
 	}
 	return tmp;
