@@ -20,6 +20,7 @@
 #include "../../include/lh2_core_types.h"
 #include "lh2_kernels.h"
 #include "lh2_w8.h"
+#include "lh2_bary.h"
 
 #define S_SPECULAR 1
 #define S_BOUNCED 2
@@ -114,13 +115,14 @@ LH2_DEV BlueNoise4 blueNoiseFetch4( const uint8_t* bn, int x, int y, const int s
 }
 LH2_DEV void blueNoiseFinish4( const uint8_t* bn, const BlueNoise4& q, float r[4] )
 {
+	/* the four sample-byte loads issued together (one round trip): the scheduler otherwise interleaved them with their uses
+	   in the primary launch's camera code, a round trip each */
+	int v[4];
 #pragma unroll
-	for (int k = 0; k < 4; k++)
-	{
-		const int ranked = (q.sampleIndex ^ (int)((q.rank >> (8 * k)) & 255)) & 255;
-		const int value = (int)bn[q.d0 + k + ranked * 256] ^ (int)((q.scr >> (8 * k)) & 255);
-		r[k] = (0.5f + (float)value) * (1.0f / 256.0f);
-	}
+	for (int k = 0; k < 4; k++) v[k] = (int)bn[q.d0 + k + ((q.sampleIndex ^ (int)((q.rank >> (8 * k)) & 255)) & 255) * 256];
+	__builtin_amdgcn_sched_barrier( 0 );
+#pragma unroll
+	for (int k = 0; k < 4; k++) r[k] = (0.5f + (float)(v[k] ^ (int)((q.scr >> (8 * k)) & 255))) * (1.0f / 256.0f);
 }
 LH2_DEV uint32_t WangHash( uint32_t s ) { s = (s ^ 61) ^ (s >> 16), s *= 9, s = s ^ (s >> 4), s *= 0x27d4eb2d, s = s ^ (s >> 15); return s; }
 LH2_DEV uint32_t RandomInt( uint32_t& s ) { s ^= s << 13, s ^= s >> 17, s ^= s << 5; return s; }
@@ -866,24 +868,14 @@ LH2_DEV float LightPickProb( const SceneDev& s, int idx, v3 O, v3 N, v3 I )
 	if (idx < 0 || idx >= s.nArea) return 0;
 	return pidx / sum;
 }
+/* RandomBarycentrics (lights_shared.h:145-164): the reference's 16-level triangle subdivision in closed form (lh2_bary.h),
+   bit-identical for every digit string (tools/bary_check.cpp sweeps all 2^32, tests/test_bary.py a sample) */
 LH2_DEV v3 RandomBarycentrics( const float r0 )
 {
 	const uint32_t uf = lh2_f2u( r0 * 4294967296.0f );
-	float Ax = 1, Ay = 0, Bx = 0, By = 1, Cx = 0, Cy = 0;
-	for (int i = 0; i < 16; ++i)
-	{
-		const int d = (uf >> (2 * (15 - i))) & 0x3;
-		float Anx, Any, Bnx, Bny, Cnx, Cny;
-		switch (d)
-		{
-		case 0: Anx = (Bx + Cx) * 0.5f, Any = (By + Cy) * 0.5f; Bnx = (Ax + Cx) * 0.5f, Bny = (Ay + Cy) * 0.5f; Cnx = (Ax + Bx) * 0.5f, Cny = (Ay + By) * 0.5f; break;
-		case 1: Anx = Ax, Any = Ay; Bnx = (Ax + Bx) * 0.5f, Bny = (Ay + By) * 0.5f; Cnx = (Ax + Cx) * 0.5f, Cny = (Ay + Cy) * 0.5f; break;
-		case 2: Anx = (Bx + Ax) * 0.5f, Any = (By + Ay) * 0.5f; Bnx = Bx, Bny = By; Cnx = (Bx + Cx) * 0.5f, Cny = (By + Cy) * 0.5f; break;
-		default: Anx = (Cx + Ax) * 0.5f, Any = (Cy + Ay) * 0.5f; Bnx = (Cx + Bx) * 0.5f, Bny = (Cy + By) * 0.5f; Cnx = Cx, Cny = Cy; break;
-		}
-		Ax = Anx, Ay = Any, Bx = Bnx, By = Bny, Cx = Cnx, Cy = Cny;
-	}
-	const float rx = (Ax + Bx + Cx) * 0.3333333f, ry = (Ay + By + Cy) * 0.3333333f;
+	float sx, sy;
+	lh2_bary_sums( uf, sx, sy );
+	const float rx = sx * 0.3333333f, ry = sy * 0.3333333f;
 	return mk3( rx, ry, 1 - rx - ry );
 }
 LH2_DEV v3 RandomPointOnLight( const SceneDev& s, float r0, float r1, const v3 I, const v3 N, float& pickProb, float& lightPdf, v3& lightColor )
@@ -1886,11 +1878,13 @@ __global__ void k_finalize( float4* __restrict__ acc, float4* __restrict__ out, 
 	if (blockIdx.x == 0 && fs.hostCounters)
 	{
 		/* block 0 also hands the frame's counters, ray-count log and scene error to the host's pinned
-		   FrameStats (system-scope stores: no device-to-host copy launches at the end) */
+		   FrameStats (system-scope stores: no device-to-host copy launches at the end): the totals and the shadow
+		   stream's segment counts, the words the host reads (RenderCore::Synchronize), not the whole record */
 		const uint32_t* src = (const uint32_t*)fs.counters;
 		uint32_t* dst = (uint32_t*)fs.hostCounters;
-		for (int k = threadIdx.x; k < (int)(sizeof( Counters ) / 4); k += blockDim.x)
-			__hip_atomic_store( dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+		constexpr int kHead = (int)(offsetof( Counters, segPath ) / 4), kShadow = (int)(offsetof( Counters, segShadow ) / 4);
+		const int k = threadIdx.x < kHead ? (int)threadIdx.x : threadIdx.x < kHead + LH2_SEGS ? kShadow + ((int)threadIdx.x - kHead) * LH2_SEGCOUNT_STRIDE : -1;
+		if (k >= 0) __hip_atomic_store( dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
 		for (int k = threadIdx.x; k < LH2_MAX_BOUNCES; k += blockDim.x)
 			__hip_atomic_store( fs.hostRayCount + k, fs.rayLog[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
 		if (threadIdx.x == 0) __hip_atomic_store( fs.hostSceneError, *fs.sceneError, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
