@@ -885,15 +885,39 @@ LH2_DEV v3 RandomPointOnLight( const SceneDev& s, float r0, float r1, const v3 I
 	const v3 bary = RandomBarycentrics( r0 );
 	float sum = 0, total = 0;
 	int lightIdx = 0;
-	for (int i = 0; i < nl; i++) sum += potential_i( s, i, I, N, bary, s3( 0 ) );
-	if (sum <= 0) { lightPdf = 0; return s3( 1 ); }
-	r1 *= sum;
-	for (int i = 0; i < nl; i++)
+	if (nl <= 4)
 	{
-		total += potential_i( s, i, I, N, bary, s3( 0 ) );
-		if (total >= r1) { lightIdx = i; break; }
+		/* up to four lights: each potential evaluated once (the reference evaluates it in the sum, again in the pick walk and
+		   once more for the pick probability; the same arithmetic on the same inputs, so the same values) */
+		float pot[4] = { 0, 0, 0, 0 };
+#pragma unroll
+		for (int i = 0; i < 4; i++) if (i < nl) pot[i] = potential_i( s, i, I, N, bary, s3( 0 ) );
+#pragma unroll
+		for (int i = 0; i < 4; i++) if (i < nl) sum += pot[i];
+		if (sum <= 0) { lightPdf = 0; return s3( 1 ); }
+		r1 *= sum;
+		bool found = false;
+#pragma unroll
+		for (int i = 0; i < 4; i++)
+			if (i < nl && !found)
+			{
+				total += pot[i];
+				if (total >= r1) lightIdx = i, found = true;
+			}
+		pickProb = (lightIdx == 0 ? pot[0] : lightIdx == 1 ? pot[1] : lightIdx == 2 ? pot[2] : pot[3]) / sum;
 	}
-	pickProb = potential_i( s, lightIdx, I, N, bary, s3( 0 ) ) / sum;
+	else
+	{
+		for (int i = 0; i < nl; i++) sum += potential_i( s, i, I, N, bary, s3( 0 ) );
+		if (sum <= 0) { lightPdf = 0; return s3( 1 ); }
+		r1 *= sum;
+		for (int i = 0; i < nl; i++)
+		{
+			total += potential_i( s, i, I, N, bary, s3( 0 ) );
+			if (total >= r1) { lightIdx = i; break; }
+		}
+		pickProb = potential_i( s, lightIdx, I, N, bary, s3( 0 ) ) / sum;
+	}
 	{ const int hi = (int)lightCount - 1; lightIdx = lightIdx < 0 ? 0 : lightIdx > hi ? hi : lightIdx; }
 	if (lightIdx < s.nArea)
 	{
