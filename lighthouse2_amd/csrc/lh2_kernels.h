@@ -46,6 +46,8 @@ struct SceneDev       /* everything the traversal and shading kernels read, by v
 	int root40;                      /* tlasRoot4 ~0 (single-instance start): the instance's BVH4 root, a kernel argument so that a
 	                                    ray's first node needs no load */
 	const lh2_CoreInstanceDesc* instDesc;
+	const float4* tris0;             /* the single instance's shading triangles (tlasRoot4 ~0), else null: a hit's triangle
+	                                    address then needs no instance-record load (HitInstance) */
 	const uint4* materials;          /* 128 B CUDAMaterial records (core_settings.h:94-104) */
 	const lh2_CoreLightTri* areaLights;
 	const lh2_CorePointLight* pointLights;

@@ -48,6 +48,23 @@ LH2_DEV uint32_t wave_alloc( bool want, uint32_t* counter )
 	return want ? base + lanes_below( m ) : 0xffffffffu;
 }
 
+/* three wave-level compactions in one atomic instruction: lane k < 3 adds the count of mask k to counter k (a null
+   counter only with an empty mask), so the three slot bases cost one round trip instead of three.  The whole wave must
+   be active (k_shade's compaction, after its per-lane branch has reconverged) */
+LH2_DEV void wave_alloc3( const uint64_t m0, const uint64_t m1, const uint64_t m2, uint32_t* c0, uint32_t* c1, uint32_t* c2,
+	uint32_t& b0, uint32_t& b1, uint32_t& b2 )
+{
+	b0 = b1 = b2 = 0;
+	if ((m0 | m1 | m2) == 0) return;
+	const uint32_t lane = lane_id();
+	const uint64_t m = lane == 0 ? m0 : lane == 1 ? m1 : m2;
+	uint32_t base = 0;
+	if (lane < 3 && m != 0) base = atomicAdd( lane == 0 ? c0 : lane == 1 ? c1 : c2, (uint32_t)__popcll( m ) );
+	b0 = (uint32_t)__builtin_amdgcn_readlane( (int)base, 0 );
+	b1 = (uint32_t)__builtin_amdgcn_readlane( (int)base, 1 );
+	b2 = (uint32_t)__builtin_amdgcn_readlane( (int)base, 2 );
+}
+
 static_assert( sizeof( ((Counters*)0)->segShadow ) == LH2_SEGS * LH2_SEGCOUNT_STRIDE * 4, "Counters segment layout" );
 
 /* [lo, hi): segment c of a trace launch's ray stream (lh2_kernels.h, LH2_SEGS).  Wave-uniform, and
@@ -559,9 +576,24 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 #include "lh2_box4.inc"
 /* the path-tail mode of lh2_trace4d.inc shades with k_shade's code (defined with the shading code below) */
 struct ShadeOut { bool ext, shadow; float4 eO, eD, eT, eQ, sO, sD, sP; };
-template <bool NL>
+/* -DLH2_SHADE_TIMES (diagnostic builds only): k_shade's wave time split over the stages of shade_path, summed over every
+   launch of the process into lh2_shade_tt (time since the lane's previous mark, recorded by the wave's first active lane;
+   the counts of marks in [8 + k]), printed by RenderCore::Shutdown (tools/shade_times.sh) */
+#ifdef LH2_SHADE_TIMES
+__device__ unsigned long long lh2_shade_tt[16];
+#define LH2_STT( k ) if (sttp) { __builtin_amdgcn_sched_barrier( 0 ); const uint64_t n_ = __builtin_amdgcn_s_memtime(); \
+	if (lane_id() == (uint32_t)__builtin_ctzll( __ballot( true ) )) atomicAdd( &lh2_shade_tt[k], n_ - *sttp ), atomicAdd( &lh2_shade_tt[8 + (k)], 1ull ); \
+	*sttp = n_; __builtin_amdgcn_sched_barrier( 0 ); }
+#define LH2_STT_PARAM , uint64_t* sttp
+#define LH2_STT_PARAM_DEFAULT , uint64_t* sttp = nullptr
+#else
+#define LH2_STT( k )
+#define LH2_STT_PARAM
+#define LH2_STT_PARAM_DEFAULT
+#endif
+template <bool NL, bool SINGLE>
 LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd, const float4 T4, const float4 O4, const float4 D4, const float4 Q4,
-	const int pathLength, const uint32_t R0, ShadeOut& o );
+	const int pathLength, const uint32_t R0, ShadeOut& o LH2_STT_PARAM_DEFAULT );
 #include "lh2_trace4d.inc"
 #include "lh2_trace_packet.inc"
 
@@ -715,11 +747,15 @@ LH2_DEV float normal_scale( const uint32_t byte, const bool absArg )   /* materi
 }
 
 /* GetShadingData, material_shared.h:35-178 (OPTIXPRIMEBUILD, CONSISTENTNORMALS, BILINEAR) */
+/* the hit triangle's records GetShadingData reads first (CoreTri4: 1 .. 5 and 7), loaded by the caller where the loads can
+   go out early (shade_path: beside the instance record's for a single instance) */
+struct TriShade { float4 t1, t2, t3, t4, t5, t7; };
+LH2_DEV TriShade tri_shade_load( const float4* __restrict__ tri ) { return { tri[1], tri[2], tri[3], tri[4], tri[5], tri[7] }; }
 LH2_DEV void GetShadingData( const SceneDev& s, const v3 D, const float u, const float v, const float coneWidth, const float4* __restrict__ tri,
-	const v3 A, const v3 B, const v3 C, ShadingData& sd, v3& N, v3& iN, v3& fN, v3& T )
+	const TriShade& tq, const v3 A, const v3 B, const v3 C, ShadingData& sd, v3& N, v3& iN, v3& fN, v3& T )
 {
 
-	const float4 tdata1 = tri[1], tdata2 = tri[2], tdata3 = tri[3], tdata4 = tri[4], tdata5 = tri[5], alpha4 = tri[7];
+	const float4 tdata1 = tq.t1, tdata2 = tq.t2, tdata3 = tq.t3, tdata4 = tq.t4, tdata5 = tq.t5, alpha4 = tq.t7;
 	const uint4* mat = s.materials + (size_t)__float_as_int( tdata1.w ) * 8;
 	const uint4 baseData = mat[0];
 	sd.params = mat[1];
@@ -803,9 +839,26 @@ LH2_DEV void GetShadingData( const SceneDev& s, const v3 D, const float u, const
 
 
 /* ---- lights (lights_shared.h:36-261) ------------------------------------------------------ */
+/* the light records are read through the constant address space: with a wave-uniform index (the potentials' loops) the
+   loads are scalar loads through the scalar cache, issued together, instead of a vector-load round trip per light (the
+   light arrays are written only by the host between frames) */
+#define LH2_AS4 __attribute__( (address_space( 4 )) )
+template <class T> LH2_DEV const LH2_AS4 T* kc( const T* p ) { return (const LH2_AS4 T*)p; }
+/* field f of light record i (a lane's own index) of the n records at arr: with few (wave-uniform: at most four lights in the
+   scene) selected from the n records' scalar loads, so the sampled light costs no vector-load round trip; else loaded */
+template <class T, class F> LH2_DEV float light_field( const T* arr, const int n, const int i, const bool few, F f )
+{
+	const LH2_AS4 T* a = kc( arr );
+	if (!few) return f( a[i] );
+	float r = f( a[0] );
+	if (n > 1) r = i == 1 ? f( a[1] ) : r;
+	if (n > 2) r = i == 2 ? f( a[2] ) : r;
+	if (n > 3) r = i == 3 ? f( a[3] ) : r;
+	return r;
+}
 LH2_DEV float PotentialArea( const SceneDev& s, int idx, v3 O, v3 N, v3 I, v3 bary )
 {
-	const lh2_CoreLightTri& l = s.areaLights[idx];
+	const LH2_AS4 lh2_CoreLightTri& l = kc( s.areaLights )[idx];
 	v3 L = I;
 	if (bary.x >= 0)
 	{
@@ -821,7 +874,7 @@ LH2_DEV float PotentialArea( const SceneDev& s, int idx, v3 O, v3 N, v3 I, v3 ba
 }
 LH2_DEV float PotentialPoint( const SceneDev& s, int idx, v3 I, v3 N )
 {
-	const lh2_CorePointLight& l = s.pointLights[idx];
+	const LH2_AS4 lh2_CorePointLight& l = kc( s.pointLights )[idx];
 	const v3 L = sub3( mk3( l.position.x, l.position.y, l.position.z ), I );
 	const float NdotL = fmaxf( 0.0f, dot3( N, L ) );
 	const float att = 1.0f / dot3( L, L );
@@ -829,7 +882,7 @@ LH2_DEV float PotentialPoint( const SceneDev& s, int idx, v3 I, v3 N )
 }
 LH2_DEV float PotentialSpot( const SceneDev& s, int idx, v3 I, v3 N )
 {
-	const lh2_CoreSpotLight& l = s.spotLights[idx];
+	const LH2_AS4 lh2_CoreSpotLight& l = kc( s.spotLights )[idx];
 	v3 L = sub3( mk3( l.position.x, l.position.y, l.position.z ), I );
 	const float att = 1.0f / dot3( L, L );
 	L = normalize3( L );
@@ -840,7 +893,7 @@ LH2_DEV float PotentialSpot( const SceneDev& s, int idx, v3 I, v3 N )
 }
 LH2_DEV float PotentialDir( const SceneDev& s, int idx, v3 N )
 {
-	const lh2_CoreDirectionalLight& l = s.dirLights[idx];
+	const LH2_AS4 lh2_CoreDirectionalLight& l = kc( s.dirLights )[idx];
 	const float LNdotL = fmaxf( 0.0f, -(l.direction.x * N.x + l.direction.y * N.y + l.direction.z * N.z) );
 	return l.energy * LNdotL;
 }
@@ -919,51 +972,60 @@ LH2_DEV v3 RandomPointOnLight( const SceneDev& s, float r0, float r1, const v3 I
 		pickProb = potential_i( s, lightIdx, I, N, bary, s3( 0 ) ) / sum;
 	}
 	{ const int hi = (int)lightCount - 1; lightIdx = lightIdx < 0 ? 0 : lightIdx > hi ? hi : lightIdx; }
+	const bool few = nl <= 4;
 	if (lightIdx < s.nArea)
 	{
-		const lh2_CoreLightTri& l = s.areaLights[lightIdx];
-		lightColor = mk3( l.radiance.x, l.radiance.y, l.radiance.z );
-		const v3 P = add3( add3( smul( bary.x, mk3( l.vertex0.x, l.vertex0.y, l.vertex0.z ) ), smul( bary.y, mk3( l.vertex1.x, l.vertex1.y, l.vertex1.z ) ) ),
-			smul( bary.z, mk3( l.vertex2.x, l.vertex2.y, l.vertex2.z ) ) );
+#define LF( fld_ ) light_field( s.areaLights, s.nArea, lightIdx, few, []( const auto& l ) { return l.fld_; } )
+		lightColor = mk3( LF( radiance.x ), LF( radiance.y ), LF( radiance.z ) );
+		const v3 P = add3( add3( smul( bary.x, mk3( LF( vertex0.x ), LF( vertex0.y ), LF( vertex0.z ) ) ), smul( bary.y, mk3( LF( vertex1.x ), LF( vertex1.y ), LF( vertex1.z ) ) ) ),
+			smul( bary.z, mk3( LF( vertex2.x ), LF( vertex2.y ), LF( vertex2.z ) ) ) );
 		v3 L = sub3( I, P );
 		const float sqDist = dot3( L, L );
 		L = normalize3( L );
-		const float LNdotL = L.x * l.N.x + L.y * l.N.y + L.z * l.N.z;
-		const float reciSolidAngle = sqDist / (l.area * LNdotL);
+		const float LNdotL = L.x * LF( N.x ) + L.y * LF( N.y ) + L.z * LF( N.z );
+		const float reciSolidAngle = sqDist / (LF( area ) * LNdotL);
 		lightPdf = (LNdotL > 0 && dot3( L, N ) < 0) ? reciSolidAngle : 0;
 		return P;
+#undef LF
 	}
 	else if (lightIdx < s.nArea + s.nPoint)
 	{
-		const lh2_CorePointLight& l = s.pointLights[lightIdx - s.nArea];
-		const v3 pos = mk3( l.position.x, l.position.y, l.position.z );
-		lightColor = mk3( l.radiance.x, l.radiance.y, l.radiance.z );
+		const int li = lightIdx - s.nArea;
+#define LF( fld_ ) light_field( s.pointLights, s.nPoint, li, few, []( const auto& l ) { return l.fld_; } )
+		const v3 pos = mk3( LF( position.x ), LF( position.y ), LF( position.z ) );
+		lightColor = mk3( LF( radiance.x ), LF( radiance.y ), LF( radiance.z ) );
 		const v3 L = sub3( I, pos );
 		const float sqDist = dot3( L, L );
 		lightPdf = dot3( L, N ) < 0 ? sqDist : 0;
 		return pos;
+#undef LF
 	}
 	else if (lightIdx < s.nArea + s.nPoint + s.nSpot)
 	{
-		const lh2_CoreSpotLight& l = s.spotLights[lightIdx - (s.nArea + s.nPoint)];
-		const v3 pos = mk3( l.position.x, l.position.y, l.position.z );
+		const int li = lightIdx - (s.nArea + s.nPoint);
+#define LF( fld_ ) light_field( s.spotLights, s.nSpot, li, few, []( const auto& l ) { return l.fld_; } )
+		const v3 pos = mk3( LF( position.x ), LF( position.y ), LF( position.z ) );
 		v3 L = sub3( I, pos );
 		const float sqDist = dot3( L, L );
 		L = normalize3( L );
-		const float d = (fmaxf( 0.0f, L.x * l.direction.x + L.y * l.direction.y + L.z * l.direction.z ) - l.cosOuter) / (l.cosInner - l.cosOuter);
+		const float cosOuter = LF( cosOuter );
+		const float d = (fmaxf( 0.0f, L.x * LF( direction.x ) + L.y * LF( direction.y ) + L.z * LF( direction.z ) ) - cosOuter) / (LF( cosInner ) - cosOuter);
 		const float LNdotL = fminf( 1.0f, d );
 		lightPdf = (LNdotL > 0 && dot3( L, N ) < 0) ? (sqDist / LNdotL) : 0;
-		lightColor = mk3( l.radiance.x, l.radiance.y, l.radiance.z );
+		lightColor = mk3( LF( radiance.x ), LF( radiance.y ), LF( radiance.z ) );
 		return pos;
+#undef LF
 	}
 	else
 	{
-		const lh2_CoreDirectionalLight& l = s.dirLights[lightIdx - (s.nArea + s.nPoint + s.nSpot)];
-		const v3 L = mk3( l.direction.x, l.direction.y, l.direction.z );
-		lightColor = mk3( l.radiance.x, l.radiance.y, l.radiance.z );
+		const int li = lightIdx - (s.nArea + s.nPoint + s.nSpot);
+#define LF( fld_ ) light_field( s.dirLights, s.nDir, li, few, []( const auto& l ) { return l.fld_; } )
+		const v3 L = mk3( LF( direction.x ), LF( direction.y ), LF( direction.z ) );
+		lightColor = mk3( LF( radiance.x ), LF( radiance.y ), LF( radiance.z ) );
 		const float NdotL = dot3( L, N );
 		lightPdf = NdotL < 0 ? 1 : 0;
 		return sub3( I, smul( 1000.0f, L ) );
+#undef LF
 	}
 }
 
@@ -1355,6 +1417,7 @@ LH2_DEV float SurvivalProbability( const v3 a ) { return fminf( 1.0f, fmaxf( fma
 
 /* the hit's instance record (lh2_CoreInstanceDesc: triangle pointer, inverse-transform rows A, B, C),
    read in one step of the dependent load chain right after the hit record; none for a miss */
+template <bool SINGLE = false>
 LH2_DEV const float4* HitInstance( const SceneDev& s, const int primIdx, const int instIdx, v3& A, v3& B, v3& C )
 {
 	/* branch-free (a miss reads record 0, which always exists: RenderCore::Init allocates it), so the
@@ -1362,7 +1425,8 @@ LH2_DEV const float4* HitInstance( const SceneDev& s, const int primIdx, const i
 	const lh2_CoreInstanceDesc* id = s.instDesc + (primIdx == NOHIT ? 0 : instIdx);
 	const float4 a = *(const float4*)&id->A, b = *(const float4*)&id->B, c = *(const float4*)&id->C;
 	A = xyz( a ), B = xyz( b ), C = xyz( c );
-	return (const float4*)id->triangles + (size_t)primIdx * 11;
+	/* SINGLE (SceneDev::tris0 set): the triangle's address needs no load, its loads go out beside the instance record's */
+	return (SINGLE ? s.tris0 : (const float4*)id->triangles) + (size_t)primIdx * 11;
 }
 
 /* a shade launch's input segment: its records (front + back), the front records, and the gap between
@@ -1389,9 +1453,9 @@ LH2_DEV float scene_chord( const ShadeParams& p, const float4 o, const float4 d 
 /* one path vertex of shadeKernel (pathtracer.h:54-245): the hit record, ray and path state of a path at
    pathLength in; its extension ray (o.ext) and shadow ray (o.shadow) out.  Shared by k_shade (one launch
    per bounce) and the path-tail kernel (k_trace_path4d: trace and shade in one loop per lane) */
-template <bool NL>
+template <bool NL, bool SINGLE>
 LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd, const float4 T4, const float4 O4, const float4 D4, const float4 Q4,
-	const int pathLength, const uint32_t R0, ShadeOut& o )
+	const int pathLength, const uint32_t R0, ShadeOut& o LH2_STT_PARAM )
 {
 	const int w = p.w, h = p.h;
 	const float HIT_T = __uint_as_float( hd.x );
@@ -1412,10 +1476,15 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 	   triangle) -> material, instead of the table lookups following the material */
 	const BlueNoise4 bnq = blueNoiseFetch4( s.blueNoise, (int)(pixelIdx % (uint32_t)w), (int)(pixelIdx / (uint32_t)w), (int)sampleIdx, 4 + 4 * pathLength );
 	v3 instA, instB, instC;
-	const float4* tri = HitInstance( s, PRIMIDX, INSTANCEIDX, instA, instB, instC );
+	const float4* tri = HitInstance<SINGLE>( s, PRIMIDX, INSTANCEIDX, instA, instB, instC );
+	/* SINGLE: the triangle's records with them (a miss reads the blue-noise table instead: always there, and large
+	   enough); else after the instance record, in GetShadingData */
+	TriShade tq;
+	if (SINGLE) tq = tri_shade_load( PRIMIDX == NOHIT ? (const float4*)s.blueNoise : tri );
 	__builtin_amdgcn_sched_barrier( 0 );
 	float bnv[4];
 	blueNoiseFinish4( s.blueNoise, bnq, bnv );
+	LH2_STT( 0 )
 	if (pathLength == 1) unsafeAtomicAdd( &p.acc[pixelIdx].w, PRIMIDX == NOHIT ? 10000.0f : HIT_T );
 	if (PRIMIDX == NOHIT)
 	{
@@ -1431,7 +1500,9 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 		ShadingData sd;
 		v3 N, iN, fN, T;
 		const v3 I = add3( RAY_O, smul( HIT_T, D ) );
-		GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, instA, instB, instC, sd, N, iN, fN, T );
+		if (!SINGLE) tq = tri_shade_load( tri );
+		GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, tq, instA, instB, instC, sd, N, iN, fN, T );
+		LH2_STT( 1 )
 		if (sd.flags & 1)
 		{
 			if (pathLength < p.maxPathLength)
@@ -1453,7 +1524,7 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 				else
 				{
 					const v3 lastN = UnpackNormal( fbits( Q4.y ) );
-					const float4 tdata0 = tri[0], tdata5 = tri[5];
+					const float4 tdata0 = tri[0], tdata5 = tq.t5;
 					const float lightPdf = (HIT_T * HIT_T) / (-dot3( D, N ) * tdata5.w);     /* CalculateLightPDF, tri.area */
 					const float pickProb = LightPickProb( s, __float_as_int( tdata0.w ), RAY_O, lastN, I );
 					if ((bsdfPdf + lightPdf * pickProb) > 0) contribution = muls( mul3( throughput, sd.color ), 1.0f / (bsdfPdf + lightPdf * pickProb) );
@@ -1470,6 +1541,7 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 		if (faceDir == 1) sd.transmittance = s3( 0 );
 		throughput = muls( throughput, 1.0f / bsdfPdf );
 		if (NL && !(data & S_SPECULAR) && sampleIdx >= 2) (void)RandomFloat( seed ), (void)RandomFloat( seed );
+		LH2_STT( 2 )
 		if (!NL && !(data & S_SPECULAR))
 		{
 			float r0, r1, pickProb = 0, lightPdf = 0;
@@ -1481,6 +1553,7 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 			}
 			v3 lightColor = s3( 0 );
 			v3 L = sub3( RandomPointOnLight( s, r0, r1, I, muls( fN, faceDir ), pickProb, lightPdf, lightColor ), I );
+			LH2_STT( 3 )
 			const float dist = length3( L );
 			L = muls( L, 1.0f / dist );
 			const float NdotL = dot3( L, muls( fN, faceDir ) );
@@ -1501,6 +1574,7 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 				}
 			}
 		}
+		LH2_STT( 4 )
 		if (data & ENOUGH_BOUNCES || pathLength == p.maxPathLength) return;
 		{
 			v3 R = s3( 0 );
@@ -1513,6 +1587,7 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 			}
 			bool specular = false;
 			const v3 bsdf = SampleBSDF( sd, fN, N, T, muls( D, -1.0f ), HIT_T, r3, r4, R, newBsdfPdf, specular );
+			LH2_STT( 5 )
 			if (newBsdfPdf < EPSILON || newBsdfPdf != newBsdfPdf) return;
 			if (specular) data |= S_SPECULAR;
 			const float pr = ((data & S_SPECULAR) || ((data & S_BOUNCED) == 0)) ? 1 : SurvivalProbability( bsdf );
@@ -1526,6 +1601,7 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 			o.ext = true;
 			o.eO = make_float4( eo.x, eo.y, eo.z, 0 ), o.eD = make_float4( R.x, R.y, R.z, 1e34f );
 			o.eT = make_float4( nt.x, nt.y, nt.z, bitsf( data ) ), o.eQ = make_float4( newBsdfPdf, bitsf( packedNormal ), 0, 0 );
+			LH2_STT( 6 )
 		}
 	}
 }
@@ -1545,7 +1621,7 @@ LH2_DEV void shade_epilogue( const ShadeParams& p );   /* the bounce hand-off, b
 /* NL: a scene without lights.  NEE (pathtracer.h:168-208) then never yields a shadow ray
    (RandomPointOnLight: lightPdf 0), so its code is compiled out, except the two random numbers it
    draws past sample 1, which later draws depend on */
-template <bool TERM, bool NL>
+template <bool TERM, bool NL, bool SINGLE>
 __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAVES ) void k_shade( const SceneDev s, const ShadeParams p )
 {
 	/* the block's segment of the path stream (its XCD's), and the segment's share of the grid */
@@ -1560,6 +1636,9 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 		for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < p.hvZeroWords; i += gridDim.x * 256u) p.hvZero[i] = 0;
 	for (uint32_t base = (blockIdx.x / LH2_SEGS) * 256u; base < count; base += gstride)
 	{
+#ifdef LH2_SHADE_TIMES
+		uint64_t stt = __builtin_amdgcn_s_memtime(), *const sttp = &stt;
+#endif
 		const uint32_t jobIndex = segBase + seg_pos( base + threadIdx.x, front, gap );
 		bool doExt = false, doShadow = false;
 		float4 eO, eD, eT, eQ, sO, sD, sP;
@@ -1575,7 +1654,11 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 			__builtin_amdgcn_sched_barrier( 0 );
 			ShadeOut so;
 			so.ext = so.shadow = false;
-			shade_path<NL>( s, p, hd, T4, O4, D4, Q4, p.pathLength, p.R0, so );
+#ifdef LH2_SHADE_TIMES
+			shade_path<NL, SINGLE>( s, p, hd, T4, O4, D4, Q4, p.pathLength, p.R0, so, &stt );
+#else
+			shade_path<NL, SINGLE>( s, p, hd, T4, O4, D4, Q4, p.pathLength, p.R0, so );
+#endif
 			doExt = so.ext, doShadow = so.shadow;
 			eO = so.eO, eD = so.eD, eT = so.eT, eQ = so.eQ, sO = so.sO, sD = so.sD, sP = so.sP;
 		}
@@ -1585,21 +1668,25 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 		{
 			/* two-ended segment: a ray with a short chord through the scene goes to the end (traced last) */
 			const bool late = doExt && p.chordCut > 0 && scene_chord( p, eO, eD ) <= p.chordCut;
-			const uint32_t es = wave_alloc( doExt && !late, &p.segOut[seg * LH2_SEGCOUNT_STRIDE] );
-			const uint32_t eb = wave_alloc( late, &p.segOutBack[seg * LH2_SEGCOUNT_STRIDE] );
+			const uint64_t mE = __ballot( doExt && !late ), mB = __ballot( late ), mS = __ballot( doShadow );
+			uint32_t bE, bB, bS;
+			wave_alloc3( mE, mB, mS, &p.segOut[seg * LH2_SEGCOUNT_STRIDE], p.segOutBack ? &p.segOutBack[seg * LH2_SEGCOUNT_STRIDE] : nullptr,
+				&p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE], bE, bB, bS );
+			const uint32_t es = bE + lanes_below( mE ), eb = bB + lanes_below( mB );
 			if (doExt)
 			{
 				const uint32_t o = segBase + (late ? p.segStride - 1u - eb : es);
 				p.rayOut[o] = eO; p.rayDOut[o] = eD; p.T4Out[o] = eT; p.Q4Out[o] = eQ;
 			}
 			/* shadow rays into the block's segment of the shadow stream */
-			const uint32_t ss = wave_alloc( doShadow, &p.counters->segShadow[seg * LH2_SEGCOUNT_STRIDE] );
+			const uint32_t ss = bS + lanes_below( mS );
 			if (doShadow)
 			{
 				if (ss < p.shadowStride) { const uint32_t o = seg * p.shadowStride + ss; p.shO[o] = sO; p.shD[o] = sD; p.shP[o] = sP; }
 				else atomicOr( &p.counters->shadowOverflow, 1u );
 			}
 		}
+		LH2_STT( 7 )
 	}
 	if (p.advance) shade_epilogue( p );
 }
@@ -1768,7 +1855,7 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const 
 				ShadingData sd;
 				v3 N, iN, fN, T;
 				const v3 I = add3( RAY_O, smul( HIT_T, D ) );
-				GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, instA, instB, instC, sd, N, iN, fN, T );
+				GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, tri_shade_load( tri ), instA, instB, instC, sd, N, iN, fN, T );
 				if (sd.color.x > 1.0f || sd.color.y > 1.0f || sd.color.z > 1.0f)
 				{
 					if (-dot3( D, N ) > 0 && (p.pathLength == 1 || (data & S_SPECULAR))) acc_add( p.acc, pixelIdx, mul3( throughput, sd.color ) );
@@ -2124,9 +2211,15 @@ void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, Launch
 	grid = grid < LH2_SEGS ? LH2_SEGS : grid;   /* every segment needs a block */
 	if (p->primeRef) LH2_LAUNCH( k_shade_ref, grid, 256, st, ev, *s, *p );
 	else if (p->terminal && p->pathLength == p->maxPathLength) LH2_LAUNCH( k_shade_last, lh2_shade_last_grid(), 256, st, ev, *s, *p );
-	else if (p->terminal) LH2_LAUNCH( (k_shade<true, true>), grid, 256, st, ev, *s, *p );
-	else if (s->nArea + s->nPoint + s->nSpot + s->nDir == 0) LH2_LAUNCH( (k_shade<false, true>), grid, 256, st, ev, *s, *p );
-	else LH2_LAUNCH( (k_shade<false, false>), grid, 256, st, ev, *s, *p );
+	else if (s->tris0)   /* one instance (SceneDev::tris0): the triangle loads need no instance record */
+	{
+		if (p->terminal) LH2_LAUNCH( (k_shade<true, true, true>), grid, 256, st, ev, *s, *p );
+		else if (s->nArea + s->nPoint + s->nSpot + s->nDir == 0) LH2_LAUNCH( (k_shade<false, true, true>), grid, 256, st, ev, *s, *p );
+		else LH2_LAUNCH( (k_shade<false, false, true>), grid, 256, st, ev, *s, *p );
+	}
+	else if (p->terminal) LH2_LAUNCH( (k_shade<true, true, false>), grid, 256, st, ev, *s, *p );
+	else if (s->nArea + s->nPoint + s->nSpot + s->nDir == 0) LH2_LAUNCH( (k_shade<false, true, false>), grid, 256, st, ev, *s, *p );
+	else LH2_LAUNCH( (k_shade<false, false, false>), grid, 256, st, ev, *s, *p );
 }
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st )
 {
@@ -2138,6 +2231,9 @@ void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int 
 	if (rows * w <= 0) { if (ev.stop) (void)hipEventRecord( ev.stop, st ); return; }
 	LH2_LAUNCH( k_unpack_rows, (rows * w + 255) / 256, 256, st, ev, src, acc, w, y0, band, bandStride, rows );
 }
+#ifdef LH2_SHADE_TIMES
+void lh2_shade_times( unsigned long long out[16] ) { (void)hipMemcpyFromSymbol( out, HIP_SYMBOL( lh2_shade_tt ), 16 * 8 ); }
+#endif
 void lh2_launch_spin( unsigned long long ticks, hipStream_t st ) { hipLaunchKernelGGL( k_spin, dim3( 1 ), dim3( 64 ), 0, st, ticks ); }
 void lh2_launch_finalize( float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st, const RowMap* rm )
 {

@@ -896,12 +896,13 @@ SceneDev RenderCore::MakeSceneDev()
 	   the TLAS root's box test, which can only cull (TopLevelBVH::Traverse bvh.cpp:594-649); the
 	   instance transform runs as at the leaf, so the hits are unchanged: one loop iteration less per ray */
 	s.w8 = w8Avail ? dW8.ptr : nullptr, s.w8Root = W8TlasBlock( tlasSlot ) * 8, s.w8Base0 = 0;
-	s.root40 = 0;
+	s.root40 = 0, s.tris0 = nullptr;
 	if (singleInstanceStart && instances.size() == 1 && instances[0].mesh >= 0 && instances[0].mesh < (int)meshes.size() &&
 		meshes[instances[0].mesh]->triCount > 0)
 	{
 		s.tlasRoot = s.tlasRoot4 = ~0;
 		s.root40 = bvh4 ? meshNode4Base[instances[0].mesh] : 0;   /* DevInstance::root4 of instance 0 (UpdateToplevel) */
+		s.tris0 = meshes[instances[0].mesh]->shadeTris.ptr;       /* lh2_CoreInstanceDesc::triangles of instance 0 */
 		if (w8Avail) s.w8Base0 = meshBlockBase[instances[0].mesh], s.w8Root = s.w8Base0 * 8;
 	}
 	s.instDesc = dInstDesc[tlasSlot].ptr, s.materials = dMaterials.ptr;
@@ -1676,10 +1677,22 @@ void RenderCore::SceneInfo( int* nodeCount, int* triCount, int* maxDepth, int* i
 	if (instCount) *instCount = (int)instances.size();
 }
 
+#ifdef LH2_SHADE_TIMES
+extern "C" void lh2_shade_times( unsigned long long out[16] );
+#endif
 void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 {
 	if (!initialized) return;
 	(void)hipStreamSynchronize( stream );
+#ifdef LH2_SHADE_TIMES
+	{
+		unsigned long long t[16];
+		lh2_shade_times( t );
+		fprintf( stderr, "LH2_SHADE_TIMES [" );
+		for (int i = 0; i < 16; i++) fprintf( stderr, "%s%llu", i ? ", " : "", t[i] );
+		fprintf( stderr, "]\n" );
+	}
+#endif
 	if (aheadStream) (void)hipStreamSynchronize( aheadStream );   /* a TLAS update nothing waited for */
 	for (auto* m : meshes) delete m;
 	meshes.clear();
