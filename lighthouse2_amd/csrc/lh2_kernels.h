@@ -179,7 +179,6 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
    reset by k_init_counters on the core stream (the launch itself may run beside the previous frame's tail) */
 void lh2_launch_trace_primary( const SceneDev* s, const TraceArgs* a, const CameraParams* cp, float4* T4, float4* Q4, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st );
-void lh2_launch_trace_any_packet( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st );
 int lh2_trace_blocks_per_cu( int waves );
 int lh2_packet_blocks_per_cu( void );
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );

@@ -605,8 +605,6 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 #define LH2_PACKET_MINWAVES 8
 #endif
 __global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet<false>( s, a ); }
-/* coherent shadow rays (the first bounce's): any hit + finalizeConnections in packets (RenderCore setting "shadowPackets") */
-__global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_any_packet( const SceneDev s, const TraceArgs a ) { trace_packet<false, true>( s, a ); }
 #ifndef LH2_PRIMARY_MINWAVES
 #define LH2_PRIMARY_MINWAVES 7
 #endif
@@ -2155,10 +2153,6 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
 	else if (a->version == 7 && s->nodes4) launch_closest4d<false>( s, a, grid, ev, st );
 	else if (a->leafBatch) LH2_LAUNCH( k_trace_closest<true>, grid, 256, st, ev, *s, *a );
 	else LH2_LAUNCH( k_trace_closest<false>, grid, 256, st, ev, *s, *a );
-}
-void lh2_launch_trace_any_packet( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st )
-{
-	LH2_LAUNCH( k_trace_any_packet, grid, 256, st, ev, *s, *a );
 }
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st )
 {

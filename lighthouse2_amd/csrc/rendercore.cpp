@@ -138,7 +138,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipEventCreate( &ps.evShadow ) );
 	CHK_HIP( hipEventCreate( &ps.evSide ) );
 	CHK_HIP( hipEventCreateWithFlags( &ps.evEarlyEnd, hipEventDisableTiming ) );
-	ps.shSnap.resize( 4 * LH2_SEGS * LH2_SEGCOUNT_STRIDE );   /* per frame parity: before the tail, after the first bounce */
+	ps.shSnap.resize( 2 * LH2_SEGS * LH2_SEGCOUNT_STRIDE );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
 	for (auto& e : evFrame) CHK_HIP( hipEventCreate( &e ) );
@@ -266,7 +266,6 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "frameOverlap" )) frameOverlap = (int)value;
 	else if (!strcmp( name, "earlyShade" )) earlyShade = value != 0;
 	else if (!strcmp( name, "sideBlocks" )) sideBlocks = std::min( 8, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "shadowPackets" )) shadowPackets = value != 0;
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "shadeBlocks" )) shadeBlocks = std::min( 64, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "finalShadowBlocks" )) finalShadowBlocks = std::min( 8, std::max( 0, (int)value ) );
@@ -303,7 +302,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "bvh4Collapse", (float)bvh4Collapse }, { "bvh4", (float)bvh4 }, { "gpuBuild", (float)gpuBuild }, { "buildThreads", (float)buildThreads }, { "gpuTlas", (float)gpuTlas },
 		{ "chordSplit", chordSplit }, { "packetHeavy", packetHeavy }, { "pathTail", (float)pathTail }, { "pathTailBatch", (float)pathTailBatch },
 		{ "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade },
-		{ "sideBlocks", (float)sideBlocks }, { "shadowPackets", (float)shadowPackets }, { "pathTailBlocks", (float)pathTailBlocks }, { "shadeBlocks", (float)shadeBlocks }, { "finalShadowBlocks", (float)finalShadowBlocks },
+		{ "sideBlocks", (float)sideBlocks }, { "pathTailBlocks", (float)pathTailBlocks }, { "shadeBlocks", (float)shadeBlocks }, { "finalShadowBlocks", (float)finalShadowBlocks },
 		{ "pathTailWaves", (float)pathTailWaves }, { "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
 		{ "terminalShade", (float)terminalShade }, { "traceBlocksPerCU", (float)blocksPerCU }, { "unitTraceWaves", (float)unitTraceWaves }, { "traceWaves", (float)traceWaves },
 		{ "unitCoherent", (float)unitCoherent }, { "traceVersion", (float)TraceVersion() }, { "traceWide", (float)traceWide }, { "w8Avail", (float)w8Avail },
@@ -959,7 +958,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	float4* const shP = ps.shP.ptr + (size_t)ps.fp * ps.shCap;
 	uint32_t* const shMask = ps.shMask.ptr + (size_t)ps.fp * ps.shMaskWords;
 	uint32_t* const shSnap = ps.shSnap.ptr + (size_t)ps.fp * LH2_SEGS * LH2_SEGCOUNT_STRIDE;   /* the rays queued before the tail */
-	uint32_t* const shSnap1 = ps.shSnap.ptr + (size_t)(2 + ps.fp) * LH2_SEGS * LH2_SEGCOUNT_STRIDE;   /* ... by the first bounce */
 	float4* const frameDelta = delta.ptr + (size_t)ps.fp * scrwidth * scrheight;
 	/* primary rays (camera.h) for every sample of the tile; the camera launch also resets the frame's
 	   counters and work-queue heads (k_init_counters) */
@@ -1073,7 +1071,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	frameShadows = shadows;
 	/* shadow overlap: the shade launch before the tail snapshots the queued shadow rays (advance_bounce) */
 	const bool overlap = shadows && tailL && shadowOverlap;
-	bool snapped = false, snapped1 = false;
+	bool snapped = false;
 	bool besideNext = false;   /* the next frame's primary launch may run beside the launches from here on */
 	ps.sideOn = false;
 	/* the bounce loop */
@@ -1139,17 +1137,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				/* the shadow rays of the bounces before the tail, beside it on the side stream (segment counts:
 				   the snapshot; the final launch's work-queue heads start behind them) */
 				CHK_HIP( hipStreamWaitEvent( sideStream, ps.prevStop, 0 ) );
-				if (snapped1)
-				{
-					/* shadowPackets: the first bounce's shadow rays in packets, [0, shSnap1) of every segment; the per-ray
-					   launch's work-queue heads start behind them (advance_bounce after the first shade launch) */
-					TraceArgs tp{};
-					tp.version = TraceVersion();
-					tp.rayO = shO, tp.rayD = shD, tp.segCounts = shSnap1, tp.segStride = ps.shadowStride;
-					tp.cursor = cursors + (size_t)(LH2_SHADOW_SLOT + 2) * LH2_CURSOR_WORDS;
-					tp.mask = shMask, tp.potentials = shP, tp.acc = accumulator.ptr, tp.gstack = ps.sideStack.ptr;
-					lh2_launch_trace_any_packet( &sd, &tp, smCount * std::min( sideBlocks > 0 ? sideBlocks : maxBlocksPerCU, packetBlocksPerCU ), {}, sideStream );
-				}
 				TraceArgs ts{};
 				ts.version = TraceVersion();
 				ts.wide = frameWide ? 1u : 0u;
@@ -1196,13 +1183,9 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		/* the hand-off to the next bounce: the shade launch's last block (no launch of its own), except
 		   in PrimeRef mode, where the bounce's shadow rays are traced (and their counts reset) first */
 		const bool snap = overlap && pathLength + 1 == tailL;
-		/* shadowPackets: the first bounce's shadow rays are counted apart (the side launch's packets), and the side
-		   launch's per-ray heads start behind them */
-		const bool snap1 = overlap && shadowPackets && tailL >= 3 && pathLength == 1 && !primeRef && UsePackets();
 		const BounceAdvance adv{ segNext, segNextBack, segIn, segInBack, rayLog, ps.activeLog, pathLength + 1 == tailL,
-			snap ? shSnap : snap1 ? shSnap1 : nullptr,
-			snap ? cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : snap1 ? cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS : nullptr };
-		snapped = snapped || snap, snapped1 = snapped1 || snap1;
+			snap ? shSnap : nullptr, snap ? cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS : nullptr };
+		snapped = snapped || snap;
 		sp.advance = pathLength < maxPL && !primeRef;
 		sp.adv = adv;
 		sp.rayO = ps.rayO[ps.in].ptr, sp.rayD = ps.rayD[ps.in].ptr, sp.T4 = ps.T4[ps.in].ptr, sp.Q4 = ps.Q4[ps.in].ptr, sp.hits = ps.hits.ptr;

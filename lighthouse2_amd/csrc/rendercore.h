@@ -367,9 +367,6 @@ private:
 	/* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's): 4 leaves the next frame's primary
 	   and early shade launches room: config 3 -0.5 %, the N = 8 share -0.8 to -1.5 % (profiles/r04m_ab.txt, r04n_ab.txt) */
 	int sideBlocks = 4;
-	/* the side launch's first-bounce shadow rays (leaving from neighbouring primary hits toward the lights) in packets
-	   (k_trace_any_packet), the later bounces' per ray behind them; needs the side launch and pathTail >= 3 */
-	bool shadowPackets = false;
 	/* heavy-first primary packets (TraceArgs::hvRead): the packets of the previous frame that took more than
 	   packetHeavy x its mean node steps are taken first; 0: off */
 	float packetHeavy = 2.0f;

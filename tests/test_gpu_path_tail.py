@@ -171,40 +171,6 @@ def test_shadow_overlap(fresh_core, blocks, tail, side, final):
     assert rel_l2(ag[..., :3], res[0][0][..., :3]) <= 1e-6
 
 
-@pytest.mark.parametrize("kind,tail,side,spp", [("room", 3, 4, 1), ("room", 4, 0, 1), ("room", 3, 4, 3), ("instanced", 3, 4, 1)])
-def test_shadow_packets(fresh_core, kind, tail, side, spp):
-    """shadowPackets: the side launch traces the first bounce's shadow rays ([0, the count after the first shade launch) of
-    every segment) in packets (k_trace_any_packet: any hit + finalizeConnections, one traversal per 64 rays) and the later
-    bounces' per ray behind them (the per-ray launch's work-queue heads start at that count).  Every shadow ray is traced
-    once and any hit is order-free: the oracle's ray counts, the frames within rel-L2 1e-4 of it and within float summation
-    order of the same frames without packets; several instances (the packets' TLAS walk) and several samples per pixel."""
-    w, h = 128, 72
-    sc = _scene(kind, w, h)
-    if kind == "instanced":
-        sc.area_lights = scene.room_scene(2000, w, h).area_lights
-    o = _load_both(fresh_core, sc, w, h, spp=spp)
-    for tgt in (fresh_core, o):
-        tgt.setting("maxPathLength", 4)
-    fresh_core.setting("pathTail", tail)
-    fresh_core.setting("sideBlocks", side)
-    assert fresh_core.get_setting("usePackets") == 1
-    res = {}
-    for sp in (1, 0):
-        fresh_core.setting("shadowPackets", sp)
-        assert fresh_core.get_setting("shadowPackets") == sp
-        for f in range(3):
-            sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
-            if sp:
-                sc.render_frame(o, converge=1 if f == 0 else 0)
-                assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), f
-        res[sp] = (fresh_core.accumulator(), fresh_core.stats())
-    ag, st = res[1]
-    co = o.ray_counts()
-    assert co[16] > 0 and st.totalShadowRays == co[16], (st.totalShadowRays, co[16])
-    assert rel_l2(ag[..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
-    assert rel_l2(ag[..., :3], res[0][0][..., :3]) <= 1e-6
-
-
 @pytest.mark.parametrize("blocks", [1, 8, 40, 64])
 def test_shade_grid(fresh_core, blocks):
     """The shade launches' grid (shadeBlocks per CU; 0, the default: about 1.3 paths per thread, between the trace grid
