@@ -189,7 +189,6 @@ void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int ba
 void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
 /* the rows of a band partition (k_pack_rows' mapping); rows 0: every pixel */
 struct RowMap { int w, y0, band, bandStride, rows; };
-void lh2_launch_connect( const Counters* c, const uint32_t* mask, const float4* pot, float4* acc, uint32_t stride, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_finalize( float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st,
 	const RowMap* rm = nullptr );
 }

@@ -1983,23 +1983,6 @@ __global__ void k_counters_next( Counters* c, const BounceAdvance a, int pathLen
 }
 /* rm.rows > 0: only the rows a tile owns (a rank's bands, the k_pack_rows mapping): the other rows are
    other ranks' and are finalized where the frame is gathered */
-/* finalizeConnections (rendercore.cpp:575-592, finalize_shared.h) as a pass of its own: the shadow launches record the occluded
-   rays' bits (k_trace_any4d<0>: fire-and-forget atomics) and this adds every unoccluded ray's potential.  Fused into the
-   trace launch, a finishing ray's potential load stalls its whole wave for a round trip (RenderCore setting shadowConnect) */
-__global__ __launch_bounds__( 256 ) void k_connect( const Counters* __restrict__ c, const uint32_t* __restrict__ mask, const float4* __restrict__ pot,
-	float4* __restrict__ acc, const uint32_t stride )
-{
-	const uint32_t seg = blockIdx.x % LH2_SEGS;
-	const uint32_t n = min( c->segShadow[seg * LH2_SEGCOUNT_STRIDE], stride );
-	const uint32_t step = (gridDim.x / LH2_SEGS) * 256u;
-	for (uint32_t j = (blockIdx.x / LH2_SEGS) * 256u + threadIdx.x; j < n; j += step)
-	{
-		const uint32_t idx = seg * stride + j;
-		if ((mask[idx >> 5] >> (idx & 31u)) & 1u) continue;
-		const float4 E = pot[idx];
-		acc_add( acc, __float_as_uint( E.w ), mk3( E.x, E.y, E.z ) );
-	}
-}
 __global__ void k_finalize( float4* __restrict__ acc, float4* __restrict__ out, const int n, const float scale, const FrameStatsDev fs,
 	const RowMap rm )
 {
@@ -2253,11 +2236,6 @@ void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int 
 void lh2_shade_times( unsigned long long out[16] ) { (void)hipMemcpyFromSymbol( out, HIP_SYMBOL( lh2_shade_tt ), 16 * 8 ); }
 #endif
 void lh2_launch_spin( unsigned long long ticks, hipStream_t st ) { hipLaunchKernelGGL( k_spin, dim3( 1 ), dim3( 64 ), 0, st, ticks ); }
-void lh2_launch_connect( const Counters* c, const uint32_t* mask, const float4* pot, float4* acc, uint32_t stride, int grid, LaunchEvents ev, hipStream_t st )
-{
-	grid = std::max( LH2_SEGS, grid / LH2_SEGS * LH2_SEGS );
-	LH2_LAUNCH( k_connect, grid, 256, st, ev, c, mask, pot, acc, stride );
-}
 void lh2_launch_finalize( float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st, const RowMap* rm )
 {
 	const FrameStatsDev none{};

@@ -221,7 +221,6 @@ void RenderCore::EnsurePaths( uint32_t paths )
 		ps.shCap = 2 * ps.cap, ps.shMaskWords = (ps.shCap + 63) / 32 + 2;
 		ps.shO.resize( 2 * ps.shCap ), ps.shD.resize( 2 * ps.shCap ), ps.shP.resize( 2 * ps.shCap );
 		ps.shMask.resize( 2 * ps.shMaskWords );
-		CHK_HIP( hipMemsetAsync( ps.shMask.ptr, 0, sizeof( uint32_t ) * 2 * ps.shMaskWords, stream ) );   /* k_connect re-zeroes after use */
 	}
 	EnsureStack();
 }
@@ -267,7 +266,6 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "frameOverlap" )) frameOverlap = (int)value;
 	else if (!strcmp( name, "earlyShade" )) earlyShade = value != 0;
 	else if (!strcmp( name, "sideBlocks" )) sideBlocks = std::min( 8, std::max( 0, (int)value ) );
-	else if (!strcmp( name, "shadowConnect" )) shadowConnect = value != 0;
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "shadeBlocks" )) shadeBlocks = std::min( 64, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "finalShadowBlocks" )) finalShadowBlocks = std::min( 8, std::max( 0, (int)value ) );
@@ -1147,7 +1145,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)kShadowLeafBatch;
 				ts.mask = shMask, ts.potentials = shP, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
 				/* the global stack (sideStack) is sized for maxBlocksPerCU blocks per CU: the grid stays within it */
-				lh2_launch_trace_any( &sd, &ts, sideBlocks > 0 ? smCount * std::min( sideBlocks, maxBlocksPerCU ) : grid, shadowConnect ? 0 : 1, { nullptr, ps.evSide }, sideStream );
+				lh2_launch_trace_any( &sd, &ts, sideBlocks > 0 ? smCount * std::min( sideBlocks, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evSide }, sideStream );
 				ps.fromSide = ps.prevStop;
 				ps.sideOn = true;
 			}
@@ -1274,18 +1272,11 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)kShadowLeafBatch;
 		ta.mask = shMask, ta.potentials = shP, ta.acc = accumulator.ptr, ta.gstack = ps.gstack.ptr;
 		/* the global stack (gstack) is sized for maxBlocksPerCU blocks per CU: the grid stays within it */
-		lh2_launch_trace_any( &sd, &ta, finalShadowBlocks > 0 ? smCount * std::min( finalShadowBlocks, maxBlocksPerCU ) : grid, shadowConnect ? 0 : 1, { nullptr, ps.evShadow }, stream );
+		lh2_launch_trace_any( &sd, &ta, finalShadowBlocks > 0 ? smCount * std::min( finalShadowBlocks, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evShadow }, stream );
 		ps.fromShadow = ps.prevStop;
 	}
 	/* the side launch's contributions are in the accumulator before the frame is finalized */
 	if (ps.sideOn) CHK_HIP( hipStreamWaitEvent( stream, ps.evSide, 0 ) );
-	if (!primeRef && shadows && shadowConnect)
-	{
-		/* the unoccluded shadow rays' contributions (every segment's rays, [0, segShadow)), then the bits cleared for this
-		   frame parity's next use */
-		lh2_launch_connect( c, shMask, shP, accumulator.ptr, ps.shadowStride, smCount * 4, {}, stream );
-		CHK_HIP( hipMemsetAsync( shMask, 0, sizeof( uint32_t ) * ps.shMaskWords, stream ) );
-	}
 	samplesTaken += scrspp;
 	/* finalize also delivers the frame's counters and ray-count log, and the scene error, to hostStats */
 	const FrameStatsDev fs{ c, rayLog + 1, &hostStats->counters, hostStats->rayCount + 1, SceneErr( frameTlas ), &hostStats->sceneError,

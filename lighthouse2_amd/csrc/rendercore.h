@@ -331,12 +331,11 @@ private:
 	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,
 	   r02y_ab_v7.txt); leafBatch 8 with the quantized nodes (bounce 0.492 -> 0.488 ms, N = 8 share 1.35 -> 1.32 ms,
 	   r03k_ab_leafbatch.txt) */
-	int refillOther = 48, leafBatch = 8;
+	int refillOther = 48, leafBatch = 8;   /* primary rays traced per ray (no packets) take the same (profiles/r04ag_refill_sweep.txt) */
 	/* the shadow launches park BLAS leaves until 16 lanes hold one (the closest-hit launches: leafBatch): config 3 -0.4 %, the
 	   4K frame -0.9 %, the N = 8 share -0.3 % against 8; 2 and 4 slower, 24 no better; their refill stays refillOther (32 and
 	   60 slower) (profiles/r05f_ab_lazy_frame_shadow_sweep.txt, r05f_ab_shadow_leafbatch.txt) */
 	static constexpr int kShadowLeafBatch = 16;
-	bool shadowConnect = false;                  /* occlusion bits + a connections pass (k_connect) instead of the fused add; A/B */   /* primary rays traced per ray (no packets) take the same (profiles/r04ag_refill_sweep.txt) */
 	int bvhMaxLeaf = 1;
 	/* spatial splits (SBVH): overlap threshold x root area; 0 = off.  1e-3 (round 4; 1e-5 before): the same node steps and
 	   triangle tests per ray (tools/bvh_quality.cpp: config 2 26.62 / 6.78 vs 26.64 / 6.68, the room 14.58 / 1.83 both)

@@ -171,34 +171,6 @@ def test_shadow_overlap(fresh_core, blocks, tail, side, final):
     assert rel_l2(ag[..., :3], res[0][0][..., :3]) <= 1e-6
 
 
-@pytest.mark.parametrize("tail,overlap,spp", [(3, 1, 1), (2, 1, 2), (3, 0, 1), (0, 0, 1)])
-def test_shadow_connect(fresh_core, tail, overlap, spp):
-    """shadowConnect: the shadow launches record occlusion bits (fire-and-forget atomics) and a connections pass (k_connect)
-    adds the unoccluded rays' contributions, instead of the add fused into the trace launch.  With and without the side
-    launch and the path tail: the oracle's ray counts, three converging frames within rel-L2 1e-4 of it and within float
-    summation order of the fused frames (so every mask bit was cleared for the frame parity's next use)."""
-    w, h = 128, 72
-    sc = _scene("room", w, h)
-    o = _load_both(fresh_core, sc, w, h, spp=spp)
-    for tgt in (fresh_core, o):
-        tgt.setting("maxPathLength", 4)
-    fresh_core.setting("pathTail", tail)
-    fresh_core.setting("shadowOverlap", overlap)
-    res = {}
-    for sc_on in (1, 0):
-        fresh_core.setting("shadowConnect", sc_on)
-        for f in range(3):
-            sc.render_frame(fresh_core, converge=1 if f == 0 else 0)
-            if sc_on:
-                sc.render_frame(o, converge=1 if f == 0 else 0)
-                assert np.array_equal(fresh_core.ray_counts(), o.ray_counts()), f
-        res[sc_on] = fresh_core.accumulator()
-    co = o.ray_counts()
-    assert co[16] > 0
-    assert rel_l2(res[1][..., :3], o.accumulator()[..., :3]) <= REL_L2_TOL
-    assert rel_l2(res[1][..., :3], res[0][..., :3]) <= 1e-6
-
-
 @pytest.mark.parametrize("blocks", [1, 8, 40, 64])
 def test_shade_grid(fresh_core, blocks):
     """The shade launches' grid (shadeBlocks per CU; 0, the default: about 1.3 paths per thread, between the trace grid
