@@ -751,14 +751,21 @@ LH2_DEV float normal_scale( const uint32_t byte, const bool absArg )   /* materi
    go out early (shade_path: beside the instance record's for a single instance) */
 struct TriShade { float4 t1, t2, t3, t4, t5, t7; };
 LH2_DEV TriShade tri_shade_load( const float4* __restrict__ tri ) { return { tri[1], tri[2], tri[3], tri[4], tri[5], tri[7] }; }
+/* the hit material's record (CUDAMaterial, 128 B) and its first two quads, read first; the caller may load them early */
+struct MatShade { const uint4* mat; uint4 m0, m1; };
+LH2_DEV MatShade mat_shade_load( const SceneDev& s, const TriShade& tq )
+{
+	const uint4* mat = s.materials + (size_t)__float_as_int( tq.t1.w ) * 8;
+	return { mat, mat[0], mat[1] };
+}
 LH2_DEV void GetShadingData( const SceneDev& s, const v3 D, const float u, const float v, const float coneWidth, const float4* __restrict__ tri,
-	const TriShade& tq, const v3 A, const v3 B, const v3 C, ShadingData& sd, v3& N, v3& iN, v3& fN, v3& T )
+	const TriShade& tq, const MatShade& mq, const v3 A, const v3 B, const v3 C, ShadingData& sd, v3& N, v3& iN, v3& fN, v3& T )
 {
 
 	const float4 tdata1 = tq.t1, tdata2 = tq.t2, tdata3 = tq.t3, tdata4 = tq.t4, tdata5 = tq.t5, alpha4 = tq.t7;
-	const uint4* mat = s.materials + (size_t)__float_as_int( tdata1.w ) * 8;
-	const uint4 baseData = mat[0];
-	sd.params = mat[1];
+	const uint4* mat = mq.mat;
+	const uint4 baseData = mq.m0;
+	sd.params = mq.m1;
 	sd.color = mk3( h2f( baseData.x & 0xffff ), h2f( baseData.x >> 16 ), h2f( baseData.y & 0xffff ) );
 	sd.flags = 0;
 	sd.transmittance = mk3( h2f( baseData.y >> 16 ), h2f( baseData.z & 0xffff ), h2f( baseData.z >> 16 ) );
@@ -1481,8 +1488,16 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 	/* SINGLE: the triangle's records with them (a miss reads the blue-noise table instead: always there, and large
 	   enough); else after the instance record, in GetShadingData */
 	TriShade tq;
+	MatShade mq;
 	if (SINGLE) tq = tri_shade_load( PRIMIDX == NOHIT ? (const float4*)s.blueNoise : tri );
 	__builtin_amdgcn_sched_barrier( 0 );
+	/* SINGLE: the material's loads go out with the blue-noise sample bytes (both wait for the previous step's loads), not
+	   after them (a miss reads the blue-noise table again) */
+	if (SINGLE)
+	{
+		mq.mat = PRIMIDX == NOHIT ? (const uint4*)s.blueNoise : s.materials + (size_t)__float_as_int( tq.t1.w ) * 8;
+		mq.m0 = mq.mat[0], mq.m1 = mq.mat[1];
+	}
 	float bnv[4];
 	blueNoiseFinish4( s.blueNoise, bnq, bnv );
 	LH2_STT( 0 )
@@ -1501,8 +1516,8 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 		ShadingData sd;
 		v3 N, iN, fN, T;
 		const v3 I = add3( RAY_O, smul( HIT_T, D ) );
-		if (!SINGLE) tq = tri_shade_load( tri );
-		GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, tq, instA, instB, instC, sd, N, iN, fN, T );
+		if (!SINGLE) tq = tri_shade_load( tri ), mq = mat_shade_load( s, tq );
+		GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, tq, mq, instA, instB, instC, sd, N, iN, fN, T );
 		LH2_STT( 1 )
 		if (sd.flags & 1)
 		{
@@ -1856,7 +1871,8 @@ __global__ __launch_bounds__( 256, LH2_SHADE_MINWAVES ) void k_shade_ref( const 
 				ShadingData sd;
 				v3 N, iN, fN, T;
 				const v3 I = add3( RAY_O, smul( HIT_T, D ) );
-				GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, tri_shade_load( tri ), instA, instB, instC, sd, N, iN, fN, T );
+				const TriShade tq = tri_shade_load( tri );
+				GetShadingData( s, D, HIT_U, HIT_V, p.spreadAngle * HIT_T, tri, tq, mat_shade_load( s, tq ), instA, instB, instC, sd, N, iN, fN, T );
 				if (sd.color.x > 1.0f || sd.color.y > 1.0f || sd.color.z > 1.0f)
 				{
 					if (-dot3( D, N ) > 0 && (p.pathLength == 1 || (data & S_SPECULAR))) acc_add( p.acc, pixelIdx, mul3( throughput, sd.color ) );

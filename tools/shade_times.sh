@@ -12,3 +12,10 @@ LH2_CORE_LIB="$ROOT/gpuab/stt/libRenderCore_MI355X.so" timeout -k 10 300 python3
   > "$OUT/config3.json" 2> "$OUT/config3.err"
 grep LH2_SHADE_TIMES "$OUT/config3.err" | tail -1 > "$OUT/times.txt"
 python3 tools/shade_times.py "$OUT/times.txt" | tee "$OUT/summary.txt"
+if [ -n "${C2:-}" ]; then
+  # config 2 (no lights: k_shade<false, true>): the bench line's frames alone
+  LH2_CORE_LIB="$ROOT/gpuab/stt/libRenderCore_MI355X.so" timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-configs --no-config4 \
+    --steps 20 > "$OUT/config2.json" 2> "$OUT/config2.err"
+  grep LH2_SHADE_TIMES "$OUT/config2.err" | tail -1 > "$OUT/times_c2.txt"
+  echo "config 2:"; python3 tools/shade_times.py "$OUT/times_c2.txt" | tee "$OUT/summary_c2.txt"
+fi
