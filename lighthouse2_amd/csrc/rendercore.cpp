@@ -1029,8 +1029,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		else
 		{
 			CHK_HIP( hipStreamWaitEvent( aheadStream, ps.overlapEv, 0 ) );
-			lh2_launch_init_counters( c, pathCount, ps.segStride, cursors, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, {}, aheadStream, -LH2_CURSOR_WORDS );
-			cp.initC = nullptr;
+			if (kPrimaryResets) cp.initC = c;   /* the primary launch resets them itself: no launch (and its gap) before it */
+			else
+			{
+				lh2_launch_init_counters( c, pathCount, ps.segStride, cursors, LH2_CURSOR_SLOTS * LH2_CURSOR_WORDS, {}, aheadStream, -LH2_CURSOR_WORDS );
+				cp.initC = nullptr;
+			}
 		}
 		if (ps.hvOn && !ps.hvNextZeroed) CHK_HIP( hipMemsetAsync( cp.hvZero, 0, sizeof( uint32_t ) * cp.hvZeroWords, primStream ) );
 		cp.hvZero = nullptr, cp.hvZeroWords = 0;

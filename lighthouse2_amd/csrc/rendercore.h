@@ -336,6 +336,12 @@ private:
 	   4K frame -0.9 %, the N = 8 share -0.3 % against 8; 2 and 4 slower, 24 no better; their refill stays refillOther (32 and
 	   60 slower) (profiles/r05f_ab_lazy_frame_shadow_sweep.txt, r05f_ab_shadow_leafbatch.txt) */
 	static constexpr int kShadowLeafBatch = 16;
+#ifndef LH2_PRIMARY_RESETS
+#define LH2_PRIMARY_RESETS 1
+#endif
+	/* an overlapped frame's counter and work-queue resets done by its primary launch (as behind the previous frame), not by
+	   a k_init_counters launch before it on the ahead stream */
+	static constexpr bool kPrimaryResets = LH2_PRIMARY_RESETS != 0;
 	int bvhMaxLeaf = 1;
 	/* spatial splits (SBVH): overlap threshold x root area; 0 = off.  1e-3 (round 4; 1e-5 before): the same node steps and
 	   triangle tests per ray (tools/bvh_quality.cpp: config 2 26.62 / 6.78 vs 26.64 / 6.68, the room 14.58 / 1.83 both)
