@@ -29,7 +29,8 @@ for r in $(seq 1 "$R"); do
   for lib in new "$@"; do
     uselib "$lib"
     n="${lib}_$r"
-    timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-config5 --no-config4 > "$OUT/bench_$n.json" 2> "$OUT/bench_$n.log"
+    # C5=1: config 5 too (the instanced loops; ~10 s more per bench)
+    timeout -k 10 300 python3 bench.py --no-cpu-baseline $([ -n "${C5:-}" ] || echo --no-config5) --no-config4 > "$OUT/bench_$n.json" 2> "$OUT/bench_$n.log"
     timeout -k 10 200 python3 tools/config4_shares.py --ranks 1,8 > "$OUT/shares_$n.jsonl" 2> "$OUT/shares_$n.err"
     python3 - "$OUT/bench_$n.json" "$OUT/shares_$n.jsonl" "$n" <<'PY'
 import json, sys
@@ -37,7 +38,7 @@ d = json.load(open(sys.argv[1]))
 sh = [json.loads(l) for l in open(sys.argv[2]) if l.strip()]
 g = lambda k: (d.get(k) or {}).get("ms_per_frame")
 c3 = d["config3"]["coreStats_ms"]
-print(sys.argv[3], "c2", d["value"], d["ms_per_step"], "| c2r", g("config2_restart"), "| c3", g("config3"), c3, "| shares", [s["ms_per_frame"] for s in sh],
+print(sys.argv[3], "c2", d["value"], d["ms_per_step"], "| c2r", g("config2_restart"), "| c3", g("config3"), c3, "| c5", g("config5"), "| shares", [s["ms_per_frame"] for s in sh],
       "ratio", round(sh[0]["ms_per_frame"] / sh[-1]["ms_per_frame"], 3), flush=True)
 PY
   done
