@@ -370,9 +370,11 @@ private:
 	                                        kSmallFramePaths paths, else 2 (without: its occupancy limit) */
 	/* the path tail kernel's variant: 0, by frame size (3 waves per SIMD for small frames, 4 for larger ones); 3 or 4 */
 	int pathTailWaves = 0;
-	/* blocks per CU of the frame's last shadow launch (0: the trace grid's): 6 leaves the next frame's primary and early
-	   shade launches room beside it: config 3 and the N = 8 share -0.5 % (profiles/r04aj_ab.txt, r04ak_ab.txt) */
-	int finalShadowBlocks = 6;
+	/* blocks per CU of the frame's last shadow launch (0: the trace grid's): fewer leave the next frame's primary and early
+	   shade launches room beside it: 6 against the trace grid's 8, config 3 and the N = 8 share -0.5 % (profiles/r04aj_ab.txt,
+	   r04ak_ab.txt); round 5, with the shorter shade launches, 4 against 6: the N = 8 share -0.9 %, config 3 -0.3 %, 8 slower
+	   (r05f_ab_final_shadow_blocks.txt) */
+	int finalShadowBlocks = 4;
 	int shadeBlocks = 0;                 /* blocks per CU of the frame's shade launches (0: by path count, Render) */
 	/* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's): 4 leaves the next frame's primary
 	   and early shade launches room: config 3 -0.5 %, the N = 8 share -0.8 to -1.5 % (profiles/r04m_ab.txt, r04n_ab.txt) */

@@ -143,7 +143,7 @@ def test_shadow_overlap(fresh_core, blocks, tail, side, final):
     """shadowOverlap: the shadow rays queued before the path tail are traced on the side stream beside it
     (their segment counts snapshotted by the shade launch before the tail; the path tail at 2 or 3 blocks per CU
     by frame size, or pathTailBlocks; the side launch at sideBlocks per CU, 0: the trace grid's), and the final shadow
-    launch (finalShadowBlocks per CU, 6 by default, 0: the trace grid's) starts behind them.
+    launch (finalShadowBlocks per CU, 4 by default, 0: the trace grid's) starts behind them.
     Every shadow ray is traced once: the same ray counts and occlusion as the oracle, three converging frames within
     rel-L2 1e-4 of it, and within float summation order of the frames traced with the overlap off."""
     w, h = 128, 72
