@@ -336,6 +336,10 @@ private:
 	   4K frame -0.9 %, the N = 8 share -0.3 % against 8; 2 and 4 slower, 24 no better; their refill stays refillOther (32 and
 	   60 slower) (profiles/r05f_ab_lazy_frame_shadow_sweep.txt, r05f_ab_shadow_leafbatch.txt) */
 	static constexpr int kShadowLeafBatch = 16;
+	/* a bounce launch beside the next frame's primary launch (config 2's frames) refills its waves once 40 lanes are idle
+	   (refillOther 48 elsewhere): config 2 +1.2 % with 40 for every launch, which slowed config 3 and the N = 8 share
+	   (profiles/r05f_ab_refill.txt) */
+	static constexpr int kBesideRefill = 40;
 #ifndef LH2_PRIMARY_RESETS
 #define LH2_PRIMARY_RESETS 1
 #endif
