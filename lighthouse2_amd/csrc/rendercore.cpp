@@ -1172,7 +1172,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			const bool beside = besideNext && !ta.packet;
 			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, kOverlapTraceBlocks ) : grid;
 			ta.traceWaves = beside ? 7u : (uint32_t)traceWaves;   /* 8 waves slow the packets beside the launch (r04ad) */
-			if (beside) ta.refill = (uint32_t)kBesideRefill;
 			lh2_launch_trace_closest( &sd, &ta, g, { nullptr, ps.evTrace[pathLength] }, stream );
 		}
 		ps.fromTrace[pathLength] = ps.prevStop, ps.prevStop = ps.evTrace[pathLength];

@@ -331,15 +331,12 @@ private:
 	   lanes hold one (lh2_trace4d.inc).  Primary rays: coherent 8x8-tiled batches (profiles/r01c_sweep_bvh4.jsonl,
 	   r02y_ab_v7.txt); leafBatch 8 with the quantized nodes (bounce 0.492 -> 0.488 ms, N = 8 share 1.35 -> 1.32 ms,
 	   r03k_ab_leafbatch.txt) */
-	int refillOther = 48, leafBatch = 8;   /* primary rays traced per ray (no packets) take the same (profiles/r04ag_refill_sweep.txt) */
+	int refillOther = 48, leafBatch = 8;   /* primary rays traced per ray (no packets) take the same (profiles/r04ag_refill_sweep.txt;
+	                                          round 5: 32 / 40 / 56 no better, r05f_ab_refill.txt, r05f_ab_beside_refill.txt) */
 	/* the shadow launches park BLAS leaves until 16 lanes hold one (the closest-hit launches: leafBatch): config 3 -0.4 %, the
 	   4K frame -0.9 %, the N = 8 share -0.3 % against 8; 2 and 4 slower, 24 no better; their refill stays refillOther (32 and
 	   60 slower) (profiles/r05f_ab_lazy_frame_shadow_sweep.txt, r05f_ab_shadow_leafbatch.txt) */
 	static constexpr int kShadowLeafBatch = 16;
-	/* a bounce launch beside the next frame's primary launch (config 2's frames) refills its waves once 40 lanes are idle
-	   (refillOther 48 elsewhere): config 2 +1.2 % with 40 for every launch, which slowed config 3 and the N = 8 share
-	   (profiles/r05f_ab_refill.txt) */
-	static constexpr int kBesideRefill = 40;
 #ifndef LH2_PRIMARY_RESETS
 #define LH2_PRIMARY_RESETS 1
 #endif
