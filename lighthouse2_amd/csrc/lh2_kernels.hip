@@ -604,19 +604,13 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 #ifndef LH2_PACKET_MINWAVES
 #define LH2_PACKET_MINWAVES 8
 #endif
-/* QN: the packets over the quantized BVH4 (lh2_trace_packet.inc), when it is built; LH2_PACKET_QN 0: the BVH2 always */
-#ifndef LH2_PACKET_QN
-#define LH2_PACKET_QN 1
-#endif
-template <bool QN>
-__global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet<false, QN>( s, a ); }
+__global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_packet( const SceneDev s, const TraceArgs a ) { trace_packet<false>( s, a ); }
 #ifndef LH2_PRIMARY_MINWAVES
 #define LH2_PRIMARY_MINWAVES 7
 #endif
 /* the camera fused into the primary packet launch: each lane makes its path's primary ray (camera_path) and traces it;
    no camera launch, no ray round trip through HBM.  The frame's resets are k_init_counters' on the core stream (the
    launch's own work-queue heads alternate between two slots, so it may run beside the previous frame's tail) */
-template <bool QN>
 __global__ __launch_bounds__( 256, LH2_PRIMARY_MINWAVES ) void k_trace_primary_packet( const CameraParams cp, const SceneDev s,
 	const TraceArgs a, float4* T4, float4* Q4 )
 {
@@ -626,7 +620,7 @@ __global__ __launch_bounds__( 256, LH2_PRIMARY_MINWAVES ) void k_trace_primary_p
 		for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < (uint32_t)max( cp.cursorWords, LH2_SEGS ); i += gridDim.x * 256u)
 			init_counters( cp.initC, cp.pathCount, cp.segStride, cp.cursors, cp.cursorWords, (int)i, cp.keepCursor );
 	/* cp first: trace_packet<true> reloads it from the start of the kernel arguments for each packet */
-	trace_packet<true, QN>( s, a, T4, Q4 );
+	trace_packet<true>( s, a, T4, Q4 );
 }
 
 /* the reference BVH2 loop (traceVersion 1; the BVH4 is not built with setting "bvh4" 0) */
@@ -2165,15 +2159,13 @@ void lh2_launch_camera( const CameraParams* p, const uint8_t* bn, float4* rayO, 
 void lh2_launch_trace_primary( const SceneDev* s, const TraceArgs* a, const CameraParams* cp, float4* T4, float4* Q4, int grid, LaunchEvents ev, hipStream_t st )
 {
 	const CameraParams c = lh2_camera_derive( *cp );
-	if (LH2_PACKET_QN && LH2_QNODES && s->nodes4q) LH2_LAUNCH( k_trace_primary_packet<true>, grid, 256, st, ev, c, *s, *a, T4, Q4 );
-	else LH2_LAUNCH( k_trace_primary_packet<false>, grid, 256, st, ev, c, *s, *a, T4, Q4 );
+	LH2_LAUNCH( k_trace_primary_packet, grid, 256, st, ev, c, *s, *a, T4, Q4 );
 }
 void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st )
 {
 	/* coherent primary rays: packets over the BVH2 (lh2_trace_packet.inc); incoherent rays: the BVH4 loop
 	   (lh2_trace4d.inc), or the reference BVH2 loop (traceVersion 1, or no BVH4) */
-	if (a->packet && LH2_PACKET_QN && LH2_QNODES && s->nodes4q) LH2_LAUNCH( k_trace_closest_packet<true>, grid, 256, st, ev, *s, *a );
-	else if (a->packet) LH2_LAUNCH( k_trace_closest_packet<false>, grid, 256, st, ev, *s, *a );
+	if (a->packet) LH2_LAUNCH( k_trace_closest_packet, grid, 256, st, ev, *s, *a );
 	else if (a->version == 7 && a->wide && s->w8) launch_closest4d<true>( s, a, grid, ev, st );
 	else if (a->version == 7 && s->nodes4) launch_closest4d<false>( s, a, grid, ev, st );
 	else if (a->leafBatch) LH2_LAUNCH( k_trace_closest<true>, grid, 256, st, ev, *s, *a );
@@ -2189,7 +2181,7 @@ void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int 
 int lh2_packet_blocks_per_cu( void )
 {
 	int n = 0;
-	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_closest_packet<LH2_PACKET_QN != 0>, 256, 0 ) != hipSuccess) n = 4;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor( &n, k_trace_closest_packet, 256, 0 ) != hipSuccess) n = 4;
 	return n;
 }
 /* the per-ray traversal kernels' occupancy (persistent grid: CUs x blocks per CU) */
