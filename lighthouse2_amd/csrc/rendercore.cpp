@@ -118,7 +118,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	traceBlocksPerCU7 = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu( 7 ) ) );
 	traceBlocksPerCU8 = std::max( 1, std::min( 8, lh2_trace_blocks_per_cu( 8 ) ) );
 	maxBlocksPerCU = std::max( traceBlocksPerCU7, traceBlocksPerCU8 );
-	blocksPerCU = traceWaves == 8 ? traceBlocksPerCU8 : traceBlocksPerCU7;
+	blocksPerCU = traceWaves == 7 ? traceBlocksPerCU7 : traceBlocksPerCU8;
 	packetBlocksPerCU = std::max( 1, std::min( 8, lh2_packet_blocks_per_cu() ) );
 	pathBlocksPerCU = std::max( 1, std::min( 8, lh2_path_blocks_per_cu( 3 ) ) );
 	pathBlocksPerCU4 = std::max( 1, std::min( 8, lh2_path_blocks_per_cu( 4 ) ) );
@@ -276,13 +276,13 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "terminalShade" )) terminalShade = value != 0;   /* drop hits that cannot contribute before shading them (ShadeParams::terminal) */
 	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (default: occupancy limit) */
 	{
-		blocksPerCU = value > 0 ? std::min( maxBlocksPerCU, std::max( 1, (int)value ) ) : traceWaves == 8 ? traceBlocksPerCU8 : traceBlocksPerCU7;
+		blocksPerCU = value > 0 ? std::min( maxBlocksPerCU, std::max( 1, (int)value ) ) : traceWaves == 7 ? traceBlocksPerCU7 : traceBlocksPerCU8;
 	}
 	else if (!strcmp( name, "unitTraceWaves" )) unitTraceWaves = (int)value == 8 ? 8 : 7;   /* the same for the unit queries (TraceClosest*) */
-	else if (!strcmp( name, "traceWaves" ))   /* closest-hit kernel variant (7 or 8 waves per SIMD); resets traceBlocksPerCU */
+	else if (!strcmp( name, "traceWaves" ))   /* closest-hit kernel variant (7 or 8 waves per SIMD; 0: by scene); resets traceBlocksPerCU */
 	{
-		traceWaves = (int)value == 7 ? 7 : 8;
-		blocksPerCU = traceWaves == 8 ? traceBlocksPerCU8 : traceBlocksPerCU7;
+		traceWaves = (int)value == 7 ? 7 : (int)value == 8 ? 8 : 0;
+		blocksPerCU = traceWaves == 7 ? traceBlocksPerCU7 : traceBlocksPerCU8;
 	}
 	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice traces as the frame traces primary rays */
 	else if (!strcmp( name, "traceVersion" )) traceVersion = (int)value == 1 ? 1 : 0;   /* 1: the reference BVH2 loop; else the BVH4 loop */
@@ -1170,8 +1170,11 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			   probably does too): fewer blocks per CU, so the packets' latency-bound waves get slots from the start instead
 			   of the bounce launch's tail (config 2: 4262-4296 -> 4437-4442 Mrays/s at 5, r03q_ab_trace_blocks.txt) */
 			const bool beside = besideNext && !ta.packet;
-			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, kOverlapTraceBlocks ) : grid;
-			ta.traceWaves = beside ? 7u : (uint32_t)traceWaves;   /* 8 waves slow the packets beside the launch (r04ad) */
+			/* traceWaves 0: 7 waves for a single instance, 8 for instanced scenes (each on its own occupancy's grid) */
+			const int waves = traceWaves ? traceWaves : sd.tlasRoot4 < 0 ? 7 : 8;
+			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, kOverlapTraceBlocks ) :
+				!traceWaves && waves == 7 ? smCount * traceBlocksPerCU7 : grid;
+			ta.traceWaves = beside ? 7u : (uint32_t)waves;   /* 8 waves slow the packets beside the launch (r04ad) */
 			lh2_launch_trace_closest( &sd, &ta, g, { nullptr, ps.evTrace[pathLength] }, stream );
 		}
 		ps.fromTrace[pathLength] = ps.prevStop, ps.prevStop = ps.evTrace[pathLength];

@@ -212,7 +212,11 @@ private:
 
 	int device = 0, smCount = 256, blocksPerCU = 8, maxBlocksPerCU = 8, packetBlocksPerCU = 8, pathBlocksPerCU = 3, pathBlocksPerCU4 = 4;
 	int traceBlocksPerCU7 = 7, traceBlocksPerCU8 = 8;   /* occupancy of the closest-hit kernel's 7- and 8-wave variants */
-	int traceWaves = 8;                  /* closest-hit launches with the chip alone: the 8-wave variant (W7 beside the packets) */
+	/* closest-hit launches with the chip alone: 0, by scene: a single instance the 7-wave variant (72 VGPRs, no spills),
+	   instanced scenes the 8-wave one (64 VGPRs); 7 or 8: that variant.  8 for every scene won in round 4; with the early
+	   node loads (single-instance loops only) the single-instance 8-wave loop spills, and 7 there is config 3 -3.4 %, 4K -3 %,
+	   the N = 8 share -2.9 %, while config 5 (instanced) stays 2 % faster at 8 (profiles/r05f_ab_trace_waves.txt) */
+	int traceWaves = 0;
 	int unitTraceWaves = 7;              /* the unit queries' variant: 7 (the config-2 bounce rays alone: 0.481 vs 0.515 ms, r04ag) */
 	bool initialized = false;
 	/* scene */
