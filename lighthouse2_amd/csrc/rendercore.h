@@ -325,7 +325,10 @@ private:
 	static constexpr int kShadeMaxBlocks = 24;
 	/* blocks per CU of a closest-hit launch that the next frame's primary launch runs beside (an overlapped frame's later
 	   bounces, no path tail): the packets' latency-bound waves get slots from the start (config 2 +4 %, r03q_ab_trace_blocks.txt) */
-	static constexpr int kOverlapTraceBlocks = 5;
+#ifndef LH2_OVERLAP_TRACE_BLOCKS
+#define LH2_OVERLAP_TRACE_BLOCKS 5
+#endif
+	static constexpr int kOverlapTraceBlocks = LH2_OVERLAP_TRACE_BLOCKS;
 	/* packets while the BVH + triangles fit the 256 MB Infinity Cache (a packet's node and triangle records come through
 	   the scalar cache, one at a time: beyond the cache each is a DRAM round trip).  Config 3 (134 MB): primary 0.29 ->
 	   0.24 ms with packets; config 5 (1.4 GB): 5.3 -> 7.8 ms (profiles/r02zc_ab_packets_configs.txt) */
