@@ -394,11 +394,10 @@ def roofline_of(core, sc, W, H, dev, kernel_iters):
     n, n_p = len(bo), len(o4)
     version = int(core.get_setting("traceVersion"))
     kname = TRACE_KERNEL.get(version, f"traceVersion {version}")
-    wide = version == 7 and core.get_setting("w8Avail") == 1 and core.get_setting("traceWide") != 0
     if version == 7:
-        # the exact variant the unit launch runs (single instance, the unit queries' waves, BVH4 or W8): its counter summaries
-        # only (tools/pmc_round.sh names it with --kernel)
-        kname = f"k_trace_closest4d<true, {int(core.get_setting('unitTraceWaves'))}, {'true' if wide else 'false'}>"
+        # the exact variant the unit launch runs (single instance, the unit queries' waves): its counter summaries only
+        # (tools/pmc_round.sh names it with --kernel; round 5's names carried a third template argument, the W8 switch)
+        kname = f"k_trace_closest4d<true, {int(core.get_setting('unitTraceWaves'))}"
     cyc, cyc_src = valu_cycles_per_instruction()
     peak = SIMDS * CLOCK_GHZ / cyc                     # G wave64 VALU instructions / s
     sq_src, sq = newest("*_pmc_trace_sq.json", lambda d: d.get("kernel", "").startswith(kname))
@@ -414,7 +413,7 @@ def roofline_of(core, sc, W, H, dev, kernel_iters):
         "bound": "valu", "achieved": round(achieved, 1) if achieved else None, "peak": round(peak, 1),
         "unit": "G wave64 VALU instructions/s", "frac": round(achieved / peak, 4) if achieved else None,
         "traffic": traffic,
-        "kernel": f"{kname} (per-ray {'W8' if wide else 'BVH4'} traversal, traceVersion {version}, the core's default settings) on the "
+        "kernel": f"{kname} (per-ray BVH4 traversal, traceVersion {version}, the core's default settings) on the "
                   f"frame's {n} diffuse bounce rays, in the frame's order (two-ended segments, chordSplit)",
         "kernel_ms": round(ms, 4), "rays_per_launch": n,
         "valu_insts_per_launch": valu, "valu_lane_utilisation": sq.get("valu_lane_utilisation") if sq else None,

@@ -1,6 +1,5 @@
 /* bvh_build.cpp - parallel binned-SAH BVH2 builder (see bvh_build.h). */
 #include "bvh_build.h"
-#include "lh2_w8.h"
 
 #include <algorithm>
 #include <atomic>
@@ -685,7 +684,7 @@ int CollapseBvh4( const float* nodes2, size_t nodeCount2, std::vector<float>& no
 
 /* ---- BVH2 -> W-wide by dynamic programming over the BVH2 (surface-area cost) ---------------------
    The collapse of Ylitie, Karras and Laine ("Efficient Incoherent Ray Traversal on GPUs Through
-   Compressed Wide BVHs", HPG 2017, section 4) for W-wide nodes (4: the BVH4, 8: the W8 of lh2_w8.h): for every
+   Compressed Wide BVHs", HPG 2017, section 4) for W-wide nodes (4: the BVH4; round 5 also built an 8-wide tree with it): for every
    BVH2 subtree and every slot count j <= W, the cheapest way to hand it to a wide parent as at most j entries -
    one wide node, one leaf (a subtree of at most maxLeafTris triangles, its leaves contiguous in the DFS perm
    order that Flatten emits), or its two children's entries side by side - under the expected cost
@@ -860,61 +859,6 @@ int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>&
 		memcpy( q + 24, refs, 16 );
 	}
 	return depth;
-}
-
-/* ---- BVH2 -> W8 (lh2_w8.h) ---------------------------------------------------------------------
-   The 8-wide DP collapse, laid out breadth-first in blocks of 8 records: block 0 holds the root's record in slot 0;
-   each node's children get the next free block, in the slots of their centroids' directions (lh2_w8_assign), a node
-   child as its quantized record, a leaf child (one triangle: the BLAS is built with one triangle per leaf) as the
-   48-B triangle record of its perm slot (tris48, 12 floats per slot).  Returns false when a leaf holds more than one
-   triangle (bvhMaxLeaf > 1: no W8 for this mesh); child blocks are relative to the mesh's first block. */
-bool BuildW8( const float* nodes2, size_t nodeCount2, const float* tris48, size_t triRecords, float cLeaf, float cTri,
-	std::vector<uint32_t>& records, int& blocks, int& depth, int& qerr )
-{
-	std::vector<std::vector<WEnt>> wide;
-	depth = CollapseWideSah( nodes2, nodeCount2, 8, cLeaf, cTri, 1, wide );
-	for (const auto& l : wide) for (const auto& e : l) if (e.ref < 0 && (((uint32_t)~e.ref) & 15u) != 0) return false;
-	/* blocks: the root block, then one per wide node */
-	blocks = (int)wide.size() + 1;
-	records.assign( (size_t)blocks * 8 * LH2_W8_WORDS, 0u );
-	qerr = 0;
-	struct Item { size_t w; size_t slot; };
-	std::vector<Item> queue{ { 0, 0 } };
-	uint32_t nextBlock = 1;
-	for (size_t qi = 0; qi < queue.size(); qi++)
-	{
-		const Item it = queue[qi];
-		const auto& list = wide[it.w];
-		const int n = std::min( 8, (int)list.size() );
-		const uint32_t blk = nextBlock++;
-		float d[8][3] = {}, lo[8][3], hi[8][3];
-		float plo[3] = { INFINITY, INFINITY, INFINITY }, phi[3] = { -INFINITY, -INFINITY, -INFINITY };
-		for (int i = 0; i < n; i++) for (int a = 0; a < 3; a++) plo[a] = std::min( plo[a], list[i].lo[a] ), phi[a] = std::max( phi[a], list[i].hi[a] );
-		for (int i = 0; i < n; i++) for (int a = 0; a < 3; a++) d[i][a] = 0.5f * (list[i].lo[a] + list[i].hi[a]) - 0.5f * (plo[a] + phi[a]);
-		int slotOf[8];
-		lh2_w8_assign( n, d, slotOf );
-		bool valid[8] = {};
-		uint32_t imask = 0;
-		for (int s = 0; s < 8; s++) for (int a = 0; a < 3; a++) lo[s][a] = hi[s][a] = 0.0f;
-		for (int i = 0; i < n; i++)
-		{
-			const int sl = slotOf[i];
-			valid[sl] = lh2_w8_box_valid( list[i].lo, list[i].hi );
-			for (int a = 0; a < 3; a++) lo[sl][a] = list[i].lo[a], hi[sl][a] = list[i].hi[a];
-			const size_t at = (size_t)blk * 8 + (size_t)sl;
-			if (list[i].ref >= 0) { imask |= 1u << sl; queue.push_back( { (size_t)list[i].ref, at } ); }
-			else
-			{
-				const uint32_t tf = (uint32_t)(~list[i].ref) >> 4;
-				if (tf >= triRecords) return false;
-				memcpy( &records[at * LH2_W8_WORDS], tris48 + (size_t)tf * 12, 48 );
-			}
-		}
-		uint32_t* rec = &records[it.slot * LH2_W8_WORDS];
-		qerr |= lh2_w8_quantize( valid, lo, hi, imask, rec );
-		rec[18] = blk;
-	}
-	return true;
 }
 
 }  // namespace lh2

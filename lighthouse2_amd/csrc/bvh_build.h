@@ -43,11 +43,5 @@ int CollapseBvh4( const float* nodes2, size_t nodeCount2, std::vector<float>& no
    triangle); subtrees of at most maxLeafTris triangles may become one leaf (BVH2 leaves in DFS order) */
 int CollapseBvh4Sah( const float* nodes2, size_t nodeCount2, std::vector<float>& nodes4, float cLeaf, float cTri, int maxLeafTris );
 
-/* BVH2 -> W8 (lh2_w8.h): the 8-wide DP collapse laid out in blocks of 8 records of LH2_W8_WORDS words (child blocks
-   relative to the mesh's first), leaves as the triangle records of tris48 (12 floats per leaf slot, triRecords of them);
-   false when a leaf holds several triangles.  blocks: the blocks written; depth: wide levels; qerr: a node beyond the
-   quantized grid's range */
-bool BuildW8( const float* nodes2, size_t nodeCount2, const float* tris48, size_t triRecords, float cLeaf, float cTri,
-	std::vector<uint32_t>& records, int& blocks, int& depth, int& qerr );
 
 }  // namespace lh2

@@ -43,7 +43,7 @@ struct GpuTlasArgs
 	int nodeBase;                /* index of the TLAS root in the node array */
 	float4* nodes;               /* node array; the TLAS is written at nodeBase (<= count - 1 nodes) */
 	int maxBlasDepth;            /* stack check: tlasFactor x TLAS depth + this must stay below LH2_STACK_TOTAL - 1 */
-	int tlasFactor = 1;          /* stack entries per TLAS level (the W8 loop: 2) */
+	int tlasFactor = 1;          /* stack entries per TLAS level */
 	int* sceneError;             /* device flag: set when the stack check fails (traversal then exits) */
 	int* tlasDepth;              /* device: TLAS depth out */
 };
@@ -77,16 +77,11 @@ public:
 	   8-bit child planes on a per-node, per-axis power-of-two grid, rounded outward; a node beyond the grid's range
 	   sets LH2_SCENE_ERR_QRANGE in *sceneError */
 	static void Quantize4( const float4* nodes4, int first, int count, uint4* q, int* sceneError, hipStream_t stream );
-	/* the TLAS BVH2 nodes [base2, base2 + count) as W8 records (lh2_w8.h) in blocks rootBlock .. rootBlock + count: the
-	   root's record in slot 0 of rootBlock, node k's children in block rootBlock + 1 + k (a node child as its quantized
-	   record, an instance leaf as its instance record: inverse rows, index, its mesh's first block meshBlock[mesh]) */
-	static void TlasToW8( const float4* nodes2, int base2, int count, const void* instances, const int* meshBlock, uint32_t rootBlock,
-		uint32_t* w8, int* sceneError, hipStream_t stream );
 
 private:
-	void Reserve( int n );
+	void Reserve( int n, hipStream_t stream );
 	void Cluster( int N, int maxLeaf, float traversalCost, int tlas, GpuBuildResult& res, hipStream_t stream );
-	void* Scratch( size_t bytes );
+	void* Scratch( size_t bytes, hipStream_t stream );
 
 	int cap = 0;
 	void* boxes = nullptr;      /* Box8[2 cap]: node boxes */
@@ -108,6 +103,8 @@ private:
 	uint32_t* hred = nullptr;   /* pinned mirror */
 	void* tmp = nullptr;
 	size_t tmpBytes = 0;
+	hipStream_t lastStream = nullptr;   /* the stream of the last build (its uses of the scratch end there) */
+	hipStream_t retireStream = nullptr; /* ... and of the build before the current one (Reserve) */
 };
 
 }  // namespace lh2

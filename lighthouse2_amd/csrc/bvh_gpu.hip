@@ -12,7 +12,6 @@
 #include "bvh_gpu.h"
 #include "lh2_device.h"
 #include "lh2_kernels.h"
-#include "lh2_w8.h"
 
 namespace lh2 {
 void FatalError( const char* fmt, ... );
@@ -90,6 +89,10 @@ __device__ __forceinline__ void init_bounds( float v[12] )
 {
 	for (int k = 0; k < 12; k++) v[k] = ((k / 3) & 1) ? -INF : INF;
 }
+
+/* the largest grid exponent of a quantized node (box4q scales the ray's clamped reciprocal +-1e30 by 2^e: 1e30 * 2^27
+   stays finite) */
+#define LH2_QEXP_MAX 27
 
 __global__ void k_reset_red( uint32_t* red )
 {
@@ -634,76 +637,6 @@ __global__ __launch_bounds__( 256 ) void k_quantize4( const float4* __restrict__
 	d[3] = make_uint4( (uint32_t)r.x, (uint32_t)r.y, (uint32_t)r.z, (uint32_t)r.w );
 }
 
-/* the W8 record of TLAS BVH2 node j (its two children in block rootBlock + 1 + j, slots by lh2_w8_tlas_slots) */
-__device__ void w8_tlas_slots( const float4* n, bool valid[2], int slot[2], float lo[2][3], float hi[2][3] )
-{
-	const float4 a = n[0], b = n[1], z = n[2];
-	lo[0][0] = a.x, hi[0][0] = a.y, lo[0][1] = a.z, hi[0][1] = a.w, lo[0][2] = z.x, hi[0][2] = z.y;
-	lo[1][0] = b.x, hi[1][0] = b.y, lo[1][1] = b.z, hi[1][1] = b.w, lo[1][2] = z.z, hi[1][2] = z.w;
-	float d[8][3] = {}, plo[3], phi[3];
-	int idx[2], m = 0;
-	for (int c = 0; c < 2; c++) { valid[c] = lh2_w8_box_valid( lo[c], hi[c] ); slot[c] = -1; if (valid[c]) idx[m++] = c; }
-	for (int a2 = 0; a2 < 3; a2++)
-	{
-		plo[a2] = INFINITY, phi[a2] = -INFINITY;
-		for (int i = 0; i < m; i++) plo[a2] = fminf( plo[a2], lo[idx[i]][a2] ), phi[a2] = fmaxf( phi[a2], hi[idx[i]][a2] );
-		for (int i = 0; i < m; i++) d[i][a2] = 0.5f * (lo[idx[i]][a2] + hi[idx[i]][a2]) - 0.5f * (plo[a2] + phi[a2]);
-	}
-	int so[8];
-	lh2_w8_assign( m, d, so );
-	for (int i = 0; i < m; i++) slot[idx[i]] = so[i];
-}
-__device__ void w8_tlas_record( const float4* __restrict__ nodes2, int base2, int j, uint32_t rootBlock, uint32_t* rec, int* err )
-{
-	const float4* n = nodes2 + (size_t)(base2 + j) * 4;
-	bool v2[2];
-	int sl[2];
-	float lo2[2][3], hi2[2][3];
-	w8_tlas_slots( n, v2, sl, lo2, hi2 );
-	const float4 r = n[3];
-	const int ref[2] = { __float_as_int( r.x ), __float_as_int( r.y ) };
-	bool valid[8] = {};
-	float lo[8][3] = {}, hi[8][3] = {};
-	uint32_t imask = 0;
-	for (int c = 0; c < 2; c++)
-		if (v2[c])
-		{
-			valid[sl[c]] = true;
-			for (int a = 0; a < 3; a++) lo[sl[c]][a] = lo2[c][a], hi[sl[c]][a] = hi2[c][a];
-			if (ref[c] >= 0) imask |= 1u << sl[c];
-		}
-	uint32_t w[LH2_W8_WORDS];
-	if (lh2_w8_quantize( valid, lo, hi, imask, w )) atomicOr( err, LH2_SCENE_ERR_QRANGE );
-	w[18] = rootBlock + 1u + (uint32_t)j, w[19] = 0;
-	for (int k = 0; k < LH2_W8_WORDS; k += 4) *(uint4*)(rec + k) = make_uint4( w[k], w[k + 1], w[k + 2], w[k + 3] );
-}
-__global__ __launch_bounds__( 256 ) void k_tlas_to_w8( const float4* __restrict__ nodes2, int base2, int count, const DevInstance* __restrict__ inst,
-	const int* __restrict__ meshBlock, uint32_t rootBlock, uint32_t* __restrict__ w8, int* __restrict__ err )
-{
-	const int t = blockIdx.x * 256 + threadIdx.x;
-	if (t > count) return;
-	if (t == count) { w8_tlas_record( nodes2, base2, 0, rootBlock, w8 + (size_t)rootBlock * 8 * LH2_W8_WORDS, err ); return; }
-	const float4* n = nodes2 + (size_t)(base2 + t) * 4;
-	bool v2[2];
-	int sl[2];
-	float lo2[2][3], hi2[2][3];
-	w8_tlas_slots( n, v2, sl, lo2, hi2 );
-	const float4 r = n[3];
-	const int ref[2] = { __float_as_int( r.x ), __float_as_int( r.y ) };
-	for (int c = 0; c < 2; c++)
-	{
-		if (!v2[c]) continue;
-		uint32_t* rec = w8 + ((size_t)(rootBlock + 1u + (uint32_t)t) * 8 + (size_t)sl[c]) * LH2_W8_WORDS;
-		if (ref[c] >= 0) w8_tlas_record( nodes2, base2, ref[c] - base2, rootBlock, rec, err );
-		else
-		{
-			const uint32_t i = LEAF_FIRST( ref[c] );
-			const DevInstance in = inst[i];
-			*(float4*)(rec + 0) = in.inv0, *(float4*)(rec + 4) = in.inv1, *(float4*)(rec + 8) = in.inv2;
-			*(uint4*)(rec + 12) = make_uint4( i, (uint32_t)meshBlock[in.mesh], 0u, 0u );
-		}
-	}
-}
 
 inline int blocks( long n, int bs = 256 ) { return (int)std::max<long>( 1, (n + bs - 1) / bs ); }
 
@@ -711,48 +644,53 @@ inline int blocks( long n, int bs = 256 ) { return (int)std::max<long>( 1, (n + 
 
 namespace lh2 {
 
-template <class T> static void grow_buf( T*& p, size_t n )
+/* the scratch is stream-ordered memory (hipMallocAsync / hipFreeAsync): a grown buffer's old block is freed on the stream
+   of the last build that used it (lastStream: the TLAS builds run on the core's ahead stream, the BLAS builds on its core
+   stream, and the callers order the two), so no device-wide synchronisation stalls the frames in flight */
+template <class T> static void grow_buf( T*& p, size_t n, hipStream_t freeSt, hipStream_t st )
 {
-	if (p) CHK( hipFree( p ) );
-	CHK( hipMalloc( (void**)&p, std::max<size_t>( n, 1 ) * sizeof( T ) ) );
+	if (p) CHK( hipFreeAsync( p, freeSt ) );
+	CHK( hipMallocAsync( (void**)&p, std::max<size_t>( n, 1 ) * sizeof( T ), st ) );
 }
 
 GpuBvhBuilder::~GpuBvhBuilder()
 {
 	void* all[] = { boxes, prim, cl[0], cl[1], clNode[0], clNode[1], child, parent, P, I, cost, leafOrig, nn, keys[0], keys[1], vals[0], vals[1], flags, scan, dred, tmp };
-	for (void* p : all) if (p) (void)hipFree( p );
+	(void)hipDeviceSynchronize();
+	for (void* p : all) if (p) (void)hipFreeAsync( p, nullptr );
+	(void)hipStreamSynchronize( nullptr );
 	if (hred) (void)hipHostFree( hred );
 }
 
-void GpuBvhBuilder::Reserve( int n )
+void GpuBvhBuilder::Reserve( int n, hipStream_t st )
 {
+	const hipStream_t freeSt = lastStream ? lastStream : st;
+	retireStream = freeSt, lastStream = st;
 	if (!dred)
 	{
-		CHK( hipMalloc( (void**)&dred, 16 * sizeof( uint32_t ) ) );
+		CHK( hipMallocAsync( (void**)&dred, 16 * sizeof( uint32_t ), st ) );
 		CHK( hipHostMalloc( (void**)&hred, 16 * sizeof( uint32_t ), hipHostMallocDefault ) );
 	}
 	if (n <= cap) return;
-	/* the TLAS builds run on the core's ahead stream and the BLAS builds on its core stream, both with this scratch: the
-	   old buffers are freed only once no launch on any stream can still use them.  That sync stalls frames in flight, so the
-	   capacity grows by half again at least (a scene that keeps adding instances syncs O(log n) times, not per
-	   instance) */
-	if (cap) CHK( hipDeviceSynchronize() );
+	/* the capacity grows by half again at least: a scene that keeps adding instances regrows O(log n) times */
 	cap = std::max( n, std::max( 64, cap + cap / 2 ) );
 	const size_t c = (size_t)cap, c2 = 2 * c;
-	grow_buf( (Box8*&)boxes, c2 ); grow_buf( (Box8*&)prim, c ); grow_buf( (Box8*&)cl[0], c ); grow_buf( (Box8*&)cl[1], c );
-	grow_buf( clNode[0], c ); grow_buf( clNode[1], c ); grow_buf( child, 2 * c2 ); grow_buf( parent, c2 );
-	grow_buf( P, c2 ); grow_buf( I, c2 ); grow_buf( cost, c2 ); grow_buf( leafOrig, c ); grow_buf( nn, c );
-	grow_buf( keys[0], c ); grow_buf( keys[1], c ); grow_buf( vals[0], c ); grow_buf( vals[1], c );
-	grow_buf( flags, c ); grow_buf( scan, c );
+	grow_buf( (Box8*&)boxes, c2, freeSt, st ); grow_buf( (Box8*&)prim, c, freeSt, st ); grow_buf( (Box8*&)cl[0], c, freeSt, st );
+	grow_buf( (Box8*&)cl[1], c, freeSt, st ); grow_buf( clNode[0], c, freeSt, st ); grow_buf( clNode[1], c, freeSt, st );
+	grow_buf( child, 2 * c2, freeSt, st ); grow_buf( parent, c2, freeSt, st ); grow_buf( P, c2, freeSt, st ); grow_buf( I, c2, freeSt, st );
+	grow_buf( cost, c2, freeSt, st ); grow_buf( leafOrig, c, freeSt, st ); grow_buf( nn, c, freeSt, st ); grow_buf( keys[0], c, freeSt, st );
+	grow_buf( keys[1], c, freeSt, st ); grow_buf( vals[0], c, freeSt, st ); grow_buf( vals[1], c, freeSt, st ); grow_buf( flags, c, freeSt, st );
+	grow_buf( scan, c, freeSt, st );
 }
 
-void* GpuBvhBuilder::Scratch( size_t bytes )
+/* the sort / scan temporaries, on the build's stream; a grown block's old one freed behind the previous build (Reserve) */
+void* GpuBvhBuilder::Scratch( size_t bytes, hipStream_t st )
 {
 	if (bytes > tmpBytes)
 	{
-		if (tmp) { CHK( hipDeviceSynchronize() ); CHK( hipFree( tmp ) ); }
+		if (tmp) CHK( hipFreeAsync( tmp, retireStream ) );
 		tmpBytes = std::max<size_t>( bytes, std::max<size_t>( 1 << 20, tmpBytes + tmpBytes / 2 ) );
-		CHK( hipMalloc( &tmp, tmpBytes ) );
+		CHK( hipMallocAsync( &tmp, tmpBytes, st ) );
 	}
 	return tmp;
 }
@@ -766,7 +704,7 @@ void GpuBvhBuilder::Cluster( int N, int maxLeaf, float ct, int tlas, GpuBuildRes
 	CHK( hipcub::DeviceRadixSort::SortPairs( nullptr, need, keys[0], keys[1], vals[0], vals[1], N, 0, 63, st ) );
 	size_t needScan = 0;
 	CHK( hipcub::DeviceScan::ExclusiveSum( nullptr, needScan, flags, scan, N, st ) );
-	void* t = Scratch( std::max( need, needScan ) );
+	void* t = Scratch( std::max( need, needScan ), st );
 	CHK( hipcub::DeviceRadixSort::SortPairs( t, need, keys[0], keys[1], vals[0], vals[1], N, 0, 63, st ) );
 	k_init_leaves<<<blocks( N ), 256, 0, st>>>( vals[1], pb, N, (Box8*)boxes, P, I, cost, parent, leafOrig, clNode[0], (Box8*)cl[0] );
 	const int r = std::min( 32, std::max( 1, radius ) );
@@ -793,7 +731,7 @@ void GpuBvhBuilder::BuildBlas( const float4* coreTris, int N, int maxLeaf, float
 {
 	if (N < 2) FatalError( "GPU BLAS build needs >= 2 triangles" );
 	maxLeaf = std::min( 16, std::max( 1, maxLeaf ) );
-	Reserve( N );
+	Reserve( N, st );
 	k_reset_red<<<1, 64, 0, st>>>( dred );
 	k_tri_bounds<<<std::min( blocks( N ), 2048 ), 256, 0, st>>>( coreTris, N, (Box8*)prim, dred );
 	Cluster( N, maxLeaf, ct, 0, res, st );
@@ -815,7 +753,7 @@ void GpuBvhBuilder::BuildTlas( const GpuTlasArgs& a, hipStream_t st )
 {
 	const int N = a.count;
 	if (N < 2) FatalError( "GPU TLAS build needs >= 2 instances" );
-	Reserve( N );
+	Reserve( N, st );
 	if (N <= LH2_TLAS_WG_MAX)
 	{
 		TlasScratch s;
@@ -846,14 +784,6 @@ void GpuBvhBuilder::Quantize4( const float4* nodes4, int first, int count, uint4
 {
 	if (count <= 0) return;
 	k_quantize4<<<blocks( count ), 256, 0, st>>>( nodes4, first, count, q, sceneError );
-	CHK( hipGetLastError() );
-}
-
-void GpuBvhBuilder::TlasToW8( const float4* nodes2, int base2, int count, const void* instances, const int* meshBlock, uint32_t rootBlock,
-	uint32_t* w8, int* sceneError, hipStream_t st )
-{
-	if (count <= 0) return;
-	k_tlas_to_w8<<<blocks( count + 1 ), 256, 0, st>>>( nodes2, base2, count, (const DevInstance*)instances, meshBlock, rootBlock, w8, sceneError );
 	CHK( hipGetLastError() );
 }
 

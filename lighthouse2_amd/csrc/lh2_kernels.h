@@ -59,10 +59,6 @@ struct SceneDev       /* everything the traversal and shading kernels read, by v
 	const uint8_t* blueNoise;
 	float geometryEpsilon, clampValue;
 	const int* sceneError;           /* nonzero: the scene is unsafe to traverse (TLAS too deep); trace kernels exit */
-	/* the 8-wide compressed BVH (lh2_w8.h; null: not built): the first record a ray steps (the TLAS root's, or with a single
-	   instance its mesh's root record), and that mesh's first block */
-	const uint32_t* w8;
-	int w8Root, w8Base0;
 	const uint32_t* argb32;          /* texel storage (rendercore.cpp:296-336): ARGB32 / NRM32 u32 texels */
 	const uint32_t* nrm32;
 	uint32_t argb32Count, nrm32Count;
@@ -133,7 +129,6 @@ struct TraceArgs      /* one ray stream: rays in, hits (closest) or occlusion (a
 	uint32_t shadeBatch;                              /* path tail (k_trace_path4d): shade once >= shadeBatch lanes finished a query */
 	uint32_t tailWaves;                               /* path tail (lh2_launch_trace_path): the kernel variant for 4 waves per SIMD (4) or 3 */
 	uint32_t traceWaves;                              /* BVH4 closest hit: the kernel variant for 8 waves per SIMD (8) or 7 */
-	uint32_t wide;                                    /* version 7: the loop over the W8 (SceneDev::w8, lh2_w8.h) instead of the BVH4 */
 	/* heavy-first packets (packet kernel, hvWrite non-null): the previous frame's packets that took more
 	   than hvFactor x its mean node steps (hvRead: per-segment counts, step sums, a bit per packet and the
 	   lists of packet bits) are taken first, the rest in order; this frame's are recorded into hvWrite.
@@ -184,6 +179,7 @@ int lh2_packet_blocks_per_cu( void );
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
 int lh2_path_blocks_per_cu( int waves );
+void lh2_touch_set( uint32_t* bitmap, uint32_t triWord );   /* LH2_TOUCH builds only (lh2_trace4d.inc) */
 void lh2_launch_spin( unsigned long long ticks, hipStream_t st );
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
 void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );

@@ -19,7 +19,6 @@
 #include "lh2_device.h"
 #include "../../include/lh2_core_types.h"
 #include "lh2_kernels.h"
-#include "lh2_w8.h"
 #include "lh2_bary.h"
 
 #define S_SPECULAR 1
@@ -609,13 +608,15 @@ __global__ __launch_bounds__( 256, LH2_PACKET_MINWAVES ) void k_trace_closest_pa
 #define LH2_PRIMARY_MINWAVES 7
 #endif
 /* the camera fused into the primary packet launch: each lane makes its path's primary ray (camera_path) and traces it;
-   no camera launch, no ray round trip through HBM.  The frame's resets are k_init_counters' on the core stream (the
-   launch's own work-queue heads alternate between two slots, so it may run beside the previous frame's tail) */
+   no camera launch, no ray round trip through HBM.  The launch also does the frame's counter and work-queue resets
+   (cp.initC), behind the previous frame on the core stream and beside it on the ahead stream alike (RenderCore::
+   kPrimaryResets): the resets touch only this frame parity's block, and the launch's own work-queue heads (a fixed slot
+   the finalize two frames back zeroes) are left alone */
 __global__ __launch_bounds__( 256, LH2_PRIMARY_MINWAVES ) void k_trace_primary_packet( const CameraParams cp, const SceneDev s,
 	const TraceArgs a, float4* T4, float4* Q4 )
 {
-	/* behind the previous frame (on the core stream, RenderCore::Render): the frame's resets, the camera launch's (every
-	   work-queue head but the launch's own); beside it: k_init_counters on the core stream, initC null */
+	/* the frame's resets, the camera launch's (every work-queue head but the launch's own); initC is null only in an
+	   LH2_PRIMARY_RESETS=0 build, where a k_init_counters launch before this one on the ahead stream does them */
 	if (cp.initC)
 		for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < (uint32_t)max( cp.cursorWords, LH2_SEGS ); i += gridDim.x * 256u)
 			init_counters( cp.initC, cp.pathCount, cp.segStride, cp.cursors, cp.cursorWords, (int)i, cp.keepCursor );
@@ -1741,12 +1742,12 @@ __global__ __launch_bounds__( 256 ) void k_shade_last( const SceneDev s, const S
 /* W: the waves per SIMD the kernel is compiled for.  3: the lit variant's 168 VGPRs, no spills; 4: 128 VGPRs and ~190 B
    of spills.  Beside the side shadow launch a large frame's tail phase is 3 % faster with 4 (the 4K frame 6.58 -> 6.39 ms),
    a small frame's 3.5 % slower (the N = 8 share 1.125 -> 1.165 ms, profiles/r04w_ab.txt): TraceArgs::tailWaves picks */
-template <bool NL, bool SINGLE, int W, bool WIDE = false>
+template <bool NL, bool SINGLE, int W>
 __global__ __launch_bounds__( 256, W ) void k_trace_path4d( const SceneDev s, const TraceArgs a, const ShadeParams p )
 {
 	__shared__ int lstack[LH2_STACK_LDS * 256];
-	__shared__ __attribute__( (aligned( 4096 )) ) int lrefs[WIDE ? 64 : 4 * 256];
-	trace_stream4d<3, SINGLE, NL, WIDE>( s, a, lstack + threadIdx.x, lrefs + (WIDE ? 0 : threadIdx.x), blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &p );
+	__shared__ __attribute__( (aligned( 4096 )) ) int lrefs[4 * 256];
+	trace_stream4d<3, SINGLE, NL>( s, a, lstack + threadIdx.x, lrefs + threadIdx.x, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256u, &p );
 }
 
 /* counters: .cuda.cu:64-84 */
@@ -2078,41 +2079,41 @@ __global__ void k_spin( const unsigned long long ticks )
 #define LH2_LAUNCH( kernel, grid, block, st, ev, ... ) \
 	hipExtLaunchKernelGGL( kernel, dim3( grid ), dim3( block ), 0, st, (ev).start, (ev).stop, 0, __VA_ARGS__ )
 
-/* the per-ray loops' kernels over the BVH4 (WIDE false) or the W8 (WIDE true, TraceArgs::wide): a single-instance scene
-   (tlasRoot4 < 0) takes the loop without instance state (lh2_trace4d.inc SINGLE) */
-template <bool WIDE> static void launch_closest4d( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st )
+/* the per-ray loops' kernels over the BVH4: a single-instance scene (tlasRoot4 < 0) takes the loop without instance state
+   (lh2_trace4d.inc SINGLE) */
+static void launch_closest4d( const SceneDev* s, const TraceArgs* a, int grid, LaunchEvents ev, hipStream_t st )
 {
 	const bool single = s->tlasRoot4 < 0;
 	if (a->traceWaves == 8)
 	{
-		if (single) LH2_LAUNCH( (k_trace_closest4d<true, 8, WIDE>), grid, 256, st, ev, *s, *a );
-		else LH2_LAUNCH( (k_trace_closest4d<false, 8, WIDE>), grid, 256, st, ev, *s, *a );
+		if (single) LH2_LAUNCH( (k_trace_closest4d<true, 8>), grid, 256, st, ev, *s, *a );
+		else LH2_LAUNCH( (k_trace_closest4d<false, 8>), grid, 256, st, ev, *s, *a );
 	}
-	else if (single) LH2_LAUNCH( (k_trace_closest4d<true, LH2_TRACE_MINWAVES, WIDE>), grid, 256, st, ev, *s, *a );
-	else LH2_LAUNCH( (k_trace_closest4d<false, LH2_TRACE_MINWAVES, WIDE>), grid, 256, st, ev, *s, *a );
+	else if (single) LH2_LAUNCH( (k_trace_closest4d<true, LH2_TRACE_MINWAVES>), grid, 256, st, ev, *s, *a );
+	else LH2_LAUNCH( (k_trace_closest4d<false, LH2_TRACE_MINWAVES>), grid, 256, st, ev, *s, *a );
 }
-template <bool WIDE> static void launch_any4d( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st )
+static void launch_any4d( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st )
 {
 	const bool single = s->tlasRoot4 < 0;
-	if (fused && single) LH2_LAUNCH( (k_trace_any4d<1, true, WIDE>), grid, 256, st, ev, *s, *a );
-	else if (fused) LH2_LAUNCH( (k_trace_any4d<1, false, WIDE>), grid, 256, st, ev, *s, *a );
-	else if (single) LH2_LAUNCH( (k_trace_any4d<0, true, WIDE>), grid, 256, st, ev, *s, *a );
-	else LH2_LAUNCH( (k_trace_any4d<0, false, WIDE>), grid, 256, st, ev, *s, *a );
+	if (fused && single) LH2_LAUNCH( (k_trace_any4d<1, true>), grid, 256, st, ev, *s, *a );
+	else if (fused) LH2_LAUNCH( (k_trace_any4d<1, false>), grid, 256, st, ev, *s, *a );
+	else if (single) LH2_LAUNCH( (k_trace_any4d<0, true>), grid, 256, st, ev, *s, *a );
+	else LH2_LAUNCH( (k_trace_any4d<0, false>), grid, 256, st, ev, *s, *a );
 }
-template <bool WIDE> static void launch_path4d( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st )
+static void launch_path4d( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st )
 {
 	const bool nl = s->nArea + s->nPoint + s->nSpot + s->nDir == 0, single = s->tlasRoot4 < 0;
 	if (a->tailWaves == 4)
 	{
-		if (nl && single) LH2_LAUNCH( (k_trace_path4d<true, true, 4, WIDE>), grid, 256, st, ev, *s, *a, *p );
-		else if (nl) LH2_LAUNCH( (k_trace_path4d<true, false, 4, WIDE>), grid, 256, st, ev, *s, *a, *p );
-		else if (single) LH2_LAUNCH( (k_trace_path4d<false, true, 4, WIDE>), grid, 256, st, ev, *s, *a, *p );
-		else LH2_LAUNCH( (k_trace_path4d<false, false, 4, WIDE>), grid, 256, st, ev, *s, *a, *p );
+		if (nl && single) LH2_LAUNCH( (k_trace_path4d<true, true, 4>), grid, 256, st, ev, *s, *a, *p );
+		else if (nl) LH2_LAUNCH( (k_trace_path4d<true, false, 4>), grid, 256, st, ev, *s, *a, *p );
+		else if (single) LH2_LAUNCH( (k_trace_path4d<false, true, 4>), grid, 256, st, ev, *s, *a, *p );
+		else LH2_LAUNCH( (k_trace_path4d<false, false, 4>), grid, 256, st, ev, *s, *a, *p );
 	}
-	else if (nl && single) LH2_LAUNCH( (k_trace_path4d<true, true, 3, WIDE>), grid, 256, st, ev, *s, *a, *p );
-	else if (nl) LH2_LAUNCH( (k_trace_path4d<true, false, 3, WIDE>), grid, 256, st, ev, *s, *a, *p );
-	else if (single) LH2_LAUNCH( (k_trace_path4d<false, true, 3, WIDE>), grid, 256, st, ev, *s, *a, *p );
-	else LH2_LAUNCH( (k_trace_path4d<false, false, 3, WIDE>), grid, 256, st, ev, *s, *a, *p );
+	else if (nl && single) LH2_LAUNCH( (k_trace_path4d<true, true, 3>), grid, 256, st, ev, *s, *a, *p );
+	else if (nl) LH2_LAUNCH( (k_trace_path4d<true, false, 3>), grid, 256, st, ev, *s, *a, *p );
+	else if (single) LH2_LAUNCH( (k_trace_path4d<false, true, 3>), grid, 256, st, ev, *s, *a, *p );
+	else LH2_LAUNCH( (k_trace_path4d<false, false, 3>), grid, 256, st, ev, *s, *a, *p );
 }
 template <class K> static int occupancy( K kernel )
 {
@@ -2166,15 +2167,13 @@ void lh2_launch_trace_closest( const SceneDev* s, const TraceArgs* a, int grid, 
 	/* coherent primary rays: packets over the BVH2 (lh2_trace_packet.inc); incoherent rays: the BVH4 loop
 	   (lh2_trace4d.inc), or the reference BVH2 loop (traceVersion 1, or no BVH4) */
 	if (a->packet) LH2_LAUNCH( k_trace_closest_packet, grid, 256, st, ev, *s, *a );
-	else if (a->version == 7 && a->wide && s->w8) launch_closest4d<true>( s, a, grid, ev, st );
-	else if (a->version == 7 && s->nodes4) launch_closest4d<false>( s, a, grid, ev, st );
+	else if (a->version == 7 && s->nodes4) launch_closest4d( s, a, grid, ev, st );
 	else if (a->leafBatch) LH2_LAUNCH( k_trace_closest<true>, grid, 256, st, ev, *s, *a );
 	else LH2_LAUNCH( k_trace_closest<false>, grid, 256, st, ev, *s, *a );
 }
 void lh2_launch_trace_any( const SceneDev* s, const TraceArgs* a, int grid, int fused, LaunchEvents ev, hipStream_t st )
 {
-	if (a->version == 7 && a->wide && s->w8) launch_any4d<true>( s, a, grid, fused, ev, st );
-	else if (a->version == 7 && s->nodes4) launch_any4d<false>( s, a, grid, fused, ev, st );
+	if (a->version == 7 && s->nodes4) launch_any4d( s, a, grid, fused, ev, st );
 	else if (fused) LH2_LAUNCH( k_trace_any<1>, grid, 256, st, ev, *s, *a );
 	else LH2_LAUNCH( k_trace_any<0>, grid, 256, st, ev, *s, *a );
 }
@@ -2190,11 +2189,9 @@ int lh2_trace_blocks_per_cu( int waves )
 	/* the smallest of the variants' (the global stack is sized for this grid) */
 	int n = 0;
 	if (waves == 8)
-		n = std::min( std::min( occupancy( k_trace_closest4d<false, 8> ), occupancy( k_trace_closest4d<true, 8> ) ),
-			std::min( occupancy( k_trace_closest4d<false, 8, true> ), occupancy( k_trace_closest4d<true, 8, true> ) ) );
+		n = std::min( occupancy( k_trace_closest4d<false, 8> ), occupancy( k_trace_closest4d<true, 8> ) );
 	else
-		n = std::min( std::min( occupancy( k_trace_closest4d<false, LH2_TRACE_MINWAVES> ), occupancy( k_trace_closest4d<true, LH2_TRACE_MINWAVES> ) ),
-			std::min( occupancy( k_trace_closest4d<false, LH2_TRACE_MINWAVES, true> ), occupancy( k_trace_closest4d<true, LH2_TRACE_MINWAVES, true> ) ) );
+		n = std::min( occupancy( k_trace_closest4d<false, LH2_TRACE_MINWAVES> ), occupancy( k_trace_closest4d<true, LH2_TRACE_MINWAVES> ) );
 	return n;
 }
 static int lh2_shade_last_grid( void )   /* k_shade_last: every CU full (occupancy x CUs), at least a block per segment */
@@ -2211,17 +2208,14 @@ static int lh2_shade_last_grid( void )   /* k_shade_last: every CU full (occupan
 }
 void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st )
 {
-	if (!s->nodes4) return;   /* the host selects the path tail only over a BVH4 (and its W8) */
-	if (a->wide && s->w8) launch_path4d<true>( s, a, p, grid, ev, st );
-	else launch_path4d<false>( s, a, p, grid, ev, st );
+	if (!s->nodes4) return;   /* the host selects the path tail only over a BVH4 */
+	launch_path4d( s, a, p, grid, ev, st );
 }
 int lh2_path_blocks_per_cu( int waves )
 {
 	if (waves == 4)
-		return std::min( std::min( occupancy( k_trace_path4d<false, false, 4> ), occupancy( k_trace_path4d<false, true, 4> ) ),
-			std::min( occupancy( k_trace_path4d<false, false, 4, true> ), occupancy( k_trace_path4d<false, true, 4, true> ) ) );
-	return std::min( std::min( occupancy( k_trace_path4d<false, false, 3> ), occupancy( k_trace_path4d<false, true, 3> ) ),
-		std::min( occupancy( k_trace_path4d<false, false, 3, true> ), occupancy( k_trace_path4d<false, true, 3, true> ) ) );
+		return std::min( occupancy( k_trace_path4d<false, false, 4> ), occupancy( k_trace_path4d<false, true, 4> ) );
+	return std::min( occupancy( k_trace_path4d<false, false, 3> ), occupancy( k_trace_path4d<false, true, 3> ) );
 }
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st )
 {
@@ -2250,6 +2244,13 @@ void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int 
 }
 #ifdef LH2_SHADE_TIMES
 void lh2_shade_times( unsigned long long out[16] ) { (void)hipMemcpyFromSymbol( out, HIP_SYMBOL( lh2_shade_tt ), 16 * 8 ); }
+#endif
+#ifdef LH2_TOUCH
+void lh2_touch_set( uint32_t* bitmap, uint32_t triWord )
+{
+	(void)hipMemcpyToSymbol( HIP_SYMBOL( lh2_touch ), &bitmap, sizeof( bitmap ) );
+	(void)hipMemcpyToSymbol( HIP_SYMBOL( lh2_touchTri ), &triWord, sizeof( triWord ) );
+}
 #endif
 void lh2_launch_spin( unsigned long long ticks, hipStream_t st ) { hipLaunchKernelGGL( k_spin, dim3( 1 ), dim3( 64 ), 0, st, ticks ); }
 void lh2_launch_finalize( float4* acc, float4* out, int n, float scale, const FrameStatsDev* fs, LaunchEvents ev, hipStream_t st, const RowMap* rm )

@@ -149,13 +149,21 @@ void MultiDevice::SetLights( const lh2_CoreLightTri* a, int na, const lh2_CorePo
 	ForEach( [&]( int i ) { cores[i]->SetLights( a, na, p, np, s, ns, d, nd ); } );
 }
 void MultiDevice::SetSkyData( const float* px, uint32_t w, uint32_t h ) { ForEach( [&]( int i ) { cores[i]->SetSkyData( px, w, h ); } ); }
-/* each sub-core builds its own BLAS (the CPU builds of the devices run concurrently) */
+/* one BLAS build per mesh, not one per device: core 0 takes the mesh (a CPU build is deferred), the other
+   sub-cores upload its shading triangles and share core 0's deferred build (RenderCore::AdoptGeometry) */
 void MultiDevice::SetGeometry( int meshIdx, const float* v, int vc, int tc, const lh2_CoreTri* t, const uint32_t* alpha )
 {
-	ForEach( [&]( int i ) { cores[i]->SetGeometry( meshIdx, v, vc, tc, t, alpha ); } );
+	cores[0]->SetGeometry( meshIdx, v, vc, tc, t, alpha );
+	ForEach( [&]( int i ) { if (i > 0) cores[i]->AdoptGeometry( meshIdx, tc, t, *cores[0] ); } );
 }
 void MultiDevice::SetInstance( int idx, int mesh, const float* m16 ) { ForEach( [&]( int i ) { cores[i]->SetInstance( idx, mesh, m16 ); } ); }
-void MultiDevice::UpdateToplevel() { ForEach( [&]( int i ) { cores[i]->UpdateToplevel(); } ); }
+/* the shared builds run first, on core 0's thread pool (the host's threads once, not N pools); then every sub-core uploads
+   them to its device and builds its TLAS */
+void MultiDevice::UpdateToplevel()
+{
+	cores[0]->FlushPendingBuilds();
+	ForEach( [&]( int i ) { cores[i]->UpdateToplevel(); } );
+}
 
 /* ---- partitioned calls ------------------------------------------------------------------- */
 void MultiDevice::SetTarget( uint32_t w, uint32_t h, uint32_t spp, uint32_t glTexture )

@@ -274,21 +274,20 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "packetPrimary" )) packetPrimary = value < 0 ? -1 : value != 0;
 	else if (!strcmp( name, "singleInstanceStart" )) singleInstanceStart = value != 0;   /* one instance: rays start at its TLAS leaf */
 	else if (!strcmp( name, "terminalShade" )) terminalShade = value != 0;   /* drop hits that cannot contribute before shading them (ShadeParams::terminal) */
-	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (default: occupancy limit) */
+	else if (!strcmp( name, "traceBlocksPerCU" ))   /* persistent trace grid: blocks per CU (0: the launched variant's occupancy) */
 	{
-		blocksPerCU = value > 0 ? std::min( maxBlocksPerCU, std::max( 1, (int)value ) ) : traceWaves == 7 ? traceBlocksPerCU7 : traceBlocksPerCU8;
+		userBlocksPerCU = value > 0 ? std::min( maxBlocksPerCU, std::max( 1, (int)value ) ) : 0;
+		blocksPerCU = userBlocksPerCU ? userBlocksPerCU : traceWaves == 7 ? traceBlocksPerCU7 : traceBlocksPerCU8;
 	}
 	else if (!strcmp( name, "unitTraceWaves" )) unitTraceWaves = (int)value == 8 ? 8 : 7;   /* the same for the unit queries (TraceClosest*) */
 	else if (!strcmp( name, "traceWaves" ))   /* closest-hit kernel variant (7 or 8 waves per SIMD; 0: by scene); resets traceBlocksPerCU */
 	{
 		traceWaves = (int)value == 7 ? 7 : (int)value == 8 ? 8 : 0;
+		userBlocksPerCU = 0;
 		blocksPerCU = traceWaves == 7 ? traceBlocksPerCU7 : traceBlocksPerCU8;
 	}
 	else if (!strcmp( name, "unitCoherent" )) unitCoherent = value != 0;   /* TraceClosestDevice traces as the frame traces primary rays */
 	else if (!strcmp( name, "traceVersion" )) traceVersion = (int)value == 1 ? 1 : 0;   /* 1: the reference BVH2 loop; else the BVH4 loop */
-	/* the W8 loop (lh2_w8.h): 0 off, 1 every per-ray launch, 2 frames of at most kSmallFramePaths paths; 0 before SetGeometry also
-	   skips building the W8 */
-	else if (!strcmp( name, "traceWide" )) traceWide = std::min( 2, std::max( 0, (int)value ) );
 	/* other names ("clampDirect", "filter", "TAA", ...) are ignored, as in the reference */
 }
 
@@ -304,9 +303,9 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 		{ "shadowOverlap", (float)shadowOverlap }, { "cameraFused", (float)cameraFused }, { "frameOverlap", (float)frameOverlap }, { "earlyShade", (float)earlyShade },
 		{ "sideBlocks", (float)sideBlocks }, { "pathTailBlocks", (float)pathTailBlocks }, { "shadeBlocks", (float)shadeBlocks }, { "finalShadowBlocks", (float)finalShadowBlocks },
 		{ "pathTailWaves", (float)pathTailWaves }, { "packetPrimary", (float)packetPrimary }, { "singleInstanceStart", (float)singleInstanceStart },
-		{ "terminalShade", (float)terminalShade }, { "traceBlocksPerCU", (float)blocksPerCU }, { "unitTraceWaves", (float)unitTraceWaves }, { "traceWaves", (float)traceWaves },
-		{ "unitCoherent", (float)unitCoherent }, { "traceVersion", (float)TraceVersion() }, { "traceWide", (float)traceWide }, { "w8Avail", (float)w8Avail },
-		{ "usePackets", (float)UsePackets() } };
+		{ "terminalShade", (float)terminalShade }, { "traceBlocksPerCU", (float)ClosestBlocksPerCU( ScenePicksWaves() ) }, { "unitTraceWaves", (float)unitTraceWaves }, { "traceWaves", (float)traceWaves },
+		{ "unitCoherent", (float)unitCoherent }, { "traceVersion", (float)TraceVersion() },
+		{ "usePackets", (float)UsePackets() }, { "blasBuilds", (float)BlasBuildCount() } };
 	for (const auto& e : t) if (!strcmp( name, e.n )) { value = e.v; return true; }
 	return false;
 }
@@ -414,6 +413,13 @@ void RenderCore::SetSkyData( const float* pixels, uint32_t width, uint32_t heigh
 	CHK_HIP( hipStreamSynchronize( stream ) );
 }
 
+static std::atomic<int> gBlasBuilds{ 0 };
+int RenderCore::BlasBuildCount() { return gBlasBuilds.load(); }
+void HostBlas::Run( int threads )
+{
+	std::call_once( once, [&] { job( *this, threads ); job = nullptr; gBlasBuilds++; } );
+}
+
 void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount, const lh2_CoreTri* tris, const uint32_t* )
 {
 	sceneVersion++;
@@ -463,16 +469,16 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 				m.aabbLo[k] = std::min( m.aabbLo[k], prims[i].lo[k] ), m.aabbHi[k] = std::max( m.aabbHi[k], prims[i].hi[k] );
 			}
 		}
-		const int maxLeaf = bvhMaxLeaf, collapse = bvh4Collapse, wide = bvh4, w8 = bvh4 && traceWide != 0;
+		const int maxLeaf = bvhMaxLeaf, collapse = bvh4Collapse, wide = bvh4;
 		const float cost = 1.0f, spatial = bvhSpatial, budget = bvhSpatialBudget;
 		const int minRefs = bvhSpatialMinRefs;
-		CoreMeshHost* mp = &m;
-		m.build = [mp, prims = std::move( prims ), verts = std::move( verts ), maxLeaf, collapse, wide, w8, cost, spatial, budget, minRefs]( int threads ) {
+		m.build = std::make_shared<HostBlas>();
+		m.build->job = [prims = std::move( prims ), verts = std::move( verts ), maxLeaf, collapse, wide, cost, spatial, budget, minRefs]( HostBlas& r, int threads ) {
 			BvhOutput bvh;
 			BuildBvh2( prims, maxLeaf, threads, bvh, cost, 0, spatial > 0 ? verts.data() : nullptr, spatial, budget, minRefs );
 			/* one triangle record per leaf slot (a spatial split can reference a triangle from several leaves):
 			   v0, e1 = v1 - v0, e2 = v2 - v0 in fp32, exactly as the oracle's intersect_tri */
-			std::vector<float>& t48 = mp->hostTris48;
+			std::vector<float>& t48 = r.tris48;
 			t48.assign( std::max<size_t>( bvh.perm.size(), 1 ) * 12, 0.0f );
 			for (size_t j = 0; j < bvh.perm.size(); j++)
 			{
@@ -483,18 +489,14 @@ void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount,
 				o[4] = v[3] - v[0], o[5] = v[4] - v[1], o[6] = v[5] - v[2], o[7] = 0;
 				o[8] = v[6] - v[0], o[9] = v[7] - v[1], o[10] = v[8] - v[2], o[11] = 0;
 			}
-			mp->leafTris = (int)bvh.perm.size();
-			mp->nodeCount = (int)(bvh.nodes.size() / 16), mp->maxDepth = bvh.maxDepth;
-			mp->hostNodes4.clear(), mp->depth4 = 0;
+			r.leafTris = (int)bvh.perm.size();
+			r.nodeCount = (int)(bvh.nodes.size() / 16), r.maxDepth = bvh.maxDepth;
+			r.nodes4.clear(), r.depth4 = 0;
 			/* BVH4 collapse: dynamic programming (surface-area costs: node step 1, leaf visit 0.4, triangle test 0.5,
 			   one triangle per leaf; merged leaves run the leaf loop divergent: slower, r02s) or greedy */
-			if (wide) mp->depth4 = collapse ? CollapseBvh4Sah( bvh.nodes.data(), (size_t)mp->nodeCount, mp->hostNodes4, 0.4f, 0.5f, 1 )
-				: CollapseBvh4( bvh.nodes.data(), (size_t)mp->nodeCount, mp->hostNodes4 );
-			/* the W8 (lh2_w8.h): the 8-wide DP collapse with one triangle per leaf (none when the BVH2 has larger leaves) */
-			mp->w8Blocks = 0, mp->hostW8.clear();
-			if (w8 && !BuildW8( bvh.nodes.data(), (size_t)mp->nodeCount, t48.data(), bvh.perm.size(), 0.4f, 0.5f, mp->hostW8, mp->w8Blocks, mp->w8Depth, mp->w8QErr ))
-				mp->w8Blocks = 0, mp->hostW8.clear();
-			mp->hostNodes2 = std::move( bvh.nodes );
+			if (wide) r.depth4 = collapse ? CollapseBvh4Sah( bvh.nodes.data(), (size_t)r.nodeCount, r.nodes4, 0.4f, 0.5f, 1 )
+				: CollapseBvh4( bvh.nodes.data(), (size_t)r.nodeCount, r.nodes4 );
+			r.nodes2 = std::move( bvh.nodes );
 		};
 		pendingBuilds = true;
 	}
@@ -541,9 +543,11 @@ void RenderCore::FlushBuilds()
 			{
 				const int remaining = (int)jobs.size() - j;
 				const int want = std::max( perJob, std::min( 8, workers / std::max( 1, remaining ) ) );
-				const int grant = std::max( 1, std::min( want, workers - inUse.load() ) );
-				inUse += grant;
-				jobs[j]->build( grant );
+				/* reserve the grant atomically out of the threads no running build holds (one at least: this worker's own) */
+				int held = inUse.load(), grant = 1;
+				do grant = std::max( 1, std::min( want, workers - held ) );
+				while (!inUse.compare_exchange_weak( held, held + grant ));
+				jobs[j]->build->Run( grant );
 				inUse -= grant;
 			}
 		}
@@ -556,16 +560,68 @@ void RenderCore::FlushBuilds()
 	for (auto& e : errors) if (!e.empty()) FatalError( "BLAS build: %s", e.c_str() );
 	for (auto* m : jobs)
 	{
-		m->bvhNodes.upload( (const float4*)m->hostNodes2.data(), m->hostNodes2.size() / 4, stream );
-		m->bvhTris.upload( (const float4*)m->hostTris48.data(), m->hostTris48.size() / 4, stream );
-		if (bvh4) m->bvh4Nodes.upload( (const float4*)m->hostNodes4.data(), m->hostNodes4.size() / 4, stream ), m->node4Count = (int)(m->hostNodes4.size() / 32);
-		if (m->w8Blocks) m->w8.upload( m->hostW8.data(), m->hostW8.size(), stream );
+		const HostBlas& r = *m->build;
+		m->leafTris = r.leafTris, m->nodeCount = r.nodeCount, m->maxDepth = r.maxDepth, m->depth4 = r.depth4;
+		m->bvhNodes.upload( (const float4*)r.nodes2.data(), r.nodes2.size() / 4, stream );
+		m->bvhTris.upload( (const float4*)r.tris48.data(), r.tris48.size() / 4, stream );
+		if (bvh4) m->bvh4Nodes.upload( (const float4*)r.nodes4.data(), r.nodes4.size() / 4, stream ), m->node4Count = (int)(r.nodes4.size() / 32);
 		CHK_HIP( hipStreamSynchronize( stream ) );
-		m->hostNodes2 = std::vector<float>(), m->hostTris48 = std::vector<float>(), m->hostNodes4 = std::vector<float>(), m->hostW8 = std::vector<uint32_t>();
-		m->build = nullptr;
+		m->build.reset();   /* the last core to upload a shared build frees its host arrays */
 	}
 	coreStats.bvhBuildTime += std::chrono::duration<float>( std::chrono::high_resolution_clock::now() - t0 ).count();
 }
+
+/* MultiDevice's sub-cores: the mesh of src (core 0, which has just taken it through SetGeometry), its shading triangles
+   uploaded to this device, its deferred CPU build shared (run once by the first core to flush, uploaded by each).  A GPU
+   build (gpuBuild), or a mesh src has already uploaded, is built here as SetGeometry builds it */
+void RenderCore::AdoptGeometry( int meshIdx, int triangleCount, const lh2_CoreTri* tris, const RenderCore& src )
+{
+	const CoreMeshHost* sm = meshIdx >= 0 && meshIdx < (int)src.meshes.size() ? src.meshes[meshIdx] : nullptr;
+	if (!sm || !sm->build || sm->triCount != triangleCount || bvh4 != src.bvh4)
+	{
+		SetGeometry( meshIdx, nullptr, 0, triangleCount, tris, nullptr );
+		return;
+	}
+	sceneVersion++;
+	if (meshIdx < 0 || meshIdx > (int)meshes.size()) FatalError( "SetGeometry: mesh index %d out of sequence", meshIdx );
+	if (meshIdx == (int)meshes.size()) meshes.push_back( new CoreMeshHost() );
+	CoreMeshHost& m = *meshes[meshIdx];
+	const auto t0 = std::chrono::high_resolution_clock::now();
+	m.triCount = triangleCount;
+	m.shadeTris.upload( (const float4*)tris, (size_t)triangleCount * 11, stream );
+	m.shadeTris.resize( 11 );
+	for (int k = 0; k < 3; k++) m.aabbLo[k] = sm->aabbLo[k], m.aabbHi[k] = sm->aabbHi[k];
+	m.build = sm->build;
+	pendingBuilds = true;
+	CHK_HIP( hipStreamSynchronize( stream ) );   /* the caller's triangle array is borrowed for this call only */
+	geometryDirty = true;
+	coreStats.bvhBuildTime += std::chrono::duration<float>( std::chrono::high_resolution_clock::now() - t0 ).count();
+}
+
+#ifdef LH2_TOUCH
+/* the unique records one closest-hit launch reads (diagnostic build): quantized BVH4 nodes (64 B) and leaf triangle records
+   (48 B), one bit each, counted after the launch; one JSON line per launch on stderr.  The launch is serialised with the
+   count (the build is for this count, not for timing) */
+void RenderCore::TouchBegin()
+{
+	const uint32_t nodeWords = (uint32_t)(((size_t)blasNode4Count + 2 * tlasCapacity + 31) / 32), triWords = (uint32_t)(((size_t)blasTriCount + 31) / 32);
+	touchMap.resize( (size_t)nodeWords + triWords );
+	CHK_HIP( hipMemsetAsync( touchMap.ptr, 0, sizeof( uint32_t ) * ((size_t)nodeWords + triWords), stream ) );
+	lh2_touch_set( touchMap.ptr, nodeWords );
+	touchNodeWords = nodeWords;
+}
+void RenderCore::TouchReport( int pathLength )
+{
+	CHK_HIP( hipStreamSynchronize( stream ) );
+	std::vector<uint32_t> h( touchMap.count );
+	CHK_HIP( hipMemcpy( h.data(), touchMap.ptr, sizeof( uint32_t ) * h.size(), hipMemcpyDeviceToHost ) );
+	uint64_t nodes = 0, tris = 0;
+	for (size_t i = 0; i < h.size(); i++) (i < touchNodeWords ? nodes : tris) += (uint64_t)__builtin_popcount( h[i] );
+	fprintf( stderr, "LH2_TOUCH {\"pathLength\": %d, \"unique_nodes\": %llu, \"unique_tri_records\": %llu, \"node_bytes\": %llu, "
+		"\"tri_bytes\": %llu, \"scene_nodes\": %d, \"scene_tri_records\": %d, \"paths\": %u}\n", pathLength, (unsigned long long)nodes,
+		(unsigned long long)tris, (unsigned long long)nodes * 64ull, (unsigned long long)tris * 48ull, blasNode4Count, blasTriCount, ps.count );
+}
+#endif
 
 void RenderCore::BuildBlas4( CoreMeshHost& m, const float* nodes2 )
 {
@@ -577,21 +633,6 @@ void RenderCore::BuildBlas4( CoreMeshHost& m, const float* nodes2 )
 		: CollapseBvh4( nodes2, (size_t)m.nodeCount, n4 );
 	m.bvh4Nodes.upload( (const float4*)n4.data(), n4.size() / 4, stream );
 	m.node4Count = (int)(n4.size() / 32);
-	/* the W8 from the same BVH2 and its leaf-ordered triangle records (one download) */
-	m.w8Blocks = 0;
-	if (traceWide != 0 && m.leafTris > 0)
-	{
-		std::vector<float> t48( (size_t)m.leafTris * 12 );
-		CHK_HIP( hipMemcpyAsync( t48.data(), m.bvhTris.ptr, t48.size() * sizeof( float ), hipMemcpyDeviceToHost, stream ) );
-		CHK_HIP( hipStreamSynchronize( stream ) );
-		std::vector<uint32_t> w;
-		if (BuildW8( nodes2, (size_t)m.nodeCount, t48.data(), (size_t)m.leafTris, 0.4f, 0.5f, w, m.w8Blocks, m.w8Depth, m.w8QErr ))
-		{
-			m.w8.upload( w.data(), w.size(), stream );
-			CHK_HIP( hipStreamSynchronize( stream ) );
-		}
-		else m.w8Blocks = 0;
-	}
 }
 
 void RenderCore::SetInstance( int instanceIdx, int meshIdx, const float* M )   /* rendercore.cpp:229-243 */
@@ -610,21 +651,14 @@ void RenderCore::ConcatenateBlas( int ni )
 {
 	FlushBuilds();
 	meshNodeBase.assign( meshes.size(), 0 ), meshTriBase.assign( meshes.size(), 0 ), meshNode4Base.assign( meshes.size(), 0 );
-	meshBlockBase.assign( std::max<size_t>( meshes.size(), 1 ), 0 );
 	int nodeTotal = 0, triTotal = 0, node4Total = 0, meshTris = 0;
-	size_t w8Total = 0;
-	int w8QErr = 0;
-	maxBlasDepth = 0, maxBlas4Depth = 0, maxBlasW8Depth = 0;
-	w8Avail = bvh4 && traceWide != 0;
+	maxBlasDepth = 0, maxBlas4Depth = 0;
 	std::vector<float> bounds( std::max<size_t>( meshes.size(), 1 ) * 6, 0.0f );
 	for (size_t mi = 0; mi < meshes.size(); mi++)
 	{
 		const CoreMeshHost& m = *meshes[mi];
 		meshNodeBase[mi] = nodeTotal, meshTriBase[mi] = triTotal, meshNode4Base[mi] = node4Total;
 		nodeTotal += m.nodeCount, triTotal += m.leafTris, node4Total += m.node4Count, meshTris += m.triCount;
-		meshBlockBase[mi] = (int)w8Total, w8Total += (size_t)m.w8Blocks, w8QErr |= m.w8QErr;
-		maxBlasW8Depth = std::max( maxBlasW8Depth, m.w8Depth );
-		if (!m.w8Blocks) w8Avail = false;
 		maxBlasDepth = std::max( maxBlasDepth, m.maxDepth ), maxBlas4Depth = std::max( maxBlas4Depth, m.depth4 );
 		for (int k = 0; k < 3; k++) bounds[mi * 6 + k] = m.aabbLo[k], bounds[mi * 6 + 3 + k] = m.aabbHi[k];
 		if (m.triCount == 0) bounds[mi * 6] = 1.0f, bounds[mi * 6 + 3] = 0.0f;   /* empty-mesh marker */
@@ -633,11 +667,7 @@ void RenderCore::ConcatenateBlas( int ni )
 	/* frames in flight may still read the old arrays, and a TLAS update may be queued on the ahead stream */
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	CHK_HIP( hipStreamSynchronize( aheadStream ) );
-	dNodes.free(), dTris.free(), dNodes4.free(), dNodes4q.free(), dW8.free();
-	/* the W8 after the BLAS: two TLAS slots of tlasCapacity + 1 blocks; blocks stay below LH2_W8_MAX_BLOCKS (stack entries) and
-	   record byte offsets below 4 GiB (the traversal's 32-bit buffer offsets) */
-	const size_t w8Blocks = w8Total + 2 * ((size_t)tlasCapacity + 1);
-	if (w8Avail && (w8Blocks > LH2_W8_MAX_BLOCKS || w8Blocks * 8 * LH2_W8_BYTES > 0xfffffff0ull)) w8Avail = false;
+	dNodes.free(), dTris.free(), dNodes4.free(), dNodes4q.free();
 	/* after the BLAS: two TLAS slots of tlasCapacity nodes each (UpdateToplevel) */
 	dNodes.resize( ((size_t)nodeTotal + 2 * tlasCapacity) * 4 );
 	/* the BVH4 loops address nodes with 32-bit buffer offsets (lh2_trace4d.inc): the array stays below 2 GiB */
@@ -658,22 +688,9 @@ void RenderCore::ConcatenateBlas( int ni )
 		if (m.leafTris) CHK_HIP( hipMemcpyAsync( dTris.ptr + (size_t)meshTriBase[mi] * 3, m.bvhTris.ptr, sizeof( float4 ) * 3 * (size_t)m.leafTris, hipMemcpyDeviceToDevice, stream ) );
 	}
 	if (bvh4) GpuBvhBuilder::Quantize4( dNodes4.ptr, 0, node4Total, dNodes4q.ptr, dBlasQError.ptr, stream );
-	if (w8Avail)
-	{
-		dW8.resize( w8Blocks * 8 * LH2_W8_WORDS );
-		for (size_t mi = 0; mi < meshes.size(); mi++)
-		{
-			const CoreMeshHost& m = *meshes[mi];
-			CHK_HIP( hipMemcpyAsync( dW8.ptr + (size_t)meshBlockBase[mi] * 8 * LH2_W8_WORDS, m.w8.ptr, sizeof( uint32_t ) * 8 * LH2_W8_WORDS * (size_t)m.w8Blocks,
-				hipMemcpyDeviceToDevice, stream ) );
-		}
-		dMeshBlock.upload( meshBlockBase.data(), meshBlockBase.size(), stream );
-		if (w8QErr) { const int e = LH2_SCENE_ERR_QRANGE; CHK_HIP( hipMemcpyAsync( dBlasQError.ptr, &e, sizeof( int ), hipMemcpyHostToDevice, stream ) ); }
-	}
 	dMeshBounds.upload( bounds.data(), bounds.size(), stream );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 	blasNodeCount = nodeTotal, blasTriCount = triTotal, blasNode4Count = node4Total, blasMeshTris = meshTris;
-	blasW8Blocks = (int)w8Total;
 	geometryDirty = false;
 }
 
@@ -774,7 +791,7 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		ta.T = dInstT.ptr, ta.instMesh = dInstMesh.ptr, ta.meshBounds = dMeshBounds.ptr, ta.count = ni;
 		ta.nodeBase = TlasBase2( ts ), ta.nodes = dNodes.ptr, ta.maxBlasDepth = StackDepthBound();
 		ta.sceneError = SceneErr( ts ), ta.tlasDepth = dTlasDepth.ptr;
-		ta.tlasFactor = w8Avail ? 2 : 1;   /* the W8 loop pushes up to two entries per TLAS level */
+		ta.tlasFactor = 1;
 		gpuBvh.BuildTlas( ta, us );
 		tlasNodes = ni - 1;   /* one instance per leaf: ni - 1 child-pair nodes, dense in preorder (bvh_gpu.hip emit_node) */
 		tlasOnDevice = true;
@@ -831,7 +848,7 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		if (tlas.nodes.size() * sizeof( float ) > need - offNodes) FatalError( "TLAS staging overflow" );
 		memcpy( sb + offNodes, tlas.nodes.data(), tlas.nodes.size() * sizeof( float ) );
 		CHK_HIP( hipMemcpyAsync( dNodes.ptr + (size_t)TlasBase2( ts ) * 4, sb + offNodes, tlas.nodes.size() * sizeof( float ), hipMemcpyHostToDevice, us ) );
-		sceneMaxDepth = (w8Avail ? 2 : 1) * tlas.maxDepth + StackDepthBound();
+		sceneMaxDepth = tlas.maxDepth + StackDepthBound();
 		tlasOnDevice = false;
 		if (sceneMaxDepth >= LH2_STACK_TOTAL - 1) FatalError( "BVH depth %d exceeds the traversal stack (%d)", sceneMaxDepth, LH2_STACK_TOTAL );
 	}
@@ -844,8 +861,6 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 		GpuBvhBuilder::TlasToBvh4( dNodes.ptr, TlasBase2( ts ), tlasNodes, TlasBase4( ts ), dNodes4.ptr, us );
 		GpuBvhBuilder::Quantize4( dNodes4.ptr, TlasBase4( ts ), tlasNodes, dNodes4q.ptr, SceneErr( ts ), us );
 	}
-	/* ... and as W8 records (lh2_w8.h) in the slot's blocks: the instance leaves carry their inverse rows */
-	if (w8Avail) GpuBvhBuilder::TlasToW8( dNodes.ptr, TlasBase2( ts ), tlasNodes, dInst[ts].ptr, dMeshBlock.ptr, (uint32_t)W8TlasBlock( ts ), dW8.ptr, SceneErr( ts ), us );
 	tlasNodeCount[ts] = tlasNodes;
 	CHK_HIP( hipEventRecord( evStage[slot], us ) );
 	CHK_HIP( hipEventRecord( evTlasReady, us ) );
@@ -895,7 +910,6 @@ SceneDev RenderCore::MakeSceneDev()
 	/* one instance of a non-empty mesh: rays start at its TLAS leaf (MAKE_LEAF( 0, 1 ) = ~0) and skip
 	   the TLAS root's box test, which can only cull (TopLevelBVH::Traverse bvh.cpp:594-649); the
 	   instance transform runs as at the leaf, so the hits are unchanged: one loop iteration less per ray */
-	s.w8 = w8Avail ? dW8.ptr : nullptr, s.w8Root = W8TlasBlock( tlasSlot ) * 8, s.w8Base0 = 0;
 	s.root40 = 0, s.tris0 = nullptr;
 	if (singleInstanceStart && instances.size() == 1 && instances[0].mesh >= 0 && instances[0].mesh < (int)meshes.size() &&
 		meshes[instances[0].mesh]->triCount > 0)
@@ -903,7 +917,6 @@ SceneDev RenderCore::MakeSceneDev()
 		s.tlasRoot = s.tlasRoot4 = ~0;
 		s.root40 = bvh4 ? meshNode4Base[instances[0].mesh] : 0;   /* DevInstance::root4 of instance 0 (UpdateToplevel) */
 		s.tris0 = meshes[instances[0].mesh]->shadeTris.ptr;       /* lh2_CoreInstanceDesc::triangles of instance 0 */
-		if (w8Avail) s.w8Base0 = meshBlockBase[instances[0].mesh], s.w8Root = s.w8Base0 * 8;
 	}
 	s.instDesc = dInstDesc[tlasSlot].ptr, s.materials = dMaterials.ptr;
 	s.areaLights = dArea.ptr, s.pointLights = dPoint.ptr, s.spotLights = dSpot.ptr, s.dirLights = dDir.ptr;
@@ -937,7 +950,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const uint32_t pathCount = (uint32_t)tileRows * (uint32_t)scrwidth * (uint32_t)scrspp;
 	const SceneDev sd = MakeSceneDev();
 	const int frameTlas = tlasSlot;   /* the TLAS slot this frame reads (evTlasFree after its finalize) */
-	const bool frameWide = UseWide( pathCount );   /* the per-ray launches walk the W8 (setting "traceWide") */
 	/* the accumulator reset of a restart is folded into the camera launch (each pixel's first sample zeroes
 	   it; rows outside this rank's tile stay zero from SetTarget); a changed tile clears the whole frame */
 	if (restart && tileChanged) CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
@@ -1019,10 +1031,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	{
 		/* beside the previous frame (on the ahead stream, after the previous frame's shade launch before its path tail, or
 		   its first without one: the last reader of the primary buffers and of the heavy-packet block this frame records
-		   into), the frame's resets are a k_init_counters launch before it on the ahead stream (this frame's parity: the
-		   frame before the previous one, the last user of these counters and heads, is done); behind it, on the core
-		   stream, the primary launch does them itself.  Its own work-queue heads are left alone: they alternate between
-		   two slots, and the resets zero the other */
+		   into) or behind it (core stream), the primary launch does the frame's resets itself (kPrimaryResets: this frame
+		   parity's counters and heads, whose last user, the frame before the previous one, is done); only an
+		   LH2_PRIMARY_RESETS=0 build queues a k_init_counters launch before it on the ahead stream instead.  Its own
+		   work-queue heads (slot primSlot, zeroed by the finalize two frames back) are left alone */
 		primStream = serialize ? stream : aheadStream;
 		cp.keepCursor = (int)(primSlot * LH2_CURSOR_WORDS);
 		if (serialize) cp.initC = c;
@@ -1090,7 +1102,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		const bool primary = pathLength == 1 && tiledRays;
 		TraceArgs ta{};
 		ta.version = TraceVersion();
-		ta.wide = frameWide ? 1u : 0u;
 		ta.rayO = ps.rayO[ps.in].ptr, ta.rayD = ps.rayD[ps.in].ptr, ta.segCounts = segIn, ta.segStride = ps.segStride, ta.segBack = segInBack;
 		ta.cursor = cursors + (size_t)(pathLength == 1 ? primSlot : (uint32_t)pathLength) * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)refillOther;
@@ -1143,7 +1154,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				CHK_HIP( hipStreamWaitEvent( sideStream, ps.prevStop, 0 ) );
 				TraceArgs ts{};
 				ts.version = TraceVersion();
-				ts.wide = frameWide ? 1u : 0u;
 				ts.rayO = shO, ts.rayD = shD, ts.segCounts = shSnap, ts.segStride = ps.shadowStride;
 				ts.cursor = cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS;
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)kShadowLeafBatch;
@@ -1172,10 +1182,15 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			const bool beside = besideNext && !ta.packet;
 			/* traceWaves 0: 7 waves for a single instance, 8 for instanced scenes (each on its own occupancy's grid) */
 			const int waves = traceWaves ? traceWaves : sd.tlasRoot4 < 0 ? 7 : 8;
-			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, kOverlapTraceBlocks ) :
-				!traceWaves && waves == 7 ? smCount * traceBlocksPerCU7 : grid;
+			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, kOverlapTraceBlocks ) : smCount * ClosestBlocksPerCU( waves );
 			ta.traceWaves = beside ? 7u : (uint32_t)waves;   /* 8 waves slow the packets beside the launch (r04ad) */
+#ifdef LH2_TOUCH
+			TouchBegin();
+#endif
 			lh2_launch_trace_closest( &sd, &ta, g, { nullptr, ps.evTrace[pathLength] }, stream );
+#ifdef LH2_TOUCH
+			TouchReport( pathLength );
+#endif
 		}
 		ps.fromTrace[pathLength] = ps.prevStop, ps.prevStop = ps.evTrace[pathLength];
 		sp.segCounts = segIn, sp.segOut = segNext, sp.segStride = ps.segStride;
@@ -1231,7 +1246,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			   connect step), fused with finalizeConnections */
 			TraceArgs ts{};
 			ts.version = TraceVersion();
-			ts.wide = frameWide ? 1u : 0u;
 			ts.rayO = shO, ts.rayD = shD, ts.segCounts = c->segShadow, ts.segStride = ps.shadowStride;
 			ts.cursor = cursors + (size_t)(LH2_MAX_BOUNCES + pathLength) * LH2_CURSOR_WORDS;
 			ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)leafBatch;
@@ -1273,7 +1287,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	{
 		TraceArgs ta{};
 		ta.version = TraceVersion();
-		ta.wide = frameWide ? 1u : 0u;
 		ta.rayO = shO, ta.rayD = shD, ta.segCounts = c->segShadow, ta.segStride = ps.shadowStride;
 		ta.cursor = cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)kShadowLeafBatch;
@@ -1547,7 +1560,6 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 	TraceArgs ta{};
 	ta.version = TraceVersion();
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.hits = h.ptr, ta.gstack = gs.ptr;
-	ta.wide = w8Avail && traceWide != 0 ? 1u : 0u;
 	ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 	ta.packet = unitCoherent && UsePackets() ? 1 : 0;
 	ta.traceWaves = (uint32_t)unitTraceWaves;
@@ -1571,7 +1583,6 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 	TraceArgs ta{};
 	ta.version = TraceVersion();
 	ta.rayO = o.ptr, ta.rayD = d.ptr, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = ovf.ptr, ta.mask = m.ptr, ta.gstack = gs.ptr, ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
-	ta.wide = w8Avail && traceWide != 0 ? 1u : 0u;
 	lh2_launch_trace_any( &sd, &ta, TraceGrid(), 0, {}, stream );
 	std::vector<uint32_t> tmp( words );
 	CHK_HIP( hipMemcpyAsync( tmp.data(), m.ptr, words * 4, hipMemcpyDeviceToHost, stream ) );
@@ -1607,8 +1618,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 		ta.version = TraceVersion();
 		ta.rayO = (const float4*)ro, ta.rayD = (const float4*)rd, ta.countFixed = (uint32_t)n, ta.segStride = (uint32_t)((n + LH2_SEGS - 1) / LH2_SEGS), ta.cursor = cursors.ptr + (size_t)i * LH2_CURSOR_WORDS;
 		ta.hits = (uint4*)hitsOut, ta.gstack = ps.gstack.ptr;
-		ta.wide = w8Avail && traceWide != 0 ? 1u : 0u;
-		/* unitCoherent: trace as the frame traces its (tiled) primary rays */
+			/* unitCoherent: trace as the frame traces its (tiled) primary rays */
 		ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)leafBatch;
 		ta.packet = unitCoherent && UsePackets() ? 1 : 0;
 #ifdef LH2_TRACE_STATS

@@ -5,13 +5,14 @@
 #include <stdint.h>
 #include <algorithm>
 #include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/lh2_core_types.h"
 #include "bvh_build.h"
 #include "bvh_gpu.h"
-#include "lh2_w8.h"
 #include "lh2_kernels.h"
 #include "lh2_device.h"
 
@@ -44,6 +45,18 @@ template <class T> struct DevBuf
 	}
 };
 
+/* a deferred CPU BLAS build (RenderCore::FlushBuilds) and its host results.  Shared by the sub-cores of a MultiDevice:
+   the first core to flush runs it (once, std::call_once), every core uploads the results to its own device, and the last
+   reference frees them (round 6, VERDICT r5 #7: no N-fold build at deviceCount N) */
+struct HostBlas
+{
+	std::once_flag once;
+	std::function<void( HostBlas&, int )> job;   /* its argument: host threads for the build */
+	std::vector<float> nodes2, tris48, nodes4;
+	int leafTris = 0, nodeCount = 0, maxDepth = 0, depth4 = 0;
+	void Run( int threads );
+};
+
 struct CoreMeshHost   /* RenderCore always copies what it needs (rendercore.h:57): all of it on the device */
 {
 	int triCount = 0;
@@ -54,12 +67,7 @@ struct CoreMeshHost   /* RenderCore always copies what it needs (rendercore.h:57
 	int nodeCount = 0, maxDepth = 0;
 	DevBuf<float4> bvh4Nodes;            /* the same BLAS collapsed to BVH4 (CollapseBvh4), mesh-local refs */
 	int node4Count = 0, depth4 = 0;
-	DevBuf<uint32_t> w8;                 /* the same BLAS as W8 records (lh2_w8.h, child blocks relative to the mesh's first); w8Blocks 0: none */
-	int w8Blocks = 0, w8Depth = 0, w8QErr = 0;
-	/* a deferred CPU build (RenderCore::FlushBuilds): the job (its argument: threads for the build) and its results */
-	std::function<void( int )> build;
-	std::vector<float> hostNodes2, hostTris48, hostNodes4;
-	std::vector<uint32_t> hostW8;
+	std::shared_ptr<HostBlas> build;     /* a deferred CPU build not uploaded yet (null: none) */
 };
 
 struct CoreInstanceHost { int mesh; float T[16]; float inv[16]; };
@@ -145,6 +153,10 @@ public:
 		const lh2_CoreSpotLight* spotLights, int spotLightCount, const lh2_CoreDirectionalLight* directionalLights, int directionalLightCount );
 	void SetSkyData( const float* pixels, uint32_t width, uint32_t height );
 	void SetGeometry( int meshIdx, const float* vertexData, int vertexCount, int triangleCount, const lh2_CoreTri* triangles, const uint32_t* alphaFlags );
+	/* MultiDevice: the same mesh as SetGeometry, sharing src's deferred CPU BLAS build (built once, uploaded here too) */
+	void AdoptGeometry( int meshIdx, int triangleCount, const lh2_CoreTri* triangles, const RenderCore& src );
+	void FlushPendingBuilds() { FlushBuilds(); }
+	static int BlasBuildCount();         /* CPU BLAS builds run in this process (the build-once check) */
 	void SetInstance( int instanceIdx, int meshIdx, const float* matrix16 );
 	void UpdateToplevel();
 	lh2_CoreStats GetCoreStats();
@@ -193,6 +205,12 @@ private:
 	void BuildBlas4( CoreMeshHost& m, const float* nodes2 );
 	void FlushBuilds();
 	bool pendingBuilds = false;
+#ifdef LH2_TOUCH
+	DevBuf<uint32_t> touchMap;           /* diagnostic build: the touched-record bitmap (lh2_trace4d.inc) */
+	uint32_t touchNodeWords = 0;
+	void TouchBegin();
+	void TouchReport( int pathLength );
+#endif
 	int buildThreads = 0;                /* host threads of the deferred BLAS builds (setting "buildThreads"; 0: LH2_BUILD_THREADS,
 	                                        OMP_NUM_THREADS or min(16, cores)) */
 	void EnsurePaths( uint32_t paths );
@@ -217,6 +235,15 @@ private:
 	   node loads (single-instance loops only) the single-instance 8-wave loop spills, and 7 there is config 3 -3.4 %, 4K -3 %,
 	   the N = 8 share -2.9 %, while config 5 (instanced) stays 2 % faster at 8 (profiles/r05f_ab_trace_waves.txt) */
 	int traceWaves = 0;
+	int userBlocksPerCU = 0;             /* setting "traceBlocksPerCU" (0: not set) */
+	/* the closest-hit kernel variant a per-ray launch with the chip alone takes (traceWaves 0: by scene), and its grid's
+	   blocks per CU: the variant's occupancy, or the user's setting within it */
+	int ScenePicksWaves() const { return traceWaves ? traceWaves : (singleInstanceStart && instances.size() == 1) ? 7 : 8; }
+	int ClosestBlocksPerCU( int waves ) const
+	{
+		const int occ = waves == 7 ? traceBlocksPerCU7 : traceBlocksPerCU8;
+		return userBlocksPerCU ? std::min( userBlocksPerCU, occ ) : occ;
+	}
 	int unitTraceWaves = 7;              /* the unit queries' variant: 7 (the config-2 bounce rays alone: 0.481 vs 0.515 ms, r04ag) */
 	bool initialized = false;
 	/* scene */
@@ -233,23 +260,11 @@ private:
 	int tlasCapacity = 0, maxBlasDepth = 0;
 	int blasNode4Count = 0, maxBlas4Depth = 0;
 	int bvh4 = 1;                        /* build BVH4 copies of the BLAS (the default traversal loop needs them) */
-	/* the W8 (lh2_w8.h, round 5): every mesh's records, then two TLAS slots of tlasCapacity + 1 blocks; w8Avail: every mesh
-	   has one (CPU or GPU builds with one triangle per leaf) */
-	DevBuf<uint32_t> dW8;
-	DevBuf<int> dMeshBlock;              /* each mesh's first block */
-	std::vector<int> meshBlockBase;
-	int blasW8Blocks = 0, maxBlasW8Depth = 0;
-	bool w8Avail = false;
-	int W8TlasBlock( int s ) const { return blasW8Blocks + s * (tlasCapacity + 1); }
-	/* the loop over the W8 for the frame's per-ray launches (setting "traceWide"): 0 off (BVH4, no W8 built), 1 on, 2 for
-	   frames of at most kSmallFramePaths paths; the unit queries take it when nonzero.  Off by default: the W8 loop's node
-	   step costs 1.8x the BVH4's issue slots for 0.72x the steps (room bounce 0.503 vs 0.432 ms, config 3 2.28 vs 1.94 ms,
-	   the N = 8 share 1.32 vs 1.15 ms: profiles/r05_ab_w8.txt) */
-	int traceWide = 0;
-	bool UseWide( uint32_t paths ) const { return w8Avail && (traceWide == 1 || (traceWide == 2 && (float)paths <= kSmallFramePaths)); }
-	/* stack entries a ray may need: the BVH2 loop's BLAS depth, the BVH4 loop's 3 per level, the W8 loop's 2 per level (a node
-	   group and a leaf group per node step) */
-	int StackDepthBound() const { return std::max( bvh4 ? std::max( maxBlasDepth, 3 * maxBlas4Depth ) : maxBlasDepth, w8Avail ? 2 * maxBlasW8Depth + 2 : 0 ); }
+	/* the 8-wide compressed BVH of round 5 (W8, Ylitie et al. 2017) measured slower in every configuration (its node step
+	   issued 1.8x the BVH4 step's VALU for 0.72x the steps: profiles/r05_ab_w8.txt) and was removed in round 6 (commit
+	   22e0032 holds it) */
+	/* stack entries a ray may need: the BVH2 loop's BLAS depth, the BVH4 loop's 3 per level */
+	int StackDepthBound() const { return bvh4 ? std::max( maxBlasDepth, 3 * maxBlas4Depth ) : maxBlasDepth; }
 	bool tlasOnDevice = false;           /* TLAS of the last UpdateToplevel built by the GPU (depth in dTlasDepth) */
 	GpuBvhBuilder gpuBvh;
 	DevBuf<float> dMeshBounds;           /* 6 per mesh */

@@ -168,3 +168,31 @@ def test_repeated_settings_each_frame():
         ref.close()
     assert np.isfinite(a3).all() and a3[..., :3].max() > a_low[..., :3].max()
     assert rel_l2(a_low[..., :3], b_low[..., :3]) <= 1e-6
+
+
+@pytest.mark.parametrize("devices", [2, 3])
+def test_blas_built_once_per_mesh(devices):
+    """the in-core multi-device path builds each mesh's BLAS once on the host and uploads it to every
+    sub-core (RenderCore::AdoptGeometry shares core 0's deferred build), instead of one build per device.  The process's
+    CPU build count ("blasBuilds") grows by the mesh count whatever deviceCount is, and the frame still equals the
+    one-device frame."""
+    w, h = 96, 54
+    sc = scene.instanced_scene(meshes=4, tris_per_mesh=3000, width=w, height=h, grid=2, spacing=12.0)
+
+    def builds_during(n):
+        c = RenderCore(device=0)
+        try:
+            b0 = c.get_setting("blasBuilds")
+            if n > 1:
+                c.setting("deviceCount", n)
+            sc.load_into(c)
+            c.set_target(w, h, 1)
+            sc.render_frame(c, converge=1)
+            return c.get_setting("blasBuilds") - b0, c.accumulator()
+        finally:
+            c.close()
+
+    b1, a1 = builds_during(1)
+    bn, an = builds_during(devices)
+    assert b1 == len(sc.meshes) and bn == len(sc.meshes), (b1, bn)
+    assert rel_l2(an[..., :3], a1[..., :3]) <= 1e-6

@@ -405,11 +405,6 @@ def test_terminal_shade_frame_parity(fresh_core, kind):
     fresh_core.setting("terminalShade", 1)
     assert rel_l2(ag[..., :3], a0[..., :3]) <= 1e-6
     assert np.array_equal(ag[..., 3], a0[..., 3])
-    # k_shade_last on a larger grid (shadeLastBlocks per CU; 0: its occupancy): the same frame
-    fresh_core.setting("shadeLastBlocks", 20)
-    sc.render_frame(fresh_core)
-    fresh_core.setting("shadeLastBlocks", 0)
-    assert rel_l2(ag[..., :3], fresh_core.accumulator()[..., :3]) <= 1e-6
 
 
 @pytest.mark.parametrize("version", [1, 7])

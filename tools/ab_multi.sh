@@ -2,7 +2,7 @@
 # A/B of setting combinations (through gpurun): per variant (comma-separated name=value list, "base" = defaults;
 # lib=<name> loads the variant build gpuab/<name>/libRenderCore_MI355X.so, tools/build_variant.sh) the
 # config-4 rank shares at N = 1 and 8, config 3 (tools/bench_configs.py) and config 2 (bench.py, no other configs),
-# the variants interleaved, REPS rounds.  usage: VARIANTS="base prioTail=2 prioTail=2,prioShadow=2" REPS=2
+# the variants interleaved, REPS rounds.  usage: VARIANTS="base sideBlocks=3 sideBlocks=3,pathTailBlocks=2" REPS=2
 set -euo pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
 OUT="$ROOT/gpurun_out/${TAG:-abm}"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # N = 1 / N = 8 config-4 rank shares only (tools/config4_shares.py), variants interleaved, REPS rounds (through gpurun).
-# usage: VARIANTS="base sideBlocks=4 corePriority=1,sideBlocks=4" REPS=3 bash tools/ab_shares.sh
+# usage: VARIANTS="base sideBlocks=4 sideBlocks=4,finalShadowBlocks=6" REPS=3 bash tools/ab_shares.sh
 set -euo pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
 OUT="$ROOT/gpurun_out/${TAG:-abs}"
