@@ -75,18 +75,24 @@ def newest(pattern, pred=lambda d: True):
 
 
 def valu_cycles_per_instruction():
-    """Measured SIMD cycles per wave64 VALU instruction at >= 4 waves per SIMD (tools/valu_rate, committed
-    under profiles/): the fastest of its instruction mixes (v_fma_f32 chains, v_pk_fma_f32 chains, and the
-    node step's mix of packed FMA, max3 / min3, compares, selects and integer key ops, whose count comes
-    from SQ_INSTS_VALU), so the peak is the highest issue rate measured; 2 (SIMD-32, MI355X_MICROARCH.md
-    per-instruction constants) when absent."""
-    files = sorted(glob.glob(str(ROOT / "profiles" / "*valu_rate*.jsonl")))
-    if files:
-        rows = [json.loads(line) for line in open(files[-1]) if line.strip().startswith("{")]
-        rows = [r for r in rows if r.get("waves_per_simd", 0) >= 4]
-        if rows:
-            return min(r["cycles_per_wave_inst"] for r in rows), pathlib.Path(files[-1]).name
-    return 2.0, None
+    """SIMD cycles per wave64 VALU instruction at 8 waves per SIMD, measured per instruction class by tools/valu_rate
+    (round 6: per-SIMD s_memtime spans, 16 independent chains per lane, the timed loops' ISA committed beside the numbers,
+    profiles/*_valu_rate.jsonl + *_valu_rate_isa.txt).  Returns (fastest class: the VOP2 adds / multiplies, the guide's
+    "2 cycles on a SIMD-32", which is the roofline peak; the node step's own instruction mix; the file).  VOP3 forms
+    (fma, max3, pk_fma, cndmask_e64, compares into SGPRs), byte conversions and ldexp take ~4 cycles, v_rcp 8, so a kernel
+    issuing only VOP3 work tops out near half the peak; the mix ceiling is reported beside it.  Without a probe file:
+    the guide's 2 cycles for both."""
+    def tag(f):
+        m = re.match(r"r(\d+)([a-z]*)_", pathlib.Path(f).name)
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    files = sorted(glob.glob(str(ROOT / "profiles" / "*_valu_rate.jsonl")), key=tag)
+    for f in reversed(files):
+        rows = [json.loads(line) for line in open(f) if line.strip().startswith("{")]
+        rows = [r for r in rows if r.get("waves_per_simd") == 8 and r.get("cycles_per_wave_inst")]
+        mix = [r["cycles_per_wave_inst"] for r in rows if r["mode"] == "mix"]
+        if rows and mix:
+            return min(r["cycles_per_wave_inst"] for r in rows), mix[0], pathlib.Path(f).name
+    return 2.0, 2.0, None
 
 
 def cpu_baseline(sc, width, height, seconds):
@@ -398,8 +404,9 @@ def roofline_of(core, sc, W, H, dev, kernel_iters):
         # the exact variant the unit launch runs (single instance, the unit queries' waves): its counter summaries only
         # (tools/pmc_round.sh names it with --kernel; round 5's names carried a third template argument, the W8 switch)
         kname = f"k_trace_closest4d<true, {int(core.get_setting('unitTraceWaves'))}"
-    cyc, cyc_src = valu_cycles_per_instruction()
+    cyc, cyc_mix, cyc_src = valu_cycles_per_instruction()
     peak = SIMDS * CLOCK_GHZ / cyc                     # G wave64 VALU instructions / s
+    peak_mix = SIMDS * CLOCK_GHZ / cyc_mix
     sq_src, sq = newest("*_pmc_trace_sq.json", lambda d: d.get("kernel", "").startswith(kname))
     tr_src, tr = newest("*_pmc_traffic.json", lambda d: d.get("kernel", "").startswith(kname))
     fix = json.load(open(ROOT / "tests" / "golden" / "config2_bounce_visits.json"))
@@ -409,16 +416,24 @@ def roofline_of(core, sc, W, H, dev, kernel_iters):
     achieved = valu / (ms * 1e-3) / 1e9 if valu else None
     traffic = tr["bytes_per_launch"] if tr else None
     hbm_gbs = traffic / (ms * 1e-3) / 1e9 if traffic else None
+    lanes = sq.get("valu_lane_utilisation") if sq else None
+    frac = achieved / peak if achieved else None
     roof = {
         "bound": "valu", "achieved": round(achieved, 1) if achieved else None, "peak": round(peak, 1),
-        "unit": "G wave64 VALU instructions/s", "frac": round(achieved / peak, 4) if achieved else None,
+        "unit": "G wave64 VALU instructions/s", "frac": round(frac, 4) if frac else None,
         "traffic": traffic,
+        # what the frac cannot hide.  Instructions per ray (a VALU roofline rewards issuing more of them) and
+        # the frac times the lanes that do work in an instruction
+        "valu_insts_per_ray": round(valu / n, 2) if valu else None,
+        "useful_frac": round(frac * lanes, 4) if frac and lanes else None,
+        "frac_vs_mix_peak": round(achieved / peak_mix, 4) if achieved else None, "mix_peak": round(peak_mix, 1),
         "kernel": f"{kname} (per-ray BVH4 traversal, traceVersion {version}, the core's default settings) on the "
                   f"frame's {n} diffuse bounce rays, in the frame's order (two-ended segments, chordSplit)",
         "kernel_ms": round(ms, 4), "rays_per_launch": n,
-        "valu_insts_per_launch": valu, "valu_lane_utilisation": sq.get("valu_lane_utilisation") if sq else None,
-        "peak_basis": f"{SIMDS} SIMDs x {CLOCK_GHZ} GHz / {cyc:.2f} cycles per wave64 VALU instruction "
-                      f"({cyc_src or 'MI355X_MICROARCH.md: 2 (SIMD-32)'})",
+        "valu_insts_per_launch": valu, "valu_lane_utilisation": lanes,
+        "peak_basis": f"{SIMDS} SIMDs x {CLOCK_GHZ} GHz / {cyc:.3f} cycles per wave64 VALU instruction: the fastest class measured, "
+                      f"VOP2 v_add_f32 / v_mul_f32 at 8 waves per SIMD ({cyc_src or 'MI355X_MICROARCH.md: 2 (SIMD-32)'}); "
+                      f"mix_peak: the node step's instruction mix, {cyc_mix:.3f} cycles",
         "evidence": {"sq": sq_src, "traffic": tr_src},
         "hbm": {"measured_GBs": round(hbm_gbs, 1) if hbm_gbs else None,
                 "measured_frac": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs else None,
@@ -464,6 +479,23 @@ def roofline_config5(c5):
     if c5:
         cs = c5["coreStats_ms"]
         out["live_launch_ms"] = {"primary": cs["trace0"], "bounce": cs["trace1"]}
+    # the other side of the bracket.  The unique node / triangle records one closest-hit launch reads (LH2_TOUCH
+    # build, *_config5_touch.json) plus its ray and hit streams, less what the 256 MiB Infinity Cache and the L2s can hold from
+    # before the launch, must cross the HBM interface at least once: a LOWER bound of its DRAM bytes.  Priced over this run's
+    # live primary and bounce launch times (CoreStats, each with its launch gap)
+    tsrc, t = newest("*_config5_touch.json")
+    if t and c5:
+        lb = {l["kind"]: l for l in t["launches"]}
+        cs = c5["coreStats_ms"]
+        if "primary" in lb and "bounce" in lb and cs["trace0"] > 0 and cs["trace1"] > 0:
+            lo_bytes = lb["primary"]["dram_lower_bound_bytes"] + lb["bounce"]["dram_lower_bound_bytes"]
+            lo_gbs = lo_bytes / ((cs["trace0"] + cs["trace1"]) * 1e-3) / 1e9
+            out["lower_bound"] = {"achieved": round(lo_gbs, 1), "frac": round(lo_gbs / HBM_PEAK_GBS, 4), "bytes_per_frame": lo_bytes,
+                                  "unique_bytes": {k: lb[k]["unique_bytes"] for k in ("primary", "bounce")},
+                                  "evidence": tsrc,
+                                  "note": "max(0, unique bytes - 288 MiB) per launch (tools/touch_summary.py) over the live "
+                                          "primary + bounce launch times; the DRAM fraction lies between frac_lower and frac"}
+            out["frac_lower"] = out["lower_bound"]["frac"]
     return out
 
 

@@ -179,7 +179,7 @@ int lh2_packet_blocks_per_cu( void );
 void lh2_launch_shade( const SceneDev* s, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
 void lh2_launch_trace_path( const SceneDev* s, const TraceArgs* a, const ShadeParams* p, int grid, LaunchEvents ev, hipStream_t st );
 int lh2_path_blocks_per_cu( int waves );
-void lh2_touch_set( uint32_t* bitmap, uint32_t triWord );   /* LH2_TOUCH builds only (lh2_trace4d.inc) */
+void lh2_touch_set( uint32_t* bitmap, uint32_t triWord, uint32_t words );   /* LH2_TOUCH builds only (lh2_trace4d.inc) */
 void lh2_launch_spin( unsigned long long ticks, hipStream_t st );
 void lh2_launch_pack_rows( const float4* acc, float4* dst, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );
 void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int band, int bandStride, int rows, LaunchEvents ev, hipStream_t st );

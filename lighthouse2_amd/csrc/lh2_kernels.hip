@@ -260,7 +260,7 @@ __global__ __launch_bounds__( 256 ) void k_camera( const CameraParams p, const u
 	float4* __restrict__ rayD, float4* __restrict__ T4, float4* __restrict__ Q4, const int jobCount )
 {
 	const int local = threadIdx.x + blockIdx.x * blockDim.x;
-	if (p.initC) init_counters( p.initC, p.pathCount, p.segStride, p.cursors, p.cursorWords, local );
+	if (p.initC) init_counters( p.initC, p.pathCount, p.segStride, p.cursors, p.cursorWords, local, p.keepCursor );
 	if (p.hvZero && (uint32_t)local < p.hvZeroWords) p.hvZero[local] = 0;
 	if (local >= jobCount) return;
 	float4 O, D;
@@ -2246,10 +2246,12 @@ void lh2_launch_unpack_rows( const float4* src, float4* acc, int w, int y0, int 
 void lh2_shade_times( unsigned long long out[16] ) { (void)hipMemcpyFromSymbol( out, HIP_SYMBOL( lh2_shade_tt ), 16 * 8 ); }
 #endif
 #ifdef LH2_TOUCH
-void lh2_touch_set( uint32_t* bitmap, uint32_t triWord )
+void lh2_touch_set( uint32_t* bitmap, uint32_t triWord, uint32_t words )
 {
+	const uint32_t bits = bitmap ? words * 32u : 0u;
 	(void)hipMemcpyToSymbol( HIP_SYMBOL( lh2_touch ), &bitmap, sizeof( bitmap ) );
 	(void)hipMemcpyToSymbol( HIP_SYMBOL( lh2_touchTri ), &triWord, sizeof( triWord ) );
+	(void)hipMemcpyToSymbol( HIP_SYMBOL( lh2_touchBits ), &bits, sizeof( bits ) );
 }
 #endif
 void lh2_launch_spin( unsigned long long ticks, hipStream_t st ) { hipLaunchKernelGGL( k_spin, dim3( 1 ), dim3( 64 ), 0, st, ticks ); }

@@ -100,9 +100,15 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	{
 		int least = 0, greatest = 0;
 		CHK_HIP( hipDeviceGetStreamPriorityRange( &least, &greatest ) );
-		CHK_HIP( hipStreamCreateWithPriority( &stream, hipStreamNonBlocking, least ) );
+		/* LH2_CHAIN_PRIORITY 1 (A/B builds): the core and ahead streams, which carry the frames' chains, at the greatest
+		   priority, the side stream (shadow launches, and the finish of frames that finish behind) at the least */
+#ifndef LH2_CHAIN_PRIORITY
+#define LH2_CHAIN_PRIORITY 0
+#endif
+		const int chain = LH2_CHAIN_PRIORITY ? greatest : least;
+		CHK_HIP( hipStreamCreateWithPriority( &stream, hipStreamNonBlocking, chain ) );
 		CHK_HIP( hipStreamCreateWithPriority( &sideStream, hipStreamNonBlocking, least ) );
-		CHK_HIP( hipStreamCreateWithPriority( &aheadStream, hipStreamNonBlocking, least ) );
+		CHK_HIP( hipStreamCreateWithPriority( &aheadStream, hipStreamNonBlocking, chain ) );
 	}
 	/* blue noise sampler tables (rendercore.cpp:125-134), shipped as data/bluenoise.bin */
 	std::string path = getenv( "LH2_BLUENOISE" ) ? getenv( "LH2_BLUENOISE" ) : LibraryDir() + "/data/bluenoise.bin";
@@ -138,6 +144,8 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipEventCreate( &ps.evShadow ) );
 	CHK_HIP( hipEventCreate( &ps.evSide ) );
 	CHK_HIP( hipEventCreateWithFlags( &ps.evEarlyEnd, hipEventDisableTiming ) );
+	CHK_HIP( hipEventCreateWithFlags( &ps.evJoin, hipEventDisableTiming ) );
+	CHK_HIP( hipEventCreateWithFlags( &ps.evFinish, hipEventDisableTiming ) );
 	ps.shSnap.resize( 2 * LH2_SEGS * LH2_SEGCOUNT_STRIDE );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
@@ -160,6 +168,7 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 
 void RenderCore::SetTarget( uint32_t w, uint32_t h, uint32_t spp )  /* rendercore.cpp:149-209 */
 {
+	JoinFinish();
 	if (spp < 1) spp = 1;
 	if ((uint64_t)w * h * spp > (1u << 24)) FatalError( "path index exceeds 24 bits (camera.h:92): %ux%u x %u spp", w, h, spp );
 	scrwidth = (int)w, scrheight = (int)h, scrspp = (int)spp;
@@ -175,6 +184,7 @@ void RenderCore::SetTarget( uint32_t w, uint32_t h, uint32_t spp )  /* rendercor
    as the reference's interop does; ID 0 (headless RenderSystem, tests, bench) skips it. */
 void RenderCore::SetInteropTexture( uint32_t glTextureId )
 {
+	JoinFinish();
 	if (glTextureId == glTexture && (glResource || !glTextureId)) return;
 	if (glResource) { CHK_HIP( hipStreamSynchronize( stream ) ); (void)hipGraphicsUnregisterResource( glResource ); glResource = nullptr; }
 	glTexture = glTextureId;
@@ -212,6 +222,9 @@ void RenderCore::EnsurePaths( uint32_t paths )
 {
 	if ((size_t)paths + 64 > ps.cap)
 	{
+		JoinFinish();
+		CHK_HIP( hipStreamSynchronize( stream ) );
+		CHK_HIP( hipStreamSynchronize( aheadStream ) );
 		ps.cap = (size_t)paths + (paths >> 4) + 64;
 		for (int i = 0; i < 2; i++) ps.rayO[i].resize( ps.cap ), ps.rayD[i].resize( ps.cap ), ps.T4[i].resize( ps.cap ), ps.Q4[i].resize( ps.cap );
 		ps.hits.resize( ps.cap );
@@ -231,6 +244,7 @@ void RenderCore::EnsureStack()
 	const size_t need = (size_t)(LH2_STACK_TOTAL - LH2_STACK_LDS) * smCount * maxBlocksPerCU * 256;
 	if (ps.gstack.count < need) ps.gstack.resize( need );
 	if (shadowOverlap && ps.sideStack.count < need) ps.sideStack.resize( need );
+	if (cameraFused && kCamAhead && ps.aheadStack.count < need) ps.aheadStack.resize( need );
 }
 
 void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439-457 */
@@ -312,6 +326,7 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 
 void RenderCore::SetTextures( const lh2_CoreTexDesc* tex, int textureCount )   /* rendercore.cpp:276-292 */
 {
+	JoinFinish();
 	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	texDescs.assign( tex, tex + std::max( 0, textureCount ) );
 	/* SyncStorageType (rendercore.cpp:299-336) for ARGB32, ARGB128 and NRM32: one continuous array per
@@ -347,6 +362,7 @@ void RenderCore::SetTextures( const lh2_CoreTexDesc* tex, int textureCount )   /
 #define TOUINT4(a,b,c,d) (TOCHAR(a)+(TOCHAR(b)<<8)+(TOCHAR(c)<<16)+(TOCHAR(d)<<24))
 void RenderCore::SetMaterials( const lh2_CoreMaterial* mat, int n )   /* rendercore.cpp:353-399 */
 {
+	JoinFinish();
 	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	std::vector<uint4> recs( (size_t)std::max( n, 1 ) * 8 );
 	memset( recs.data(), 0, recs.size() * sizeof( uint4 ) );
@@ -397,6 +413,7 @@ void RenderCore::SetMaterials( const lh2_CoreMaterial* mat, int n )   /* renderc
 void RenderCore::SetLights( const lh2_CoreLightTri* a, int na, const lh2_CorePointLight* p, int np, const lh2_CoreSpotLight* s, int ns,
 	const lh2_CoreDirectionalLight* d, int nd )   /* rendercore.cpp:405-419 */
 {
+	JoinFinish();
 	sceneVersion++;
 	dArea.upload( a, na, stream ), dPoint.upload( p, np, stream ), dSpot.upload( s, ns, stream ), dDir.upload( d, nd, stream );
 	dArea.resize( 1 ), dPoint.resize( 1 ), dSpot.resize( 1 ), dDir.resize( 1 );
@@ -406,6 +423,7 @@ void RenderCore::SetLights( const lh2_CoreLightTri* a, int na, const lh2_CorePoi
 
 void RenderCore::SetSkyData( const float* pixels, uint32_t width, uint32_t height )   /* rendercore.cpp:425-433 */
 {
+	JoinFinish();
 	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	dSky.upload( pixels, (size_t)width * height * 3, stream );
 	dSky.resize( 1 );
@@ -422,6 +440,7 @@ void HostBlas::Run( int threads )
 
 void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount, const lh2_CoreTri* tris, const uint32_t* )
 {
+	JoinFinish();
 	sceneVersion++;
 	/* rendercore.cpp:215-223 + core_mesh.cpp:36-67: meshes arrive first-time in sequential order */
 	if (meshIdx < 0 || meshIdx > (int)meshes.size()) FatalError( "SetGeometry: mesh index %d out of sequence", meshIdx );
@@ -576,6 +595,7 @@ void RenderCore::FlushBuilds()
    build (gpuBuild), or a mesh src has already uploaded, is built here as SetGeometry builds it */
 void RenderCore::AdoptGeometry( int meshIdx, int triangleCount, const lh2_CoreTri* tris, const RenderCore& src )
 {
+	JoinFinish();
 	const CoreMeshHost* sm = meshIdx >= 0 && meshIdx < (int)src.meshes.size() ? src.meshes[meshIdx] : nullptr;
 	if (!sm || !sm->build || sm->triCount != triangleCount || bvh4 != src.bvh4)
 	{
@@ -604,15 +624,16 @@ void RenderCore::AdoptGeometry( int meshIdx, int triangleCount, const lh2_CoreTr
    count (the build is for this count, not for timing) */
 void RenderCore::TouchBegin()
 {
+	CHK_HIP( hipDeviceSynchronize() );   /* nothing in flight reads the bitmap pointer while it changes */
 	const uint32_t nodeWords = (uint32_t)(((size_t)blasNode4Count + 2 * tlasCapacity + 31) / 32), triWords = (uint32_t)(((size_t)blasTriCount + 31) / 32);
 	touchMap.resize( (size_t)nodeWords + triWords );
 	CHK_HIP( hipMemsetAsync( touchMap.ptr, 0, sizeof( uint32_t ) * ((size_t)nodeWords + triWords), stream ) );
-	lh2_touch_set( touchMap.ptr, nodeWords );
+	lh2_touch_set( touchMap.ptr, nodeWords, nodeWords + triWords );
 	touchNodeWords = nodeWords;
 }
 void RenderCore::TouchReport( int pathLength )
 {
-	CHK_HIP( hipStreamSynchronize( stream ) );
+	CHK_HIP( hipDeviceSynchronize() );
 	std::vector<uint32_t> h( touchMap.count );
 	CHK_HIP( hipMemcpy( h.data(), touchMap.ptr, sizeof( uint32_t ) * h.size(), hipMemcpyDeviceToHost ) );
 	uint64_t nodes = 0, tris = 0;
@@ -620,6 +641,7 @@ void RenderCore::TouchReport( int pathLength )
 	fprintf( stderr, "LH2_TOUCH {\"pathLength\": %d, \"unique_nodes\": %llu, \"unique_tri_records\": %llu, \"node_bytes\": %llu, "
 		"\"tri_bytes\": %llu, \"scene_nodes\": %d, \"scene_tri_records\": %d, \"paths\": %u}\n", pathLength, (unsigned long long)nodes,
 		(unsigned long long)tris, (unsigned long long)nodes * 64ull, (unsigned long long)tris * 48ull, blasNode4Count, blasTriCount, ps.count );
+	lh2_touch_set( nullptr, 0, 0 );   /* later closest-hit launches (unit queries) record nothing */
 }
 #endif
 
@@ -649,6 +671,7 @@ void RenderCore::SetInstance( int instanceIdx, int meshIdx, const float* M )   /
 /* scene node array = all BLAS (relocated, device to device) followed by room for the TLAS */
 void RenderCore::ConcatenateBlas( int ni )
 {
+	JoinFinish();
 	FlushBuilds();
 	meshNodeBase.assign( meshes.size(), 0 ), meshTriBase.assign( meshes.size(), 0 ), meshNode4Base.assign( meshes.size(), 0 );
 	int nodeTotal = 0, triTotal = 0, node4Total = 0, meshTris = 0;
@@ -773,6 +796,7 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 	/* a slot's tables grow only with the work that may read them drained (DevBuf::resize frees the old buffer) */
 	if (dInst[ts].count < nRec * sizeof( DevInstance ) || dInstDesc[ts].count < nRec || dInstT.count < nRec * 16 || dInstMesh.count < nRec)
 	{
+		JoinFinish();
 		CHK_HIP( hipStreamSynchronize( stream ) );
 		CHK_HIP( hipStreamSynchronize( us ) );
 		dInst[ts].resize( nRec * sizeof( DevInstance ) ), dInstDesc[ts].resize( nRec ), dInstT.resize( nRec * 16 ), dInstMesh.resize( nRec );
@@ -952,7 +976,11 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const int frameTlas = tlasSlot;   /* the TLAS slot this frame reads (evTlasFree after its finalize) */
 	/* the accumulator reset of a restart is folded into the camera launch (each pixel's first sample zeroes
 	   it; rows outside this rank's tile stay zero from SetTarget); a changed tile clears the whole frame */
-	if (restart && tileChanged) CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
+	if (restart && tileChanged)
+	{
+		JoinFinish();
+		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
+	}
 	EnsurePaths( pathCount );
 	/* segmented path / ray streams (lh2_kernels.h): LH2_SEGS segments of segStride records; shadow rays in
 	   segments of shadowStride */
@@ -1012,22 +1040,49 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	/* the camera fused into the primary packet launch: the heavy-packet block it records into must be zero (the previous
 	   fused frame's first shade launch zeroed it) */
 	const bool fusedCam = cameraFused && tiledRays && UsePackets() && !primeRef;
-	/* the fused primary launch beside the previous frame (frame overlap), or behind it on the core stream: on a restart
-	   (the launch zeroes accumulator pixels), after a change of scene data, buffers or tile, or when the previous frame
-	   had no fused primary launch */
+	/* round 6: a frame whose primary rays are traced per ray (no packets: a scene beyond the Infinity Cache,
+	   config 5) takes the same frame overlap.  Its camera launch (with the frame's resets) and its per-ray primary launch
+	   write the frame parity's primary buffers on the ahead stream, the primary launch with a global stack of its own
+	   (PathStreams::aheadStack: the previous frame's bounce launch still uses gstack) */
+	const bool camAhead = kCamAhead && !fusedCam && cameraFused && !primeRef && TraceVersion() == 7;
+	const bool pFrame = fusedCam || camAhead;   /* the frame's primary stage may run beside the previous frame */
+	/* the primary stage beside the previous frame (frame overlap), or behind it on the core stream: on a restart (the
+	   launch zeroes accumulator pixels), after a change of scene data, buffers or tile, or when the previous frame had no
+	   such primary stage */
 	const bool serialize = !frameOverlap || !ps.lastFused || ps.relaid || tileChanged || sceneVersion != ps.lastSceneVersion;
-	/* a restart beside the previous frame: the accumulator is zeroed on the core stream, behind the previous frame's finalize
-	   and before this frame's first addition there (the early shade adds into the delta), not by the primary launch */
-	if (fusedCam && !serialize && cp.clearAcc)
+	int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
+	/* no specular event and no alpha cut-out in any material: every path ends at its second vertex,
+	   so the bounce after it would be empty; not launching it saves three launches (~25 us) */
+	if (!primeRef && diffuseOnly) maxPL = std::min( maxPL, 2 );
+	/* the path tail (setting "pathTail"): bounces pathTail .. maxPL in one launch of k_trace_path4d */
+	const int tailL = (!primeRef && pathTail >= 2 && pathTail <= maxPL && TraceVersion() == 7) ? pathTail : 0;
+	/* without lights no path samples one (RandomPointOnLight: lightPdf 0), so there are no shadow
+	   rays and their launches are not queued */
+	const bool shadows = nArea + nPoint + nSpot + nDir > 0;
+	/* round 6: a small lit frame beside the previous one finishes behind its chain.  Its shadow launches and
+	   its finalize run on the side stream, and every addition of the frame goes into its accumulator delta, which the
+	   finalize folds in (in frame order: the finalizes are in side-stream order), so the next frame's chain (primary ->
+	   first shade -> bounce -> shade -> path tail) follows this frame's path tail on the core stream at once, and this
+	   frame's shadow rays fill the chip beside it.  The next frame's primary launch (its resets of the parity block the frame
+	   before this one used) waits for a side-stream marker past that frame's finalize (PathStreams::evJoin) */
+	const bool behind = kFinishBehind && !primeRef && shadows && tailL && shadowOverlap && (float)pathCount <= kSmallFramePaths && pFrame &&
+		!serialize;
+	if (!behind) JoinFinish();   /* the previous frame finished behind: this frame's launches order after its finalize */
+	/* a restart beside the previous frame: the accumulator is zeroed behind the previous frame's finalize and before this
+	   frame's first addition there (the early shade, and every launch of a frame that finishes behind, add into the delta),
+	   not by the primary launch: on the core stream, or for a frame that finishes behind on the side stream */
+	if (pFrame && !serialize && cp.clearAcc)
 	{
-		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
+		if (behind && !finishTrailing && frameEndRecorded) CHK_HIP( hipStreamWaitEvent( sideStream, evFrame[1], 0 ) );
+		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, behind ? sideStream : stream ) );
 		cp.clearAcc = nullptr;
 	}
 	hipStream_t primStream = stream;
 	/* the primary launch's work-queue heads: slot 1 of the frame parity's block, zeroed by the finalize of the frame before
 	   the previous one (FrameStatsDev::zeroHeads) */
 	const uint32_t primSlot = 1u;
-	if (fusedCam)
+	cp.keepCursor = -1;   /* a camera launch behind the previous frame resets every work-queue head */
+	if (pFrame)
 	{
 		/* beside the previous frame (on the ahead stream, after the previous frame's shade launch before its path tail, or
 		   its first without one: the last reader of the primary buffers and of the heavy-packet block this frame records
@@ -1054,36 +1109,33 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	}
 	ps.hvNextZeroed = false;
 	uint32_t* hvReadBlock = nullptr;
-	int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
-	/* no specular event and no alpha cut-out in any material: every path ends at its second vertex,
-	   so the bounce after it would be empty; not launching it saves three launches (~25 us) */
-	if (!primeRef && diffuseOnly) maxPL = std::min( maxPL, 2 );
-	/* the path tail (setting "pathTail"): bounces pathTail .. maxPL in one launch of k_trace_path4d */
-	const int tailL = (!primeRef && pathTail >= 2 && pathTail <= maxPL && TraceVersion() == 7) ? pathTail : 0;
 	/* early shade: the first shade launch follows the primary launch on the ahead stream and writes the ping-pong buffer
 	   the previous frame's launches after its overlap event do not use (PathStreams::busy / earlyOk).  Only when this
 	   frame has a path tail from bounce 3 on: else its first shade launch is its overlap event (and, with the tail from
 	   bounce 2, its shadow snapshot), and on the ahead stream neither would follow the previous frame's finalize (the
 	   side shadow launch and the next frames' early shades would add into the accumulator and the delta before the
 	   previous frame is finalized) */
-	const bool early = fusedCam && !serialize && earlyShade && frameOverlap == 1 && ps.earlyOk && (float)pathCount <= kSmallFramePaths &&
+	const bool early = pFrame && !serialize && earlyShade && frameOverlap == 1 && ps.earlyOk && (float)pathCount <= kSmallFramePaths &&
 		tailL >= 3;
 	ps.early = early;
 	ps.in = early ? ps.busy : 0;
 	ps.earlyOk = false;
 	/* the frame's start: a marker before the camera launch (~4 us of idle GPU), not the launch's own start
 	   event (hipExtLaunchKernelGGL start events cost ~8 us: tools/launch_gap.hip, profiles/r02q_launch_gap.txt) */
-	CHK_HIP( hipEventRecord( evFrame[0], fusedCam ? primStream : stream ) );
+	CHK_HIP( hipEventRecord( evFrame[0], pFrame ? primStream : stream ) );
 	if (fusedCam) ps.prevStop = evFrame[0];
+	else if (camAhead)
+	{
+		lh2_launch_camera( &cp, dBlueNoise.ptr, ps.rayOP[ps.fp].ptr, ps.rayDP[ps.fp].ptr, ps.T4P[ps.fp].ptr, ps.Q4P[ps.fp].ptr, (int)pathCount,
+			{ nullptr, ps.evCamera }, primStream );
+		ps.prevStop = ps.evCamera;
+	}
 	else
 	{
 		lh2_launch_camera( &cp, dBlueNoise.ptr, ps.rayO[0].ptr, ps.rayD[0].ptr, ps.T4[0].ptr, ps.Q4[0].ptr, (int)pathCount, { nullptr, ps.evCamera }, stream );
 		ps.prevStop = ps.evCamera;
 	}
 	if (restart) tileChanged = false;
-	/* without lights no path samples one (RandomPointOnLight: lightPdf 0), so there are no shadow
-	   rays and their launches are not queued */
-	const bool shadows = nArea + nPoint + nSpot + nDir > 0;
 	frameShadows = shadows;
 	/* shadow overlap: the shade launch before the tail snapshots the queued shadow rays (advance_bounce) */
 	const bool overlap = shadows && tailL && shadowOverlap;
@@ -1108,7 +1160,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.packet = primary && UsePackets() ? 1 : 0;
 		ta.leafBatch = (uint32_t)leafBatch;
 		ta.hits = ps.hits.ptr, ta.gstack = ps.gstack.ptr;
-		const bool fusedPrimary = pathLength == 1 && fusedCam;   /* the primary buffers (PathStreams::rayOP ..) */
+		const bool fusedPrimary = pathLength == 1 && pFrame;   /* the primary buffers (PathStreams::rayOP ..) */
 		if (fusedPrimary) ta.rayO = ps.rayOP[ps.fp].ptr, ta.rayD = ps.rayDP[ps.fp].ptr, ta.hits = ps.hitsP[ps.fp].ptr;
 		if (pathLength == 1 && ta.packet && ps.hvOn)
 		{
@@ -1126,7 +1178,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ShadeParams sp{};
 		sp.shadowStride = ps.shadowStride;
 		sp.shO = shO, sp.shD = shD, sp.shP = shP;
-		sp.acc = accumulator.ptr, sp.counters = c;
+		sp.acc = behind ? frameDelta : accumulator.ptr, sp.counters = c;
 		sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
 		sp.probePixel = probeX + scrwidth * probeY;
 		sp.spreadAngle = view.spreadAngle;
@@ -1152,12 +1204,13 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				/* the shadow rays of the bounces before the tail, beside it on the side stream (segment counts:
 				   the snapshot; the final launch's work-queue heads start behind them) */
 				CHK_HIP( hipStreamWaitEvent( sideStream, ps.prevStop, 0 ) );
+				if (behind) CHK_HIP( hipEventRecord( ps.evJoin, sideStream ) );   /* past the previous frame's finalize too */
 				TraceArgs ts{};
 				ts.version = TraceVersion();
 				ts.rayO = shO, ts.rayD = shD, ts.segCounts = shSnap, ts.segStride = ps.shadowStride;
 				ts.cursor = cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS;
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)kShadowLeafBatch;
-				ts.mask = shMask, ts.potentials = shP, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
+				ts.mask = shMask, ts.potentials = shP, ts.acc = behind ? frameDelta : accumulator.ptr, ts.gstack = ps.sideStack.ptr;
 				/* the global stack (sideStack) is sized for maxBlocksPerCU blocks per CU: the grid stays within it */
 				lh2_launch_trace_any( &sd, &ts, sideBlocks > 0 ? smCount * std::min( sideBlocks, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evSide }, sideStream );
 				ps.fromSide = ps.prevStop;
@@ -1167,7 +1220,17 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			ps.tailL = pathLength;   /* no shade interval of its own (Synchronize) */
 			break;
 		}
-		if (fusedPrimary)
+		if (fusedPrimary && camAhead)
+		{
+			/* the per-ray primary launch after its camera launch (the camera's resets set the dense segment counts); beside the
+			   previous frame it walks with a global stack of its own; the core stream waits for it */
+			const int waves = traceWaves ? traceWaves : sd.tlasRoot4 < 0 ? 7 : 8;
+			ta.traceWaves = (uint32_t)waves;
+			if (primStream != stream) ta.gstack = ps.aheadStack.ptr;
+			lh2_launch_trace_closest( &sd, &ta, smCount * ClosestBlocksPerCU( waves ), { nullptr, ps.evTrace[pathLength] }, primStream );
+			if (primStream != stream && !early) CHK_HIP( hipStreamWaitEvent( stream, ps.evTrace[pathLength], 0 ) );
+		}
+		else if (fusedPrimary)
 		{
 			/* the paths are dense (camera order): fixed counts, no segment counters; the core stream waits for it */
 			ta.segCounts = nullptr, ta.segBack = nullptr, ta.countFixed = pathCount;
@@ -1278,10 +1341,18 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipEventRecord( ps.evEarlyEnd, stream ) );
 		ps.overlapEv = ps.evEarlyEnd;
 	}
+	/* the frame's finish: its final shadow launch and finalize on the core stream, or, finishing behind, on the side stream
+	   after the chain's last launch (the path tail), with the side stream's global stack */
+	hipStream_t fin = stream;
+	if (behind)
+	{
+		fin = sideStream;
+		CHK_HIP( hipStreamWaitEvent( sideStream, ps.prevStop, 0 ) );
+	}
 	/* a snapshot whose side launch did not happen (the frame ended before its path tail): the final launch
 	   traces every shadow ray, from the first */
 	if (snapped && !ps.sideOn)
-		CHK_HIP( hipMemsetAsync( cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
+		CHK_HIP( hipMemsetAsync( cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, fin ) );
 	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
 	if (!primeRef && shadows)
 	{
@@ -1290,17 +1361,17 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.rayO = shO, ta.rayD = shD, ta.segCounts = c->segShadow, ta.segStride = ps.shadowStride;
 		ta.cursor = cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)kShadowLeafBatch;
-		ta.mask = shMask, ta.potentials = shP, ta.acc = accumulator.ptr, ta.gstack = ps.gstack.ptr;
+		ta.mask = shMask, ta.potentials = shP, ta.acc = behind ? frameDelta : accumulator.ptr, ta.gstack = behind ? ps.sideStack.ptr : ps.gstack.ptr;
 		/* the global stack (gstack) is sized for maxBlocksPerCU blocks per CU: the grid stays within it */
-		lh2_launch_trace_any( &sd, &ta, finalShadowBlocks > 0 ? smCount * std::min( finalShadowBlocks, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evShadow }, stream );
+		lh2_launch_trace_any( &sd, &ta, finalShadowBlocks > 0 ? smCount * std::min( finalShadowBlocks, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evShadow }, fin );
 		ps.fromShadow = ps.prevStop;
 	}
 	/* the side launch's contributions are in the accumulator before the frame is finalized */
-	if (ps.sideOn) CHK_HIP( hipStreamWaitEvent( stream, ps.evSide, 0 ) );
+	if (ps.sideOn && !behind) CHK_HIP( hipStreamWaitEvent( stream, ps.evSide, 0 ) );
 	samplesTaken += scrspp;
 	/* finalize also delivers the frame's counters and ray-count log, and the scene error, to hostStats */
 	const FrameStatsDev fs{ c, rayLog + 1, &hostStats->counters, hostStats->rayCount + 1, SceneErr( frameTlas ), &hostStats->sceneError,
-		cursors + (size_t)primSlot * LH2_CURSOR_WORDS, early ? frameDelta : nullptr };
+		cursors + (size_t)primSlot * LH2_CURSOR_WORDS, early || behind ? frameDelta : nullptr };
 	/* a tile finalizes its own rows only (a rank of the band partition: the gathered frame is finalized
 	   where it is assembled, MultiDevice / FinalizeFrame) */
 	RowMap rm{};
@@ -1308,21 +1379,31 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	/* the previous frame's end stays recorded (evFrame[2]): an overlapped frame's render time starts at the later of
 	   its primary launch's start and the previous frame's end (Synchronize), so per-frame times sum to wall time */
 	std::swap( evFrame[1], evFrame[2] );
-	prevFrameEndValid = frameEndRecorded, frameWasOverlapped = fusedCam && !serialize;
-	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, &fs, { nullptr, evFrame[1] }, stream, &rm );
+	prevFrameEndValid = frameEndRecorded, frameWasOverlapped = pFrame && !serialize;
+	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, &fs, { nullptr, evFrame[1] }, fin, &rm );
 	frameEndRecorded = true;
-	CHK_HIP( hipEventRecord( evTlasFree[frameTlas], stream ) );   /* the next update of this TLAS slot waits for it */
+	CHK_HIP( hipEventRecord( evTlasFree[frameTlas], fin ) );   /* the next update of this TLAS slot waits for it */
 	tlasFreeValid[frameTlas] = true;
 	if (glResource && !displayAtFinalize)
 	{
 		hipArray_t arr = nullptr;
-		CHK_HIP( hipGraphicsMapResources( 1, &glResource, stream ) );
+		CHK_HIP( hipGraphicsMapResources( 1, &glResource, fin ) );
 		CHK_HIP( hipGraphicsSubResourceGetMappedArray( &arr, glResource, 0, 0 ) );
-		CHK_HIP( hipMemcpy2DToArrayAsync( arr, 0, 0, frame.ptr, sizeof( float4 ) * scrwidth, sizeof( float4 ) * scrwidth, scrheight, hipMemcpyDeviceToDevice, stream ) );
-		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, stream ) );
+		CHK_HIP( hipMemcpy2DToArrayAsync( arr, 0, 0, frame.ptr, sizeof( float4 ) * scrwidth, sizeof( float4 ) * scrwidth, scrheight, hipMemcpyDeviceToDevice, fin ) );
+		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, fin ) );
 	}
+	if (behind)
+	{
+		/* the frame's end on the side stream: what later calls order themselves after (JoinFinish); the next frame's primary
+		   launch waits for the marker past the previous frame's finalize (evJoin), or for this frame's end when its side
+		   launch did not happen */
+		CHK_HIP( hipEventRecord( ps.evFinish, sideStream ) );
+		if (!ps.sideOn) CHK_HIP( hipEventRecord( ps.evJoin, sideStream ) );
+		ps.overlapEv = ps.evJoin;
+	}
+	finishTrailing = behind;
 	hostStats->rayCount[0] = ps.count;
-	ps.lastFused = fusedCam, ps.lastSceneVersion = sceneVersion;
+	ps.lastFused = pFrame, ps.lastSceneVersion = sceneVersion;
 	framePathLengths = ps.tailL ? maxPL : ps.pl;
 	framePrimeRef = primeRef;
 	statsPending = true;
@@ -1331,6 +1412,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 
 void RenderCore::UnpackTile( const void* devSrc, int rank, int nranks, int band )
 {
+	JoinFinish();
 	int rows = 0;
 	for (int y = rank * band; y < scrheight; y += nranks * band) rows += std::min( band, scrheight - y );
 	lh2_launch_unpack_rows( (const float4*)devSrc, accumulator.ptr, scrwidth, rank * band, band, nranks * band, rows, {}, stream );
@@ -1338,6 +1420,7 @@ void RenderCore::UnpackTile( const void* devSrc, int rank, int nranks, int band 
 
 void RenderCore::FinalizeFrame()
 {
+	JoinFinish();
 	if (!samplesTaken) return;
 	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, nullptr, {}, stream );
 	if (glResource)
@@ -1352,6 +1435,7 @@ void RenderCore::FinalizeFrame()
 
 void RenderCore::CopyFrameAsync( void* devDst )
 {
+	JoinFinish();
 	CHK_HIP( hipMemcpyAsync( devDst, frame.ptr, sizeof( float4 ) * (size_t)scrwidth * scrheight, hipMemcpyDeviceToDevice, stream ) );
 }
 
@@ -1379,6 +1463,8 @@ void RenderCore::Synchronize()
 {
 	CHK_HIP( hipStreamSynchronize( aheadStream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
+	CHK_HIP( hipStreamSynchronize( sideStream ) );   /* a frame finished behind its chain (kFinishBehind) */
+	finishTrailing = false;
 	if (!statsPending) return;
 	statsPending = false;
 	const Counters& cn = hostStats->counters;
@@ -1450,6 +1536,7 @@ void RenderCore::GetRayCounts( uint32_t* out17 )
 
 int RenderCore::DebugShadowRays( float* o4, float* d4, float* p4, int cap )
 {
+	JoinFinish();
 	Synchronize();
 	int n = 0;
 	for (int k = 0; k < LH2_SEGS; k++)
@@ -1468,6 +1555,7 @@ int RenderCore::DebugShadowRays( float* o4, float* d4, float* p4, int cap )
 
 int RenderCore::DebugBvh4( float* f32Nodes, uint32_t* qNodes, int cap )
 {
+	JoinFinish();
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	Synchronize();
 	SyncTlas();
@@ -1491,6 +1579,7 @@ int RenderCore::DebugBvh4( float* f32Nodes, uint32_t* qNodes, int cap )
    earlier, larger TLAS or an uninitialised allocation leaves behind the nodes a TLAS update writes */
 void RenderCore::DebugPoisonTlas( float value )
 {
+	JoinFinish();
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	Synchronize();
 	SyncTlas();
@@ -1507,18 +1596,21 @@ void RenderCore::DebugPoisonTlas( float value )
 
 void RenderCore::GetAccumulator( float* hostOut4 )
 {
+	JoinFinish();
 	Synchronize();
 	CHK_HIP( hipMemcpy( hostOut4, accumulator.ptr, sizeof( float4 ) * (size_t)scrwidth * scrheight, hipMemcpyDeviceToHost ) );
 }
 
 void RenderCore::CopyAccumulatorRows( void* devDst, int y0, int y1 )
 {
+	JoinFinish();
 	CHK_HIP( hipMemcpyAsync( devDst, accumulator.ptr + (size_t)y0 * scrwidth, sizeof( float4 ) * (size_t)(y1 - y0) * scrwidth, hipMemcpyDeviceToDevice, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 }
 
 void RenderCore::PackTile( void* devDst, bool ordered, void* consumer )
 {
+	JoinFinish();
 	const int rows = TileRows();
 	const int band = tileBand > 0 ? tileBand : std::max( 1, rows ), stride = tileBand > 0 ? tileStride : std::max( 1, rows );
 	/* asynchronous: consumers on other streams order themselves after the core stream (lh2_core_stream),
@@ -1544,12 +1636,14 @@ void RenderCore::PackTile( void* devDst, bool ordered, void* consumer )
 
 void RenderCore::GetFrame( float* hostOut4 )
 {
+	JoinFinish();
 	Synchronize();
 	CHK_HIP( hipMemcpy( hostOut4, frame.ptr, sizeof( float4 ) * (size_t)scrwidth * scrheight, hipMemcpyDeviceToHost ) );
 }
 
 void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t* hits4 )
 {
+	JoinFinish();
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	DevBuf<float4> o, d; DevBuf<uint4> h; DevBuf<int> gs; DevBuf<uint32_t> ovf;
 	o.upload( (const float4*)ot, n, stream ), d.upload( (const float4*)dt, n, stream );
@@ -1571,6 +1665,7 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 
 void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* occluded )
 {
+	JoinFinish();
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	DevBuf<float4> o, d; DevBuf<uint32_t> m; DevBuf<int> gs; DevBuf<uint32_t> ovf;
 	o.upload( (const float4*)ot, n, stream ), d.upload( (const float4*)dt, n, stream );
@@ -1593,6 +1688,7 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 
 void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void* hitsOut, int iterations, float* msOut )
 {
+	JoinFinish();
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	EnsureStack();
 	const SceneDev sd = MakeSceneDev();
@@ -1658,6 +1754,7 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 
 void RenderCore::GenerateEyeRays( const lh2_ViewPyramid& view, uint32_t R0, int pass, float* ot, float* dt, float* st )
 {
+	JoinFinish();
 	const int n = scrwidth * scrheight * scrspp;
 	DevBuf<float4> o, d, t4, q4;
 	o.resize( n ), d.resize( n ), t4.resize( n ), q4.resize( n );
@@ -1701,6 +1798,7 @@ extern "C" void lh2_shade_times( unsigned long long out[16] );
 void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 {
 	if (!initialized) return;
+	JoinFinish();
 	(void)hipStreamSynchronize( stream );
 #ifdef LH2_SHADE_TIMES
 	{
@@ -1719,7 +1817,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto& e : ps.evShade) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evShadowB) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evCount) (void)hipEventDestroy( e ), e = nullptr;
-	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow, &ps.evSide, &ps.evEarlyEnd }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
+	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow, &ps.evSide, &ps.evEarlyEnd, &ps.evJoin, &ps.evFinish }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
 	if (ps.activeLog) (void)hipHostFree( ps.activeLog );
 	ps.activeLog = nullptr;
 	for (hipEvent_t* e : { &evConsumer, &evPacked }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }

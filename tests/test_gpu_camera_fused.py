@@ -50,11 +50,15 @@ def _animate(sc, tgt, f):
     tgt.update_toplevel()
 
 
+# packets -1: the core's choice (packets for these scenes: the fused camera + packet launch); 0: primary rays traced per ray
+# (config 5's case: round 6 overlaps those frames too, a camera launch + per-ray primary launch on the ahead stream)
+@pytest.mark.parametrize("packets", [-1, 0])
 @pytest.mark.parametrize("kind", ["room", "config2", "instanced"])
-def test_camera_fused_frames(fresh_core, kind):
+def test_camera_fused_frames(fresh_core, kind, packets):
     w, h = 128, 72
     sc, depth = _scene(kind, w, h)
     anim = kind == "instanced"            # instances move every frame: each primary launch waits for the update
+    fresh_core.setting("packetPrimary", packets)
     sc.load_into(fresh_core)
     fresh_core.set_target(w, h, 1)
     o = Oracle()
@@ -93,8 +97,9 @@ def test_camera_fused_frames(fresh_core, kind):
         assert np.array_equal(a[..., 3], res[k][..., 3]), k
 
 
+@pytest.mark.parametrize("packets", [-1, 0])
 @pytest.mark.parametrize("kind", ["room", "config2", "instanced"])
-def test_animated_restart_frames(fresh_core, kind):
+def test_animated_restart_frames(fresh_core, kind, packets):
     """tinyapp's animated loop (apps/tinyapp/main.cpp:98-118): SetInstance + UpdateToplevel and Render(Restart) every
     frame.  An instance-only UpdateToplevel writes the TLAS slot no frame in flight reads, on the ahead stream behind
     the last frame that read it, and a restart beside the previous frame zeroes the accumulator on the core stream, so
@@ -106,6 +111,7 @@ def test_animated_restart_frames(fresh_core, kind):
     if kind == "config2":
         sc.sky = scene.gradient_sky(64, 32)   # something to accumulate (config 2 has no lights)
     base = list(sc.instances)
+    fresh_core.setting("packetPrimary", packets)
     sc.load_into(fresh_core)
     fresh_core.set_target(w, h, 1)
     fresh_core.setting("maxPathLength", depth)
@@ -183,7 +189,8 @@ def test_animated_frames_with_new_geometry(gpu_build):
         assert rel_l2(b[..., :3], a[..., :3]) <= 1e-6, overlap
 
 
-def test_early_frame_ending_before_its_tail(fresh_core):
+@pytest.mark.parametrize("packets", [-1, 0])
+def test_early_frame_ending_before_its_tail(fresh_core, packets):
     """with the path tail from bounce 4, an early frame (its first shade launch on the ahead stream, beside the
     previous frame's tail) whose paths all end at their first vertex (every primary ray misses: the camera looks away from
     the room) leaves the bounce loop before the shade launch before its tail.  Its overlap event, which the next frames'
@@ -194,6 +201,7 @@ def test_early_frame_ending_before_its_tail(fresh_core):
     sc = scene.room_scene(40000, w, h)
     room_view = sc.view
     away = scene.camera_view((0, 6, 200), (0, 0, 1), fov_deg=60, aspect=w / h, focal=5, pixel_height=h)
+    fresh_core.setting("packetPrimary", packets)
     sc.load_into(fresh_core)
     fresh_core.set_target(w, h, 1)
     fresh_core.setting("maxPathLength", 6)
