@@ -100,15 +100,9 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	{
 		int least = 0, greatest = 0;
 		CHK_HIP( hipDeviceGetStreamPriorityRange( &least, &greatest ) );
-		/* LH2_CHAIN_PRIORITY 1 (A/B builds): the core and ahead streams, which carry the frames' chains, at the greatest
-		   priority, the side stream (shadow launches, and the finish of frames that finish behind) at the least */
-#ifndef LH2_CHAIN_PRIORITY
-#define LH2_CHAIN_PRIORITY 0
-#endif
-		const int chain = LH2_CHAIN_PRIORITY ? greatest : least;
-		CHK_HIP( hipStreamCreateWithPriority( &stream, hipStreamNonBlocking, chain ) );
+		CHK_HIP( hipStreamCreateWithPriority( &stream, hipStreamNonBlocking, least ) );
 		CHK_HIP( hipStreamCreateWithPriority( &sideStream, hipStreamNonBlocking, least ) );
-		CHK_HIP( hipStreamCreateWithPriority( &aheadStream, hipStreamNonBlocking, chain ) );
+		CHK_HIP( hipStreamCreateWithPriority( &aheadStream, hipStreamNonBlocking, least ) );
 	}
 	/* blue noise sampler tables (rendercore.cpp:125-134), shipped as data/bluenoise.bin */
 	std::string path = getenv( "LH2_BLUENOISE" ) ? getenv( "LH2_BLUENOISE" ) : LibraryDir() + "/data/bluenoise.bin";
@@ -144,8 +138,6 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 	CHK_HIP( hipEventCreate( &ps.evShadow ) );
 	CHK_HIP( hipEventCreate( &ps.evSide ) );
 	CHK_HIP( hipEventCreateWithFlags( &ps.evEarlyEnd, hipEventDisableTiming ) );
-	CHK_HIP( hipEventCreateWithFlags( &ps.evJoin, hipEventDisableTiming ) );
-	CHK_HIP( hipEventCreateWithFlags( &ps.evFinish, hipEventDisableTiming ) );
 	ps.shSnap.resize( 2 * LH2_SEGS * LH2_SEGCOUNT_STRIDE );
 	CHK_HIP( hipHostMalloc( (void**)&hostStats, sizeof( FrameStats ), hipHostMallocCoherent ) );   /* written by k_finalize (system scope) */
 	memset( hostStats, 0, sizeof( FrameStats ) );
@@ -168,7 +160,6 @@ void RenderCore::Init()   /* rendercore.cpp:96-143 */
 
 void RenderCore::SetTarget( uint32_t w, uint32_t h, uint32_t spp )  /* rendercore.cpp:149-209 */
 {
-	JoinFinish();
 	if (spp < 1) spp = 1;
 	if ((uint64_t)w * h * spp > (1u << 24)) FatalError( "path index exceeds 24 bits (camera.h:92): %ux%u x %u spp", w, h, spp );
 	scrwidth = (int)w, scrheight = (int)h, scrspp = (int)spp;
@@ -184,7 +175,6 @@ void RenderCore::SetTarget( uint32_t w, uint32_t h, uint32_t spp )  /* rendercor
    as the reference's interop does; ID 0 (headless RenderSystem, tests, bench) skips it. */
 void RenderCore::SetInteropTexture( uint32_t glTextureId )
 {
-	JoinFinish();
 	if (glTextureId == glTexture && (glResource || !glTextureId)) return;
 	if (glResource) { CHK_HIP( hipStreamSynchronize( stream ) ); (void)hipGraphicsUnregisterResource( glResource ); glResource = nullptr; }
 	glTexture = glTextureId;
@@ -222,9 +212,6 @@ void RenderCore::EnsurePaths( uint32_t paths )
 {
 	if ((size_t)paths + 64 > ps.cap)
 	{
-		JoinFinish();
-		CHK_HIP( hipStreamSynchronize( stream ) );
-		CHK_HIP( hipStreamSynchronize( aheadStream ) );
 		ps.cap = (size_t)paths + (paths >> 4) + 64;
 		for (int i = 0; i < 2; i++) ps.rayO[i].resize( ps.cap ), ps.rayD[i].resize( ps.cap ), ps.T4[i].resize( ps.cap ), ps.Q4[i].resize( ps.cap );
 		ps.hits.resize( ps.cap );
@@ -326,7 +313,6 @@ bool RenderCore::GetSetting( const char* name, float& value ) const
 
 void RenderCore::SetTextures( const lh2_CoreTexDesc* tex, int textureCount )   /* rendercore.cpp:276-292 */
 {
-	JoinFinish();
 	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	texDescs.assign( tex, tex + std::max( 0, textureCount ) );
 	/* SyncStorageType (rendercore.cpp:299-336) for ARGB32, ARGB128 and NRM32: one continuous array per
@@ -362,7 +348,6 @@ void RenderCore::SetTextures( const lh2_CoreTexDesc* tex, int textureCount )   /
 #define TOUINT4(a,b,c,d) (TOCHAR(a)+(TOCHAR(b)<<8)+(TOCHAR(c)<<16)+(TOCHAR(d)<<24))
 void RenderCore::SetMaterials( const lh2_CoreMaterial* mat, int n )   /* rendercore.cpp:353-399 */
 {
-	JoinFinish();
 	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	std::vector<uint4> recs( (size_t)std::max( n, 1 ) * 8 );
 	memset( recs.data(), 0, recs.size() * sizeof( uint4 ) );
@@ -413,7 +398,6 @@ void RenderCore::SetMaterials( const lh2_CoreMaterial* mat, int n )   /* renderc
 void RenderCore::SetLights( const lh2_CoreLightTri* a, int na, const lh2_CorePointLight* p, int np, const lh2_CoreSpotLight* s, int ns,
 	const lh2_CoreDirectionalLight* d, int nd )   /* rendercore.cpp:405-419 */
 {
-	JoinFinish();
 	sceneVersion++;
 	dArea.upload( a, na, stream ), dPoint.upload( p, np, stream ), dSpot.upload( s, ns, stream ), dDir.upload( d, nd, stream );
 	dArea.resize( 1 ), dPoint.resize( 1 ), dSpot.resize( 1 ), dDir.resize( 1 );
@@ -423,7 +407,6 @@ void RenderCore::SetLights( const lh2_CoreLightTri* a, int na, const lh2_CorePoi
 
 void RenderCore::SetSkyData( const float* pixels, uint32_t width, uint32_t height )   /* rendercore.cpp:425-433 */
 {
-	JoinFinish();
 	sceneVersion++;   /* device-resident scene data: the next fused frame's primary launch waits for the previous frame */
 	dSky.upload( pixels, (size_t)width * height * 3, stream );
 	dSky.resize( 1 );
@@ -440,7 +423,6 @@ void HostBlas::Run( int threads )
 
 void RenderCore::SetGeometry( int meshIdx, const float*, int, int triangleCount, const lh2_CoreTri* tris, const uint32_t* )
 {
-	JoinFinish();
 	sceneVersion++;
 	/* rendercore.cpp:215-223 + core_mesh.cpp:36-67: meshes arrive first-time in sequential order */
 	if (meshIdx < 0 || meshIdx > (int)meshes.size()) FatalError( "SetGeometry: mesh index %d out of sequence", meshIdx );
@@ -595,7 +577,6 @@ void RenderCore::FlushBuilds()
    build (gpuBuild), or a mesh src has already uploaded, is built here as SetGeometry builds it */
 void RenderCore::AdoptGeometry( int meshIdx, int triangleCount, const lh2_CoreTri* tris, const RenderCore& src )
 {
-	JoinFinish();
 	const CoreMeshHost* sm = meshIdx >= 0 && meshIdx < (int)src.meshes.size() ? src.meshes[meshIdx] : nullptr;
 	if (!sm || !sm->build || sm->triCount != triangleCount || bvh4 != src.bvh4)
 	{
@@ -671,7 +652,6 @@ void RenderCore::SetInstance( int instanceIdx, int meshIdx, const float* M )   /
 /* scene node array = all BLAS (relocated, device to device) followed by room for the TLAS */
 void RenderCore::ConcatenateBlas( int ni )
 {
-	JoinFinish();
 	FlushBuilds();
 	meshNodeBase.assign( meshes.size(), 0 ), meshTriBase.assign( meshes.size(), 0 ), meshNode4Base.assign( meshes.size(), 0 );
 	int nodeTotal = 0, triTotal = 0, node4Total = 0, meshTris = 0;
@@ -796,7 +776,6 @@ void RenderCore::UpdateToplevel()   /* rendercore.cpp:250-270 (TLAS) + :481-505 
 	/* a slot's tables grow only with the work that may read them drained (DevBuf::resize frees the old buffer) */
 	if (dInst[ts].count < nRec * sizeof( DevInstance ) || dInstDesc[ts].count < nRec || dInstT.count < nRec * 16 || dInstMesh.count < nRec)
 	{
-		JoinFinish();
 		CHK_HIP( hipStreamSynchronize( stream ) );
 		CHK_HIP( hipStreamSynchronize( us ) );
 		dInst[ts].resize( nRec * sizeof( DevInstance ) ), dInstDesc[ts].resize( nRec ), dInstT.resize( nRec * 16 ), dInstMesh.resize( nRec );
@@ -976,11 +955,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	const int frameTlas = tlasSlot;   /* the TLAS slot this frame reads (evTlasFree after its finalize) */
 	/* the accumulator reset of a restart is folded into the camera launch (each pixel's first sample zeroes
 	   it; rows outside this rank's tile stay zero from SetTarget); a changed tile clears the whole frame */
-	if (restart && tileChanged)
-	{
-		JoinFinish();
-		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
-	}
+	if (restart && tileChanged) CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
 	EnsurePaths( pathCount );
 	/* segmented path / ray streams (lh2_kernels.h): LH2_SEGS segments of segStride records; shadow rays in
 	   segments of shadowStride */
@@ -1050,31 +1025,11 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	   launch zeroes accumulator pixels), after a change of scene data, buffers or tile, or when the previous frame had no
 	   such primary stage */
 	const bool serialize = !frameOverlap || !ps.lastFused || ps.relaid || tileChanged || sceneVersion != ps.lastSceneVersion;
-	int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
-	/* no specular event and no alpha cut-out in any material: every path ends at its second vertex,
-	   so the bounce after it would be empty; not launching it saves three launches (~25 us) */
-	if (!primeRef && diffuseOnly) maxPL = std::min( maxPL, 2 );
-	/* the path tail (setting "pathTail"): bounces pathTail .. maxPL in one launch of k_trace_path4d */
-	const int tailL = (!primeRef && pathTail >= 2 && pathTail <= maxPL && TraceVersion() == 7) ? pathTail : 0;
-	/* without lights no path samples one (RandomPointOnLight: lightPdf 0), so there are no shadow
-	   rays and their launches are not queued */
-	const bool shadows = nArea + nPoint + nSpot + nDir > 0;
-	/* round 6: a small lit frame beside the previous one finishes behind its chain.  Its shadow launches and
-	   its finalize run on the side stream, and every addition of the frame goes into its accumulator delta, which the
-	   finalize folds in (in frame order: the finalizes are in side-stream order), so the next frame's chain (primary ->
-	   first shade -> bounce -> shade -> path tail) follows this frame's path tail on the core stream at once, and this
-	   frame's shadow rays fill the chip beside it.  The next frame's primary launch (its resets of the parity block the frame
-	   before this one used) waits for a side-stream marker past that frame's finalize (PathStreams::evJoin) */
-	const bool behind = kFinishBehind && !primeRef && shadows && tailL && shadowOverlap && (float)pathCount <= kSmallFramePaths && pFrame &&
-		!serialize;
-	if (!behind) JoinFinish();   /* the previous frame finished behind: this frame's launches order after its finalize */
-	/* a restart beside the previous frame: the accumulator is zeroed behind the previous frame's finalize and before this
-	   frame's first addition there (the early shade, and every launch of a frame that finishes behind, add into the delta),
-	   not by the primary launch: on the core stream, or for a frame that finishes behind on the side stream */
+	/* a restart beside the previous frame: the accumulator is zeroed on the core stream, behind the previous frame's finalize
+	   and before this frame's first addition there (the early shade adds into the delta), not by the primary launch */
 	if (pFrame && !serialize && cp.clearAcc)
 	{
-		if (behind && !finishTrailing && frameEndRecorded) CHK_HIP( hipStreamWaitEvent( sideStream, evFrame[1], 0 ) );
-		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, behind ? sideStream : stream ) );
+		CHK_HIP( hipMemsetAsync( accumulator.ptr, 0, sizeof( float4 ) * (size_t)scrwidth * scrheight, stream ) );
 		cp.clearAcc = nullptr;
 	}
 	hipStream_t primStream = stream;
@@ -1109,6 +1064,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	}
 	ps.hvNextZeroed = false;
 	uint32_t* hvReadBlock = nullptr;
+	int maxPL = primeRef ? LH2_MAX_BOUNCES : maxPathLength;
+	/* no specular event and no alpha cut-out in any material: every path ends at its second vertex,
+	   so the bounce after it would be empty; not launching it saves three launches (~25 us) */
+	if (!primeRef && diffuseOnly) maxPL = std::min( maxPL, 2 );
+	/* the path tail (setting "pathTail"): bounces pathTail .. maxPL in one launch of k_trace_path4d */
+	const int tailL = (!primeRef && pathTail >= 2 && pathTail <= maxPL && TraceVersion() == 7) ? pathTail : 0;
 	/* early shade: the first shade launch follows the primary launch on the ahead stream and writes the ping-pong buffer
 	   the previous frame's launches after its overlap event do not use (PathStreams::busy / earlyOk).  Only when this
 	   frame has a path tail from bounce 3 on: else its first shade launch is its overlap event (and, with the tail from
@@ -1136,6 +1097,9 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ps.prevStop = ps.evCamera;
 	}
 	if (restart) tileChanged = false;
+	/* without lights no path samples one (RandomPointOnLight: lightPdf 0), so there are no shadow
+	   rays and their launches are not queued */
+	const bool shadows = nArea + nPoint + nSpot + nDir > 0;
 	frameShadows = shadows;
 	/* shadow overlap: the shade launch before the tail snapshots the queued shadow rays (advance_bounce) */
 	const bool overlap = shadows && tailL && shadowOverlap;
@@ -1178,7 +1142,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ShadeParams sp{};
 		sp.shadowStride = ps.shadowStride;
 		sp.shO = shO, sp.shD = shD, sp.shP = shP;
-		sp.acc = behind ? frameDelta : accumulator.ptr, sp.counters = c;
+		sp.acc = accumulator.ptr, sp.counters = c;
 		sp.w = scrwidth, sp.h = scrheight, sp.pass = samplesTaken, sp.pathLength = pathLength, sp.maxPathLength = maxPL;
 		sp.probePixel = probeX + scrwidth * probeY;
 		sp.spreadAngle = view.spreadAngle;
@@ -1204,13 +1168,12 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				/* the shadow rays of the bounces before the tail, beside it on the side stream (segment counts:
 				   the snapshot; the final launch's work-queue heads start behind them) */
 				CHK_HIP( hipStreamWaitEvent( sideStream, ps.prevStop, 0 ) );
-				if (behind) CHK_HIP( hipEventRecord( ps.evJoin, sideStream ) );   /* past the previous frame's finalize too */
 				TraceArgs ts{};
 				ts.version = TraceVersion();
 				ts.rayO = shO, ts.rayD = shD, ts.segCounts = shSnap, ts.segStride = ps.shadowStride;
 				ts.cursor = cursors + (size_t)(LH2_SHADOW_SLOT + 1) * LH2_CURSOR_WORDS;
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)kShadowLeafBatch;
-				ts.mask = shMask, ts.potentials = shP, ts.acc = behind ? frameDelta : accumulator.ptr, ts.gstack = ps.sideStack.ptr;
+				ts.mask = shMask, ts.potentials = shP, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
 				/* the global stack (sideStack) is sized for maxBlocksPerCU blocks per CU: the grid stays within it */
 				lh2_launch_trace_any( &sd, &ts, sideBlocks > 0 ? smCount * std::min( sideBlocks, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evSide }, sideStream );
 				ps.fromSide = ps.prevStop;
@@ -1341,18 +1304,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		CHK_HIP( hipEventRecord( ps.evEarlyEnd, stream ) );
 		ps.overlapEv = ps.evEarlyEnd;
 	}
-	/* the frame's finish: its final shadow launch and finalize on the core stream, or, finishing behind, on the side stream
-	   after the chain's last launch (the path tail), with the side stream's global stack */
-	hipStream_t fin = stream;
-	if (behind)
-	{
-		fin = sideStream;
-		CHK_HIP( hipStreamWaitEvent( sideStream, ps.prevStop, 0 ) );
-	}
 	/* a snapshot whose side launch did not happen (the frame ended before its path tail): the final launch
 	   traces every shadow ray, from the first */
 	if (snapped && !ps.sideOn)
-		CHK_HIP( hipMemsetAsync( cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, fin ) );
+		CHK_HIP( hipMemsetAsync( cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS, 0, sizeof( uint32_t ) * LH2_CURSOR_WORDS, stream ) );
 	/* shadow rays + fused finalizeConnections (rendercore.cpp:575-592) */
 	if (!primeRef && shadows)
 	{
@@ -1361,17 +1316,17 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		ta.rayO = shO, ta.rayD = shD, ta.segCounts = c->segShadow, ta.segStride = ps.shadowStride;
 		ta.cursor = cursors + (size_t)LH2_SHADOW_SLOT * LH2_CURSOR_WORDS;
 		ta.refill = (uint32_t)refillOther, ta.leafBatch = (uint32_t)kShadowLeafBatch;
-		ta.mask = shMask, ta.potentials = shP, ta.acc = behind ? frameDelta : accumulator.ptr, ta.gstack = behind ? ps.sideStack.ptr : ps.gstack.ptr;
+		ta.mask = shMask, ta.potentials = shP, ta.acc = accumulator.ptr, ta.gstack = ps.gstack.ptr;
 		/* the global stack (gstack) is sized for maxBlocksPerCU blocks per CU: the grid stays within it */
-		lh2_launch_trace_any( &sd, &ta, finalShadowBlocks > 0 ? smCount * std::min( finalShadowBlocks, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evShadow }, fin );
+		lh2_launch_trace_any( &sd, &ta, finalShadowBlocks > 0 ? smCount * std::min( finalShadowBlocks, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evShadow }, stream );
 		ps.fromShadow = ps.prevStop;
 	}
 	/* the side launch's contributions are in the accumulator before the frame is finalized */
-	if (ps.sideOn && !behind) CHK_HIP( hipStreamWaitEvent( stream, ps.evSide, 0 ) );
+	if (ps.sideOn) CHK_HIP( hipStreamWaitEvent( stream, ps.evSide, 0 ) );
 	samplesTaken += scrspp;
 	/* finalize also delivers the frame's counters and ray-count log, and the scene error, to hostStats */
 	const FrameStatsDev fs{ c, rayLog + 1, &hostStats->counters, hostStats->rayCount + 1, SceneErr( frameTlas ), &hostStats->sceneError,
-		cursors + (size_t)primSlot * LH2_CURSOR_WORDS, early || behind ? frameDelta : nullptr };
+		cursors + (size_t)primSlot * LH2_CURSOR_WORDS, early ? frameDelta : nullptr };
 	/* a tile finalizes its own rows only (a rank of the band partition: the gathered frame is finalized
 	   where it is assembled, MultiDevice / FinalizeFrame) */
 	RowMap rm{};
@@ -1380,28 +1335,18 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	   its primary launch's start and the previous frame's end (Synchronize), so per-frame times sum to wall time */
 	std::swap( evFrame[1], evFrame[2] );
 	prevFrameEndValid = frameEndRecorded, frameWasOverlapped = pFrame && !serialize;
-	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, &fs, { nullptr, evFrame[1] }, fin, &rm );
+	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, &fs, { nullptr, evFrame[1] }, stream, &rm );
 	frameEndRecorded = true;
-	CHK_HIP( hipEventRecord( evTlasFree[frameTlas], fin ) );   /* the next update of this TLAS slot waits for it */
+	CHK_HIP( hipEventRecord( evTlasFree[frameTlas], stream ) );   /* the next update of this TLAS slot waits for it */
 	tlasFreeValid[frameTlas] = true;
 	if (glResource && !displayAtFinalize)
 	{
 		hipArray_t arr = nullptr;
-		CHK_HIP( hipGraphicsMapResources( 1, &glResource, fin ) );
+		CHK_HIP( hipGraphicsMapResources( 1, &glResource, stream ) );
 		CHK_HIP( hipGraphicsSubResourceGetMappedArray( &arr, glResource, 0, 0 ) );
-		CHK_HIP( hipMemcpy2DToArrayAsync( arr, 0, 0, frame.ptr, sizeof( float4 ) * scrwidth, sizeof( float4 ) * scrwidth, scrheight, hipMemcpyDeviceToDevice, fin ) );
-		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, fin ) );
+		CHK_HIP( hipMemcpy2DToArrayAsync( arr, 0, 0, frame.ptr, sizeof( float4 ) * scrwidth, sizeof( float4 ) * scrwidth, scrheight, hipMemcpyDeviceToDevice, stream ) );
+		CHK_HIP( hipGraphicsUnmapResources( 1, &glResource, stream ) );
 	}
-	if (behind)
-	{
-		/* the frame's end on the side stream: what later calls order themselves after (JoinFinish); the next frame's primary
-		   launch waits for the marker past the previous frame's finalize (evJoin), or for this frame's end when its side
-		   launch did not happen */
-		CHK_HIP( hipEventRecord( ps.evFinish, sideStream ) );
-		if (!ps.sideOn) CHK_HIP( hipEventRecord( ps.evJoin, sideStream ) );
-		ps.overlapEv = ps.evJoin;
-	}
-	finishTrailing = behind;
 	hostStats->rayCount[0] = ps.count;
 	ps.lastFused = pFrame, ps.lastSceneVersion = sceneVersion;
 	framePathLengths = ps.tailL ? maxPL : ps.pl;
@@ -1412,7 +1357,6 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 
 void RenderCore::UnpackTile( const void* devSrc, int rank, int nranks, int band )
 {
-	JoinFinish();
 	int rows = 0;
 	for (int y = rank * band; y < scrheight; y += nranks * band) rows += std::min( band, scrheight - y );
 	lh2_launch_unpack_rows( (const float4*)devSrc, accumulator.ptr, scrwidth, rank * band, band, nranks * band, rows, {}, stream );
@@ -1420,7 +1364,6 @@ void RenderCore::UnpackTile( const void* devSrc, int rank, int nranks, int band 
 
 void RenderCore::FinalizeFrame()
 {
-	JoinFinish();
 	if (!samplesTaken) return;
 	lh2_launch_finalize( accumulator.ptr, frame.ptr, scrwidth * scrheight, 1.0f / (float)samplesTaken, nullptr, {}, stream );
 	if (glResource)
@@ -1435,7 +1378,6 @@ void RenderCore::FinalizeFrame()
 
 void RenderCore::CopyFrameAsync( void* devDst )
 {
-	JoinFinish();
 	CHK_HIP( hipMemcpyAsync( devDst, frame.ptr, sizeof( float4 ) * (size_t)scrwidth * scrheight, hipMemcpyDeviceToDevice, stream ) );
 }
 
@@ -1463,8 +1405,6 @@ void RenderCore::Synchronize()
 {
 	CHK_HIP( hipStreamSynchronize( aheadStream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
-	CHK_HIP( hipStreamSynchronize( sideStream ) );   /* a frame finished behind its chain (kFinishBehind) */
-	finishTrailing = false;
 	if (!statsPending) return;
 	statsPending = false;
 	const Counters& cn = hostStats->counters;
@@ -1536,7 +1476,6 @@ void RenderCore::GetRayCounts( uint32_t* out17 )
 
 int RenderCore::DebugShadowRays( float* o4, float* d4, float* p4, int cap )
 {
-	JoinFinish();
 	Synchronize();
 	int n = 0;
 	for (int k = 0; k < LH2_SEGS; k++)
@@ -1555,7 +1494,6 @@ int RenderCore::DebugShadowRays( float* o4, float* d4, float* p4, int cap )
 
 int RenderCore::DebugBvh4( float* f32Nodes, uint32_t* qNodes, int cap )
 {
-	JoinFinish();
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	Synchronize();
 	SyncTlas();
@@ -1579,7 +1517,6 @@ int RenderCore::DebugBvh4( float* f32Nodes, uint32_t* qNodes, int cap )
    earlier, larger TLAS or an uninitialised allocation leaves behind the nodes a TLAS update writes */
 void RenderCore::DebugPoisonTlas( float value )
 {
-	JoinFinish();
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	Synchronize();
 	SyncTlas();
@@ -1596,21 +1533,18 @@ void RenderCore::DebugPoisonTlas( float value )
 
 void RenderCore::GetAccumulator( float* hostOut4 )
 {
-	JoinFinish();
 	Synchronize();
 	CHK_HIP( hipMemcpy( hostOut4, accumulator.ptr, sizeof( float4 ) * (size_t)scrwidth * scrheight, hipMemcpyDeviceToHost ) );
 }
 
 void RenderCore::CopyAccumulatorRows( void* devDst, int y0, int y1 )
 {
-	JoinFinish();
 	CHK_HIP( hipMemcpyAsync( devDst, accumulator.ptr + (size_t)y0 * scrwidth, sizeof( float4 ) * (size_t)(y1 - y0) * scrwidth, hipMemcpyDeviceToDevice, stream ) );
 	CHK_HIP( hipStreamSynchronize( stream ) );
 }
 
 void RenderCore::PackTile( void* devDst, bool ordered, void* consumer )
 {
-	JoinFinish();
 	const int rows = TileRows();
 	const int band = tileBand > 0 ? tileBand : std::max( 1, rows ), stride = tileBand > 0 ? tileStride : std::max( 1, rows );
 	/* asynchronous: consumers on other streams order themselves after the core stream (lh2_core_stream),
@@ -1636,14 +1570,12 @@ void RenderCore::PackTile( void* devDst, bool ordered, void* consumer )
 
 void RenderCore::GetFrame( float* hostOut4 )
 {
-	JoinFinish();
 	Synchronize();
 	CHK_HIP( hipMemcpy( hostOut4, frame.ptr, sizeof( float4 ) * (size_t)scrwidth * scrheight, hipMemcpyDeviceToHost ) );
 }
 
 void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t* hits4 )
 {
-	JoinFinish();
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	DevBuf<float4> o, d; DevBuf<uint4> h; DevBuf<int> gs; DevBuf<uint32_t> ovf;
 	o.upload( (const float4*)ot, n, stream ), d.upload( (const float4*)dt, n, stream );
@@ -1665,7 +1597,6 @@ void RenderCore::TraceClosest( const float* ot, const float* dt, int n, uint32_t
 
 void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* occluded )
 {
-	JoinFinish();
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	DevBuf<float4> o, d; DevBuf<uint32_t> m; DevBuf<int> gs; DevBuf<uint32_t> ovf;
 	o.upload( (const float4*)ot, n, stream ), d.upload( (const float4*)dt, n, stream );
@@ -1688,7 +1619,6 @@ void RenderCore::TraceAny( const float* ot, const float* dt, int n, uint32_t* oc
 
 void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void* hitsOut, int iterations, float* msOut )
 {
-	JoinFinish();
 	if (geometryDirty || instancesDirty) UpdateToplevel();
 	EnsureStack();
 	const SceneDev sd = MakeSceneDev();
@@ -1754,7 +1684,6 @@ void RenderCore::TraceClosestDevice( const void* ro, const void* rd, int n, void
 
 void RenderCore::GenerateEyeRays( const lh2_ViewPyramid& view, uint32_t R0, int pass, float* ot, float* dt, float* st )
 {
-	JoinFinish();
 	const int n = scrwidth * scrheight * scrspp;
 	DevBuf<float4> o, d, t4, q4;
 	o.resize( n ), d.resize( n ), t4.resize( n ), q4.resize( n );
@@ -1798,7 +1727,6 @@ extern "C" void lh2_shade_times( unsigned long long out[16] );
 void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 {
 	if (!initialized) return;
-	JoinFinish();
 	(void)hipStreamSynchronize( stream );
 #ifdef LH2_SHADE_TIMES
 	{
@@ -1817,7 +1745,7 @@ void RenderCore::Shutdown()   /* rendercore.cpp:615-650 */
 	for (auto& e : ps.evShade) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evShadowB) (void)hipEventDestroy( e ), e = nullptr;
 	for (auto& e : ps.evCount) (void)hipEventDestroy( e ), e = nullptr;
-	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow, &ps.evSide, &ps.evEarlyEnd, &ps.evJoin, &ps.evFinish }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
+	for (hipEvent_t* e : { &ps.evCamera, &ps.evShadow, &ps.evSide, &ps.evEarlyEnd }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }
 	if (ps.activeLog) (void)hipHostFree( ps.activeLog );
 	ps.activeLog = nullptr;
 	for (hipEvent_t* e : { &evConsumer, &evPacked }) { if (*e) (void)hipEventDestroy( *e ); *e = nullptr; }

@@ -121,9 +121,6 @@ struct PathStreams
 	uint64_t lastSceneVersion = 0;
 	hipEvent_t overlapEv = nullptr;      /* the last frame's shade launch the next primary launch waits for (not owned) */
 	hipEvent_t evEarlyEnd = nullptr;     /* an early frame that ended before its path tail: overlapEv on the core stream (owned) */
-	/* a frame that finishes behind its chain (RenderCore::kFinishBehind): the side-stream marker past the previous frame's
-	   finalize (the next frame's overlap event) and the frame's end on the side stream (owned) */
-	hipEvent_t evJoin = nullptr, evFinish = nullptr;
 	hipEvent_t prevStop = nullptr;
 	int fp = 0;                          /* this (the last) frame's parity */
 	/* early shade (setting "earlyShade"): the next frame's first shade launch also runs beside this frame's launches
@@ -372,25 +369,14 @@ private:
 #ifndef LH2_CAM_AHEAD
 #define LH2_CAM_AHEAD 1
 #endif
-	/* frames traced per ray (no packets) overlap like packet frames: camera + per-ray primary launch on the ahead stream */
+	/* frames traced per ray (no packets) overlap like packet frames: camera + per-ray primary launch on the ahead stream
+	   (config 5 9.70-9.73 -> 9.48-9.51 ms, profiles/r06b_ab_cam_ahead.txt); the touch build counts one closest-hit launch at a
+	   time (TouchReport), so it keeps them behind the previous frame */
 #ifdef LH2_TOUCH
-	static constexpr bool kCamAhead = false;   /* the touch build counts one closest-hit launch at a time (TouchReport) */
+	static constexpr bool kCamAhead = false;
 #else
 	static constexpr bool kCamAhead = LH2_CAM_AHEAD != 0;
 #endif
-#ifndef LH2_FINISH_BEHIND
-#define LH2_FINISH_BEHIND 1
-#endif
-	/* small lit frames beside the previous frame finish (shadow launches, finalize) on the side stream (Render) */
-	static constexpr bool kFinishBehind = LH2_FINISH_BEHIND != 0;
-	bool finishTrailing = false;         /* the last frame finished behind: the core stream has not waited for it yet */
-	/* calls other than the next overlapped frame order the core stream after the last frame's end (its side-stream work) */
-	void JoinFinish()
-	{
-		if (!finishTrailing) return;
-		if (hipStreamWaitEvent( stream, ps.evFinish, 0 ) != hipSuccess) FatalError( "hipStreamWaitEvent (JoinFinish) failed" );
-		finishTrailing = false;
-	}
 	int bvhMaxLeaf = 1;
 	/* spatial splits (SBVH): overlap threshold x root area; 0 = off.  1e-3 (round 4; 1e-5 before): the same node steps and
 	   triangle tests per ray (tools/bvh_quality.cpp: config 2 26.62 / 6.78 vs 26.64 / 6.68, the room 14.58 / 1.83 both)

@@ -27,12 +27,13 @@ CLOCK_GHZ = 2.4
 
 
 def cycles_per_valu():
-    """SIMD cycles per wave64 VALU instruction measured by tools/valu_rate (committed jsonl), else 2."""
+    """SIMD cycles per wave64 VALU instruction of the fastest class tools/valu_rate measured at 8 waves per SIMD (round 6:
+    the VOP2 fp32 add / multiply, 2.17; bench.py's roofline peak), else the guide's 2."""
     import glob
-    files = sorted(glob.glob(str(ROOT / "profiles" / "*valu_rate*.jsonl")))
+    files = sorted(glob.glob(str(ROOT / "profiles" / "*_valu_rate.jsonl")))
     if files:
         rows = [json.loads(x) for x in open(files[-1]) if x.strip().startswith("{")]
-        rows = [r for r in rows if r.get("waves_per_simd", 0) >= 4]
+        rows = [r for r in rows if r.get("waves_per_simd") == 8 and r.get("cycles_per_wave_inst")]
         if rows:
             return min(r["cycles_per_wave_inst"] for r in rows)
     return 2.0
@@ -62,7 +63,8 @@ def trace_sq(src, kernel, p1="sq1", p2="sq2", what="config-2 bounce rays from th
     # GRBM_GUI_ACTIVE counts the GPU's busy clocks over the counter pass's sampling window of the dispatch, summed over the 8
     # XCDs; for short launches (fills, k_finalize, k_shade: a few us) that window is longer than the kernel's own
     # timestamps and the quotient exceeds the chip's 2.4 GHz.  Only a clock the chip can run is kept;
-    # otherwise the fields that divide by it are null (not evidence) and the issue fraction uses the nominal clock
+    # otherwise the fields that divide by it are null (not evidence) and the issue fraction uses the nominal clock.  The raw
+    # quotient is not published (it read 3.5-12.9 GHz for short launches)
     clk_raw = med(ds, "GRBM_GUI_ACTIVE") / 8 / ns      # GHz
     clk = clk_raw if 0.5 <= clk_raw <= 2.45 else None
     cycles = ns * (clk or CLOCK_GHZ)
@@ -77,7 +79,6 @@ def trace_sq(src, kernel, p1="sq1", p2="sq2", what="config-2 bounce rays from th
         "launches": len(ds), "launch_ms_median": ns / 1e6,
         "counters_per_launch_median": counters,
         "effective_clock_ghz": round(clk, 3) if clk else None,
-        "grbm_clock_quotient_ghz": round(clk_raw, 3),
         "valu_wave_insts_per_launch": valu,
         "valu_issue_rate_g_per_s": round(rate, 1),
         "valu_issue_peak_g_per_s": peak,
@@ -85,12 +86,13 @@ def trace_sq(src, kernel, p1="sq1", p2="sq2", what="config-2 bounce rays from th
         "valu_issue_frac_at_effective_clock": round(valu * cyc / (SIMDS * cycles), 4) if clk else None,
         "cycles_per_valu_instruction": cyc,
         "valu_lane_utilisation": round(counters["SQ_THREAD_CYCLES_VALU"] / (64 * counters["SQ_ACTIVE_INST_VALU"]), 4),
-        "valu_busy_frac_quad_cycles": round(counters["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cycles), 4),
         "wave_cycles_waiting_frac": round(counters["SQ_WAIT_ANY"] / counters["SQ_WAVE_CYCLES"], 4)
         if "SQ_WAIT_ANY" in counters else None,
-        "note": "VALU issue peak = 1024 SIMDs x 2.4 GHz / cycles per wave64 VALU instruction, measured by "
-                "tools/valu_rate (profiles/*valu_rate*.jsonl: the fastest instruction mix at 4-8 waves/SIMD); SQ_ACTIVE_INST_* and "
-                "SQ_WAVE_CYCLES count quad-cycles (MI355X_MICROARCH.md)",
+        "note": "VALU issue peak = 1024 SIMDs x 2.4 GHz / cycles per wave64 VALU instruction of the fastest class tools/valu_rate "
+                "measured at 8 waves/SIMD (profiles/*_valu_rate.jsonl, round 6: VOP2 fp32 add / mul 2.17; VOP3 forms, fmac, "
+                "max, compares and conversions ~4, the node step's mix 3.51); SQ_ACTIVE_INST_VALU counts one quad-cycle per VALU "
+                "instruction whatever its issue cost (= SQ_INSTS_VALU on every probe class, profiles/r06b_valu_pmc/), so it is "
+                "not a busy measure; SQ_WAVE_CYCLES and SQ_WAIT_* count quad-cycles (MI355X_MICROARCH.md)",
     }
 
 
