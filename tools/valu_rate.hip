@@ -88,6 +88,23 @@ __device__ inline void stamp_end( WaveRec* rec, unsigned long long t0 )
 #define OP_CMP32( v ) asm volatile( "v_cmp_lt_f32_e32 vcc, %0, %1" : : "v"( v ), "v"( a ) : "vcc" )
 #define OP_MAX( v ) asm volatile( "v_max_f32_e32 %0, %0, %1" : "+v"( v ) : "v"( a ) )
 #define OP_CVTU( v ) asm volatile( "v_cvt_f32_u32_e32 %0, %0" : "+v"( v ) )
+/* round 6, second batch: the operations a node step could use instead of the 4-cycle ones above: integer max / min
+   (ordered like the floats they hold when the floats are not negative), a byte select by SDWA (an OR with a magic
+   exponent turns a node byte b into the float 2^23 + b), a float subtract, packed add / multiply, a shift, a bit-field
+   extract, a byte permute, a median */
+#define OP_MAXI( v ) asm volatile( "v_max_i32_e32 %0, %0, %1" : "+v"( v ) : "v"( a ) )
+#define OP_MINU( v ) asm volatile( "v_min_u32_e32 %0, %0, %1" : "+v"( v ) : "v"( a ) )
+#define OP_MAX3I( v ) asm volatile( "v_max3_i32 %0, %0, %1, %2" : "+v"( v ) : "v"( a ), "v"( b ) )
+#define OP_ORSDWA( v ) asm volatile( "v_or_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "+v"( v ) : "v"( a ) )
+#define OP_SUB( v ) asm volatile( "v_sub_f32_e32 %0, %0, %1" : "+v"( v ) : "v"( a ) )
+#define OP_PKADD( v ) asm volatile( "v_pk_add_f32 %0, %0, %1" : "+v"( v ) : "v"( a2 ) )
+#define OP_PKMUL( v ) asm volatile( "v_pk_mul_f32 %0, %0, %1" : "+v"( v ) : "v"( a2 ) )
+#define OP_SHR( v ) asm volatile( "v_lshrrev_b32_e32 %0, 3, %0" : "+v"( v ) )
+#define OP_BFE( v ) asm volatile( "v_bfe_u32 %0, %0, 8, 8" : "+v"( v ) )
+#define OP_PERM( v ) asm volatile( "v_perm_b32 %0, %0, %1, %2" : "+v"( v ) : "v"( a ), "v"( b ) )
+#define OP_MED3( v ) asm volatile( "v_med3_f32 %0, %0, %1, %2" : "+v"( v ) : "v"( a ), "v"( b ) )
+#define OP_CMPI( v ) asm volatile( "v_cmp_lt_i32_e32 vcc, %0, %1" : : "v"( v ), "v"( a ) : "vcc" )
+#define OP_MINF( v ) asm volatile( "v_min_f32_e32 %0, %0, %1" : "+v"( v ) : "v"( a ) )
 /* a compare writing an SGPR pair: the chain register is only read (no VALU result to wait on) */
 #define OP_CMP( v ) do { uint64_t sdst; asm volatile( "v_cmp_lt_f32_e64 %0, %1, %2" : "=s"( sdst ) : "v"( v ), "v"( a ) ); } while (0)
 
@@ -109,6 +126,19 @@ DEFINE_PROBE( cnd32, float, INITF, OP_CND32, FOLDF )
 DEFINE_PROBE( cmp32, float, INITF, OP_CMP32, FOLDF )
 DEFINE_PROBE( max, float, INITF, OP_MAX, FOLDF )
 DEFINE_PROBE( cvtu, float, INITF, OP_CVTU, FOLDF )
+DEFINE_PROBE( maxi, float, INITF, OP_MAXI, FOLDF )
+DEFINE_PROBE( minu, float, INITF, OP_MINU, FOLDF )
+DEFINE_PROBE( max3i, float, INITF, OP_MAX3I, FOLDF )
+DEFINE_PROBE( orsdwa, float, INITF, OP_ORSDWA, FOLDF )
+DEFINE_PROBE( sub, float, INITF, OP_SUB, FOLDF )
+DEFINE_PROBE( pkadd, f2, INITP, OP_PKADD, FOLDP )
+DEFINE_PROBE( pkmul, f2, INITP, OP_PKMUL, FOLDP )
+DEFINE_PROBE( shr, float, INITF, OP_SHR, FOLDF )
+DEFINE_PROBE( bfe, float, INITF, OP_BFE, FOLDF )
+DEFINE_PROBE( perm, float, INITF, OP_PERM, FOLDF )
+DEFINE_PROBE( med3, float, INITF, OP_MED3, FOLDF )
+DEFINE_PROBE( cmpi, float, INITF, OP_CMPI, FOLDF )
+DEFINE_PROBE( minf, float, INITF, OP_MINF, FOLDF )
 
 /* the BVH4 node step's mix, compiler-scheduled (round 3's probe): two packed slab-plane FMAs, an entry max3 and an exit
    min3, the padded exit, two compares and a select into an integer sort key, an unsigned compare-exchange; 8 chains.
@@ -163,7 +193,10 @@ int main( int argc, char** argv )
 		{ "fma", k_fma, 64 }, { "add", k_add, 64 }, { "mul", k_mul, 64 }, { "pkfma", k_pkfma, 64 }, { "max3", k_max3, 64 },
 		{ "and", k_and, 64 }, { "addu", k_addu, 64 }, { "cvtb", k_cvtb, 64 }, { "cnd", k_cnd, 64 }, { "mov", k_mov, 64 },
 		{ "ldexp", k_ldexp, 64 }, { "rcp", k_rcp, 64 }, { "cmp", k_cmp, 64 }, { "fmac", k_fmac, 64 }, { "cnd32", k_cnd32, 64 },
-		{ "cmp32", k_cmp32, 64 }, { "max", k_max, 64 }, { "cvtu", k_cvtu, 64 }, { "mix", k_mix, 0 } };
+		{ "cmp32", k_cmp32, 64 }, { "max", k_max, 64 }, { "cvtu", k_cvtu, 64 }, { "mix", k_mix, 0 },
+		{ "maxi", k_maxi, 64 }, { "minu", k_minu, 64 }, { "max3i", k_max3i, 64 }, { "orsdwa", k_orsdwa, 64 }, { "sub", k_sub, 64 },
+		{ "pkadd", k_pkadd, 64 }, { "pkmul", k_pkmul, 64 }, { "shr", k_shr, 64 }, { "bfe", k_bfe, 64 }, { "perm", k_perm, 64 },
+		{ "med3", k_med3, 64 }, { "cmpi", k_cmpi, 64 }, { "minf", k_minf, 64 } };
 	for (auto& md : modes)
 	{
 		if (only && strcmp( only, md.name )) continue;
