@@ -556,10 +556,11 @@ __global__ __launch_bounds__( 256 ) void k_tlas_to_bvh4( const float4* __restric
 }
 
 /* quantized BVH4 node (64 B, read by box4q in lh2_box4.inc):
-     uint4 [0]  origin x, y, z (f32 bits: the smallest lo of the node's children), then the grid exponents
-                e_x, e_y, e_z as signed bytes (plane = origin + q * 2^e)
+     uint4 [0]  origin x, y, z (f32 bits: the smallest lo of the node's children), then the x grid step 2^e_x (f32 bits;
+                plane = origin + q * 2^e)
      uint4 [1]  x lo bytes of children 0..3, x hi bytes, y lo bytes, y hi bytes
-     uint4 [2]  z lo bytes, z hi bytes, 0, 0
+     uint4 [2]  z lo bytes, z hi bytes, the y and z grid steps 2^e_y, 2^e_z (f32 bits; round 6: exponent bytes before, which
+                cost box4q a bit-field extract and an ldexp per axis, 4-cycle instructions, where a multiply is a 2-cycle one)
      uint4 [3]  the four child references (as the f32 node's)
    Child planes round outward (lo down, hi up, computed in double, so the quantized box holds the f32 one
    exactly); an empty slot (NaN planes) is the inverted box lo = 255, hi = 0 with the pop marker as its
@@ -622,10 +623,10 @@ __global__ __launch_bounds__( 256 ) void k_quantize4( const float4* __restrict__
 		}
 	}
 	uint4* d = q + (size_t)(first + i) * 4;
-	d[0] = make_uint4( __float_as_uint( origin[0] ), __float_as_uint( origin[1] ), __float_as_uint( origin[2] ),
-		(uint32_t)(e[0] & 255) | ((uint32_t)(e[1] & 255) << 8) | ((uint32_t)(e[2] & 255) << 16) );
+	/* the grid steps 2^e as f32 (exact: -100 <= e <= LH2_QEXP_MAX): box4q scales the ray's reciprocal with one multiply */
+	d[0] = make_uint4( __float_as_uint( origin[0] ), __float_as_uint( origin[1] ), __float_as_uint( origin[2] ), __float_as_uint( ldexpf( 1.0f, e[0] ) ) );
 	d[1] = make_uint4( qlo[0], qhi[0], qlo[1], qhi[1] );
-	d[2] = make_uint4( qlo[2], qhi[2], 0u, 0u );
+	d[2] = make_uint4( qlo[2], qhi[2], __float_as_uint( ldexpf( 1.0f, e[1] ) ), __float_as_uint( ldexpf( 1.0f, e[2] ) ) );
 	/* an empty slot's reference is the traversal's pop marker (INT_MIN, LH2_POP in lh2_kernels.hip): if the
 	   inverted box is ever entered (a small node far down the ray, where the exit pad exceeds its grid), the
 	   ray just pops on (the f32 nodes keep 0 there, a real node, behind boxes of NaN that never hit) */

@@ -550,8 +550,8 @@ def test_quantized_nodes_hold_the_f32_boxes(fresh_core):
     hi = np.stack([f[:, 4:8], f[:, 12:16], f[:, 20:24]], 1).astype(np.float64)
     valid = (np.isfinite(lo) & np.isfinite(hi) & (lo <= hi)).all(1)              # (n, child)
     origin = q[:, 0:3].view(np.float32).astype(np.float64)
-    exps = ((q[:, 3:4] >> np.array([0, 8, 16], np.uint32)) & 255).astype(np.int8).astype(np.int64)
-    step = np.ldexp(1.0, exps)                                                     # (n, axis)
+    step = q[:, [3, 10, 11]].view(np.float32).astype(np.float64)                  # (n, axis): the grid steps 2^e
+    assert np.all(np.frexp(step)[0] == 0.5)                                        # powers of two
     shifts = np.array([0, 8, 16, 24], np.uint32)
     qlo = np.stack([(q[:, 4 + 2 * a, None] >> shifts) & 255 for a in range(3)], 1).astype(np.float64)
     qhi = np.stack([(q[:, 5 + 2 * a, None] >> shifts) & 255 for a in range(3)], 1).astype(np.float64)
