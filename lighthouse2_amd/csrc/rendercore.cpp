@@ -1187,7 +1187,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		{
 			/* the per-ray primary launch after its camera launch (the camera's resets set the dense segment counts); beside the
 			   previous frame it walks with a global stack of its own; the core stream waits for it */
-			const int waves = traceWaves ? traceWaves : sd.tlasRoot4 < 0 ? 7 : 8;
+			const int waves = traceWaves ? traceWaves : 7;
 			ta.traceWaves = (uint32_t)waves;
 			if (primStream != stream) ta.gstack = ps.aheadStack.ptr;
 			lh2_launch_trace_closest( &sd, &ta, smCount * ClosestBlocksPerCU( waves ), { nullptr, ps.evTrace[pathLength] }, primStream );
@@ -1206,8 +1206,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			   probably does too): fewer blocks per CU, so the packets' latency-bound waves get slots from the start instead
 			   of the bounce launch's tail (config 2: 4262-4296 -> 4437-4442 Mrays/s at 5, r03q_ab_trace_blocks.txt) */
 			const bool beside = besideNext && !ta.packet;
-			/* traceWaves 0: 7 waves for a single instance, 8 for instanced scenes (each on its own occupancy's grid) */
-			const int waves = traceWaves ? traceWaves : sd.tlasRoot4 < 0 ? 7 : 8;
+			/* traceWaves 0: the 7-wave variant for every scene (round 6: instanced scenes too, with the early node loads), on its occupancy's grid */
+			const int waves = traceWaves ? traceWaves : 7;
 			const int g = ta.packet ? PacketGrid() : beside ? smCount * std::min( blocksPerCU, kOverlapTraceBlocks ) : smCount * ClosestBlocksPerCU( waves );
 			ta.traceWaves = beside ? 7u : (uint32_t)waves;   /* 8 waves slow the packets beside the launch (r04ad) */
 #ifdef LH2_TOUCH

@@ -231,15 +231,16 @@ private:
 
 	int device = 0, smCount = 256, blocksPerCU = 8, maxBlocksPerCU = 8, packetBlocksPerCU = 8, pathBlocksPerCU = 3, pathBlocksPerCU4 = 4;
 	int traceBlocksPerCU7 = 7, traceBlocksPerCU8 = 8;   /* occupancy of the closest-hit kernel's 7- and 8-wave variants */
-	/* closest-hit launches with the chip alone: 0, by scene: a single instance the 7-wave variant (72 VGPRs, no spills),
-	   instanced scenes the 8-wave one (64 VGPRs); 7 or 8: that variant.  8 for every scene won in round 4; with the early
-	   node loads (single-instance loops only) the single-instance 8-wave loop spills, and 7 there is config 3 -3.4 %, 4K -3 %,
-	   the N = 8 share -2.9 %, while config 5 (instanced) stays 2 % faster at 8 (profiles/r05f_ab_trace_waves.txt) */
+	/* closest-hit launches with the chip alone: 0, the 7-wave variant (72 VGPRs); 7 or 8: that variant.  8 for every scene won
+	   in round 4; with the early node loads (round 5: single-instance loops only) the single-instance 8-wave loop spills, and 7
+	   there is config 3 -3.4 %, 4K -3 %, the N = 8 share -2.9 % (profiles/r05f_ab_trace_waves.txt); round 6 gave the instanced
+	   loops the early loads too, at 7 waves (config 5 9.31-9.32 -> 9.19-9.21 ms; at 8 they spill: 13.2 ms,
+	   profiles/r06l_ab_instanced_early.txt) */
 	int traceWaves = 0;
 	int userBlocksPerCU = 0;             /* setting "traceBlocksPerCU" (0: not set) */
-	/* the closest-hit kernel variant a per-ray launch with the chip alone takes (traceWaves 0: by scene), and its grid's
+	/* the closest-hit kernel variant a per-ray launch with the chip alone takes (traceWaves 0: 7), and its grid's
 	   blocks per CU: the variant's occupancy, or the user's setting within it */
-	int ScenePicksWaves() const { return traceWaves ? traceWaves : (singleInstanceStart && instances.size() == 1) ? 7 : 8; }
+	int ScenePicksWaves() const { return traceWaves ? traceWaves : 7; }
 	int ClosestBlocksPerCU( int waves ) const
 	{
 		const int occ = waves == 7 ? traceBlocksPerCU7 : traceBlocksPerCU8;
