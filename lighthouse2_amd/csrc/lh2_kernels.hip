@@ -574,7 +574,7 @@ LH2_DEV void trace_stream( const SceneDev& s, const TraceArgs& a, int* __restric
 
 #include "lh2_box4.inc"
 /* the path-tail mode of lh2_trace4d.inc shades with k_shade's code (defined with the shading code below) */
-struct ShadeOut { bool ext, shadow; float4 eO, eD, eT, eQ, sO, sD, sP; };
+struct ShadeOut { bool ext, shadow; float4 eO, eD, eT, eQ, sO, sD, sP; uint32_t seg; /* in: EMIT's shadow segment */ };
 /* -DLH2_SHADE_TIMES (diagnostic builds only): k_shade's wave time split over the stages of shade_path, summed over every
    launch of the process into lh2_shade_tt (time since the lane's previous mark, recorded by the wave's first active lane;
    the counts of marks in [8 + k]), printed by RenderCore::Shutdown (tools/shade_times.sh) */
@@ -590,7 +590,7 @@ __device__ unsigned long long lh2_shade_tt[16];
 #define LH2_STT_PARAM
 #define LH2_STT_PARAM_DEFAULT
 #endif
-template <bool NL, bool SINGLE>
+template <bool NL, bool SINGLE, bool EMIT = false>
 LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd, const float4 T4, const float4 O4, const float4 D4, const float4 Q4,
 	const int pathLength, const uint32_t R0, ShadeOut& o LH2_STT_PARAM_DEFAULT );
 #include "lh2_trace4d.inc"
@@ -1462,7 +1462,7 @@ LH2_DEV float scene_chord( const ShadeParams& p, const float4 o, const float4 d 
 /* one path vertex of shadeKernel (pathtracer.h:54-245): the hit record, ray and path state of a path at
    pathLength in; its extension ray (o.ext) and shadow ray (o.shadow) out.  Shared by k_shade (one launch
    per bounce) and the path-tail kernel (k_trace_path4d: trace and shade in one loop per lane) */
-template <bool NL, bool SINGLE>
+template <bool NL, bool SINGLE, bool EMIT>
 LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd, const float4 T4, const float4 O4, const float4 D4, const float4 Q4,
 	const int pathLength, const uint32_t R0, ShadeOut& o LH2_STT_PARAM )
 {
@@ -1584,10 +1584,20 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 					contribution = fixnan( contribution );
 					contribution = clampintensity( s.clampValue, contribution );
 					const v3 so = SafeOrigin( I, L, muls( N, faceDir ), s.geometryEpsilon );
-					o.shadow = true;
-					o.sO = make_float4( so.x, so.y, so.z, 0 );
-					o.sD = make_float4( L.x, L.y, L.z, dist - 2 * s.geometryEpsilon );
-					o.sP = make_float4( contribution.x, contribution.y, contribution.z, __uint_as_float( pixelIdx ) );
+					const float4 sO = make_float4( so.x, so.y, so.z, 0 ), sD = make_float4( L.x, L.y, L.z, dist - 2 * s.geometryEpsilon );
+					const float4 sP = make_float4( contribution.x, contribution.y, contribution.z, __uint_as_float( pixelIdx ) );
+					if (EMIT)
+					{
+						/* k_shade (round 6): the shadow ray goes into the block's shadow segment here, one atomic for the lanes
+						   that reach this point, so its twelve registers are not live across SampleBSDF */
+						const uint64_t mS = __ballot( true );
+						uint32_t b = 0;
+						if (lane_id() == (uint32_t)__builtin_ctzll( mS )) b = atomicAdd( &p.counters->segShadow[o.seg * LH2_SEGCOUNT_STRIDE], (uint32_t)__popcll( mS ) );
+						const uint32_t ss = (uint32_t)__builtin_amdgcn_readfirstlane( (int)b ) + lanes_below( mS );
+						if (ss < p.shadowStride) { const uint32_t so2 = o.seg * p.shadowStride + ss; p.shO[so2] = sO; p.shD[so2] = sD; p.shP[so2] = sP; }
+						else atomicOr( &p.counters->shadowOverflow, 1u );
+					}
+					else o.shadow = true, o.sO = sO, o.sD = sD, o.sP = sP;
 				}
 			}
 		}
@@ -1632,6 +1642,10 @@ LH2_DEV void shade_epilogue( const ShadeParams& p );   /* the bounce hand-off, b
 #ifndef LH2_SHADE_MINWAVES
 #define LH2_SHADE_MINWAVES 4
 #endif
+/* k_shade writes each shadow ray where shade_path makes it (EMIT), not in the end-of-iteration compaction */
+#ifndef LH2_SHADE_EMIT
+#define LH2_SHADE_EMIT 1
+#endif
 #ifndef LH2_SHADE_NL_MINWAVES
 #define LH2_SHADE_NL_MINWAVES 4   /* 128 VGPRs, 9 spilled; 3 waves: 144, none (A/B: profiles/r01g_ab_shade_nolights.jsonl) */
 #endif
@@ -1670,11 +1684,11 @@ __global__ __launch_bounds__( 256, NL ? LH2_SHADE_NL_MINWAVES : LH2_SHADE_MINWAV
 			const float4 O4 = p.rayO[jobIndex], D4 = p.rayD[jobIndex], Q4 = p.Q4[jobIndex];
 			__builtin_amdgcn_sched_barrier( 0 );
 			ShadeOut so;
-			so.ext = so.shadow = false;
+			so.ext = so.shadow = false, so.seg = seg;
 #ifdef LH2_SHADE_TIMES
-			shade_path<NL, SINGLE>( s, p, hd, T4, O4, D4, Q4, p.pathLength, p.R0, so, &stt );
+			shade_path<NL, SINGLE, LH2_SHADE_EMIT != 0>( s, p, hd, T4, O4, D4, Q4, p.pathLength, p.R0, so, &stt );
 #else
-			shade_path<NL, SINGLE>( s, p, hd, T4, O4, D4, Q4, p.pathLength, p.R0, so );
+			shade_path<NL, SINGLE, LH2_SHADE_EMIT != 0>( s, p, hd, T4, O4, D4, Q4, p.pathLength, p.R0, so );
 #endif
 			doExt = so.ext, doShadow = so.shadow;
 			eO = so.eO, eD = so.eD, eT = so.eT, eQ = so.eQ, sO = so.sO, sD = so.sD, sP = so.sP;
