@@ -1590,12 +1590,23 @@ LH2_DEV void shade_path( const SceneDev& s, const ShadeParams& p, const uint4 hd
 					{
 						/* k_shade (round 6): the shadow ray goes into the block's shadow segment here, one atomic for the lanes
 						   that reach this point, so its twelve registers are not live across SampleBSDF */
-						const uint64_t mS = __ballot( true );
-						uint32_t b = 0;
-						if (lane_id() == (uint32_t)__builtin_ctzll( mS )) b = atomicAdd( &p.counters->segShadow[o.seg * LH2_SEGCOUNT_STRIDE], (uint32_t)__popcll( mS ) );
-						const uint32_t ss = (uint32_t)__builtin_amdgcn_readfirstlane( (int)b ) + lanes_below( mS );
-						if (ss < p.shadowStride) { const uint32_t so2 = o.seg * p.shadowStride + ss; p.shO[so2] = sO; p.shD[so2] = sD; p.shP[so2] = sP; }
-						else atomicOr( &p.counters->shadowOverflow, 1u );
+						uint64_t rem = __ballot( true );
+						while (rem)   /* k_shade: one segment per wave; the path tail: each lane its path's segment */
+						{
+							const uint32_t l0 = (uint32_t)__builtin_ctzll( rem );
+							const uint32_t segv = (uint32_t)__builtin_amdgcn_readlane( (int)o.seg, l0 );
+							const uint64_t mm = __ballot( o.seg == segv ) & rem;
+							uint32_t b = 0;
+							if (lane_id() == l0) b = atomicAdd( &p.counters->segShadow[segv * LH2_SEGCOUNT_STRIDE], (uint32_t)__popcll( mm ) );
+							b = (uint32_t)__builtin_amdgcn_readlane( (int)b, l0 );
+							if ((mm >> lane_id()) & 1ull)
+							{
+								const uint32_t ss = b + lanes_below( mm );
+								if (ss < p.shadowStride) { const uint32_t so2 = segv * p.shadowStride + ss; p.shO[so2] = sO; p.shD[so2] = sD; p.shP[so2] = sP; }
+								else atomicOr( &p.counters->shadowOverflow, 1u );
+							}
+							rem &= ~mm;
+						}
 					}
 					else o.shadow = true, o.sO = sO, o.sD = sD, o.sP = sP;
 				}
