@@ -1158,8 +1158,10 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 			   (pathTailBlocks; 0: 3 for small frames, whose tail phase is the frame's longest, else 2) */
 			const bool side = overlap && snapped;
 			const bool small = (float)pathCount <= kSmallFramePaths;
-			/* the kernel variant: 3 waves per SIMD (no spills) for small frames, 4 (128 VGPRs) for large ones (pathTailWaves) */
-			ta.tailWaves = pathTailWaves == 3 || pathTailWaves == 4 ? (uint32_t)pathTailWaves : small ? 3u : 4u;
+			/* the kernel variant (pathTailWaves 0): 4 waves per SIMD (128 VGPRs) for every frame since the shade batches write their
+			   shadow rays at once (its spills 68 -> 40 VGPRs; small frames: config 3 -0.8 %, profiles/r06s_ab_tail_waves.txt); 3
+			   (no spills) was the small frames' variant before */
+			ta.tailWaves = pathTailWaves == 3 || pathTailWaves == 4 ? (uint32_t)pathTailWaves : 4u;
 			const int occ = ta.tailWaves == 4 ? pathBlocksPerCU4 : pathBlocksPerCU;
 			const int ptBlocks = pathTailBlocks > 0 ? pathTailBlocks : side ? (small ? 3 : 2) : occ;
 			lh2_launch_trace_path( &sd, &ta, &sp, smCount * std::min( std::min( blocksPerCU, occ ), ptBlocks ), { nullptr, ps.evTrace[pathLength] }, stream );
