@@ -266,7 +266,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "cameraFused" )) cameraFused = value != 0;
 	else if (!strcmp( name, "frameOverlap" )) frameOverlap = (int)value;
 	else if (!strcmp( name, "earlyShade" )) earlyShade = value != 0;
-	else if (!strcmp( name, "sideBlocks" )) sideBlocks = std::min( 8, std::max( 0, (int)value ) );
+	else if (!strcmp( name, "sideBlocks" )) sideBlocks = std::min( 8, std::max( -1, (int)value ) );
 	else if (!strcmp( name, "pathTailBlocks" )) pathTailBlocks = std::min( 8, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "shadeBlocks" )) shadeBlocks = std::min( 64, std::max( 0, (int)value ) );
 	else if (!strcmp( name, "finalShadowBlocks" )) finalShadowBlocks = std::min( 8, std::max( 0, (int)value ) );
@@ -1177,7 +1177,8 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 				ts.refill = (uint32_t)refillOther, ts.leafBatch = (uint32_t)kShadowLeafBatch;
 				ts.mask = shMask, ts.potentials = shP, ts.acc = accumulator.ptr, ts.gstack = ps.sideStack.ptr;
 				/* the global stack (sideStack) is sized for maxBlocksPerCU blocks per CU: the grid stays within it */
-				lh2_launch_trace_any( &sd, &ts, sideBlocks > 0 ? smCount * std::min( sideBlocks, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evSide }, sideStream );
+				const int sb = sideBlocks >= 0 ? sideBlocks : small ? 3 : 4;
+				lh2_launch_trace_any( &sd, &ts, sb > 0 ? smCount * std::min( sb, maxBlocksPerCU ) : grid, 1, { nullptr, ps.evSide }, sideStream );
 				ps.fromSide = ps.prevStop;
 				ps.sideOn = true;
 			}

@@ -412,9 +412,11 @@ private:
 	   (r05f_ab_final_shadow_blocks.txt) */
 	int finalShadowBlocks = 4;
 	int shadeBlocks = 0;                 /* blocks per CU of the frame's shade launches (0: by path count, Render) */
-	/* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's): 4 leaves the next frame's primary
-	   and early shade launches room: config 3 -0.5 %, the N = 8 share -0.8 to -1.5 % (profiles/r04m_ab.txt, r04n_ab.txt) */
-	int sideBlocks = 4;
+	/* blocks per CU of the side shadow launch beside the path tail (0: the trace grid's; -1: by frame size): 4 leaves the next
+	   frame's primary and early shade launches room: config 3 -0.5 %, the N = 8 share -0.8 to -1.5 % (profiles/r04m_ab.txt,
+	   r04n_ab.txt); round 6, with the lighter 4-wave path tail, small frames (<= kSmallFramePaths) 3: config 3 -1.2 %, the N = 8
+	   share -1.8 %, while the 4K frame stays at 4 (3 there: +2 %, profiles/r06y_ab_side_blocks.txt) */
+	int sideBlocks = -1;
 	/* heavy-first primary packets (TraceArgs::hvRead): the packets of the previous frame that took more than
 	   packetHeavy x its mean node steps are taken first; 0: off */
 	float packetHeavy = 2.0f;
