@@ -259,7 +259,7 @@ void RenderCore::Setting( const char* name, float value )  /* rendercore.cpp:439
 	else if (!strcmp( name, "buildThreads" )) buildThreads = std::max( 0, (int)value );   /* host threads of the deferred CPU builds */
 	else if (!strcmp( name, "gpuTlas" )) { gpuTlas = value != 0; instancesDirty = true; }
 	else if (!strcmp( name, "chordSplit" )) chordSplit = std::max( 0.0f, value );   /* two-ended path segments (longest first); 0: off */
-	else if (!strcmp( name, "packetHeavy" )) packetHeavy = std::max( 0.0f, value );   /* heavy-first primary packets; 0: off */
+	else if (!strcmp( name, "packetHeavy" )) packetHeavy = value < 0 ? -1.0f : value;   /* heavy-first primary packets; 0: off; -1: by frame */
 	else if (!strcmp( name, "pathTail" )) pathTail = std::max( 0, (int)value );   /* bounces from this one in one trace-and-shade launch; 0: off */
 	else if (!strcmp( name, "pathTailBatch" )) pathTailBatch = std::min( 64, std::max( 1, (int)value ) );
 	else if (!strcmp( name, "shadowOverlap" )) shadowOverlap = value != 0;
@@ -992,7 +992,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 	cp.clearAcc = restart && !tileChanged ? accumulator.ptr : nullptr;
 	/* heavy-first primary packets: this frame reads the block the previous one recorded, and records into the
 	   other one, which the camera launch zeroes (a new layout zeroes both) */
-	ps.hvOn = packetHeavy > 0 && tiledRays && UsePackets() && !primeRef;
+	ps.hvOn = packetHeavy != 0 && tiledRays && UsePackets() && !primeRef;
 	if (ps.hvOn)
 	{
 		const uint32_t cap = (ps.segStride + 63) / 64, maskWords = (LH2_SEGS * cap + 31) / 32;
@@ -1129,7 +1129,7 @@ void RenderCore::Render( const lh2_ViewPyramid& view, int converge )   /* render
 		if (pathLength == 1 && ta.packet && ps.hvOn)
 		{
 			ta.hvRead = ps.hv.ptr + (size_t)ps.hvParity * ps.hvBlock, ta.hvWrite = ps.hv.ptr + (size_t)(1 - ps.hvParity) * ps.hvBlock;
-			ta.hvCap = ps.hvCap, ta.hvMaskWords = ps.hvMaskWords, ta.hvFactor = packetHeavy;
+			ta.hvCap = ps.hvCap, ta.hvMaskWords = ps.hvMaskWords, ta.hvFactor = packetHeavy > 0 ? packetHeavy : tailL ? 3.0f : 2.0f;
 			hvReadBlock = (uint32_t*)ta.hvRead;
 			ta.hvTiles = 0;
 			for (int k = 0; k < LH2_SEGS; k++)

@@ -418,8 +418,10 @@ private:
 	   share -1.8 %, while the 4K frame stays at 4 (3 there: +2 %, profiles/r06y_ab_side_blocks.txt) */
 	int sideBlocks = -1;
 	/* heavy-first primary packets (TraceArgs::hvRead): the packets of the previous frame that took more than
-	   packetHeavy x its mean node steps are taken first; 0: off */
-	float packetHeavy = 2.0f;
+	   packetHeavy x its mean node steps are taken first; 0: off; -1 (default, round 6): 3 for frames with a path tail, whose
+	   primary launch runs beside the previous frame's tail (config 3 -1.2 %, the 4K frame -0.8 %), 2 otherwise (config 2: 3
+	   is 1.5 % slower), profiles/r06zg_ab_overlap_heavy.txt */
+	float packetHeavy = -1.0f;
 	int traceVersion = 0;                /* 0: auto (TraceVersion) */
 	int TraceVersion() const;
 	int unitCoherent = 0;
